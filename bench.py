@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py -- hypotheses/s of the hypothesize-and-verify hot path on MI355X.
+
+Metric (BASELINE.json): "model hypotheses/sec + wall-time to 0.99 confidence,
+N=10k corrs 50% outliers".  Workload (BASELINE.json configs[1], the hybrid
+rectification path on one MI355X): synthetic M2 problem,
+N_s = 5000 scale + N_o = 5000 orientation features, 50 % outliers each, fp64.
+
+One step = one pass of the hot path over one batch: `--slots` outer-iteration
+slots are drawn (Philox), validated and solved (k_generate), every resulting
+model is MSAC-scored against all 10 000 features (k_score), and the batch's
+first strict best (the reference's update rule) is selected on the host.
+Features are uploaded once before timing (HBM-resident).  `value` is the
+whole-job hypotheses/s; the end-to-end latency of a full estimator call at
+confidence 0.99 (including LO and the final refit) is reported beside it.
+
+Multi-GPU (torchrun): one process per GPU, each rank solves its own image
+pair (weak scaling, no data-path collective); the final per-rank best models
+are gathered to rank 0 with one RCCL all_gather.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "graph-cut-ransac_amd"))
+
+METRIC = "model hypotheses/sec + wall-time to 0.99 confidence, N=10k corrs 50% outliers"
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector fp64 spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["m2", "m1"], default="m2")
+    ap.add_argument("--slots", type=int, default=65536, help="outer-iteration slots (hypotheses) per launch")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-latency", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    import numpy as np
+    import pygcransac
+    from pygcransac import _native as N
+    from pygcransac import synthetic as S
+
+    ctx = N.context(local_rank)
+    seed = 20251121 + rank
+    if args.workload == "m2":
+        f0, f1, _, _, thr0, thr1 = S.problem_m2(5000, 5000, seed=seed)
+        solver = N.SOLVER_SIFT22
+        workload = "M2 hybrid 2+2-SIFT rectification (findRectifyingHomographySIFT), 5000 scale + 5000 orientation"
+    else:
+        f0, _, thr0 = S.problem_m1(10_000, seed=seed)
+        f1, thr1 = None, 0.0
+        solver = N.SOLVER_SCALE3
+        workload = "M1 3-SIFT scale-only rectification (findRectifyingHomographyScaleOnly), 10000 scale"
+    n_total = f0.shape[0] + (0 if f1 is None else f1.shape[0])
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    f0c = np.ascontiguousarray(f0)
+    f1c = None if f1 is None else np.ascontiguousarray(f1)
+    ph = C.c_void_p()
+    N.check(N.lib.gcr_problem_create(ctx, solver, dp(f0c), f0c.shape[0], dp(f1c) if f1c is not None else None,
+                                     0 if f1c is None else f1c.shape[0], C.byref(ph)))
+    prob = ph.value
+    p = N.default_params()
+    p.scale_residual_thresh = thr0
+    p.orientation_residual_thresh = thr1
+    p.seed = seed
+
+    def step(k, st_acc):
+        res = N.BatchResult()
+        st = N.Stats()
+        N.check(N.lib.gcr_problem_verify_batch(prob, C.byref(p), k * args.slots, args.slots, C.byref(res),
+                                               C.byref(st)))
+        if st_acc is not None:
+            st_acc["models"] += res.models
+            st_acc["kernel_ms"] += st.ms_score_kernel
+            st_acc["launches"] += 1
+            if res.best_slot >= 0 and res.best_score > st_acc["best_score"]:
+                st_acc["best_score"] = res.best_score
+                st_acc["best_model"] = (res.best_model.h7, res.best_model.h8, res.best_model.alpha,
+                                        res.best_model.phi)
+        return res
+
+    def barrier():
+        N.check(N.lib.gcr_synchronize(ctx))
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for k in range(args.warmup):
+        step(k, None)
+    acc = dict(models=0, kernel_ms=0.0, launches=0, best_score=-1.0, best_model=(0.0, 0.0, 0.0, 0.0))
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k, acc)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    models_total = acc["models"]
+    gathered = 1
+    if dist is not None:
+        import torch
+
+        dev = torch.device("cuda", local_rank)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        m = torch.tensor([float(models_total)], dtype=torch.float64, device=dev)
+        dist.all_reduce(m, op=dist.ReduceOp.SUM)
+        models_total = int(m.item())
+        # RCCL gather of the final per-rank models (the only collective)
+        mine = torch.tensor([acc["best_score"], *acc["best_model"]], dtype=torch.float64, device=dev)
+        outs = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(outs, mine)
+        gathered = len(outs)
+
+    value = models_total / elapsed
+    avg_kernel_s = acc["kernel_ms"] / max(1, acc["launches"]) / 1e3
+    models_per_launch = acc["models"] / max(1, acc["launches"])
+    bytes_per_launch = models_per_launch * 24.0 * n_total
+    achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
+
+    # wall time to 0.99 confidence: full estimator call (incl. upload, LO, refit)
+    latency = None
+    if not args.no_latency and rank == 0:
+        lat = []
+        for r in range(3):
+            t1 = time.perf_counter()
+            if solver == N.SOLVER_SIFT22:
+                out = pygcransac.findRectifyingHomographySIFT(f0, f1, thr0, thr1, 0.0, 0, 10**7, 50, seed=100 + r,
+                                                              confidence=0.99, device=local_rank, return_stats=True)
+            else:
+                out = pygcransac.findRectifyingHomographyScaleOnly(f0, thr0, 0.0, 0, 10**7, 50, seed=100 + r,
+                                                                   confidence=0.99, device=local_rank,
+                                                                   return_stats=True)
+            lat.append((time.perf_counter() - t1) * 1e3)
+            last_stats = out[-1]
+        latency = dict(ms_median=statistics.median(lat), ms_all=lat,
+                       iterations=last_stats["iteration_number"], hypotheses=last_stats["hypotheses"],
+                       ms_breakdown={k: last_stats[k] for k in ("ms_setup", "ms_generate", "ms_score", "ms_replay",
+                                                                "ms_lo", "ms_refit", "ms_total")})
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ffi as O
+
+        kind = 2 if solver == N.SOLVER_SIFT22 else 0
+        n_cal, s_cal, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, 64)
+        rate = n_cal / max(s_cal, 1e-6)
+        nslots = max(64, int(rate * args.cpu_seconds))
+        n_cpu, s_cpu, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, nslots)
+        cpu = dict(value=n_cpu / s_cpu, unit="hypotheses/s", cores=1, kind="port",
+                   sample=f"{nslots} outer-iteration slots of the same workload, CPU oracle (glibc math, "
+                          f"reference-faithful random_device+mt19937+shuffle sampler, -O2), single thread, "
+                          f"{s_cpu:.1f} s")
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "hypotheses/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded M2/M1 generator, pygcransac/synthetic.py; notebook features absent)",
+            "config": {
+                "workload": workload,
+                "n_features": n_total,
+                "outlier_ratio": 0.5,
+                "hypotheses_per_launch": args.slots,
+                "parallelism": f"problem-sharded x{world}" if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "k_score",
+                "bytes_per_hypothesis": 24 * n_total,
+                "avg_kernel_ms": avg_kernel_s * 1e3,
+                "hypotheses_per_launch": models_per_launch,
+            },
+            "cpu_baseline": cpu,
+            "wall_time_to_0.99_confidence": latency,
+            "gathered_models": gathered,
+        }
+        print(json.dumps(line))
+    N.lib.gcr_problem_destroy(prob)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

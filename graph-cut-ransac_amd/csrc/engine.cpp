@@ -1,0 +1,875 @@
+// engine.cpp -- host engine behind the C ABI (include/gcr.h).
+//
+// GCRANSAC::run (HDR/GCRANSAC.h:192-685) is a strictly sequential loop.  The
+// engine keeps its semantics exactly while moving all per-hypothesis work to
+// the GPU:
+//
+//   * every outer-iteration slot s draws its sample from a Philox stream keyed
+//     by (seed, s, attempt), so slots are independent and are generated and
+//     MSAC-scored in batches (kernels.hip);
+//   * the host then REPLAYS the slots in order with the reference's control
+//     flow: iteration accounting (:293-339), strict best update + isValidModel
+//     (:440-484), LO trigger (:467-477, :494-515), adaptive termination
+//     (:286-287, :738-757), the two inlier buffers (:241-246, :460, :563-594)
+//     and the final refit (:628-675).  Results are independent of batch size.
+//   * local optimisation (:873-1062) runs on the host (relabel masks and the
+//     50 trial scores come from GPU launches, the least-squares fits are host
+//     C++); graph-cut labeling runs on the empty neighbourhood graph that every
+//     Python entry point builds (gcransac_python.cpp:63-68), i.e. a per-node
+//     terminal-capacity test evaluated in k_mask.
+//
+// An inlier buffer is represented by the model whose MSAC inliers it holds and
+// its per-class sizes; index lists are materialised (k_mask) only when needed.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "gcr.h"
+#include "host_fit.h"
+#include "kernels.h"
+#include "philox.h"
+
+using namespace gcr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+struct HipError {
+    hipError_t e;
+    const char* what;
+};
+
+inline void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw HipError{e, what};
+}
+#define HIPC(x) hip_check((x), #x)
+
+using Clock = std::chrono::steady_clock;
+inline double ms_since(Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        HIPC(hipMalloc(reinterpret_cast<void**>(&p), sizeof(T) * n));
+        cap = n;
+    }
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+template <class T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        HIPC(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(T) * n, hipHostMallocDefault));
+        cap = n;
+    }
+    ~PinBuf() { if (p) (void)hipHostFree(p); }
+};
+
+// Score arrays for `cap` hypotheses, device and pinned host mirrors.
+struct ScoreBufs {
+    DevBuf<uint32_t> n0, n1;
+    DevBuf<double> v0, v1, tot;
+    PinBuf<uint32_t> hn0, hn1;
+    PinBuf<double> hv0, hv1, htot;
+    void ensure(size_t n) {
+        n0.ensure(n); n1.ensure(n); v0.ensure(n); v1.ensure(n); tot.ensure(n);
+        hn0.ensure(n); hn1.ensure(n); hv0.ensure(n); hv1.ensure(n); htot.ensure(n);
+    }
+    ScoreOut dev() const { return ScoreOut{n0.p, n1.p, v0.p, v1.p, tot.p}; }
+    void d2h(size_t n, hipStream_t s) {
+        HIPC(hipMemcpyAsync(hn0.p, n0.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(hn1.p, n1.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(hv0.p, v0.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(hv1.p, v1.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(htot.p, tot.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+};
+
+// Score<K> (score.hpp:11-102) with the MSAC post-processing of
+// MSACScoringFunction::getScore (MSAC_scoring_function.hpp:108-127).
+struct HScore {
+    uint64_t n[2] = {0, 0};
+    double v[2] = {0.0, 0.0};
+    uint64_t total = 0;
+    double sum = 0.0;
+};
+
+struct Buffer {              // one of temp_inner_inliers[2]
+    bool has = false;
+    RectModel model{};
+    uint64_t n[2] = {0, 0};  // list sizes (raw inlier counts of `model`)
+};
+
+}  // namespace
+
+struct gcr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+struct gcr_problem {
+    gcr_ctx* ctx = nullptr;
+    int solver = 0;
+    int K = 1;
+    HostClass hc[2];
+    double* dmem = nullptr;
+    DevProblem dp{};
+    // work buffers
+    DevBuf<uint8_t> inc;
+    DevBuf<RectModel> models;
+    PinBuf<uint8_t> h_inc;
+    PinBuf<RectModel> h_models;
+    ScoreBufs sb;
+    DevBuf<RectModel> lo_models;
+    ScoreBufs lo_sb;
+    DevBuf<uint8_t> mask[2];
+    PinBuf<uint8_t> h_mask[2];
+    ~gcr_problem() { if (dmem) (void)hipFree(dmem); }
+};
+
+namespace {
+
+// ------------------------------------------------------------- problem ----
+int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
+                 gcr_problem** out) {
+    if (!ctx || !out) return set_err(GCR_EINVAL, "null context or output pointer");
+    if (solver < 0 || solver > 2) return set_err(GCR_EINVAL, "unknown solver %d", solver);
+    const int K = solver == 2 ? 2 : 1;
+    const size_t m0 = solver == 2 ? 2 : 3;
+    if (!f0 || (K == 2 && !f1)) return set_err(GCR_EINVAL, "null feature pointer");
+    if (n0 < m0 || (K == 2 && n1 < 2))
+        return set_err(GCR_EINTERNAL, "Data set smaller than minimal sample size for corresponding data type");
+    if (n0 > 0xffffffffull || n1 > 0xffffffffull) return set_err(GCR_EINVAL, "too many features");
+    auto P = std::unique_ptr<gcr_problem>(new (std::nothrow) gcr_problem());
+    if (!P) return set_err(GCR_ENOMEM, "out of host memory");
+    P->ctx = ctx;
+    P->solver = solver;
+    P->K = K;
+    const double kScalePower = (solver == 1) ? (-1.0 / 3.0) : (1.0 / 3.0);
+    const double* src[2] = {f0, f1};
+    const size_t ns[2] = {n0, K == 2 ? n1 : 0};
+    for (int c = 0; c < K; ++c) {
+        HostClass& h = P->hc[c];
+        const size_t n = ns[c];
+        h.n = n;
+        h.x.resize(n); h.y.resize(n); h.a.resize(n); h.c0.resize(n); h.c1.resize(n);
+        for (size_t i = 0; i < n; ++i) {
+            h.x[i] = src[c][3 * i];
+            h.y[i] = src[c][3 * i + 1];
+            h.a[i] = src[c][3 * i + 2];
+            if (c == 0) {            // scale: pow(s, kScalePower) exactly as the solvers call it
+                h.c0[i] = std::pow(h.a[i], kScalePower);
+                h.c1[i] = 0.0;
+            } else {                 // orientation: lineFromPointAndAngle's cos / sin
+                h.c0[i] = std::cos(h.a[i]);
+                h.c1[i] = std::sin(h.a[i]);
+            }
+        }
+    }
+    const size_t total = 5 * (ns[0] + ns[1]);
+    HIPC(hipSetDevice(ctx->device));
+    HIPC(hipMalloc(reinterpret_cast<void**>(&P->dmem), total * sizeof(double)));
+    double* cur = P->dmem;
+    P->dp.solver = solver;
+    for (int c = 0; c < 2; ++c) {
+        DevClass& d = P->dp.cls[c];
+        d.n = (uint32_t)ns[c];
+        if (ns[c] == 0) { d.x = d.y = d.a = d.c0 = d.c1 = nullptr; continue; }
+        const std::vector<double>* arrs[5] = {&P->hc[c].x, &P->hc[c].y, &P->hc[c].a, &P->hc[c].c0, &P->hc[c].c1};
+        const double** dst[5] = {&d.x, &d.y, &d.a, &d.c0, &d.c1};
+        for (int q = 0; q < 5; ++q) {
+            HIPC(hipMemcpyAsync(cur, arrs[q]->data(), ns[c] * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+            *dst[q] = cur;
+            cur += ns[c];
+        }
+    }
+    HIPC(hipStreamSynchronize(ctx->stream));
+    *out = P.release();
+    return GCR_OK;
+}
+
+// ---------------------------------------------------------------- runner ----
+class Runner {
+public:
+    Runner(gcr_problem* P, const gcr_params& prm) : P_(P), prm_(prm), s_(P->ctx->stream) {
+        K_ = P->K;
+        m_[0] = P->solver == 2 ? 2 : 3;
+        m_[1] = 2;
+        thr_[0] = prm.scale_residual_thresh;
+        thr_[1] = prm.orientation_residual_thresh;
+        for (int c = 0; c < 2; ++c) {
+            Tm_[c] = (2.25 * thr_[c]) * thr_[c];            // MSAC_scoring_function.hpp:64
+            const double t = 1.5 * thr_[c];                 // GCRANSAC.h:207-208
+            Tlo_[c] = t * t;
+        }
+        N_[0] = P->hc[0].n;
+        N_[1] = K_ == 2 ? P->hc[1].n : 0;
+        log_prob_ = std::log(1.0 - prm.confidence);
+        do_lo_ = (prm.flags & GCR_FLAG_NO_LO) == 0;
+        std::memset(&st_, 0, sizeof(st_));
+    }
+
+    // Full GCRANSAC::run; fills outputs, returns total inlier count.
+    int run(uint8_t* mask0, uint8_t* mask1, double* H, gcr_rect_model* model_out) {
+        const auto t_all = Clock::now();
+        const uint64_t ones[2] = {1, 1};
+        uint64_t max_iteration = iteration_number(ones);
+        const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
+        const uint64_t L = std::max(min_it, max_it);
+        uint64_t slot = 0, chunk_begin = 0, chunk_end = 0, chunk_no = 0, last_chunk = 0;
+        double replay_ms = 0;
+        auto t_rep = Clock::now();
+        while (min_it > it_ || it_ < std::min(max_iteration, max_it)) {
+            if (slot == chunk_end) {
+                replay_ms += ms_since(t_rep);
+                uint64_t B;
+                if (prm_.batch_slots) B = prm_.batch_slots;
+                else if (min_it >= max_it) B = 65536;
+                else B = chunk_no == 0 ? 512 : std::min<uint64_t>(65536, last_chunk * 4);
+                B = std::min<uint64_t>(B, L - it_);
+                B = std::max<uint64_t>(B, 1);
+                last_chunk = B;
+                chunk_begin = slot;
+                chunk_end = slot + fetch_chunk(slot, (uint32_t)B, L);
+                ++chunk_no;
+                t_rep = Clock::now();
+            }
+            const size_t j = slot - chunk_begin;
+            bool do_lo = false;
+            ++it_;
+            const uint8_t inc = P_->h_inc.p[j];
+            it_ += (uint64_t)inc - 1;
+            ++slot;
+            if (inc <= 101) {
+                const RectModel& model = P_->h_models.p[j];
+                const uint32_t rn[2] = {P_->sb.hn0.p[j], P_->sb.hn1.p[j]};
+                const HScore cur = finish(rn, P_->sb.hv0.p[j], P_->sb.hv1.p[j], P_->sb.htot.p[j]);
+                bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
+                ++st_.hypotheses;
+                if (best_.sum < cur.sum && valid_model(model)) {
+                    off_ = 1 - off_;
+                    best_model_ = model;
+                    best_ = cur;
+                    bool nonmin = false;
+                    for (int c = 0; c < K_; ++c) if (best_.n[c] > m_[c]) { nonmin = true; break; }
+                    do_lo = (it_ > 20) && nonmin;
+                    max_iteration = iteration_number(best_.n);
+                }
+            }
+            if (do_lo_ && do_lo) {
+                replay_ms += ms_since(t_rep);
+                ++lo_number_;
+                local_optimization(bufs_[off_]);
+                max_iteration = iteration_number(best_.n);
+                t_rep = Clock::now();
+            }
+        }
+        replay_ms += ms_since(t_rep);
+        st_.slots = slot;
+        st_.ms_replay = replay_ms;
+
+        int total = 0;
+        RectModel out_model = default_model();
+        std::memset(mask0, 0, N_[0]);
+        if (K_ == 2 && mask1) std::memset(mask1, 0, N_[1]);
+        bool minimal = true;
+        for (int c = 0; c < K_; ++c) if (best_.n[c] > m_[c]) minimal = false;
+        if (!minimal) {
+            if (do_lo_ && lo_number_ == 0) {
+                ++lo_number_;
+                local_optimization(bufs_[off_]);
+            }
+            const auto t_ref = Clock::now();
+            bool diff = false;
+            for (int c = 0; c < K_; ++c) if (bufs_[off_].n[c] != best_.n[c]) diff = true;
+            if (diff) off_ = 1 - off_;
+            diff = false;
+            for (int c = 0; c < K_; ++c) if (bufs_[off_].n[c] != best_.n[c]) diff = true;
+            if (diff) {
+                HScore s;
+                uint32_t rn[2];
+                score_models(&best_model_, 1, &s, rn);
+                best_ = s;
+                bufs_[off_] = Buffer{true, best_model_, {rn[0], rn[1]}};
+            }
+            // iteratedLeastSquaresFitting never succeeds (GCRANSAC.h:1092-1098):
+            // one non-minimal fit on the buffer's inliers, kept if strictly better.
+            std::vector<uint32_t> lists[2];
+            inlier_lists(bufs_[off_].model, Tm_, 0, lists);
+            RectModel refit;
+            if (fit_nonminimal(P_->solver, P_->hc, lists, refit)) {
+                HScore s;
+                uint32_t rn[2];
+                score_models(&refit, 1, &s, rn);
+                const int idx = 1 - off_;
+                bufs_[idx] = Buffer{true, refit, {rn[0], rn[1]}};
+                if (best_.sum < s.sum) {
+                    best_model_ = refit;
+                    off_ = idx;
+                    inlier_lists(bufs_[off_].model, Tm_, 0, lists);
+                }
+            }
+            for (uint32_t i : lists[0]) mask0[i] = 1;
+            if (K_ == 2 && mask1) for (uint32_t i : lists[1]) mask1[i] = 1;
+            total = (int)(lists[0].size() + lists[1].size());
+            out_model = best_model_;
+            st_.score = best_.sum;
+            st_.ms_refit = ms_since(t_ref);
+        }
+        homography_of(out_model, H);
+        if (model_out) {
+            *model_out = gcr_rect_model{out_model.x0, out_model.y0, out_model.s, out_model.h7,
+                                        out_model.h8, out_model.alpha, out_model.phi};
+        }
+        st_.iteration_number = it_;
+        st_.local_optimization_number = lo_number_;
+        st_.graph_cut_number = gc_number_;
+        st_.ms_total = ms_since(t_all);
+        return total;
+    }
+
+    gcr_stats stats() const { return st_; }
+
+    // One hot-path batch (bench): generate + score + first strict maximum.
+    void verify_batch(uint64_t slot0, uint32_t nslots, gcr_batch_result* out) {
+        const auto t0 = Clock::now();
+        P_->inc.ensure(nslots); P_->models.ensure(nslots); P_->sb.ensure(nslots);
+        P_->h_inc.ensure(nslots); P_->h_models.ensure(nslots);
+        HIPC(launch_generate(P_->dp, prm_.seed, slot0, nslots, P_->inc.p, P_->models.p, s_));
+        HIPC(hipEventRecord(P_->ctx->ev0, s_));
+        HIPC(launch_score(P_->dp, Tm_, P_->models.p, P_->inc.p, nslots, true, P_->sb.dev(), s_));
+        HIPC(hipEventRecord(P_->ctx->ev1, s_));
+        P_->sb.d2h(nslots, s_);
+        HIPC(hipMemcpyAsync(P_->h_inc.p, P_->inc.p, nslots, hipMemcpyDeviceToHost, s_));
+        HIPC(hipMemcpyAsync(P_->h_models.p, P_->models.p, nslots * sizeof(RectModel), hipMemcpyDeviceToHost, s_));
+        HIPC(hipStreamSynchronize(s_));
+        float kms = 0;
+        HIPC(hipEventElapsedTime(&kms, P_->ctx->ev0, P_->ctx->ev1));
+        st_.ms_score_kernel += kms;
+        st_.launches += 2;
+        out->models = 0;
+        out->iterations = 0;
+        out->best_slot = -1;
+        out->best_score = 0.0;
+        out->best_inliers[0] = out->best_inliers[1] = 0;
+        HScore best;
+        int64_t bj = -1;
+        for (uint32_t j = 0; j < nslots; ++j) {
+            const uint8_t inc = P_->h_inc.p[j];
+            out->iterations += inc;
+            if (inc > 101) continue;
+            ++out->models;
+            const uint32_t rn[2] = {P_->sb.hn0.p[j], P_->sb.hn1.p[j]};
+            const HScore cur = finish(rn, P_->sb.hv0.p[j], P_->sb.hv1.p[j], P_->sb.htot.p[j]);
+            if (best.sum < cur.sum && valid_model(P_->h_models.p[j])) { best = cur; bj = j; }
+        }
+        if (bj >= 0) {
+            const RectModel& bm = P_->h_models.p[bj];
+            out->best_model = gcr_rect_model{bm.x0, bm.y0, bm.s, bm.h7, bm.h8, bm.alpha, bm.phi};
+            out->best_slot = (int64_t)(slot0 + (uint64_t)bj);
+            out->best_score = best.sum;
+            out->best_inliers[0] = best.n[0];
+            out->best_inliers[1] = best.n[1];
+        }
+        st_.hypotheses += out->models;
+        st_.hypotheses_computed += nslots;
+        st_.ms_total += ms_since(t0);
+    }
+
+private:
+    gcr_problem* P_;
+    gcr_params prm_;
+    hipStream_t s_;
+    int K_;
+    uint64_t m_[2];
+    double thr_[2], Tm_[2], Tlo_[2];
+    uint64_t N_[2];
+    double log_prob_;
+    bool do_lo_;
+    gcr_stats st_;
+
+    uint64_t it_ = 0;
+    HScore best_{};
+    RectModel best_model_ = default_model();
+    Buffer bufs_[2];
+    int off_ = 0;
+    uint64_t lo_number_ = 0, gc_number_ = 0;
+
+    bool valid_model(const RectModel& m) const { return P_->solver == 2 ? valid_model_sift22(m) : true; }
+
+    HScore finish(const uint32_t rn[2], double v0, double v1, double tot) const {
+        HScore s;
+        s.n[0] = rn[0];
+        s.n[1] = K_ == 2 ? rn[1] : 0;
+        s.v[0] = v0;
+        s.v[1] = K_ == 2 ? v1 : 0.0;
+        s.total = s.n[0] + s.n[1];
+        s.sum = tot;
+        for (int c = 0; c < K_; ++c) {
+            if (s.n[c] < m_[c]) return HScore{};
+            const double normed = s.v[c] / Tm_[c];
+            const double msac = normed + static_cast<double>(s.n[c]);
+            s.sum -= s.v[c];
+            s.v[c] = msac;
+            s.sum += msac;
+        }
+        return s;
+    }
+
+    // GCRANSAC::getIterationNumber (GCRANSAC.h:738-757)
+    uint64_t iteration_number(const uint64_t inl[2]) const {
+        double q = 1.0;
+        for (int c = 0; c < K_; ++c) {
+            const double ratio = static_cast<double>(inl[c]) / static_cast<double>(N_[c]);
+            q *= std::pow(ratio, static_cast<double>(m_[c]));
+        }
+        const double lg = std::log(1 - q);
+        if (std::fabs(lg) < std::numeric_limits<double>::epsilon()) return std::numeric_limits<uint64_t>::max();
+        return static_cast<uint64_t>(std::ceil(log_prob_ / lg));
+    }
+
+    // Generate [s0, s0+B), then score only the slots the loop can still reach
+    // (iterations can never pass max(min_it, max_it)).  Returns slots scored.
+    uint64_t fetch_chunk(uint64_t s0, uint32_t B, uint64_t L) {
+        P_->inc.ensure(B); P_->models.ensure(B); P_->sb.ensure(B);
+        P_->h_inc.ensure(B); P_->h_models.ensure(B);
+        auto t0 = Clock::now();
+        HIPC(launch_generate(P_->dp, prm_.seed, s0, B, P_->inc.p, P_->models.p, s_));
+        HIPC(hipMemcpyAsync(P_->h_inc.p, P_->inc.p, B, hipMemcpyDeviceToHost, s_));
+        HIPC(hipStreamSynchronize(s_));
+        st_.ms_generate += ms_since(t0);
+        uint64_t itp = it_, cnt = 0;
+        while (cnt < B && itp < L) itp += P_->h_inc.p[cnt++];
+        if (cnt == 0) cnt = 1;
+        t0 = Clock::now();
+        HIPC(hipEventRecord(P_->ctx->ev0, s_));
+        HIPC(launch_score(P_->dp, Tm_, P_->models.p, P_->inc.p, (uint32_t)cnt, true, P_->sb.dev(), s_));
+        HIPC(hipEventRecord(P_->ctx->ev1, s_));
+        P_->sb.d2h(cnt, s_);
+        HIPC(hipMemcpyAsync(P_->h_models.p, P_->models.p, cnt * sizeof(RectModel), hipMemcpyDeviceToHost, s_));
+        HIPC(hipStreamSynchronize(s_));
+        float kms = 0;
+        HIPC(hipEventElapsedTime(&kms, P_->ctx->ev0, P_->ctx->ev1));
+        st_.ms_score_kernel += kms;
+        st_.ms_score += ms_since(t0);
+        st_.launches += 2;
+        st_.hypotheses_computed += cnt;
+        return cnt;
+    }
+
+    // Score explicit host models on the GPU (LO trials, refit, reconcile).
+    void score_models(const RectModel* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */) {
+        P_->lo_models.ensure(n);
+        P_->lo_sb.ensure(n);
+        bool identity = true;
+        for (uint32_t i = 0; i < n; ++i) identity = identity && identity_norm(models[i]);
+        HIPC(hipMemcpyAsync(P_->lo_models.p, models, n * sizeof(RectModel), hipMemcpyHostToDevice, s_));
+        HIPC(launch_score(P_->dp, Tm_, P_->lo_models.p, nullptr, n, identity, P_->lo_sb.dev(), s_));
+        P_->lo_sb.d2h(n, s_);
+        HIPC(hipStreamSynchronize(s_));
+        st_.launches += 1;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t rn[2] = {P_->lo_sb.hn0.p[i], P_->lo_sb.hn1.p[i]};
+            out[i] = finish(rn, P_->lo_sb.hv0.p[i], P_->lo_sb.hv1.p[i], P_->lo_sb.htot.p[i]);
+            raw_n[2 * i] = rn[0];
+            raw_n[2 * i + 1] = K_ == 2 ? rn[1] : 0;
+        }
+    }
+
+    // Inlier index lists of one model: rule 0 with thresholds T, or (1-class
+    // LO) the graph-cut labeling (rule 2).
+    void inlier_lists(const RectModel& model, const double T[2], int rule, std::vector<uint32_t> lists[2]) {
+        for (int c = 0; c < K_; ++c) {
+            P_->mask[c].ensure(N_[c]);
+            P_->h_mask[c].ensure(N_[c]);
+            HIPC(launch_mask(P_->dp, c, model, rule, T[c], prm_.spatial_coherence_weight, P_->mask[c].p, s_));
+            HIPC(hipMemcpyAsync(P_->h_mask[c].p, P_->mask[c].p, N_[c], hipMemcpyDeviceToHost, s_));
+        }
+        HIPC(hipStreamSynchronize(s_));
+        st_.launches += K_;
+        for (int c = 0; c < 2; ++c) {
+            lists[c].clear();
+            if (c >= K_) continue;
+            const uint8_t* mk = P_->h_mask[c].p;
+            for (uint64_t i = 0; i < N_[c]; ++i)
+                if (mk[i]) lists[c].push_back((uint32_t)i);
+        }
+    }
+
+    // graphCutLocalOptimization (GCRANSAC.h:873-1062)
+    bool local_optimization(Buffer& sfb_buf) {
+        const auto t0 = Clock::now();
+        HScore max_score = best_;
+        RectModel lo_model = best_model_;
+        Buffer lo_buf;
+        const uint64_t limit[2] = {7 * m_[0], 7 * m_[1]};
+        ++lo_number_;
+        std::vector<uint32_t> inl[2], sample[2];
+        std::vector<RectModel> trial_models;
+        std::vector<HScore> trial_scores;
+        std::vector<uint32_t> trial_raw;
+        const uint64_t T = prm_.max_local_optimization_number;
+        while (++gc_number_ < 10) {
+            bool updated = false;
+            inlier_lists(lo_model, Tlo_, K_ == 2 ? 0 : 2, inl);
+            uint64_t ssz[2] = {0, 0};
+            bool all_deterministic = true;
+            for (int c = 0; c < K_; ++c) {
+                ssz[c] = std::min<uint64_t>(limit[c], inl[c].size());
+                if (ssz[c] < inl[c].size()) all_deterministic = false;
+            }
+            const uint64_t round_id = gc_number_;
+            trial_models.clear();
+            // when every class uses all its inliers each trial refits the same
+            // set: one trial decides the round (later ones cannot be strictly better)
+            const uint64_t ntrials = all_deterministic ? std::min<uint64_t>(T, 1) : T;
+            for (uint64_t trial = 0; trial < ntrials; ++trial) {
+                bool ok = true;
+                for (int c = 0; c < K_ && ok; ++c) {
+                    if (ssz[c] < inl[c].size()) {
+                        uint32_t pos[32];
+                        WordStream ws(prm_.seed, round_id, (uint32_t)trial, kStreamLO, (uint32_t)c);
+                        if (!sample_distinct<32>(ws, inl[c].size(), (int)ssz[c], pos)) { ok = false; break; }
+                        sample[c].resize(ssz[c]);
+                        for (uint64_t q = 0; q < ssz[c]; ++q) sample[c][q] = inl[c][pos[q]];
+                    } else if (m_[c] < inl[c].size()) {
+                        sample[c] = inl[c];
+                    } else {
+                        ok = false;
+                    }
+                }
+                if (!ok) break;
+                RectModel fm;
+                if (!fit_nonminimal(P_->solver, P_->hc, sample, fm)) continue;
+                trial_models.push_back(fm);
+            }
+            if (!trial_models.empty()) {
+                trial_scores.resize(trial_models.size());
+                trial_raw.resize(2 * trial_models.size());
+                score_models(trial_models.data(), (uint32_t)trial_models.size(), trial_scores.data(),
+                             trial_raw.data());
+                st_.lo_models += trial_models.size();
+                for (size_t q = 0; q < trial_models.size(); ++q) {
+                    if (max_score.sum < trial_scores[q].sum) {
+                        updated = true;
+                        max_score = trial_scores[q];
+                        lo_model = trial_models[q];
+                        lo_buf = Buffer{true, trial_models[q], {trial_raw[2 * q], trial_raw[2 * q + 1]}};
+                    }
+                }
+            }
+            if (!updated) break;
+        }
+        st_.ms_lo += ms_since(t0);
+        if (best_.sum < max_score.sum) {
+            best_ = max_score;
+            best_model_ = lo_model;
+            sfb_buf = lo_buf;
+            return true;
+        }
+        return false;
+    }
+};
+
+}  // namespace
+
+// ================================================================= C ABI ====
+namespace {
+int guard(const std::function<int()>& fn) {
+    try {
+        return fn();
+    } catch (const HipError& e) {
+        return set_err(GCR_EHIP, "HIP error %d (%s) in %s", (int)e.e, hipGetErrorString(e.e), e.what);
+    } catch (const std::bad_alloc&) {
+        return set_err(GCR_ENOMEM, "out of host memory");
+    } catch (const std::exception& e) {
+        return set_err(GCR_EINTERNAL, "%s", e.what());
+    } catch (...) {
+        return set_err(GCR_EINTERNAL, "unknown error");
+    }
+}
+
+int check_params(const gcr_params* p, int solver) {
+    if (!p) return set_err(GCR_EINVAL, "null params");
+    if (!(p->confidence > 0.0 && p->confidence < 1.0))
+        return set_err(GCR_EINVAL, "confidence must be in (0, 1)");
+    (void)solver;
+    return GCR_OK;
+}
+
+void fill_stats(gcr_stats* out, const gcr_stats& st) {
+    if (out) *out = st;
+}
+}  // namespace
+
+extern "C" {
+
+const char* gcr_last_error(void) { return g_err.c_str(); }
+int gcr_abi_version(void) { return GCR_ABI_VERSION; }
+
+int gcr_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void gcr_default_params(gcr_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->scale_residual_thresh = 2.0;          // settings.h:71 default threshold
+    p->orientation_residual_thresh = 2.0;
+    p->spatial_coherence_weight = 0.0;       // bindings.cpp:370
+    p->min_iteration_number = 10000;         // bindings.cpp:371
+    p->max_iteration_number = 10000;         // bindings.cpp:372
+    p->max_local_optimization_number = 50;   // bindings.cpp:373
+    p->confidence = 0.95;                    // settings.h:60
+    p->seed = 0;
+    p->batch_slots = 0;
+    p->flags = 0;
+}
+
+int gcr_create(int device, gcr_ctx** out) {
+    if (!out) return set_err(GCR_EINVAL, "null output pointer");
+    return guard([&]() -> int {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return set_err(GCR_ENODEV, "no HIP device available");
+        if (device < 0 || device >= n) return set_err(GCR_ENODEV, "device %d out of range (%d devices)", device, n);
+        auto c = std::unique_ptr<gcr_ctx>(new gcr_ctx());
+        c->device = device;
+        HIPC(hipSetDevice(device));
+        HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIPC(hipEventCreate(&c->ev0));
+        HIPC(hipEventCreate(&c->ev1));
+        *out = c.release();
+        return GCR_OK;
+    });
+}
+
+int gcr_synchronize(gcr_ctx* ctx) {
+    if (!ctx) return set_err(GCR_EINVAL, "null context");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(ctx->device));
+        HIPC(hipDeviceSynchronize());
+        return GCR_OK;
+    });
+}
+
+void gcr_destroy(gcr_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int gcr_problem_create(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
+                       gcr_problem** out) {
+    return guard([&]() { return make_problem(ctx, solver, f0, n0, f1, n1, out); });
+}
+
+void gcr_problem_destroy(gcr_problem* prob) {
+    if (!prob) return;
+    (void)hipSetDevice(prob->ctx->device);
+    delete prob;
+}
+
+int gcr_problem_run(gcr_problem* prob, const gcr_params* params, uint8_t* mask0_out, uint8_t* mask1_out,
+                    double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out) {
+    if (!prob) return set_err(GCR_EINVAL, "null problem");
+    if (int e = check_params(params, prob->solver)) return e;
+    if (!mask0_out || !H_out || (prob->K == 2 && !mask1_out)) return set_err(GCR_EINVAL, "null output buffer");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        Runner r(prob, *params);
+        const int total = r.run(mask0_out, mask1_out, H_out, model_out);
+        fill_stats(stats_out, r.stats());
+        return total;
+    });
+}
+
+int gcr_problem_verify_batch(gcr_problem* prob, const gcr_params* params, uint64_t slot0, uint32_t nslots,
+                             gcr_batch_result* out, gcr_stats* stats_out) {
+    if (!prob || !out) return set_err(GCR_EINVAL, "null problem or output");
+    if (int e = check_params(params, prob->solver)) return e;
+    if (nslots == 0) return set_err(GCR_EINVAL, "nslots must be > 0");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        Runner r(prob, *params);
+        r.verify_batch(slot0, nslots, out);
+        fill_stats(stats_out, r.stats());
+        return (int)out->models;
+    });
+}
+
+static int run_oneshot(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
+                       const gcr_params* params, uint8_t* m0, uint8_t* m1, double* H, gcr_rect_model* model,
+                       gcr_stats* stats) {
+    if (!ctx) return set_err(GCR_EINVAL, "null context");
+    if (int e = check_params(params, solver)) return e;
+    const auto t0 = Clock::now();
+    gcr_problem* prob = nullptr;
+    int rc = gcr_problem_create(ctx, solver, f0, n0, f1, n1, &prob);
+    if (rc != GCR_OK) return rc;
+    const double setup = ms_since(t0);
+    rc = gcr_problem_run(prob, params, m0, m1, H, model, stats);
+    gcr_problem_destroy(prob);
+    if (stats) {
+        stats->ms_setup = setup;
+        stats->ms_total += setup;
+    }
+    return rc;
+}
+
+int gcr_rect_scale_only(gcr_ctx* ctx, const double* features, size_t n, const gcr_params* params, int original,
+                        uint8_t* mask_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out) {
+    return run_oneshot(ctx, original ? GCR_SOLVER_SCALE3_ORIGINAL : GCR_SOLVER_SCALE3, features, n, nullptr, 0,
+                       params, mask_out, nullptr, H_out, model_out, stats_out);
+}
+
+int gcr_rect_sift(gcr_ctx* ctx, const double* scale_features, size_t n_scale, const double* orientation_features,
+                  size_t n_orientation, const gcr_params* params, uint8_t* scale_mask_out,
+                  uint8_t* orientation_mask_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out) {
+    return run_oneshot(ctx, GCR_SOLVER_SIFT22, scale_features, n_scale, orientation_features, n_orientation, params,
+                       scale_mask_out, orientation_mask_out, H_out, model_out, stats_out);
+}
+
+// ---------------------------------------------------------------- debug ----
+int gcr_debug_generate(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc_out,
+                       gcr_rect_model* models_out) {
+    if (!prob || !inc_out || !models_out) return set_err(GCR_EINVAL, "null argument");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        prob->inc.ensure(nslots);
+        prob->models.ensure(nslots);
+        hipStream_t s = prob->ctx->stream;
+        HIPC(launch_generate(prob->dp, seed, slot0, nslots, prob->inc.p, prob->models.p, s));
+        HIPC(hipMemcpyAsync(inc_out, prob->inc.p, nslots, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(models_out, prob->models.p, nslots * sizeof(RectModel), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        return GCR_OK;
+    });
+}
+
+int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* models, uint32_t nmodels,
+                    uint32_t* n0, uint32_t* n1, double* v0, double* v1, double* tot) {
+    if (!prob || !params || !models) return set_err(GCR_EINVAL, "null argument");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        hipStream_t s = prob->ctx->stream;
+        double T[2];
+        const double thr[2] = {params->scale_residual_thresh, params->orientation_residual_thresh};
+        for (int c = 0; c < 2; ++c) T[c] = (2.25 * thr[c]) * thr[c];
+        bool identity = true;
+        std::vector<RectModel> hm(nmodels);
+        for (uint32_t i = 0; i < nmodels; ++i) {
+            hm[i] = RectModel{models[i].x0, models[i].y0, models[i].s, models[i].h7, models[i].h8, models[i].alpha,
+                              models[i].phi};
+            identity = identity && identity_norm(hm[i]);
+        }
+        prob->lo_models.ensure(nmodels);
+        prob->lo_sb.ensure(nmodels);
+        HIPC(hipMemcpyAsync(prob->lo_models.p, hm.data(), nmodels * sizeof(RectModel), hipMemcpyHostToDevice, s));
+        HIPC(launch_score(prob->dp, T, prob->lo_models.p, nullptr, nmodels, identity, prob->lo_sb.dev(), s));
+        prob->lo_sb.d2h(nmodels, s);
+        HIPC(hipStreamSynchronize(s));
+        std::memcpy(n0, prob->lo_sb.hn0.p, nmodels * sizeof(uint32_t));
+        std::memcpy(n1, prob->lo_sb.hn1.p, nmodels * sizeof(uint32_t));
+        std::memcpy(v0, prob->lo_sb.hv0.p, nmodels * sizeof(double));
+        std::memcpy(v1, prob->lo_sb.hv1.p, nmodels * sizeof(double));
+        std::memcpy(tot, prob->lo_sb.htot.p, nmodels * sizeof(double));
+        return GCR_OK;
+    });
+}
+
+int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* model, int cls, int rule,
+                   uint8_t* mask_out) {
+    if (!prob || !params || !model || !mask_out) return set_err(GCR_EINVAL, "null argument");
+    if (cls < 0 || cls >= prob->K) return set_err(GCR_EINVAL, "class %d out of range", cls);
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        hipStream_t s = prob->ctx->stream;
+        const double thr = cls == 0 ? params->scale_residual_thresh : params->orientation_residual_thresh;
+        double T;
+        if (rule == 0) T = (2.25 * thr) * thr;
+        else { const double t = 1.5 * thr; T = t * t; }
+        const RectModel m{model->x0, model->y0, model->s, model->h7, model->h8, model->alpha, model->phi};
+        const size_t n = prob->hc[cls].n;
+        prob->mask[cls].ensure(n);
+        HIPC(launch_mask(prob->dp, cls, m, rule == 2 ? 2 : 0, T, params->spatial_coherence_weight,
+                         prob->mask[cls].p, s));
+        HIPC(hipMemcpyAsync(mask_out, prob->mask[cls].p, n, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        return GCR_OK;
+    });
+}
+
+double gcr_host_log(double x) { return dm::dm_log(x); }
+double gcr_host_pow_m3(double t) { return dm::dm_pow_m3(t); }
+double gcr_host_atan2(double y, double x) { return dm::dm_atan2(y, x); }
+
+int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls, uint64_t n,
+                    uint32_t m, uint32_t* out) {
+    if (!out || m > 32) return set_err(GCR_EINVAL, "bad sample request");
+    WordStream ws(seed, index, sub, stream, cls);
+    return sample_distinct<32>(ws, n, (int)m, out) ? GCR_OK : set_err(GCR_EINTERNAL, "sample budget exhausted");
+}
+
+int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out) {
+    if (!ctx || !a || !out || ((op == 2 || op == 3) && b == nullptr)) return set_err(GCR_EINVAL, "null argument");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(ctx->device));
+        double *da = nullptr, *db = nullptr, *dout = nullptr;
+        HIPC(hipMalloc(reinterpret_cast<void**>(&da), n * sizeof(double) + 8));
+        HIPC(hipMalloc(reinterpret_cast<void**>(&db), n * sizeof(double) + 8));
+        HIPC(hipMalloc(reinterpret_cast<void**>(&dout), n * sizeof(double) + 8));
+        HIPC(hipMemcpy(da, a, n * sizeof(double), hipMemcpyHostToDevice));
+        if (b) HIPC(hipMemcpy(db, b, n * sizeof(double), hipMemcpyHostToDevice));
+        HIPC(launch_math(op, da, db, n, dout, ctx->stream));
+        HIPC(hipStreamSynchronize(ctx->stream));
+        HIPC(hipMemcpy(out, dout, n * sizeof(double), hipMemcpyDeviceToHost));
+        (void)hipFree(da);
+        (void)hipFree(db);
+        (void)hipFree(dout);
+        return GCR_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,39 @@
+// host_fit.h -- host-side model fitting for local optimisation and the final
+// refit (the parts north_star keeps in host C++).  Per-feature constants come
+// from the problem's precomputed SoA arrays; hypothesis-dependent angles use
+// detmath so the results match what the kernels would compute.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "rect.h"
+
+namespace gcr {
+
+// Per-class host copy of the features plus the precomputed per-feature
+// constants (same values the GPU holds):
+//   scale class:       c0 = pow(s, kScalePower)      (glibc, +1/3 or -1/3)
+//   orientation class: c0 = cos(theta), c1 = sin(theta)
+struct HostClass {
+    std::vector<double> x, y, a, c0, c1;
+    size_t n = 0;
+};
+
+// Eigen ColPivHouseholderQR<MatrixX3d>::compute(A).solve(b) restated for an
+// m x 3 column-major matrix (A and b are overwritten).
+void colpiv_qr_solve3(std::vector<double>& A, size_t m, std::vector<double>& b, double x[3]);
+
+// RectifyingHomographyEstimator::estimateModelNonminimal for the three solvers
+// (rectifying_homography_estimator.h:164-227): normalisation check, then the
+// minimal solver when the subset is exactly minimal, else weighted LS (+ mode).
+bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out);
+
+// findWeightedMode (two_sift.hpp:354-394), libstdc++ unordered_map order.
+double weighted_mode(const std::vector<double>& angles, const std::vector<double>& weights, double bin_width);
+
+// RectifyingHomography::getHomography (model.h:211-226), row-major, / H22.
+void homography_of(const RectModel& m, double H[9]);
+
+}  // namespace gcr

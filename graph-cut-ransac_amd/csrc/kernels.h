@@ -1,0 +1,61 @@
+// kernels.h -- launch interface of the gfx950 kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "rect.h"
+
+namespace gcr {
+
+// One feature class resident in HBM, structure-of-arrays fp64.
+//   scale class:       a = s,      c0 = pow(s, +-1/3)
+//   orientation class: a = theta,  c0 = cos(theta), c1 = sin(theta)
+struct DevClass {
+    const double* x;
+    const double* y;
+    const double* a;
+    const double* c0;
+    const double* c1;
+    uint32_t n;
+};
+
+struct DevProblem {
+    int solver;     // GCR_SOLVER_*
+    DevClass cls[2];
+};
+
+// Raw MSAC accumulators per hypothesis (host finishes the score exactly as
+// MSACScoringFunction::getScore does, MSAC_scoring_function.hpp:108-127).
+struct ScoreOut {
+    uint32_t* n0;
+    uint32_t* n1;
+    double* v0;
+    double* v1;
+    double* tot;
+};
+
+// Draw + validate + solve `nslots` outer-iteration slots [slot0, slot0+nslots).
+// inc[i] = attempt index + 1 of the first success (1..101), 102 when all 101
+// attempts failed (GCRANSAC.h:296-339).
+hipError_t launch_generate(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
+                           RectModel* models, hipStream_t stream);
+
+// Exact sequential MSAC accumulation of `nh` models over every feature;
+// T[c] = (2.25 * thr_c) * thr_c.
+// models with inc[i] > 101 (no model) produce zeros.  inc may be null.
+// identity: every model has x0 = y0 = 0, s = 1 (true for all models of this
+// fork: normalizePoints resets the transform), skips the normalisation ops.
+hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc,
+                        uint32_t nh, bool identity, const ScoreOut& out, hipStream_t stream);
+
+// Per-feature inlier mask of one model for class `cls`.
+// rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)
+// rule 2: 1-class graph-cut labeling with weight lambda, T = (1.5 thr)^2
+hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int rule, double T, double lambda,
+                       uint8_t* mask, hipStream_t stream);
+
+// element-wise evaluation of the device math primitives (parity tests)
+hipError_t launch_math(int op, const double* a, const double* b, size_t n, double* out, hipStream_t stream);
+
+}  // namespace gcr

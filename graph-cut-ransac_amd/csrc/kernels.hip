@@ -1,0 +1,226 @@
+// kernels.hip -- gfx950 kernels of the hypothesize-and-verify hot path.
+//
+//   k_generate   one lane per outer-iteration slot: up to 101 attempts of
+//                Philox sample -> sample validity -> 3x4 Gauss minimal solve,
+//                all in fp64 registers (GCRANSAC.h:296-339, solvers' minimal fits)
+//   k_score      one lane per hypothesis, features streamed in index order
+//                through the scalar unit (uniform addresses), exact sequential
+//                MSAC accumulation (MSAC_scoring_function.hpp:53-130): the
+//                running sums are bit-identical to the reference's loop order
+//   k_mask       one lane per feature, inlier mask of one model (LO relabel,
+//                graph-cut labeling, final inlier sets)
+//
+// Compiled with -ffp-contract=off: every fp64 expression rounds exactly like
+// the host restatement.
+#include "kernels.h"
+#include "philox.h"
+
+namespace gcr {
+
+namespace {
+
+constexpr int kGenBlock = 256;
+constexpr int kScoreBlock = 256;
+constexpr int kMaskBlock = 256;
+
+// ------------------------------------------------------------- generate ----
+template <int KIND>
+__global__ __launch_bounds__(kGenBlock) void k_generate(DevProblem p, uint64_t seed, uint64_t slot0,
+                                                        uint32_t nslots, uint8_t* __restrict__ inc,
+                                                        RectModel* __restrict__ models) {
+    const uint32_t s = blockIdx.x * kGenBlock + threadIdx.x;
+    if (s >= nslots) return;
+    const uint64_t slot = slot0 + s;
+    RectModel m = default_model();
+    for (uint32_t a = 0; a < 101; ++a) {
+        if constexpr (KIND != 2) {
+            const DevClass& c = p.cls[0];
+            uint32_t idx[3];
+            WordStream ws(seed, slot, a, kStreamMain, 0);
+            if (!sample_distinct<3>(ws, c.n, 3, idx)) continue;
+            double x[3], y[3], pw[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                x[j] = c.x[idx[j]];
+                y[j] = c.y[idx[j]];
+                pw[j] = c.c0[idx[j]];
+            }
+            // areAllPointsCollinear on the single consecutive triplet
+            if (are_collinear(x[0], y[0], x[1], y[1], x[2], y[2], 1.0)) continue;
+            const bool ok = (KIND == 1) ? solve_scale3<true>(x, y, pw, m) : solve_scale3<false>(x, y, pw, m);
+            if (ok) {
+                models[s] = m;
+                inc[s] = (uint8_t)(a + 1);
+                return;
+            }
+        } else {
+            const DevClass& sc = p.cls[0];
+            const DevClass& oc = p.cls[1];
+            uint32_t si[2], oi[2];
+            WordStream ws0(seed, slot, a, kStreamMain, 0);
+            if (!sample_distinct<2>(ws0, sc.n, 2, si)) continue;
+            WordStream ws1(seed, slot, a, kStreamMain, 1);
+            if (!sample_distinct<2>(ws1, oc.n, 2, oi)) continue;
+            double sx[2], sy[2], sp[2], ox[2], oy[2], oco[2], osi[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                sx[j] = sc.x[si[j]];
+                sy[j] = sc.y[si[j]];
+                sp[j] = sc.c0[si[j]];
+                ox[j] = oc.x[oi[j]];
+                oy[j] = oc.y[oi[j]];
+                oco[j] = oc.c0[oi[j]];
+                osi[j] = oc.c1[oi[j]];
+            }
+            if (!valid_sample_sift22(sx, sy, ox, oy, oco, osi)) continue;
+            if (solve_sift22(sx, sy, sp, ox, oy, oco, osi, m)) {
+                models[s] = m;
+                inc[s] = (uint8_t)(a + 1);
+                return;
+            }
+        }
+    }
+    models[s] = default_model();
+    inc[s] = 102;
+}
+
+// ---------------------------------------------------------------- score ----
+template <int KIND, bool kIdentity>
+__global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, double T1,
+                                                       const RectModel* __restrict__ models,
+                                                       const uint8_t* __restrict__ inc, uint32_t nh, ScoreOut out) {
+    const uint32_t h = blockIdx.x * kScoreBlock + threadIdx.x;
+    if (h >= nh) return;
+    if (inc != nullptr && inc[h] > 101) {
+        out.n0[h] = 0; out.n1[h] = 0; out.v0[h] = 0.0; out.v1[h] = 0.0; out.tot[h] = 0.0;
+        return;
+    }
+    const RectModel m = models[h];
+    const DevClass c0 = p.cls[0];
+    const double ac = alpha_cube(m);
+    uint32_t cnt0 = 0;
+    double acc0 = 0.0;
+    for (uint32_t i = 0; i < c0.n; ++i) {
+        const double r2 = scale_sq_residual<KIND == 1, kIdentity>(c0.x[i], c0.y[i], c0.a[i], m, ac);
+        if (r2 <= T0) {
+            cnt0 += 1;
+            acc0 += -r2;
+        }
+    }
+    uint32_t cnt1 = 0;
+    double acc1 = 0.0, tot = acc0;
+    if constexpr (KIND == 2) {
+        const DevClass c1 = p.cls[1];
+        const OrientConst oc = orient_const(m);
+        for (uint32_t i = 0; i < c1.n; ++i) {
+            const double r2 = orient_sq_residual<kIdentity>(c1.x[i], c1.y[i], c1.c0[i], c1.c1[i], m, oc);
+            if (r2 <= T1) {
+                cnt1 += 1;
+                acc1 += -r2;
+                tot += -r2;
+            }
+        }
+    }
+    out.n0[h] = cnt0;
+    out.n1[h] = cnt1;
+    out.v0[h] = acc0;
+    out.v1[h] = acc1;
+    out.tot[h] = tot;
+}
+
+// ----------------------------------------------------------------- mask ----
+template <int KIND>
+__global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, RectModel m, int rule, double T,
+                                                     double lambda, uint8_t* __restrict__ mask) {
+    const uint32_t i = blockIdx.x * kMaskBlock + threadIdx.x;
+    if (i >= c.n) return;
+    double r2;
+    if (cls == 0) r2 = scale_sq_residual<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
+    else r2 = orient_sq_residual<false>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
+    bool inl;
+    if (rule == 2) {
+        // labeling(): BK max-flow with no pairwise edges (empty grid graph,
+        // gcransac_python.cpp:63-68) -> SINK iff terminal capacity < 0.
+        const double oml = 1.0 - lambda;
+        double q = r2 / T;
+        q = (q < 0.0) ? 0.0 : ((1.0 < q) ? 1.0 : q);      // std::clamp
+        const double energy = 1.0 - q;
+        const double tr = (r2 <= T) ? (0.0 - oml * energy) : (oml * (1.0 - energy) - 0.0);
+        inl = tr < 0.0;
+    } else {
+        inl = r2 <= T;
+    }
+    mask[i] = inl ? 1 : 0;
+}
+
+// ----------------------------------------------------------------- math ----
+__global__ void k_math(int op, const double* __restrict__ a, const double* __restrict__ b, size_t n,
+                       double* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double r;
+    switch (op) {
+        case 0: r = dm::dm_log(a[i]); break;
+        case 1: r = dm::dm_pow_m3(a[i]); break;
+        case 2: r = dm::dm_atan2(a[i], b[i]); break;
+        case 3: r = a[i] / b[i]; break;
+        default: r = sqrt(a[i]); break;
+    }
+    out[i] = r;
+}
+
+inline unsigned blocks_for(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+hipError_t launch_generate(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
+                           RectModel* models, hipStream_t stream) {
+    if (nslots == 0) return hipSuccess;
+    const dim3 grid(blocks_for(nslots, kGenBlock)), block(kGenBlock);
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL(k_generate<0>, grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
+        case 1: hipLaunchKernelGGL(k_generate<1>, grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
+        default: hipLaunchKernelGGL(k_generate<2>, grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
+    }
+    return hipGetLastError();
+}
+
+template <bool kIdentity>
+void launch_score_t(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc, uint32_t nh,
+                    const ScoreOut& out, hipStream_t stream) {
+    const dim3 grid(blocks_for(nh, kScoreBlock)), block(kScoreBlock);
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL((k_score<0, kIdentity>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
+        case 1: hipLaunchKernelGGL((k_score<1, kIdentity>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
+        default: hipLaunchKernelGGL((k_score<2, kIdentity>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
+    }
+}
+
+hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc,
+                        uint32_t nh, bool identity, const ScoreOut& out, hipStream_t stream) {
+    if (nh == 0) return hipSuccess;
+    if (identity) launch_score_t<true>(p, T, models, inc, nh, out, stream);
+    else launch_score_t<false>(p, T, models, inc, nh, out, stream);
+    return hipGetLastError();
+}
+
+hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int rule, double T, double lambda,
+                       uint8_t* mask, hipStream_t stream) {
+    const DevClass& c = p.cls[cls];
+    if (c.n == 0) return hipSuccess;
+    const dim3 grid(blocks_for(c.n, kMaskBlock)), block(kMaskBlock);
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL(k_mask<0>, grid, block, 0, stream, c, cls, model, rule, T, lambda, mask); break;
+        case 1: hipLaunchKernelGGL(k_mask<1>, grid, block, 0, stream, c, cls, model, rule, T, lambda, mask); break;
+        default: hipLaunchKernelGGL(k_mask<2>, grid, block, 0, stream, c, cls, model, rule, T, lambda, mask); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_math(int op, const double* a, const double* b, size_t n, double* out, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_math, dim3(blocks_for(n, 256)), dim3(256), 0, stream, op, a, b, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace gcr

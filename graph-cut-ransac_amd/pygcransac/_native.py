@@ -1,0 +1,167 @@
+"""ctypes view of the engine's C ABI (include/gcr.h).
+
+The shared library ``libgcr.so`` is built in-tree next to this file (see
+``graph-cut-ransac_amd/csrc/Makefile``).  Importing this module fails loudly if
+it is missing: there is no CPU fallback for the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgcr.so")
+
+GCR_OK = 0
+GCR_EINVAL = -22
+GCR_ENODEV = -19
+SOLVER_SCALE3, SOLVER_SCALE3_ORIGINAL, SOLVER_SIFT22 = 0, 1, 2
+FLAG_NO_LO = 1
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("scale_residual_thresh", C.c_double),
+        ("orientation_residual_thresh", C.c_double),
+        ("spatial_coherence_weight", C.c_double),
+        ("min_iteration_number", C.c_uint64),
+        ("max_iteration_number", C.c_uint64),
+        ("max_local_optimization_number", C.c_uint64),
+        ("confidence", C.c_double),
+        ("seed", C.c_uint64),
+        ("batch_slots", C.c_uint32),
+        ("flags", C.c_uint32),
+    ]
+
+
+class RectModel(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("x0", "y0", "s", "h7", "h8", "alpha", "phi")]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("iteration_number", C.c_uint64),
+        ("local_optimization_number", C.c_uint64),
+        ("graph_cut_number", C.c_uint64),
+        ("slots", C.c_uint64),
+        ("hypotheses", C.c_uint64),
+        ("hypotheses_computed", C.c_uint64),
+        ("lo_models", C.c_uint64),
+        ("launches", C.c_uint64),
+        ("score", C.c_double),
+        ("ms_setup", C.c_double),
+        ("ms_generate", C.c_double),
+        ("ms_score", C.c_double),
+        ("ms_replay", C.c_double),
+        ("ms_lo", C.c_double),
+        ("ms_refit", C.c_double),
+        ("ms_total", C.c_double),
+        ("ms_score_kernel", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class BatchResult(C.Structure):
+    _fields_ = [
+        ("models", C.c_uint64),
+        ("iterations", C.c_uint64),
+        ("best_slot", C.c_int64),
+        ("best_score", C.c_double),
+        ("best_inliers", C.c_uint64 * 2),
+        ("best_model", RectModel),
+    ]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"pygcransac: HIP engine library not found at {LIB_PATH}; build it with "
+            "`make -C graph-cut-ransac_amd/csrc` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    dp, u8p, u32p = C.POINTER(C.c_double), C.POINTER(C.c_uint8), C.POINTER(C.c_uint32)
+    vp = C.c_void_p
+    L.gcr_last_error.restype = C.c_char_p
+    L.gcr_abi_version.restype = C.c_int
+    L.gcr_device_count.restype = C.c_int
+    L.gcr_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.gcr_synchronize.argtypes = [vp]
+    L.gcr_destroy.argtypes = [vp]
+    L.gcr_destroy.restype = None
+    L.gcr_default_params.argtypes = [C.POINTER(Params)]
+    L.gcr_default_params.restype = None
+    L.gcr_rect_scale_only.argtypes = [vp, dp, C.c_size_t, C.POINTER(Params), C.c_int, u8p, dp,
+                                      C.POINTER(RectModel), C.POINTER(Stats)]
+    L.gcr_rect_sift.argtypes = [vp, dp, C.c_size_t, dp, C.c_size_t, C.POINTER(Params), u8p, u8p, dp,
+                                C.POINTER(RectModel), C.POINTER(Stats)]
+    L.gcr_problem_create.argtypes = [vp, C.c_int, dp, C.c_size_t, dp, C.c_size_t, C.POINTER(vp)]
+    L.gcr_problem_destroy.argtypes = [vp]
+    L.gcr_problem_destroy.restype = None
+    L.gcr_problem_run.argtypes = [vp, C.POINTER(Params), u8p, u8p, dp, C.POINTER(RectModel), C.POINTER(Stats)]
+    L.gcr_problem_verify_batch.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.POINTER(BatchResult),
+                                           C.POINTER(Stats)]
+    L.gcr_debug_generate.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, u8p, C.POINTER(RectModel)]
+    L.gcr_debug_score.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_uint32, u32p, u32p, dp, dp, dp]
+    L.gcr_debug_mask.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_int, C.c_int, u8p]
+    L.gcr_host_log.argtypes = [C.c_double]
+    L.gcr_host_log.restype = C.c_double
+    L.gcr_host_pow_m3.argtypes = [C.c_double]
+    L.gcr_host_pow_m3.restype = C.c_double
+    L.gcr_host_atan2.argtypes = [C.c_double, C.c_double]
+    L.gcr_host_atan2.restype = C.c_double
+    L.gcr_host_sample.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                  C.c_uint32, u32p]
+    L.gcr_debug_math.argtypes = [vp, C.c_int, dp, dp, C.c_size_t, dp]
+    return L
+
+
+lib = _load()
+
+_ctx_lock = threading.Lock()
+_contexts: dict[int, int] = {}
+
+
+def default_device() -> int:
+    for var in ("GCR_DEVICE", "LOCAL_RANK"):
+        if var in os.environ:
+            try:
+                return int(os.environ[var])
+            except ValueError:
+                pass
+    return 0
+
+
+def context(device: int | None = None) -> int:
+    """Per-device engine context (created lazily, kept for the process)."""
+    dev = default_device() if device is None else int(device)
+    with _ctx_lock:
+        h = _contexts.get(dev)
+        if h is None:
+            out = C.c_void_p()
+            rc = lib.gcr_create(dev, C.byref(out))
+            check(rc)
+            h = out.value
+            _contexts[dev] = h
+        return h
+
+
+def last_error() -> str:
+    msg = lib.gcr_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc: int) -> int:
+    if rc >= 0:
+        return rc
+    msg = last_error() or f"engine error {rc}"
+    if rc == GCR_EINVAL:
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def default_params() -> Params:
+    p = Params()
+    lib.gcr_default_params(C.byref(p))
+    return p

@@ -1,0 +1,350 @@
+"""pygcransac -- drop-in Python API of yuvalnis/graph-cut-ransac, MI355X engine.
+
+Surface mirrors ``src/pygcransac/src/bindings.cpp:315-396`` of the reference:
+three functions with the same positional/keyword arguments, defaults, input
+validation messages and return tuples, and the five model classes with the
+same names, inheritance, attributes and methods.  Extensions are keyword-only
+(``seed``, ``confidence``, ``device``, ``batch_slots``, ``return_stats``).
+
+Compute goes through the C ABI in ``include/gcr.h`` (libgcr.so: HIP kernels for
+gfx950 plus the host engine).  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import numbers
+
+import numpy as np
+
+from . import _native as N
+
+__all__ = [
+    "NormalizingTransform",
+    "RectifyingHomography",
+    "ScaleBasedRectifyingHomography",
+    "OrientationBasedRectifyingHomography",
+    "SIFTRectifyingHomography",
+    "findRectifyingHomographyScaleOnly",
+    "findRectifyingHomographyScaleOnlyOriginal",
+    "findRectifyingHomographySIFT",
+]
+
+_TWO_PI = 2.0 * math.pi
+
+
+# ----------------------------------------------------------- model classes --
+class _F64:
+    """double data member with pybind11 def_readwrite semantics."""
+
+    def __set_name__(self, owner, name):
+        self.name = "_" + name
+
+    def __get__(self, obj, objtype=None):
+        if obj is None:
+            return self
+        return obj.__dict__[self.name]
+
+    def __set__(self, obj, value):
+        if isinstance(value, (str, bytes)) or not isinstance(value, (numbers.Real, np.floating, np.integer)):
+            raise TypeError(f"incompatible type for double attribute: {type(value).__name__}")
+        obj.__dict__[self.name] = float(value)
+
+
+def _cpow(x, y):
+    """C pow() semantics (inf/nan instead of Python exceptions)."""
+    with np.errstate(all="ignore"):
+        return float(np.power(np.float64(x), np.float64(y)))
+
+
+def _clip_angle(a):
+    # math_utils.hpp:78-88 (std::fmod, then + 2pi if negative)
+    if math.isinf(a) or math.isnan(a):
+        return math.nan
+    a = math.fmod(a, _TWO_PI)
+    if a < 0.0:
+        a += _TWO_PI
+    return a
+
+
+def _atan2(y, x):
+    return math.atan2(y, x)
+
+
+class NormalizingTransform:
+    """model.h:42-120"""
+    x0 = _F64()
+    y0 = _F64()
+    s = _F64()
+
+    def __init__(self):
+        self.x0 = 0.0
+        self.y0 = 0.0
+        self.s = 1.0
+
+    def _fields(self):
+        return {k: getattr(self, k) for k in ("x0", "y0", "s")}
+
+    def __repr__(self):
+        inner = ", ".join(f"{k}={v!r}" for k, v in self._fields().items())
+        return f"{type(self).__name__}({inner})"
+
+
+class RectifyingHomography(NormalizingTransform):
+    """model.h:122-227 (+ the pybind11 lambdas at bindings.cpp:335-353)."""
+    h7 = _F64()
+    h8 = _F64()
+
+    def __init__(self):
+        super().__init__()
+        self.h7 = 0.0
+        self.h8 = 0.0
+
+    def _fields(self):
+        d = super()._fields()
+        d.update(h7=self.h7, h8=self.h8)
+        return d
+
+    def rectifiedScale(self, dx, dy, ds):
+        return float(ds) * _cpow(-self.h7 * float(dx) - self.h8 * float(dy) + 1.0, -3.0)
+
+    def unrectifiedScale(self, udx, udy, uds):
+        return float(uds) * _cpow(self.h7 * float(udx) + self.h8 * float(udy) + 1.0, -3.0)
+
+    def rectifiedAngle(self, x, y, angle):
+        x, y, angle = float(x), float(y), float(angle)
+        ct, st = math.cos(angle), math.sin(angle)
+        numer = (-x * st + y * ct) * self.h7 + st
+        denom = (x * st - y * ct) * self.h8 + ct
+        return _clip_angle(_atan2(numer, denom))
+
+    def unrectifiedAngle(self, x, y, angle):
+        x, y, angle = float(x), float(y), float(angle)
+        ct, st = math.cos(angle), math.sin(angle)
+        numer = (x * st - y * ct) * self.h7 + st
+        denom = (-x * st + y * ct) * self.h8 + ct
+        return _clip_angle(_atan2(numer, denom))
+
+    def rectifiedPoint(self, x, y):
+        x, y = float(x), float(y)
+        w = -self.h7 * x - self.h8 * y + 1.0
+        with np.errstate(all="ignore"):
+            return (float(np.float64(x) / w), float(np.float64(y) / w))
+
+    def unrectifiedPoint(self, x, y):
+        x, y = float(x), float(y)
+        w = self.h7 * x + self.h8 * y + 1.0
+        with np.errstate(all="ignore"):
+            return (float(np.float64(x) / w), float(np.float64(y) / w))
+
+    def getHomography(self):
+        # N.inverse() * [[1,0,0],[0,1,0],[h7,h8,1]] * N / H22 with Eigen's
+        # 3x3 cofactor inverse, evaluated in IEEE double like the C++ code.
+        s, x0, y0 = self.s, self.x0, self.y0
+        Nm = [s, 0.0, -s * x0, 0.0, s, -s * y0, 0.0, 0.0, 1.0]
+        Hn = [1.0, 0.0, 0.0, 0.0, 1.0, 0.0, self.h7, self.h8, 1.0]
+
+        def cof(i, j):
+            i1, i2, j1, j2 = (i + 1) % 3, (i + 2) % 3, (j + 1) % 3, (j + 2) % 3
+            return Nm[i1 * 3 + j1] * Nm[i2 * 3 + j2] - Nm[i1 * 3 + j2] * Nm[i2 * 3 + j1]
+
+        with np.errstate(all="ignore"):
+            det = (cof(0, 0) * Nm[0] + cof(1, 0) * Nm[3]) + cof(2, 0) * Nm[6]
+            invdet = float(np.float64(1.0) / det)
+            Ni = [cof(c, r) * invdet for r in range(3) for c in range(3)]
+            T = [(Ni[i * 3] * Hn[j] + Ni[i * 3 + 1] * Hn[3 + j]) + Ni[i * 3 + 2] * Hn[6 + j]
+                 for i in range(3) for j in range(3)]
+            R = [(T[i * 3] * Nm[j] + T[i * 3 + 1] * Nm[3 + j]) + T[i * 3 + 2] * Nm[6 + j]
+                 for i in range(3) for j in range(3)]
+            d = np.float64(R[8])
+            return np.array([np.float64(v) / d for v in R], dtype=np.float64).reshape(3, 3)
+
+
+class ScaleBasedRectifyingHomography(RectifyingHomography):
+    """model.h:229-234"""
+    alpha = _F64()
+
+    def __init__(self):
+        super().__init__()
+        self.alpha = 1.0
+
+    def _fields(self):
+        d = super()._fields()
+        d.update(alpha=self.alpha)
+        return d
+
+
+class OrientationBasedRectifyingHomography(RectifyingHomography):
+    """model.h:236-241"""
+    phi = _F64()
+
+    def __init__(self):
+        super().__init__()
+        self.phi = 0.0
+
+    def _fields(self):
+        d = super()._fields()
+        d.update(phi=self.phi)
+        return d
+
+
+class SIFTRectifyingHomography(ScaleBasedRectifyingHomography, OrientationBasedRectifyingHomography):
+    """model.h:243-246"""
+
+
+# --------------------------------------------------------------- helpers ---
+def _as_features(arr):
+    """py::array_t<double> conversion (forcecast) + flat C-contiguous buffer."""
+    try:
+        a = np.asarray(arr, dtype=np.float64)
+    except (TypeError, ValueError) as exc:
+        raise TypeError(f"incompatible function arguments: cannot convert to float64 array ({exc})") from None
+    return a
+
+
+def _as_size_t(v, name):
+    if isinstance(v, (bool, np.bool_)):
+        v = int(v)
+    if not isinstance(v, (numbers.Integral, np.integer)) or v < 0:
+        raise TypeError(f"incompatible function arguments: {name} must be a non-negative integer")
+    if int(v) > 0xFFFFFFFFFFFFFFFF:
+        raise TypeError(f"incompatible function arguments: {name} does not fit size_t")
+    return int(v)
+
+
+def _as_double(v, name):
+    if isinstance(v, (str, bytes)) or not isinstance(v, (numbers.Real, np.floating, np.integer)):
+        raise TypeError(f"incompatible function arguments: {name} must be a float")
+    return float(v)
+
+
+def _params(thr0, thr1, lam, min_it, max_it, lo, seed, confidence, batch_slots):
+    p = N.default_params()
+    p.scale_residual_thresh = _as_double(thr0, "scale_residual_thresh")
+    p.orientation_residual_thresh = _as_double(thr1, "orientation_residual_thresh")
+    p.spatial_coherence_weight = _as_double(lam, "spatial_coherence_weight")
+    p.min_iteration_number = _as_size_t(min_it, "min_iteration_number")
+    p.max_iteration_number = _as_size_t(max_it, "max_iteration_number")
+    p.max_local_optimization_number = _as_size_t(lo, "max_local_optimization_number")
+    p.seed = _as_size_t(seed, "seed")
+    p.confidence = _as_double(confidence, "confidence")
+    p.batch_slots = _as_size_t(batch_slots, "batch_slots") & 0xFFFFFFFF
+    return p
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _u8(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def _fill(model, m: N.RectModel, sift: bool):
+    model.x0, model.y0, model.s = m.x0, m.y0, m.s
+    model.h7, model.h8, model.alpha = m.h7, m.h8, m.alpha
+    if sift:
+        model.phi = m.phi
+    return model
+
+
+def _validate_scale_only(features):
+    f = _as_features(features)
+    if f.ndim != 2:
+        raise ValueError("Number of dimensions must be 2.")
+    n, cols = f.shape
+    if n < 3 or cols != 3:
+        raise ValueError(f"Features should be an array with 3 columns and at least 3 rows. "
+                         f"It has {cols} columns and {n} rows.")
+    return np.ascontiguousarray(f)
+
+
+def _scale_only(original, features, scale_residual_thresh, spatial_coherence_weight, min_iteration_number,
+                max_iteration_number, max_local_optimization_number, seed, confidence, device, batch_slots,
+                return_stats):
+    f = _validate_scale_only(features)
+    p = _params(scale_residual_thresh, 2.0, spatial_coherence_weight, min_iteration_number, max_iteration_number,
+                max_local_optimization_number, seed, confidence, batch_slots)
+    n = f.shape[0]
+    mask = np.zeros(n, dtype=np.uint8)
+    H = np.zeros(9, dtype=np.float64)
+    m = N.RectModel()
+    st = N.Stats()
+    ctx = N.context(device)
+    rc = N.lib.gcr_rect_scale_only(ctx, _dp(f), n, C.byref(p), 1 if original else 0, _u8(mask), _dp(H),
+                                   C.byref(m), C.byref(st))
+    num_inliers = N.check(rc)
+    inliers = mask.astype(bool)
+    extra = (st.as_dict(),) if return_stats else ()
+    if num_inliers == 0:
+        return (None, inliers) + extra
+    model = _fill(ScaleBasedRectifyingHomography(), m, sift=False)
+    return (H.reshape(3, 3), inliers, model) + extra
+
+
+# -------------------------------------------------------------- entry points
+def findRectifyingHomographyScaleOnly(features, scale_residual_thresh, spatial_coherence_weight=0.0,
+                                      min_iteration_number=10000, max_iteration_number=10000,
+                                      max_local_optimization_number=50, *, seed=0, confidence=0.95, device=None,
+                                      batch_slots=0, return_stats=False):
+    """3-SIFT scale-only rectification (bindings.cpp:19-98, 366-374).
+
+    Returns ``(H, inliers, ScaleBasedRectifyingHomography)`` or ``(None, inliers)``
+    when no model is found.
+    """
+    return _scale_only(False, features, scale_residual_thresh, spatial_coherence_weight, min_iteration_number,
+                       max_iteration_number, max_local_optimization_number, seed, confidence, device, batch_slots,
+                       return_stats)
+
+
+def findRectifyingHomographyScaleOnlyOriginal(features, scale_residual_thresh, spatial_coherence_weight=0.0,
+                                              min_iteration_number=10000, max_iteration_number=10000,
+                                              max_local_optimization_number=50, *, seed=0, confidence=0.95,
+                                              device=None, batch_slots=0, return_stats=False):
+    """Original-parametrisation 3-SIFT solver (bindings.cpp:100-179, 376-384)."""
+    return _scale_only(True, features, scale_residual_thresh, spatial_coherence_weight, min_iteration_number,
+                       max_iteration_number, max_local_optimization_number, seed, confidence, device, batch_slots,
+                       return_stats)
+
+
+def findRectifyingHomographySIFT(scale_features, orientation_features, scale_residual_thresh,
+                                 orientation_residual_thresh, spatial_coherence_weight=0.0,
+                                 min_iteration_number=10000, max_iteration_number=10000,
+                                 max_local_optimization_number=50, *, seed=0, confidence=0.95, device=None,
+                                 batch_slots=0, return_stats=False):
+    """Hybrid 2+2 SIFT rectification (bindings.cpp:181-311, 386-396).
+
+    Returns ``(H, scale_inliers, orientation_inliers, SIFTRectifyingHomography)``
+    or ``(None, scale_inliers, orientation_inliers, None)``.
+    """
+    fs = _as_features(scale_features)
+    fo = _as_features(orientation_features)
+    if fs.ndim != 2 or fo.ndim != 2:
+        raise ValueError("Number of dimensions must be 2.")
+    ns, cs = fs.shape
+    no, co = fo.shape
+    if ns < 2 or cs != 3:
+        raise ValueError(f"Scale features should be an array with 3 columns and at least 2 rows. "
+                         f"It has {cs} columns and {ns} rows.")
+    if no < 2 or co != 3:
+        raise ValueError(f"Orientation features should be an array with 3 columns and at least 2 rows. "
+                         f"It has {co} columns and {no} rows.")
+    fs = np.ascontiguousarray(fs)
+    fo = np.ascontiguousarray(fo)
+    p = _params(scale_residual_thresh, orientation_residual_thresh, spatial_coherence_weight, min_iteration_number,
+                max_iteration_number, max_local_optimization_number, seed, confidence, batch_slots)
+    ms = np.zeros(ns, dtype=np.uint8)
+    mo = np.zeros(no, dtype=np.uint8)
+    H = np.zeros(9, dtype=np.float64)
+    m = N.RectModel()
+    st = N.Stats()
+    ctx = N.context(device)
+    rc = N.lib.gcr_rect_sift(ctx, _dp(fs), ns, _dp(fo), no, C.byref(p), _u8(ms), _u8(mo), _dp(H), C.byref(m),
+                             C.byref(st))
+    num_inliers = N.check(rc)
+    s_in, o_in = ms.astype(bool), mo.astype(bool)
+    extra = (st.as_dict(),) if return_stats else ()
+    if num_inliers == 0:
+        return (None, s_in, o_in, None) + extra
+    model = _fill(SIFTRectifyingHomography(), m, sift=True)
+    return (H.reshape(3, 3), s_in, o_in, model) + extra

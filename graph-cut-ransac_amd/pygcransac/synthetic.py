@@ -1,0 +1,96 @@
+"""Synthetic rectification problems (inputs M1 / M2).
+
+The reference's example notebook and its SIFT features are not in the snapshot
+(``.MISSING_LARGE_BLOBS:1``) and cv2 is absent, so benchmarks and tests use
+seeded synthetic features with a known rectifying homography instead.
+
+Feature conventions follow ``examples/utils.py:5-49`` of the reference:
+scale features are rows ``(x, y, size)``, orientation features rows
+``(x, y, angle_rad)``.  Ground truth uses the reference's own model maths
+(``model.h:122-204``): an inlier scale feature satisfies
+``alpha^3 * s * (1 - h7 x - h8 y)^-3 = exp(eps)``; an inlier orientation
+feature rectifies (``rectifiedAngle``) to ``phi`` or ``phi + pi/2`` plus noise.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+WIDTH, HEIGHT = 1368.0, 1824.0          # examples/img/tiled_floor_001.jpg
+DEFAULT_SEED = 20251121
+
+
+@dataclass
+class GroundTruth:
+    h7: float = 2.0e-4
+    h8: float = -1.5e-4
+    alpha: float = 0.5
+    phi: float = 0.35
+
+
+def _unrectified_angle(h7, h8, x, y, angle):
+    # model.h:167-174 (glibc cos/sin/atan2 via Python's math module)
+    ct, st = math.cos(angle), math.sin(angle)
+    numer = (x * st - y * ct) * h7 + st
+    denom = (-x * st + y * ct) * h8 + ct
+    a = math.fmod(math.atan2(numer, denom), 2.0 * math.pi)
+    return a + 2.0 * math.pi if a < 0.0 else a
+
+
+def scale_features(n: int, outlier_ratio: float = 0.5, seed: int = DEFAULT_SEED,
+                   gt: GroundTruth = GroundTruth(), noise: float = 0.02):
+    """M1: n scale features (x, y, s); returns (features[n,3], inlier_mask)."""
+    rng = np.random.default_rng(seed)
+    n_out = int(round(n * outlier_ratio))
+    n_in = n - n_out
+    x = rng.uniform(0.0, WIDTH, n)
+    y = rng.uniform(0.0, HEIGHT, n)
+    t = 1.0 - gt.h7 * x[:n_in] - gt.h8 * y[:n_in]
+    s_in = (t / gt.alpha) ** 3 * np.exp(rng.normal(0.0, noise, n_in))
+    s_out = np.exp(rng.uniform(math.log(2.0), math.log(64.0), n_out))
+    s = np.concatenate([s_in, s_out])
+    truth = np.zeros(n, dtype=bool)
+    truth[:n_in] = True
+    perm = rng.permutation(n)
+    feats = np.stack([x, y, s], axis=1)[perm]
+    return np.ascontiguousarray(feats), truth[perm]
+
+
+def orientation_features(n: int, outlier_ratio: float = 0.5, seed: int = DEFAULT_SEED + 1,
+                         gt: GroundTruth = GroundTruth(), noise_deg: float = 0.5):
+    """M2 orientation part: n features (x, y, angle); returns (features, inlier_mask)."""
+    rng = np.random.default_rng(seed)
+    n_out = int(round(n * outlier_ratio))
+    n_in = n - n_out
+    x = rng.uniform(0.0, WIDTH, n)
+    y = rng.uniform(0.0, HEIGHT, n)
+    theta = np.empty(n)
+    which = rng.integers(0, 2, n_in)
+    noise = np.deg2rad(rng.normal(0.0, noise_deg, n_in))
+    for i in range(n_in):
+        w = 1.0 - gt.h7 * x[i] - gt.h8 * y[i]          # rectifyPoint
+        u, v = x[i] / w, y[i] / w
+        tr = gt.phi + (math.pi / 2.0) * which[i] + noise[i]
+        theta[i] = _unrectified_angle(gt.h7, gt.h8, u, v, tr)
+    theta[n_in:] = rng.uniform(0.0, 2.0 * math.pi, n_out)
+    truth = np.zeros(n, dtype=bool)
+    truth[:n_in] = True
+    perm = rng.permutation(n)
+    feats = np.stack([x, y, theta], axis=1)[perm]
+    return np.ascontiguousarray(feats), truth[perm]
+
+
+def problem_m1(n: int = 10_000, outlier_ratio: float = 0.5, seed: int = DEFAULT_SEED):
+    """Scale-only problem (3-SIFT): features, truth mask, thresholds."""
+    f, t = scale_features(n, outlier_ratio, seed)
+    return f, t, 0.05
+
+
+def problem_m2(n_scale: int = 5_000, n_orient: int = 5_000, outlier_ratio: float = 0.5,
+               seed: int = DEFAULT_SEED):
+    """Hybrid problem (2+2 SIFT): scale feats, orientation feats, truths, thresholds."""
+    fs, ts = scale_features(n_scale, outlier_ratio, seed)
+    fo, to = orientation_features(n_orient, outlier_ratio, seed + 1)
+    return fs, fo, ts, to, 0.05, math.radians(1.0)

@@ -1,0 +1,162 @@
+/*
+ * gcr.h -- C ABI of the MI355X-native Graph-Cut RANSAC rectification engine.
+ *
+ * This is the drop-in boundary for the reference's hot path.  Each entry point
+ * replaces one C++ function that pygcransac's pybind11 layer binds today
+ * (yuvalnis/graph-cut-ransac, src/pygcransac/include/gcransac_python.h):
+ *
+ *   gcr_rect_scale_only(..., original=0)  <- findRectifyingHomographyScaleOnly_
+ *                                            (gcransac_python.h:7-18, .cpp:32-142)
+ *   gcr_rect_scale_only(..., original=1)  <- findRectifyingHomographyScaleOnlyOriginal_
+ *                                            (gcransac_python.h:20-31, .cpp:144-254)
+ *   gcr_rect_sift(...)                    <- findRectifyingHomographySIFT_
+ *                                            (gcransac_python.h:33-47, .cpp:256-406)
+ *
+ * Conventions (no C++ or torch types cross this boundary):
+ *   - features are row-major N x 3 float64 arrays, exactly the flat buffers the
+ *     reference copies out of numpy (bindings.cpp:12-17, 234-250);
+ *   - the caller owns every buffer; masks are N bytes (0/1);
+ *   - H_out is the row-major 3x3 homography model.getHomography() / H22
+ *     (gcransac_python.cpp:95-104);
+ *   - return value >= 0 is the total number of inliers (the reference's int
+ *     return, gcransac_python.cpp:141/405), < 0 is an error code; the message is
+ *     available from gcr_last_error() (thread-local).  -EINVAL maps to Python
+ *     ValueError, everything else to RuntimeError.
+ *   - no exceptions cross the ABI; functions are thread-safe for distinct
+ *     contexts; one context per device.
+ */
+#ifndef GCR_H_
+#define GCR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCR_ABI_VERSION 1
+
+/* error codes */
+#define GCR_OK 0
+#define GCR_EINTERNAL (-1)
+#define GCR_EHIP (-5)
+#define GCR_ENOMEM (-12)
+#define GCR_ENODEV (-19)
+#define GCR_EINVAL (-22)
+
+/* solver kinds (types.h:43-59 estimator typedefs) */
+#define GCR_SOLVER_SCALE3 0          /* RectifyingHomographyThreeSIFTSolver         */
+#define GCR_SOLVER_SCALE3_ORIGINAL 1 /* RectifyingHomographyThreeSIFTSolverOriginal */
+#define GCR_SOLVER_SIFT22 2          /* RectifyingHomographyTwoSIFTSolver           */
+
+typedef struct gcr_ctx gcr_ctx;
+typedef struct gcr_problem gcr_problem;
+
+/* Mirrors utils::Settings (settings.h:42-74) for the fields the Python entry
+ * points set (gcransac_python.cpp:79-85, 191-197, 314-321), plus extensions. */
+typedef struct gcr_params {
+    double scale_residual_thresh;        /* settings.threshold(0)                         */
+    double orientation_residual_thresh;  /* settings.threshold(1) (SIFT only)             */
+    double spatial_coherence_weight;     /* lambda; binding default 0.0                   */
+    uint64_t min_iteration_number;       /* binding default 10000                         */
+    uint64_t max_iteration_number;       /* binding default 10000                         */
+    uint64_t max_local_optimization_number; /* binding default 50                        */
+    double confidence;                   /* settings.h:60 default 0.95 (not set by Python) */
+    uint64_t seed;                       /* extension: Philox key (reference is unseeded) */
+    uint32_t batch_slots;                /* extension: outer-iteration slots per launch, 0 = auto */
+    uint32_t flags;                      /* bit 0: disable local optimisation (bench only) */
+} gcr_params;
+
+#define GCR_FLAG_NO_LO 1u
+
+/* model.h: NormalizingTransform{x0,y0,s}, RectifyingHomography{h7,h8},
+ * ScaleBased{alpha}, OrientationBased{phi}. */
+typedef struct gcr_rect_model {
+    double x0, y0, s, h7, h8, alpha, phi;
+} gcr_rect_model;
+
+/* utils::RANSACStatistics (statistics.h:43-64) plus per-phase timings. */
+typedef struct gcr_stats {
+    uint64_t iteration_number;
+    uint64_t local_optimization_number;
+    uint64_t graph_cut_number;
+    uint64_t slots;               /* outer-loop bodies executed                     */
+    uint64_t hypotheses;          /* models scored in the main loop                 */
+    uint64_t hypotheses_computed; /* models scored on the GPU incl. speculative     */
+    uint64_t lo_models;           /* models scored inside local optimisation        */
+    uint64_t launches;
+    double score;                 /* statistics.score                               */
+    double ms_setup, ms_generate, ms_score, ms_replay, ms_lo, ms_refit, ms_total;
+    double ms_score_kernel;       /* summed HIP-event time of the scoring kernels   */
+} gcr_stats;
+
+/* ---- context ---------------------------------------------------------- */
+const char* gcr_last_error(void);
+int gcr_abi_version(void);
+int gcr_device_count(void);
+int gcr_create(int device, gcr_ctx** out);
+void gcr_destroy(gcr_ctx* ctx);
+/* hipDeviceSynchronize on the context's device */
+int gcr_synchronize(gcr_ctx* ctx);
+void gcr_default_params(gcr_params* p);
+
+/* ---- drop-in entry points (one call = one reference call) ---------------- */
+int gcr_rect_scale_only(gcr_ctx* ctx, const double* features, size_t n, const gcr_params* params, int original,
+                        uint8_t* mask_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
+
+int gcr_rect_sift(gcr_ctx* ctx, const double* scale_features, size_t n_scale, const double* orientation_features,
+                  size_t n_orientation, const gcr_params* params, uint8_t* scale_mask_out,
+                  uint8_t* orientation_mask_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
+
+/* ---- device-resident problems (benchmarks, problem batches) -------------- */
+/* Uploads the features once; runs reuse the HBM-resident copy.  f1 is the
+ * orientation set for GCR_SOLVER_SIFT22 and NULL otherwise. */
+int gcr_problem_create(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
+                       gcr_problem** out);
+void gcr_problem_destroy(gcr_problem* prob);
+/* full estimator call on the resident problem (same semantics as gcr_rect_*) */
+int gcr_problem_run(gcr_problem* prob, const gcr_params* params, uint8_t* mask0_out, uint8_t* mask1_out,
+                    double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
+
+/* One pass of the hot path over one batch: draw and solve `nslots`
+ * outer-iteration slots starting at `slot0`, MSAC-score every resulting model
+ * against all features on the GPU, and return the best-scoring slot (first
+ * strict maximum, the reference's update rule).  Timings go to stats_out. */
+typedef struct gcr_batch_result {
+    uint64_t models;        /* hypotheses scored                        */
+    uint64_t iterations;    /* sum of iteration increments of the batch */
+    int64_t best_slot;      /* -1 if no model scored > 0                */
+    double best_score;
+    uint64_t best_inliers[2];
+    gcr_rect_model best_model;
+} gcr_batch_result;
+int gcr_problem_verify_batch(gcr_problem* prob, const gcr_params* params, uint64_t slot0, uint32_t nslots,
+                             gcr_batch_result* out, gcr_stats* stats_out);
+
+/* ---- parity / debug hooks (used by tests; GPU required unless noted) ---- */
+/* inc[i] in 1..101 (attempt of success) or 102 (no model), models[i] */
+int gcr_debug_generate(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc_out,
+                       gcr_rect_model* models_out);
+/* raw MSAC accumulators for explicit models: counts, per-class sums, total */
+int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* models, uint32_t nmodels,
+                    uint32_t* n0, uint32_t* n1, double* v0, double* v1, double* tot);
+/* inlier mask of one model: rule 0 = MSAC (2.25 thr^2), 1 = LO threshold
+ * ((1.5 thr)^2), 2 = 1-class graph-cut labeling */
+int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* model, int cls, int rule,
+                   uint8_t* mask_out);
+/* host-only (no GPU): deterministic math and sampler used on both sides */
+double gcr_host_log(double x);
+double gcr_host_pow_m3(double t);
+double gcr_host_atan2(double y, double x);
+int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls, uint64_t n,
+                    uint32_t m, uint32_t* out);
+/* device evaluation of the same primitives over arrays (GPU parity tests):
+ * op 0 log(a), 1 pow_m3(a), 2 atan2(a, b), 3 a / b, 4 sqrt(a) */
+int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GCR_H_ */

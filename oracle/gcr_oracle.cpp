@@ -1,0 +1,1272 @@
+// =============================================================================
+// gcr_oracle.cpp -- CPU ORACLE (TEST INFRASTRUCTURE ONLY).
+//
+// A plain C++17 (standard library only: no Eigen, no OpenCV) restatement of the
+// hybrid GC-RANSAC path of yuvalnis/graph-cut-ransac (snapshot 2025-11-21), used
+// exclusively as the checker by tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg.  The product (graph-cut-ransac_amd/) never links, imports or
+// executes anything under oracle/.
+//
+// Parity status: the reference itself cannot be compiled in this image (Eigen3
+// and OpenCV headers are absent), so this restatement is pinned by
+// the reference's own known-answer tests (tests/unit_tests.cpp, ported to
+// tests/test_oracle_kat.py) and, for the one third-party numeric kernel (Eigen's
+// colPivHouseholderQr), follows Eigen's published algorithm -- parity at that
+// boundary is "unpinned" beyond ~1e-12.  The reference is unseeded
+// (std::random_device per sample, GCRANSAC.h:53-80); this oracle replaces it
+// with the Philox sampler documented in graph-cut-ransac_amd/csrc/philox.h
+// (restated independently below) and keeps a "faithful" sampler
+// (random_device + mt19937 + full shuffle) for CPU-baseline timing.
+//
+// Math modes:
+//   GLIBC (0): std::log / std::pow(t,-3.0) / std::atan2, exactly the reference.
+//   TWIN  (1): those three hypothesis-dependent functions come from the
+//              product's detmath.h so GPU results can be compared bitwise;
+//              tests cross-check TWIN against GLIBC.
+// =============================================================================
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <random>
+#include <stdexcept>
+#include <unordered_map>
+#include <vector>
+
+#include "../graph-cut-ransac_amd/csrc/detmath.h"   // TWIN mode primitives only
+
+namespace oracle {
+
+// ----------------------------------------------------------------- math ----
+enum MathMode { MATH_GLIBC = 0, MATH_TWIN = 1 };
+static thread_local int g_math = MATH_GLIBC;
+
+static inline double m_log(double x) { return g_math == MATH_TWIN ? gcr::dm::dm_log(x) : std::log(x); }
+static inline double m_pow_m3(double t) { return g_math == MATH_TWIN ? gcr::dm::dm_pow_m3(t) : std::pow(t, -3.0); }
+static inline double m_atan2(double y, double x) {
+    return g_math == MATH_TWIN ? gcr::dm::dm_atan2(y, x) : std::atan2(y, x);
+}
+
+// ------------------------------------------------------ math_utils.hpp ----
+// (HDR/math_utils.hpp:45-321)
+static inline double sqr(double x) { return x * x; }
+static inline double cube(double x) { return x * x * x; }
+static inline size_t nChoose2(size_t n) { return n == 0 ? 0 : (n * (n - 1)) / 2; }
+static inline double deg2rad(double a) { return a * (M_PI / 180.0); }
+static inline double rad2deg(double a) { return a * (M_1_PI * 180.0); }
+
+static inline double clipAngle(double angle) {
+    const double kTwoPI = 2.0 * M_PI;
+    angle = std::fmod(angle, kTwoPI);
+    if (angle < 0.0) angle += kTwoPI;
+    return angle;
+}
+static inline double minAngleDiff(double a1, double a2) {
+    const double kTwoPI = 2.0 * M_PI;
+    double diff = std::fabs(clipAngle(a1) - clipAngle(a2));
+    return std::fmin(diff, kTwoPI - diff);
+}
+static inline double linesAnglesDiff(double a1, double a2) {
+    double d1 = minAngleDiff(a1, a2);
+    double d2 = minAngleDiff(a1, a2 - M_PI);
+    return std::fmin(d1, d2);
+}
+struct V3 { double v[3]; double& operator[](int i) { return v[i]; } double operator[](int i) const { return v[i]; } };
+static inline V3 lineFromPointAndAngle(double x, double y, double theta) {
+    const double c = std::cos(theta), s = std::sin(theta);
+    return V3{{s, -c, y * c - x * s}};
+}
+static inline V3 cross(const V3& a, const V3& b) {
+    return V3{{a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]}};
+}
+static inline double dot(const V3& a, const V3& b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+
+struct Point2D {
+    double x, y;
+    bool operator<(const Point2D& p) const { return x < p.x || (x == p.x && y < p.y); }
+};
+
+static inline bool areCollinear(double x1, double y1, double x2, double y2, double x3, double y3, double tol) {
+    V3 p1{{x1, y1, 1.0}}, p2{{x2, y2, 1.0}}, p3{{x3, y3, 1.0}};
+    V3 l = cross(p1, p2);
+    const double n = std::sqrt(sqr(l[0]) + sqr(l[1]));
+    for (int i = 0; i < 3; ++i) l[i] = l[i] / n;
+    const double dist = dot(l, p3);
+    return dist < tol;   // signed, as in the reference
+}
+
+// gaussElimination<3> on [A | b]
+static void gaussElimination3(double m[3][4], double r[3]) {
+    for (size_t i = 0; i < 3; i++)
+        for (size_t k = i + 1; k < 3; k++)
+            if (std::fabs(m[i][i]) < std::fabs(m[k][i]))
+                for (size_t j = 0; j <= 3; j++) std::swap(m[i][j], m[k][j]);
+    for (size_t i = 0; i < 2; i++)
+        for (size_t k = i + 1; k < 3; k++) {
+            const double temp = m[k][i] / m[i][i];
+            for (size_t j = 0; j <= 3; j++) m[k][j] = m[k][j] - temp * m[i][j];
+        }
+    for (size_t i = 0; i < 3; i++) {
+        const size_t row = 3 - 1 - i;
+        r[row] = m[row][3];
+        for (size_t c = row + 1; c < 3; c++)
+            if (c != row) r[row] = r[row] - m[row][c] * r[c];
+        r[row] = r[row] / m[row][row];
+    }
+}
+
+static inline double crossProduct(const Point2D& O, const Point2D& P, const Point2D& Q) {
+    return (P.x - O.x) * (Q.y - O.y) - (P.y - O.y) * (Q.x - O.x);
+}
+
+static std::vector<Point2D> computeConvexHull(std::vector<Point2D>& points) {
+    const size_t n = points.size();
+    if (n <= 1) return points;
+    std::vector<Point2D> result(2 * n);
+    std::sort(points.begin(), points.end());
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        while (k >= 2 && crossProduct(result[k - 2], result[k - 1], points[i]) <= 0) k--;
+        result[k++] = points[i];
+    }
+    const size_t t = k + 1;
+    for (size_t i = n - 1; i > 0; --i) {
+        while (k >= t && crossProduct(result[k - 2], result[k - 1], points[i - 1]) <= 0) k--;
+        result[k++] = points[i - 1];
+    }
+    result.resize(k - 1);
+    if (result.size() == 2) {
+        bool cx = std::abs(result[0].x - result[1].x) < 1e-9;
+        bool cy = std::abs(result[0].y - result[1].y) < 1e-9;
+        if (cx && cy) result.resize(1);
+    }
+    return result;
+}
+
+static bool pointInConvexPolygon(const Point2D& p, const std::vector<Point2D>& poly) {
+    const size_t nv = poly.size();
+    if (nv < 3) return false;
+    bool pos = false, neg = false;
+    for (size_t i = 0; i < nv; i++) {
+        double cp = crossProduct(poly[i], poly[(i + 1) % nv], p);
+        if (cp > 0) pos = true;
+        else if (cp < 0) neg = true;
+        if (pos && neg) return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- model.h ----
+struct Model {
+    double x0 = 0.0, y0 = 0.0, s = 1.0;   // NormalizingTransform
+    double h7 = 0.0, h8 = 0.0;            // RectifyingHomography
+    double alpha = 1.0;                    // ScaleBased
+    double phi = 0.0;                      // OrientationBased
+
+    void normalize(double& x, double& y, double w) const { x = s * (x - x0 * w); y = s * (y - y0 * w); }
+    void normalizeScale(double& sc) const { sc *= s; }
+    void rectifyPoint3(V3& p) const { p[2] = -h7 * p[0] - h8 * p[1] + p[2]; }
+    void unrectifyPoint3(V3& p) const { p[2] = h7 * p[0] + h8 * p[1] + p[2]; }
+    void rectifyPoint(double& x, double& y) const { V3 p{{x, y, 1.0}}; rectifyPoint3(p); x = p[0] / p[2]; y = p[1] / p[2]; }
+    void unrectifyPoint(double& x, double& y) const { V3 p{{x, y, 1.0}}; unrectifyPoint3(p); x = p[0] / p[2]; y = p[1] / p[2]; }
+    // rectifiedAngle takes cos/sin of the raw angle: identical to std::cos/sin(angle)
+    double rectifiedAngleCS(double x, double y, double ct, double st) const {
+        const double numer = (-x * st + y * ct) * h7 + st;
+        const double denom = (x * st - y * ct) * h8 + ct;
+        return clipAngle(m_atan2(numer, denom));
+    }
+    double rectifiedAngle(double x, double y, double angle) const {
+        return rectifiedAngleCS(x, y, std::cos(angle), std::sin(angle));
+    }
+    double unrectifiedAngle(double x, double y, double angle) const {
+        const double ct = std::cos(angle), st = std::sin(angle);
+        const double numer = (x * st - y * ct) * h7 + st;
+        const double denom = (-x * st + y * ct) * h8 + ct;
+        return clipAngle(std::atan2(numer, denom));
+    }
+    double localScalePerspectiveWarp(double x, double y) const { return std::pow(h7 * x + h8 * y + 1.0, -3.0); }
+    double localScaleAffineRectification(double x, double y) const { return m_pow_m3(-h7 * x - h8 * y + 1.0); }
+    double rectifiedScale(double x, double y, double sc) const { return sc * localScaleAffineRectification(x, y); }
+    double unrectifiedScale(double x, double y, double sc) const { return sc * localScalePerspectiveWarp(x, y); }
+    // getHomography (model.h:211-226): N.inverse() * H * N / result(2,2), with
+    // Eigen's 3x3 cofactor inverse and left-to-right coefficient products.
+    void getHomography(double H[9]) const {
+        const double N[9] = {s, 0, -s * x0, 0, s, -s * y0, 0, 0, 1};
+        const double Hn[9] = {1, 0, 0, 0, 1, 0, h7, h8, 1};
+        auto cof = [&](int i, int j) {
+            const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+            return N[i1 * 3 + j1] * N[i2 * 3 + j2] - N[i1 * 3 + j2] * N[i2 * 3 + j1];
+        };
+        const double c00 = cof(0, 0), c10 = cof(1, 0), c20 = cof(2, 0);
+        const double det = (c00 * N[0] + c10 * N[3]) + c20 * N[6];
+        const double invdet = 1.0 / det;
+        double Ni[9];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) Ni[r * 3 + c] = cof(c, r) * invdet;
+        double T[9], R[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                T[i * 3 + j] = (Ni[i * 3 + 0] * Hn[0 * 3 + j] + Ni[i * 3 + 1] * Hn[1 * 3 + j]) + Ni[i * 3 + 2] * Hn[2 * 3 + j];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                R[i * 3 + j] = (T[i * 3 + 0] * N[0 * 3 + j] + T[i * 3 + 1] * N[1 * 3 + j]) + T[i * 3 + 2] * N[2 * 3 + j];
+        const double d = R[8];
+        for (int i = 0; i < 9; ++i) H[i] = R[i] / d;
+    }
+};
+
+// ------------------------------------------------------- Philox sampler ----
+// Independent restatement of the product's sampler contract (philox.h).
+static void philox10(uint32_t c[4], uint32_t k[2], uint32_t out[4]) {
+    uint32_t x0 = c[0], x1 = c[1], x2 = c[2], x3 = c[3], k0 = k[0], k1 = k[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t a = (uint64_t)0xD2511F53u * x0, b = (uint64_t)0xCD9E8D57u * x2;
+        uint32_t y0 = (uint32_t)(b >> 32) ^ x1 ^ k0, y1 = (uint32_t)b;
+        uint32_t y2 = (uint32_t)(a >> 32) ^ x3 ^ k1, y3 = (uint32_t)a;
+        x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
+}
+
+struct PhiloxWords {
+    uint32_t key[2], ctr[4], blk[4];
+    uint32_t n = 0;
+    PhiloxWords(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls) {
+        key[0] = (uint32_t)seed; key[1] = (uint32_t)(seed >> 32);
+        ctr[0] = (uint32_t)index; ctr[1] = (uint32_t)(index >> 32); ctr[2] = sub;
+        ctr[3] = (stream << 24) | ((cls & 0xff) << 16);
+    }
+    uint64_t next() {
+        uint32_t w = n++;
+        if (w % 2 == 0) {
+            uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3] | ((w / 2) & 0xffff)};
+            philox10(c, key, blk);
+            return (uint64_t)blk[0] | ((uint64_t)blk[1] << 32);
+        }
+        return (uint64_t)blk[2] | ((uint64_t)blk[3] << 32);
+    }
+};
+
+// ordered m-subset of {0..n-1} by rejection; false if the 4096-word budget runs out
+static bool philox_subset(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls, size_t n,
+                          size_t m, std::vector<size_t>& out) {
+    PhiloxWords pw(seed, index, sub, stream, cls);
+    out.clear();
+    while (out.size() < m) {
+        if (pw.n >= 4096) return false;
+        const size_t v = (size_t)(((unsigned __int128)pw.next() * (unsigned __int128)n) >> 64);
+        if (std::find(out.begin(), out.end(), v) == out.end()) out.push_back(v);
+    }
+    return true;
+}
+
+enum SamplerMode { SAMPLER_PHILOX = 0, SAMPLER_FAITHFUL = 1 };
+
+// get_random_subset (GCRANSAC.h:53-80), verbatim semantics (unseeded)
+static bool faithful_subset(const std::vector<size_t>& indices, size_t N, std::vector<size_t>& output) {
+    if (N > indices.size()) return false;
+    std::random_device rd;
+    std::mt19937 gen(rd());
+    std::vector<size_t> v(indices.begin(), indices.end());
+    std::shuffle(v.begin(), v.end(), gen);
+    output.clear();
+    output.insert(output.end(), v.begin(), v.begin() + N);
+    return true;
+}
+
+// ---------------------------------------------- ColPivHouseholderQR (Eigen) ----
+// Restatement of Eigen::ColPivHouseholderQR<MatrixX3d>::compute + solve for an
+// m x 3 column-major matrix; sums run in plain sequential order.
+static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_t m, std::vector<double>& b,
+                             double x[3]) {
+    const size_t cols = 3, rows = m, size = std::min(rows, cols);
+    auto at = [&](size_t i, size_t j) -> double& { return A[j * rows + i]; };
+    double hc[3] = {0, 0, 0};
+    size_t transp[3] = {0, 1, 2};
+    double normsU[3], normsD[3];
+    for (size_t k = 0; k < cols; ++k) {
+        double s = 0;
+        for (size_t i = 0; i < rows; ++i) s += at(i, k) * at(i, k);
+        normsD[k] = std::sqrt(s);
+        normsU[k] = normsD[k];
+    }
+    const double eps = std::numeric_limits<double>::epsilon();
+    double maxn = normsU[0];
+    for (size_t k = 1; k < cols; ++k) if (maxn < normsU[k]) maxn = normsU[k];
+    const double threshold_helper = sqr(maxn * eps) / (double)rows;
+    const double norm_downdate_threshold = std::sqrt(eps);
+    size_t nonzero = size;
+    for (size_t k = 0; k < size; ++k) {
+        size_t big = k;
+        double bign = normsU[k];
+        for (size_t j = k + 1; j < cols; ++j) if (bign < normsU[j]) { bign = normsU[j]; big = j; }
+        const double big_sq = sqr(bign);
+        if (nonzero == size && big_sq < threshold_helper * (double)(rows - k)) nonzero = k;
+        transp[k] = big;
+        if (k != big) {
+            for (size_t i = 0; i < rows; ++i) std::swap(at(i, k), at(i, big));
+            std::swap(normsU[k], normsU[big]);
+            std::swap(normsD[k], normsD[big]);
+        }
+        // makeHouseholderInPlace on column k, rows k..m-1
+        double tail = 0;
+        for (size_t i = k + 1; i < rows; ++i) tail += at(i, k) * at(i, k);
+        const double c0 = at(k, k);
+        double tau, beta;
+        const double tol = std::numeric_limits<double>::min();
+        if (tail <= tol) {
+            tau = 0.0;
+            beta = c0;
+            for (size_t i = k + 1; i < rows; ++i) at(i, k) = 0.0;
+        } else {
+            beta = std::sqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            const double den = c0 - beta;
+            for (size_t i = k + 1; i < rows; ++i) at(i, k) = at(i, k) / den;
+            tau = (beta - c0) / beta;
+        }
+        hc[k] = tau;
+        at(k, k) = beta;
+        // applyHouseholderOnTheLeft to columns k+1..2, rows k..m-1
+        if (rows - k == 1) {
+            for (size_t j = k + 1; j < cols; ++j) at(k, j) *= (1.0 - tau);
+        } else if (tau != 0.0) {
+            for (size_t j = k + 1; j < cols; ++j) {
+                double t = 0;
+                for (size_t i = k + 1; i < rows; ++i) t += at(i, k) * at(i, j);
+                t += at(k, j);
+                at(k, j) -= tau * t;
+                for (size_t i = k + 1; i < rows; ++i) at(i, j) -= (tau * at(i, k)) * t;
+            }
+        }
+        for (size_t j = k + 1; j < cols; ++j) {
+            if (normsU[j] != 0.0) {
+                double temp = std::fabs(at(k, j)) / normsU[j];
+                temp = (1.0 + temp) * (1.0 - temp);
+                temp = temp < 0.0 ? 0.0 : temp;
+                double temp2 = temp * sqr(normsU[j] / normsD[j]);
+                if (temp2 <= norm_downdate_threshold) {
+                    double s = 0;
+                    for (size_t i = k + 1; i < rows; ++i) s += at(i, j) * at(i, j);
+                    normsD[j] = std::sqrt(s);
+                    normsU[j] = normsD[j];
+                } else {
+                    normsU[j] *= std::sqrt(temp);
+                }
+            }
+        }
+    }
+    size_t perm[3] = {0, 1, 2};
+    for (size_t k = 0; k < size; ++k) std::swap(perm[k], perm[transp[k]]);
+    if (nonzero == 0) { x[0] = x[1] = x[2] = 0.0; return true; }
+    // c = Q^T b with the first `nonzero` reflectors (H_0 first)
+    for (size_t k = 0; k < nonzero; ++k) {
+        const double tau = hc[k];
+        if (rows - k == 1) { b[k] *= (1.0 - tau); continue; }
+        if (tau == 0.0) continue;
+        double t = 0;
+        for (size_t i = k + 1; i < rows; ++i) t += at(i, k) * b[i];
+        t += b[k];
+        b[k] -= tau * t;
+        for (size_t i = k + 1; i < rows; ++i) b[i] -= (tau * at(i, k)) * t;
+    }
+    // upper-triangular solve, column oriented (Eigen triangular_solve_vector)
+    double c[3] = {b[0], b[1], b[2]};
+    for (size_t jj = nonzero; jj-- > 0;) {
+        c[jj] = c[jj] / at(jj, jj);
+        for (size_t i = 0; i < jj; ++i) c[i] -= c[jj] * at(i, jj);
+    }
+    for (size_t i = 0; i < nonzero; ++i) x[perm[i]] = c[i];
+    for (size_t i = nonzero; i < cols; ++i) x[perm[i]] = 0.0;
+    return true;
+}
+
+// ------------------------------------------------------------- data ----
+struct Features {
+    std::vector<double> d;   // row-major n x 3
+    size_t n = 0;
+    double at(size_t i, size_t j) const { return d[i * 3 + j]; }
+};
+
+template <size_t K>
+using Inliers = std::array<std::vector<size_t>, K>;
+template <size_t K>
+using Data = std::array<const Features*, K>;
+
+// ------------------------------------------------------------- Score ----
+template <size_t K>
+struct Score {
+    std::array<size_t, K> n{};
+    std::array<double, K> v{};
+    size_t total = 0;
+    double sum = 0.0;
+    double value() const { return sum; }
+    bool operator<(const Score& o) const { return value() < o.value(); }
+    void inc_n(size_t i) { n[i] += 1; total++; }
+    void inc_v(size_t i, double x) { v[i] += x; sum += x; }
+    void reset_v(size_t i, double x) { sum -= v[i]; v[i] = x; sum += x; }
+};
+
+// ------------------------------------------------------------- solvers ----
+// kind 0: ThreeSIFT, 1: ThreeSIFTOriginal, 2: TwoSIFT
+template <int KIND>
+struct Solver {
+    static constexpr size_t K = (KIND == 2) ? 2 : 1;
+    static constexpr double kScalePower = (KIND == 1) ? (-1.0 / 3.0) : (1.0 / 3.0);
+    std::array<size_t, K> sampleSize() const {
+        if constexpr (K == 2) return {2, 2}; else return {3};
+    }
+
+    static double scaleResidual(double x, double y, double s, const Model& m) {
+        V3 p{{x, y, 1.0}};
+        double scale = s;
+        m.normalize(p[0], p[1], p[2]);
+        m.normalizeScale(scale);
+        const double rs = m.rectifiedScale(p[0], p[1], scale);
+        if (rs < 1e-9) return DBL_MAX;
+        const double ac = cube(m.alpha);
+        if constexpr (KIND == 1) return std::fabs(m_log(rs / ac));
+        else return std::fabs(m_log(ac * rs));
+    }
+    static double orientationResidual(double x, double y, double t, const Model& m) {
+        V3 p{{x, y, 1.0}};
+        m.normalize(p[0], p[1], p[2]);
+        const double ro = m.rectifiedAngle(p[0], p[1], t);
+        return std::fmin(linesAnglesDiff(m.phi, ro), linesAnglesDiff(clipAngle(m.phi + M_PI_2), ro));
+    }
+    double squaredResidual(size_t type, const Features& f, size_t i, const Model& m) const {
+        double r;
+        if (type == 0) r = scaleResidual(f.at(i, 0), f.at(i, 1), f.at(i, 2), m);
+        else r = orientationResidual(f.at(i, 0), f.at(i, 1), f.at(i, 2), m);
+        return r * r;
+    }
+
+    bool isValidSample(const Data<K>& data, const Inliers<K>& s) const {
+        if constexpr (K == 1) {
+            const Features& f = *data[0];
+            const auto& in = s[0];
+            if (in.size() < 3) return false;   // all collinear by definition
+            for (size_t i = 0; i < in.size() - 2; i++) {
+                if (!areCollinear(f.at(in[i], 0), f.at(in[i], 1), f.at(in[i + 1], 0), f.at(in[i + 1], 1),
+                                  f.at(in[i + 2], 0), f.at(in[i + 2], 1), 1.0))
+                    return true;
+            }
+            return false;
+        } else {
+            const Features& sf = *data[0];
+            const Features& of = *data[1];
+            if (s[0].size() != 2 || s[1].size() != 2) return false;
+            size_t idx = s[1][0];
+            double x1 = of.at(idx, 0), y1 = of.at(idx, 1), t1 = of.at(idx, 2);
+            V3 l1 = lineFromPointAndAngle(x1, y1, t1);
+            idx = s[1][1];
+            double x2 = of.at(idx, 0), y2 = of.at(idx, 1), t2 = of.at(idx, 2);
+            V3 l2 = lineFromPointAndAngle(x2, y2, t2);
+            V3 vp = cross(l1, l2);
+            if (std::fabs(vp[0]) < 1e-6 && std::fabs(vp[1]) < 1e-6 && std::fabs(vp[2]) < 1e-6) return false;
+            if (std::abs(vp[2]) < 1e-6) return true;
+            const double z = vp[2];
+            for (int i = 0; i < 3; ++i) vp[i] = vp[i] / z;
+            Point2D v{vp[0], vp[1]};
+            Point2D p1{sf.at(s[0][0], 0), sf.at(s[0][0], 1)};
+            Point2D p2{sf.at(s[0][1], 0), sf.at(s[0][1], 1)};
+            if (areCollinear(p1.x, p1.y, p2.x, p2.y, v.x, v.y, 1.0)) return false;
+            std::vector<Point2D> pts{p1, p2, {x1, y1}, {x2, y2}};
+            const auto hull = computeConvexHull(pts);
+            if (pointInConvexPolygon(v, hull)) return false;
+            return true;
+        }
+    }
+
+    bool isValidModel(const Model& m) const {
+        if constexpr (K == 2) return !(std::fmax(std::fabs(m.h7), std::fabs(m.h8)) >= 1e-3);
+        else return true;
+    }
+
+    // ---- minimal
+    bool estimateMinimal1(const Features& f, const std::vector<size_t>& in, std::vector<Model>& models) const {
+        if (in.size() != 3) return false;
+        double c[3][4];
+        for (size_t i = 0; i < 3; i++) {
+            const size_t j = in[i];
+            c[i][0] = f.at(j, 0);
+            c[i][1] = f.at(j, 1);
+            if constexpr (KIND == 1) { c[i][2] = -std::pow(f.at(j, 2), kScalePower); c[i][3] = -1.0; }
+            else { c[i][2] = std::pow(f.at(j, 2), kScalePower); c[i][3] = 1.0; }
+        }
+        double sol[3];
+        gaussElimination3(c, sol);
+        if (std::isnan(sol[0]) || std::isnan(sol[1]) || std::isnan(sol[2])) return false;
+        Model m;
+        m.h7 = sol[0]; m.h8 = sol[1]; m.alpha = sol[2];
+        if (m.alpha < 1e-9) return false;
+        models.push_back(m);
+        return true;
+    }
+    bool estimateMinimal2(const Features& sf, const std::vector<size_t>& si, const Features& of,
+                          const std::vector<size_t>& oi, std::vector<Model>& models) const {
+        if (si.size() != 2 || nChoose2(oi.size()) != 1) return false;
+        double c[3][4];
+        for (size_t r = 0; r < 2; ++r) {
+            c[r][0] = sf.at(si[r], 0); c[r][1] = sf.at(si[r], 1);
+            c[r][2] = std::pow(sf.at(si[r], 2), kScalePower); c[r][3] = 1.0;
+        }
+        V3 l1 = lineFromPointAndAngle(of.at(oi[0], 0), of.at(oi[0], 1), of.at(oi[0], 2));
+        V3 l2 = lineFromPointAndAngle(of.at(oi[1], 0), of.at(oi[1], 1), of.at(oi[1], 2));
+        V3 vp = cross(l1, l2);
+        c[2][0] = vp[0]; c[2][1] = vp[1]; c[2][2] = 0; c[2][3] = vp[2];
+        double sol[3];
+        gaussElimination3(c, sol);
+        if (std::isnan(sol[0]) || std::isnan(sol[1]) || std::isnan(sol[2])) return false;
+        Model m;
+        m.h7 = sol[0]; m.h8 = sol[1]; m.alpha = sol[2];
+        if (m.alpha < 1e-9) return false;
+        m.rectifyPoint3(vp);
+        if (std::abs(vp[2]) > 1e-9) return false;
+        m.phi = clipAngle(m_atan2(vp[1], vp[0]));
+        models.push_back(m);
+        return true;
+    }
+
+    // ---- non-minimal
+    bool estimateNonMinimal1(const Features& f, const std::vector<size_t>& in, std::vector<Model>& models) const {
+        const size_t n = in.size();
+        std::vector<double> A(n * 3), b(n);
+        for (size_t i = 0; i < n; ++i) {
+            const size_t j = in[i];
+            const double w = 1.0;
+            A[0 * n + i] = w * f.at(j, 0);
+            A[1 * n + i] = w * f.at(j, 1);
+            if constexpr (KIND == 1) { A[2 * n + i] = -w * std::pow(f.at(j, 2), kScalePower); b[i] = -w; }
+            else { A[2 * n + i] = w * std::pow(f.at(j, 2), kScalePower); b[i] = w; }
+        }
+        double sol[3];
+        colpiv_qr_solve3(A, n, b, sol);
+        if (std::isnan(sol[0]) || std::isnan(sol[1]) || std::isnan(sol[2])) return false;
+        Model m;
+        m.h7 = sol[0]; m.h8 = sol[1]; m.alpha = sol[2];
+        if (m.alpha < 1e-9) return false;
+        models.push_back(m);
+        return true;
+    }
+
+    static double findWeightedMode(const std::vector<double>& angles, const std::vector<double>& weights, double bw) {
+        std::unordered_map<int, double> wmap, vmap;
+        for (size_t i = 0; i < angles.size(); i++) {
+            const int bin = static_cast<int>(std::round(angles[i] / bw));
+            wmap[bin] += weights[i];
+            vmap[bin] += angles[i] * weights[i];
+        }
+        int mode_bin = 0;
+        double maxw = -1;
+        for (const auto& p : wmap)
+            if (p.second > maxw) { maxw = p.second; mode_bin = p.first; }
+        return vmap[mode_bin] / wmap[mode_bin];
+    }
+
+    bool estimateNonMinimal2(const Features& sf, const std::vector<size_t>& si, const Features& of,
+                             const std::vector<size_t>& oi, std::vector<Model>& models) const {
+        const double kBinWidth = deg2rad(0.5);
+        const size_t ns = si.size(), no = oi.size();
+        const size_t nc_o = nChoose2(no);
+        if (ns < 2 || nc_o < 1) return false;
+        const size_t rows = ns + nc_o;
+        std::vector<double> A(rows * 3), b(rows);
+        size_t r = 0;
+        for (size_t i = 0; i < ns; ++i, ++r) {
+            const size_t j = si[i];
+            const double w = 1.0;
+            A[0 * rows + r] = w * sf.at(j, 0);
+            A[1 * rows + r] = w * sf.at(j, 1);
+            A[2 * rows + r] = w * std::pow(sf.at(j, 2), kScalePower);
+            b[r] = w;
+        }
+        for (size_t i = 0; i + 1 < no; i++) {
+            const size_t a = oi[i];
+            const V3 l1 = lineFromPointAndAngle(of.at(a, 0), of.at(a, 1), of.at(a, 2));
+            for (size_t j = i + 1; j < no; j++, ++r) {
+                const size_t c = oi[j];
+                const double w = 1.0 * 1.0;
+                const V3 l2 = lineFromPointAndAngle(of.at(c, 0), of.at(c, 1), of.at(c, 2));
+                V3 vp = cross(l1, l2);
+                const double a0 = std::fabs(vp[0]), a1 = std::fabs(vp[1]), a2 = std::fabs(vp[2]);
+                double mx = (a0 < a1) ? a1 : a0;
+                mx = (mx < a2) ? a2 : mx;
+                if (mx > 1.0) for (int q = 0; q < 3; ++q) vp[q] = vp[q] / mx;
+                A[0 * rows + r] = w * vp[0];
+                A[1 * rows + r] = w * vp[1];
+                A[2 * rows + r] = 0.0;
+                b[r] = w * vp[2];
+            }
+        }
+        double sol[3];
+        colpiv_qr_solve3(A, rows, b, sol);
+        if (std::isnan(sol[0]) || std::isnan(sol[1]) || std::isnan(sol[2])) return false;
+        Model m;
+        m.h7 = sol[0]; m.h8 = sol[1]; m.alpha = sol[2];
+        if (m.alpha < 1e-9) return false;
+        std::vector<double> ang(no), wts(no);
+        double wsum = 0;
+        for (size_t i = 0; i < no; i++) {
+            const size_t j = oi[i];
+            ang[i] = m.rectifiedAngle(of.at(j, 0), of.at(j, 1), of.at(j, 2));
+            wts[i] = 1.0;
+            wsum += 1.0;
+        }
+        if (wsum < 1e-9) return false;
+        for (size_t i = 0; i < no; i++) {
+            if (ang[i] > M_PI) ang[i] -= M_PI;
+            wts[i] /= wsum;
+        }
+        m.phi = findWeightedMode(ang, wts, kBinWidth);
+        models.push_back(m);
+        return true;
+    }
+
+    // estimateModel dispatch (solver-level): minimal iff exactly minimal
+    bool estimateModel(const Data<K>& data, const Inliers<K>& in, std::vector<Model>& models) const {
+        if constexpr (K == 1) {
+            if (in[0].size() < 3) return false;
+            if (in[0].size() == 3) return estimateMinimal1(*data[0], in[0], models);
+            return estimateNonMinimal1(*data[0], in[0], models);
+        } else {
+            const size_t ns = in[0].size(), nco = nChoose2(in[1].size());
+            if (ns < 2 || nco < 1) return false;
+            if (ns == 2 && nco == 1) return estimateMinimal2(*data[0], in[0], *data[1], in[1], models);
+            return estimateNonMinimal2(*data[0], in[0], *data[1], in[1], models);
+        }
+    }
+
+    // normalizePoints: only its failure condition matters (transform reset to identity)
+    bool normalizeOk(const Data<K>& data, const Inliers<K>& in) const {
+        size_t tot = 0;
+        for (size_t c = 0; c < K; ++c) tot += in[c].size();
+        if (tot < 1) return false;
+        double x0 = 0.0, y0 = 0.0;
+        for (size_t c = 0; c < K; ++c)
+            for (size_t j = 0; j < in[c].size(); ++j) { x0 += data[c]->at(in[c][j], 0); y0 += data[c]->at(in[c][j], 1); }
+        const double inv_n = 1.0 / static_cast<double>(tot);
+        x0 *= inv_n;
+        y0 *= inv_n;
+        double avg = 0.0;
+        for (size_t c = 0; c < K; ++c)
+            for (size_t j = 0; j < in[c].size(); ++j) {
+                const double dx = data[c]->at(in[c][j], 0) - x0, dy = data[c]->at(in[c][j], 1) - y0;
+                avg += std::sqrt(dx * dx + dy * dy);
+            }
+        avg *= inv_n;
+        return !(avg < 1e-9);
+    }
+
+    // RectifyingHomographyEstimator::estimateModelNonminimal
+    bool estimateModelNonminimal(const Data<K>& data, const Inliers<K>& in, std::vector<Model>& models) const {
+        const auto ss = sampleSize();
+        for (size_t c = 0; c < K; ++c) if (in[c].size() < ss[c]) return false;
+        if (!normalizeOk(data, in)) return false;
+        // the normalised copy equals the selected rows (identity transform)
+        Features copies[K];
+        Data<K> cd;
+        Inliers<K> ci;
+        for (size_t c = 0; c < K; ++c) {
+            copies[c].n = in[c].size();
+            copies[c].d.resize(in[c].size() * 3);
+            for (size_t j = 0; j < in[c].size(); ++j) {
+                for (int q = 0; q < 3; ++q) copies[c].d[j * 3 + q] = data[c]->at(in[c][j], q);
+                ci[c].push_back(j);
+            }
+            cd[c] = &copies[c];
+        }
+        const size_t before = models.size();
+        if (!estimateModel(cd, ci, models)) return false;
+        for (size_t q = before; q < models.size(); ++q) { models[q].x0 = 0.0; models[q].y0 = 0.0; models[q].s = 1.0; }
+        return true;
+    }
+};
+
+// --------------------------------------------------------------- MSAC ----
+template <class S>
+static Score<S::K> getScore(const S& solver, const Data<S::K>& data, const Model& m, const double thr[S::K],
+                            Inliers<S::K>& inliers) {
+    constexpr size_t K = S::K;
+    Score<K> score{};
+    double T[K];
+    for (size_t c = 0; c < K; ++c) T[c] = (2.25 * thr[c]) * thr[c];
+    for (auto& s : inliers) s.clear();
+    for (size_t c = 0; c < K; ++c) {
+        const Features& f = *data[c];
+        for (size_t i = 0; i < f.n; ++i) {
+            const double r2 = solver.squaredResidual(c, f, i, m);
+            if (r2 <= T[c]) {
+                inliers[c].emplace_back(i);
+                score.inc_n(c);
+                score.inc_v(c, -r2);
+            }
+        }
+    }
+    const auto ss = solver.sampleSize();
+    for (size_t c = 0; c < K; ++c) {
+        const size_t ni = score.n[c];
+        if (ni < ss[c]) { score = Score<K>{}; break; }
+        const double normed = score.v[c] / T[c];
+        score.reset_v(c, normed + static_cast<double>(ni));
+    }
+    return score;
+}
+
+// -------------------------------------------------------------- GCRANSAC ----
+struct Settings {
+    double threshold[2] = {2.0, 2.0};
+    double spatial_coherence_weight = 0.14;
+    size_t min_iteration_number = 20, max_iteration_number = std::numeric_limits<size_t>::max();
+    size_t max_local_optimization_number = 10;
+    size_t min_iteration_number_before_lo = 20;
+    size_t max_unsuccessful_model_generations = 100;
+    size_t max_graph_cut_number = 10;
+    double confidence = 0.95;
+    bool do_local_optimization = true;
+    bool do_final_iterated_least_squares = true;
+    uint64_t seed = 0;
+    int sampler = SAMPLER_PHILOX;
+};
+
+struct Statistics {
+    size_t iteration_number = 0, local_optimization_number = 0, graph_cut_number = 0, slots = 0, hypotheses = 0;
+    double score = 0.0, seconds = 0.0;
+};
+
+template <class S>
+class GCRANSAC {
+public:
+    static constexpr size_t K = S::K;
+    Settings settings;
+    Statistics stats;
+    Inliers<K> final_inliers{};
+
+    void run(const Data<K>& data, const S& solver, Model& out_model) {
+        auto t0 = std::chrono::steady_clock::now();
+        double trunc[K], sq_trunc[K];
+        for (size_t c = 0; c < K; ++c) {
+            trunc[c] = 1.5 * settings.threshold[c];
+            sq_trunc[c] = trunc[c] * trunc[c];
+        }
+        stats = Statistics{};
+        const auto m = solver.sampleSize();
+        for (size_t c = 0; c < K; ++c) {
+            npts[c] = data[c]->n;
+            if (npts[c] < m[c]) throw std::runtime_error("Data set smaller than minimal sample size for corresponding data type");
+        }
+        log_probability = std::log(1.0 - settings.confidence);
+        std::array<size_t, K> ones;
+        ones.fill(1);
+        size_t max_iteration = getIterationNumber(ones, m);
+
+        Inliers<K> current_sample{};
+        bool do_lo = false;
+        size_t off = 0;
+        Model best_model;
+        Score<K> cur, best;
+        std::array<Inliers<K>, 2> tmp{};
+        Inliers<K> pool{};
+        for (size_t c = 0; c < K; ++c) for (size_t j = 0; j < npts[c]; ++j) pool[c].push_back(j);
+        std::vector<Model> models;
+
+        size_t slot = 0;
+        while (settings.min_iteration_number > stats.iteration_number ||
+               stats.iteration_number < std::min(max_iteration, settings.max_iteration_number)) {
+            do_lo = false;
+            ++stats.iteration_number;
+            models.resize(0);
+            size_t umg = 0;
+            uint32_t attempt = 0;
+            while (umg++ <= settings.max_unsuccessful_model_generations) {
+                const uint32_t a = attempt++;
+                bool ok = true;
+                for (size_t c = 0; c < K && ok; ++c) {
+                    if (settings.sampler == SAMPLER_PHILOX)
+                        ok = philox_subset(settings.seed, slot, a, 0, (uint32_t)c, npts[c], m[c], current_sample[c]);
+                    else
+                        ok = faithful_subset(pool[c], m[c], current_sample[c]);
+                }
+                if (!ok) continue;
+                if (!solver.isValidSample(data, current_sample)) continue;
+                if (solver.estimateModel(data, current_sample, models)) break;
+            }
+            stats.iteration_number += (umg - 1);
+            ++slot;
+
+            for (auto& model : models) {
+                cur = getScore(solver, data, model, settings.threshold, tmp[off]);
+                ++stats.hypotheses;
+                if (best < cur && solver.isValidModel(model)) {
+                    off = 1 - off;
+                    best_model = model;
+                    best = cur;
+                    bool nonmin = false;
+                    for (size_t c = 0; c < K; ++c) if (best.n[c] > m[c]) { nonmin = true; break; }
+                    const bool enough = stats.iteration_number > settings.min_iteration_number_before_lo;
+                    do_lo = enough && nonmin;
+                    max_iteration = getIterationNumber(best.n, m);
+                }
+            }
+            if (settings.do_local_optimization && do_lo) {
+                ++stats.local_optimization_number;
+                localOptimization(data, solver, tmp[off], best_model, best, sq_trunc);
+                max_iteration = getIterationNumber(best.n, m);
+            }
+        }
+        stats.slots = slot;
+
+        bool minimal = true;
+        for (size_t c = 0; c < K; ++c) if (best.n[c] > m[c]) minimal = false;
+        if (minimal) {
+            stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            return;   // out_model untouched, no inliers
+        }
+        if (settings.do_local_optimization && stats.local_optimization_number == 0) {
+            ++stats.local_optimization_number;
+            localOptimization(data, solver, tmp[off], best_model, best, sq_trunc);
+        }
+        bool diff = false;
+        for (size_t c = 0; c < K; ++c) if (tmp[off][c].size() != best.n[c]) { diff = true; break; }
+        if (diff) off = 1 - off;
+        diff = false;
+        for (size_t c = 0; c < K; ++c) if (tmp[off][c].size() != best.n[c]) { diff = true; break; }
+        if (diff) best = getScore(solver, data, best_model, settings.threshold, tmp[off]);
+
+        // iteratedLeastSquaresFitting is dead code in the reference (models by value,
+        // GCRANSAC.h:1092-1098) and always returns false: single final refit.
+        models.clear();
+        solver.estimateModelNonminimal(data, tmp[off], models);
+        for (auto& model : models) {
+            const size_t idx = 1 - off;
+            for (auto& s : tmp[idx]) s.clear();
+            cur = getScore(solver, data, model, settings.threshold, tmp[idx]);
+            if (best < cur) { best_model = model; off = idx; }
+        }
+        final_inliers.swap(tmp[off]);
+        stats.score = best.value();
+        out_model = best_model;
+        stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+
+private:
+    std::array<size_t, K> npts{};
+    double log_probability = 0;
+
+    size_t getIterationNumber(const std::array<size_t, K>& in, const std::array<size_t, K>& ss) const {
+        double q = 1.0;
+        for (size_t c = 0; c < K; ++c) {
+            const double ratio = static_cast<double>(in[c]) / static_cast<double>(npts[c]);
+            q *= std::pow(ratio, static_cast<double>(ss[c]));
+        }
+        const double lg = std::log(1 - q);
+        if (std::fabs(lg) < std::numeric_limits<double>::epsilon()) return std::numeric_limits<size_t>::max();
+        return static_cast<size_t>(std::ceil(log_probability / lg));
+    }
+
+    // labeling(): BK max-flow on the empty neighbourhood graph (no pairwise
+    // terms): node i ends in SINK iff its terminal residual capacity is < 0.
+    void labeling1(const Data<K>& data, const S& solver, const Model& model, double lambda, double sqt,
+                   std::vector<size_t>& inliers) const {
+        const Features& f = *data[0];
+        const double oml = 1.0 - lambda;
+        for (size_t i = 0; i < f.n; ++i) {
+            const double r2 = solver.squaredResidual(0, f, i, model);
+            const double q = std::clamp(r2 / sqt, 0.0, 1.0);
+            const double energy = 1.0 - q;
+            double tr;
+            if (r2 <= sqt) tr = 0.0 - oml * energy;          // add_term1(i, A, 0) -> tweights(0, A)
+            else tr = oml * (1.0 - energy) - 0.0;             // add_term1(i, 0, B) -> tweights(B, 0)
+            if (tr < 0) inliers.push_back(i);
+        }
+    }
+
+    bool localOptimization(const Data<K>& data, const S& solver, Inliers<K>& sfb_inliers, Model& sfb_model,
+                           Score<K>& sfb_score, const double* sq_trunc) {
+        std::array<size_t, K> limit;
+        const auto m = solver.sampleSize();
+        for (size_t c = 0; c < K; ++c) limit[c] = 7 * m[c];
+        Score<K> max_score = sfb_score;
+        Model best_model = sfb_model;
+        std::vector<Model> models;
+        Inliers<K> best_inliers{}, inliers{}, tmp_inl{}, sample{};
+        std::array<size_t, K> ssz{};
+        ++stats.local_optimization_number;
+        bool updated = false;
+        while (++stats.graph_cut_number < settings.max_graph_cut_number) {
+            updated = false;
+            for (size_t c = 0; c < K; ++c) inliers[c].clear();
+            if constexpr (K > 1) {
+                for (size_t c = 0; c < K; ++c) {
+                    const Features& f = *data[c];
+                    for (size_t i = 0; i < f.n; ++i)
+                        if (solver.squaredResidual(c, f, i, best_model) <= sq_trunc[c]) inliers[c].push_back(i);
+                    ssz[c] = inliers[c].size();
+                }
+            } else {
+                labeling1(data, solver, best_model, settings.spatial_coherence_weight, sq_trunc[0], inliers[0]);
+                ssz[0] = inliers[0].size();
+            }
+            for (size_t c = 0; c < K; ++c) ssz[c] = std::min(limit[c], ssz[c]);
+            const uint64_t round_id = stats.graph_cut_number;
+            for (size_t trial = 0; trial < settings.max_local_optimization_number; ++trial) {
+                models.clear();
+                bool ok = true;
+                for (size_t c = 0; c < K; ++c) {
+                    if (ssz[c] < inliers[c].size()) {
+                        bool s_ok;
+                        if (settings.sampler == SAMPLER_PHILOX) {
+                            std::vector<size_t> pos;
+                            s_ok = philox_subset(settings.seed, round_id, (uint32_t)trial, 1, (uint32_t)c,
+                                                 inliers[c].size(), ssz[c], pos);
+                            sample[c].clear();
+                            for (size_t p : pos) sample[c].push_back(inliers[c][p]);
+                        } else {
+                            s_ok = faithful_subset(inliers[c], ssz[c], sample[c]);
+                        }
+                        if (!s_ok) { ok = false; break; }
+                    } else if (m[c] < inliers[c].size()) {
+                        sample[c] = inliers[c];
+                    } else {
+                        ok = false;
+                        break;
+                    }
+                }
+                if (!ok) break;
+                if (!solver.estimateModelNonminimal(data, sample, models)) continue;
+                for (auto& model : models) {
+                    for (auto& s : tmp_inl) s.clear();
+                    Score<K> sc = getScore(solver, data, model, settings.threshold, tmp_inl);
+                    if (max_score < sc) {
+                        updated = true;
+                        max_score = sc;
+                        best_model = model;
+                        best_inliers.swap(tmp_inl);
+                    }
+                }
+            }
+            if (!updated) break;
+        }
+        if (sfb_score < max_score) {
+            sfb_score = max_score;
+            sfb_model = best_model;
+            sfb_inliers.swap(best_inliers);
+            return true;
+        }
+        return false;
+    }
+};
+
+}  // namespace oracle
+
+// ============================================================== C API ====
+using namespace oracle;
+
+struct oracle_params {
+    double thr0, thr1, spatial_coherence_weight;
+    uint64_t min_iteration_number, max_iteration_number, max_local_optimization_number;
+    double confidence;
+    uint64_t seed;
+    int32_t math_mode;   // 0 glibc, 1 twin
+    int32_t sampler;     // 0 philox, 1 faithful
+};
+
+struct oracle_stats {
+    uint64_t iteration_number, local_optimization_number, graph_cut_number, slots, hypotheses;
+    double score, seconds;
+};
+
+static Features make_features(const double* p, size_t n) {
+    Features f;
+    f.n = n;
+    f.d.assign(p, p + n * 3);
+    return f;
+}
+
+static void fill_model(const Model& m, double* out7) {
+    out7[0] = m.x0; out7[1] = m.y0; out7[2] = m.s; out7[3] = m.h7; out7[4] = m.h8; out7[5] = m.alpha; out7[6] = m.phi;
+}
+static Model read_model(const double* m7) {
+    Model m;
+    m.x0 = m7[0]; m.y0 = m7[1]; m.s = m7[2]; m.h7 = m7[3]; m.h8 = m7[4]; m.alpha = m7[5]; m.phi = m7[6];
+    return m;
+}
+
+template <int KIND>
+static int run_generic(const Data<Solver<KIND>::K>& data, const oracle_params* p, uint8_t** masks, double* H9,
+                       double* model7, oracle_stats* st) {
+    g_math = p->math_mode;
+    GCRANSAC<Solver<KIND>> g;
+    g.settings.threshold[0] = p->thr0;
+    g.settings.threshold[1] = p->thr1;
+    g.settings.spatial_coherence_weight = p->spatial_coherence_weight;
+    g.settings.min_iteration_number = p->min_iteration_number;
+    g.settings.max_iteration_number = p->max_iteration_number;
+    g.settings.max_local_optimization_number = p->max_local_optimization_number;
+    g.settings.confidence = p->confidence;
+    g.settings.seed = p->seed;
+    g.settings.sampler = p->sampler;
+    Solver<KIND> solver;
+    Model model;
+    try {
+        g.run(data, solver, model);
+    } catch (const std::exception& e) {
+        fprintf(stderr, "oracle: %s\n", e.what());
+        return -1;
+    }
+    double H[9];
+    model.getHomography(H);
+    std::memcpy(H9, H, sizeof(H));
+    fill_model(model, model7);
+    size_t total = 0;
+    for (size_t c = 0; c < Solver<KIND>::K; ++c) {
+        std::memset(masks[c], 0, data[c]->n);
+        for (size_t i : g.final_inliers[c]) masks[c][i] = 1;
+        total += g.final_inliers[c].size();
+    }
+    if (st) {
+        st->iteration_number = g.stats.iteration_number;
+        st->local_optimization_number = g.stats.local_optimization_number;
+        st->graph_cut_number = g.stats.graph_cut_number;
+        st->slots = g.stats.slots;
+        st->hypotheses = g.stats.hypotheses;
+        st->score = g.stats.score;
+        st->seconds = g.stats.seconds;
+    }
+    return (int)total;
+}
+
+extern "C" {
+
+int oracle_rect_scale_only(const double* feat, size_t n, const oracle_params* p, int original, uint8_t* mask,
+                           double* H9, double* model7, oracle_stats* st) {
+    Features f = make_features(feat, n);
+    uint8_t* masks[1] = {mask};
+    if (original) return run_generic<1>({&f}, p, masks, H9, model7, st);
+    return run_generic<0>({&f}, p, masks, H9, model7, st);
+}
+
+int oracle_rect_sift(const double* sfeat, size_t ns, const double* ofeat, size_t no, const oracle_params* p,
+                     uint8_t* smask, uint8_t* omask, double* H9, double* model7, oracle_stats* st) {
+    Features a = make_features(sfeat, ns), b = make_features(ofeat, no);
+    uint8_t* masks[2] = {smask, omask};
+    return run_generic<2>({&a, &b}, p, masks, H9, model7, st);
+}
+
+// ---- fine-grained hooks used by the parity tests -------------------------
+// One main-loop slot: returns inc (1..101 on success at that attempt, 102 if
+// every attempt failed), writes the model when valid.
+int oracle_slot(int kind, const double* f0, size_t n0, const double* f1, size_t n1, uint64_t seed, uint64_t slot,
+                int math_mode, double* model7) {
+    g_math = math_mode;
+    Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
+    auto go = [&](auto solver, auto data) -> int {
+        constexpr size_t K = decltype(solver)::K;
+        Inliers<K> smp{};
+        std::vector<Model> models;
+        const auto m = solver.sampleSize();
+        size_t umg = 0;
+        uint32_t attempt = 0;
+        while (umg++ <= 100) {
+            const uint32_t at = attempt++;
+            bool ok = true;
+            for (size_t c = 0; c < K && ok; ++c) ok = philox_subset(seed, slot, at, 0, (uint32_t)c, data[c]->n, m[c], smp[c]);
+            if (!ok) continue;
+            if (!solver.isValidSample(data, smp)) continue;
+            if (solver.estimateModel(data, smp, models)) break;
+        }
+        if (!models.empty()) fill_model(models[0], model7);
+        return (int)umg;   // == inc
+    };
+    if (kind == 0) return go(Solver<0>{}, Data<1>{&a});
+    if (kind == 1) return go(Solver<1>{}, Data<1>{&a});
+    return go(Solver<2>{}, Data<2>{&a, &b});
+}
+
+// MSAC score of one model: writes counts, per-class values and the total
+int oracle_score(int kind, const double* f0, size_t n0, const double* f1, size_t n1, const double* model7,
+                 double thr0, double thr1, int math_mode, uint64_t* counts, double* values, double* value,
+                 uint8_t* mask0, uint8_t* mask1) {
+    g_math = math_mode;
+    Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
+    Model m = read_model(model7);
+    const double thr[2] = {thr0, thr1};
+    auto go = [&](auto solver, auto data) {
+        constexpr size_t K = decltype(solver)::K;
+        Inliers<K> in{};
+        auto s = getScore(solver, data, m, thr, in);
+        for (size_t c = 0; c < K; ++c) { counts[c] = s.n[c]; values[c] = s.v[c]; }
+        *value = s.value();
+        uint8_t* mk[2] = {mask0, mask1};
+        for (size_t c = 0; c < K; ++c)
+            if (mk[c]) { std::memset(mk[c], 0, data[c]->n); for (size_t i : in[c]) mk[c][i] = 1; }
+    };
+    if (kind == 0) go(Solver<0>{}, Data<1>{&a});
+    else if (kind == 1) go(Solver<1>{}, Data<1>{&a});
+    else go(Solver<2>{}, Data<2>{&a, &b});
+    return 0;
+}
+
+// per-feature squared residuals of one model
+int oracle_residuals(int kind, int cls, const double* f, size_t n, const double* model7, int math_mode, double* r2) {
+    g_math = math_mode;
+    Features a = make_features(f, n);
+    Model m = read_model(model7);
+    for (size_t i = 0; i < n; ++i) {
+        if (kind == 1) r2[i] = Solver<1>{}.squaredResidual(0, a, i, m);
+        else if (kind == 0) r2[i] = Solver<0>{}.squaredResidual(0, a, i, m);
+        else r2[i] = Solver<2>{}.squaredResidual((size_t)cls, a, i, m);
+    }
+    return 0;
+}
+
+int oracle_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls, uint64_t n, uint32_t m,
+                  uint64_t* out) {
+    std::vector<size_t> v;
+    if (!philox_subset(seed, index, sub, stream, cls, n, m, v)) return -1;
+    for (size_t i = 0; i < v.size(); ++i) out[i] = v[i];
+    return 0;
+}
+
+void oracle_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+    uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]}, k[2] = {key[0], key[1]};
+    philox10(c, k, out);
+}
+
+// non-minimal fit over explicit index lists (LO / final refit path)
+int oracle_fit_nonminimal(int kind, const double* f0, size_t n0, const double* f1, size_t n1, const uint64_t* i0,
+                          size_t k0, const uint64_t* i1, size_t k1, int math_mode, double* model7) {
+    g_math = math_mode;
+    Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
+    auto go = [&](auto solver, auto data) -> int {
+        constexpr size_t K = decltype(solver)::K;
+        Inliers<K> in{};
+        in[0].assign(i0, i0 + k0);
+        if constexpr (K == 2) in[1].assign(i1, i1 + k1);
+        std::vector<Model> models;
+        if (!solver.estimateModelNonminimal(data, in, models) || models.empty()) return 0;
+        fill_model(models[0], model7);
+        return 1;
+    };
+    if (kind == 0) return go(Solver<0>{}, Data<1>{&a});
+    if (kind == 1) return go(Solver<1>{}, Data<1>{&a});
+    return go(Solver<2>{}, Data<2>{&a, &b});
+}
+
+
+// CPU baseline of the hot path: sample + validity + minimal solve + MSAC score
+// for `nslots` outer-iteration slots (no replay/LO/refit), single thread.
+// sampler: 0 Philox, 1 faithful (random_device + mt19937 + full shuffle, the
+// reference's per-sample cost).  Returns models scored; *seconds = wall time.
+int64_t oracle_hot_batch(int kind, const double* f0, size_t n0, const double* f1, size_t n1, double thr0, double thr1,
+                         uint64_t seed, uint64_t slot0, uint64_t nslots, int sampler, int math_mode, double* seconds,
+                         double* best_value) {
+    g_math = math_mode;
+    Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
+    const double thr[2] = {thr0, thr1};
+    auto go = [&](auto solver, auto data) -> int64_t {
+        constexpr size_t K = decltype(solver)::K;
+        Inliers<K> smp{}, pool{}, inl{};
+        for (size_t c = 0; c < K; ++c) for (size_t j = 0; j < data[c]->n; ++j) pool[c].push_back(j);
+        std::vector<Model> models;
+        const auto m = solver.sampleSize();
+        int64_t scored = 0;
+        Score<K> best{};
+        auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t s = slot0; s < slot0 + nslots; ++s) {
+            models.clear();
+            size_t umg = 0;
+            uint32_t attempt = 0;
+            while (umg++ <= 100) {
+                const uint32_t at = attempt++;
+                bool ok = true;
+                for (size_t c = 0; c < K && ok; ++c) {
+                    if (sampler == SAMPLER_PHILOX) ok = philox_subset(seed, s, at, 0, (uint32_t)c, data[c]->n, m[c], smp[c]);
+                    else ok = faithful_subset(pool[c], m[c], smp[c]);
+                }
+                if (!ok) continue;
+                if (!solver.isValidSample(data, smp)) continue;
+                if (solver.estimateModel(data, smp, models)) break;
+            }
+            for (auto& model : models) {
+                auto sc = getScore(solver, data, model, thr, inl);
+                ++scored;
+                if (best < sc && solver.isValidModel(model)) best = sc;
+            }
+        }
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        *best_value = best.value();
+        return scored;
+    };
+    if (kind == 0) return go(Solver<0>{}, Data<1>{&a});
+    if (kind == 1) return go(Solver<1>{}, Data<1>{&a});
+    return go(Solver<2>{}, Data<2>{&a, &b});
+}
+
+// ---- math_utils / model known-answer hooks (tests/unit_tests.cpp ports) ---
+double oracle_clip_angle(double a) { return clipAngle(a); }
+double oracle_min_angle_diff(double a, double b) { return minAngleDiff(a, b); }
+double oracle_lines_angles_diff(double a, double b) { return linesAnglesDiff(a, b); }
+double oracle_deg2rad(double a) { return deg2rad(a); }
+double oracle_rad2deg(double a) { return rad2deg(a); }
+uint64_t oracle_nchoose2(uint64_t n) { return nChoose2(n); }
+int oracle_are_collinear(double x1, double y1, double x2, double y2, double x3, double y3, double tol) {
+    return areCollinear(x1, y1, x2, y2, x3, y3, tol) ? 1 : 0;
+}
+void oracle_line_from_point_angle(double x, double y, double t, double* l3) {
+    V3 l = lineFromPointAndAngle(x, y, t);
+    l3[0] = l[0]; l3[1] = l[1]; l3[2] = l[2];
+}
+// hull of n points (xy interleaved); returns vertex count, vertices into out
+int oracle_convex_hull(const double* xy, size_t n, double* out) {
+    std::vector<Point2D> pts(n);
+    for (size_t i = 0; i < n; ++i) pts[i] = Point2D{xy[2 * i], xy[2 * i + 1]};
+    auto h = computeConvexHull(pts);
+    for (size_t i = 0; i < h.size(); ++i) { out[2 * i] = h[i].x; out[2 * i + 1] = h[i].y; }
+    return (int)h.size();
+}
+int oracle_point_in_polygon(double px, double py, const double* xy, size_t n) {
+    std::vector<Point2D> poly(n);
+    for (size_t i = 0; i < n; ++i) poly[i] = Point2D{xy[2 * i], xy[2 * i + 1]};
+    return pointInConvexPolygon(Point2D{px, py}, poly) ? 1 : 0;
+}
+// model methods: op 0 rectifiedScale, 1 unrectifiedScale, 2 rectifiedAngle, 3 unrectifiedAngle
+double oracle_model_op(const double* model7, int op, double x, double y, double v, int math_mode) {
+    g_math = math_mode;
+    Model m = read_model(model7);
+    switch (op) {
+        case 0: return m.rectifiedScale(x, y, v);
+        case 1: return m.unrectifiedScale(x, y, v);
+        case 2: return m.rectifiedAngle(x, y, v);
+        default: return m.unrectifiedAngle(x, y, v);
+    }
+}
+void oracle_model_point(const double* model7, int rectify, double x, double y, double* out2) {
+    Model m = read_model(model7);
+    if (rectify) m.rectifyPoint(x, y); else m.unrectifyPoint(x, y);
+    out2[0] = x; out2[1] = y;
+}
+void oracle_get_homography(const double* model7, double* H9) { read_model(model7).getHomography(H9); }
+int oracle_gauss3(const double* m12, double* out3) {
+    double m[3][4];
+    for (int i = 0; i < 3; ++i) for (int j = 0; j < 4; ++j) m[i][j] = m12[i * 4 + j];
+    gaussElimination3(m, out3);
+    return 0;
+}
+int oracle_lstsq3(const double* A_rowmajor, size_t m, const double* b, double* x) {
+    std::vector<double> A(m * 3), bb(b, b + m);
+    for (size_t i = 0; i < m; ++i) for (size_t j = 0; j < 3; ++j) A[j * m + i] = A_rowmajor[i * 3 + j];
+    return colpiv_qr_solve3(A, m, bb, x) ? 0 : -1;
+}
+double oracle_weighted_mode(const double* angles, const double* weights, size_t n, double bw) {
+    std::vector<double> a(angles, angles + n), w(weights, weights + n);
+    return Solver<2>::findWeightedMode(a, w, bw);
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+"""Helpers shared by the parity tests: device-resident problems through the C
+ABI and an exact restatement of Score finalisation for raw GPU accumulators."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from pygcransac import _native as N
+
+KINDS = (N.SOLVER_SCALE3, N.SOLVER_SCALE3_ORIGINAL, N.SOLVER_SIFT22)
+
+
+def dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Problem:
+    def __init__(self, kind, f0, f1=None, device=0):
+        self.kind = kind
+        self.f0 = np.ascontiguousarray(f0, dtype=np.float64)
+        self.f1 = None if f1 is None else np.ascontiguousarray(f1, dtype=np.float64)
+        self.ctx = N.context(device)
+        h = C.c_void_p()
+        rc = N.lib.gcr_problem_create(self.ctx, kind, dp(self.f0), self.f0.shape[0],
+                                      dp(self.f1) if self.f1 is not None else None,
+                                      0 if self.f1 is None else self.f1.shape[0], C.byref(h))
+        N.check(rc)
+        self.h = h.value
+
+    def close(self):
+        if self.h:
+            N.lib.gcr_problem_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def generate(self, seed, slot0, nslots):
+        inc = np.zeros(nslots, dtype=np.uint8)
+        models = (N.RectModel * nslots)()
+        N.check(N.lib.gcr_debug_generate(self.h, seed, slot0, nslots, inc.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                         models))
+        arr = np.array([[m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi] for m in models])
+        return inc, arr
+
+    def score_raw(self, models7, thr0, thr1=0.0):
+        n = len(models7)
+        ms = (N.RectModel * n)(*[N.RectModel(*map(float, m)) for m in models7])
+        p = N.default_params()
+        p.scale_residual_thresh = thr0
+        p.orientation_residual_thresh = thr1
+        n0 = np.zeros(n, dtype=np.uint32)
+        n1 = np.zeros(n, dtype=np.uint32)
+        v0, v1, tot = np.zeros(n), np.zeros(n), np.zeros(n)
+        u32 = C.POINTER(C.c_uint32)
+        N.check(N.lib.gcr_debug_score(self.h, C.byref(p), ms, n, n0.ctypes.data_as(u32), n1.ctypes.data_as(u32),
+                                      dp(v0), dp(v1), dp(tot)))
+        return n0, n1, v0, v1, tot
+
+    def mask(self, model7, cls, rule, thr0, thr1=0.0, lam=0.0):
+        p = N.default_params()
+        p.scale_residual_thresh = thr0
+        p.orientation_residual_thresh = thr1
+        p.spatial_coherence_weight = lam
+        n = (self.f0 if cls == 0 else self.f1).shape[0]
+        out = np.zeros(n, dtype=np.uint8)
+        m = N.RectModel(*map(float, model7))
+        N.check(N.lib.gcr_debug_mask(self.h, C.byref(p), C.byref(m), cls, rule,
+                                     out.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return out.astype(bool)
+
+
+def finish_score(kind, n0, n1, v0, v1, tot, thr0, thr1):
+    """MSACScoringFunction::getScore post-processing (MSAC_scoring_function.hpp:108-127)."""
+    K = 2 if kind == N.SOLVER_SIFT22 else 1
+    m = (2, 2) if K == 2 else (3,)
+    T = [(2.25 * thr0) * thr0, (2.25 * thr1) * thr1]
+    n = [int(n0), int(n1)]
+    v = [float(v0), float(v1)]
+    s = float(tot)
+    for c in range(K):
+        if n[c] < m[c]:
+            return dict(counts=[0, 0], values=[0.0, 0.0], value=0.0)
+        nv = v[c] / T[c] + float(n[c])
+        s -= v[c]
+        v[c] = nv
+        s += nv
+    if K == 1:
+        n[1], v[1] = 0, 0.0
+    return dict(counts=n, values=v, value=s)
+
+
+def bits(x):
+    return np.asarray(x, dtype=np.float64).view(np.uint64)

@@ -1,0 +1,271 @@
+"""GPU <-> oracle parity (run on an MI355X: pytest -m gpu).
+
+The oracle runs in TWIN math mode (its three hypothesis-dependent libm calls
+use detmath, everything else is its own restatement), so every comparison
+here is BITWISE: Philox samples, attempt counts, minimal-solver models, MSAC
+counts and running sums, inlier masks, final models, H and run statistics.
+The oracle's glibc mode is tied to twin mode separately (test_oracle_modes.py).
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import pygcransac
+from gcr_testutil import KINDS, Problem, bits, finish_score
+from pygcransac import _native as N
+from pygcransac import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if N.lib.gcr_device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    N.context(0)
+
+
+def _problem_data(kind, n, seed):
+    if kind == N.SOLVER_SIFT22:
+        fs, fo, ts, to, thr_s, thr_o = S.problem_m2(n, n, seed=seed)
+        return fs, fo, thr_s, thr_o
+    f, t, thr = S.problem_m1(n, seed=seed)
+    return f, None, thr, 0.0
+
+
+# ----------------------------------------------------------------- math ----
+def _dev_math(op, a, b=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    out = np.zeros_like(a)
+    dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    N.check(N.lib.gcr_debug_math(N.context(0), op, dp(a), dp(b) if b is not None else None, a.size, dp(out)))
+    return out
+
+
+def test_device_math_matches_host_bitwise():
+    rng = np.random.default_rng(3)
+    x = np.concatenate([np.exp(rng.uniform(-30, 30, 20000)), rng.uniform(0.5, 1.5, 20000),
+                        [0.0, -0.0, -1.0, np.inf, np.nan, 5e-324, 1e-310, 1.0, 2.0]])
+    got = _dev_math(0, x)
+    exp = np.array([N.lib.gcr_host_log(v) for v in x])
+    assert np.array_equal(bits(got), bits(exp))
+    t = np.concatenate([rng.uniform(-2, 2, 20000), 10.0 ** rng.uniform(-320, 320, 2000),
+                        [0.0, -0.0, np.inf, -np.inf, np.nan]])
+    got = _dev_math(1, t)
+    exp = np.array([N.lib.gcr_host_pow_m3(v) for v in t])
+    assert np.array_equal(bits(got), bits(exp))
+    y = rng.normal(size=20000) * 10.0 ** rng.uniform(-5, 5, 20000)
+    xx = rng.normal(size=20000) * 10.0 ** rng.uniform(-5, 5, 20000)
+    y = np.concatenate([y, [0.0, -0.0, 0.0, -0.0, 1.0, np.inf, -np.inf, np.nan]])
+    xx = np.concatenate([xx, [1.0, 1.0, -1.0, -1.0, 0.0, np.inf, -np.inf, 1.0]])
+    got = _dev_math(2, y, xx)
+    exp = np.array([N.lib.gcr_host_atan2(a, b) for a, b in zip(y, xx)])
+    assert np.array_equal(bits(got), bits(exp))
+
+
+def test_device_division_and_sqrt_are_ieee():
+    rng = np.random.default_rng(4)
+    a = rng.normal(size=50000) * 10.0 ** rng.uniform(-100, 100, 50000)
+    b = rng.normal(size=50000) * 10.0 ** rng.uniform(-100, 100, 50000)
+    assert np.array_equal(bits(_dev_math(3, a, b)), bits(a / b))
+    s = np.abs(a)
+    assert np.array_equal(bits(_dev_math(4, s)), bits(np.sqrt(s)))
+
+
+# -------------------------------------------------------------- sampler ----
+def test_sampler_matches_oracle():
+    for (seed, idx, sub, stream, cls, n, m) in [(0, 0, 0, 0, 0, 10, 3), (20251121, 123456789012, 7, 0, 1, 5000, 2),
+                                                 (2 ** 63 + 5, 3, 49, 1, 0, 4321, 21), (9, 1, 2, 1, 1, 15, 14)]:
+        out = (C.c_uint32 * m)()
+        N.check(N.lib.gcr_host_sample(seed, idx, sub, stream, cls, n, m, out))
+        assert list(out) == list(O.sample(seed, idx, sub, stream, cls, n, m))
+
+
+# ------------------------------------------------------- generate kernel ----
+@pytest.mark.parametrize("kind", KINDS)
+def test_generate_kernel_matches_oracle_slots(kind):
+    f0, f1, thr0, thr1 = _problem_data(kind, 400, seed=11 + kind)
+    prob = Problem(kind, f0, f1)
+    seed = 977
+    inc, models = prob.generate(seed, 1000, 512)
+    for s in range(512):
+        oinc, om = O.slot(kind, f0, f1, seed, 1000 + s)
+        assert int(inc[s]) == oinc, f"slot {s}"
+        if oinc <= 101:
+            assert np.array_equal(bits(models[s]), bits(om)), f"slot {s}"
+    assert (inc <= 101).mean() > 0.9
+
+
+# ---------------------------------------------------------- score kernel ----
+@pytest.mark.parametrize("kind", KINDS)
+def test_score_kernel_matches_oracle_bitwise(kind):
+    f0, f1, thr0, thr1 = _problem_data(kind, 1500, seed=21 + kind)
+    prob = Problem(kind, f0, f1)
+    inc, models = prob.generate(5, 0, 256)
+    models = models[inc <= 101][:128]
+    n0, n1, v0, v1, tot = prob.score_raw(models, thr0, thr1)
+    for i, m in enumerate(models):
+        ref = O.score(kind, f0, f1, m, thr0, thr1)
+        got = finish_score(kind, n0[i], n1[i], v0[i], v1[i], tot[i], thr0, thr1)
+        assert got["counts"] == [int(c) for c in ref["counts"]]
+        assert np.array_equal(bits(got["values"]), bits(ref["values"]))
+        assert bits(got["value"]) == bits(ref["value"])
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_mask_kernel_matches_oracle(kind):
+    f0, f1, thr0, thr1 = _problem_data(kind, 800, seed=31 + kind)
+    prob = Problem(kind, f0, f1)
+    inc, models = prob.generate(8, 0, 64)
+    for m in models[inc <= 101][:16]:
+        ref = O.score(kind, f0, f1, m, thr0, thr1, want_masks=True)["masks"]
+        assert np.array_equal(prob.mask(m, 0, 0, thr0, thr1), ref[0])
+        if f1 is not None:
+            assert np.array_equal(prob.mask(m, 1, 0, thr0, thr1), ref[1])
+        # LO threshold rule (1.5 thr)^2 against the oracle's residuals
+        r2 = O.residuals(kind, 0, f0, m)
+        t = 1.5 * thr0
+        assert np.array_equal(prob.mask(m, 0, 1, thr0, thr1), r2 <= t * t)
+
+
+# ------------------------------------------------------------ end to end ----
+def _run_product(kind, f0, f1, thr0, thr1, **kw):
+    kw = dict(kw)
+    kw["return_stats"] = True
+    if kind == N.SOLVER_SIFT22:
+        pos = {k: kw.pop(k) for k in ("spatial_coherence_weight", "min_iteration_number", "max_iteration_number",
+                                      "max_local_optimization_number") if k in kw}
+        r = pygcransac.findRectifyingHomographySIFT(f0, f1, thr0, thr1, **pos, **kw)
+        H, ms, mo, model, st = r
+        return H, (ms, mo), model, st
+    fn = (pygcransac.findRectifyingHomographyScaleOnly if kind == N.SOLVER_SCALE3
+          else pygcransac.findRectifyingHomographyScaleOnlyOriginal)
+    r = fn(f0, thr0, **kw)
+    if r[0] is None:
+        return None, (r[1],), None, r[2]
+    H, m, model, st = r
+    return H, (m,), model, st
+
+
+def _run_oracle(kind, f0, f1, thr0, thr1, seed=0, spatial_coherence_weight=0.0, min_iteration_number=10000,
+                max_iteration_number=10000, max_local_optimization_number=50, confidence=0.95, **_):
+    kw = dict(lam=spatial_coherence_weight, min_it=min_iteration_number, max_it=max_iteration_number,
+              lo=max_local_optimization_number, confidence=confidence, seed=seed, math_mode=O.MATH_TWIN)
+    if kind == N.SOLVER_SIFT22:
+        r = O.rect_sift(f0, f1, thr0, thr1, **kw)
+        return r, (r["scale_mask"], r["orientation_mask"])
+    r = O.rect_scale_only(f0, thr0, original=(kind == N.SOLVER_SCALE3_ORIGINAL), **kw)
+    return r, (r["mask"],)
+
+
+def _assert_same(kind, f0, f1, thr0, thr1, **kw):
+    H, masks, model, st = _run_product(kind, f0, f1, thr0, thr1, **kw)
+    ref, rmasks = _run_oracle(kind, f0, f1, thr0, thr1, **kw)
+    for a, b in zip(masks, rmasks):
+        assert np.array_equal(a, b)
+    rs = ref["stats"]
+    assert st["iteration_number"] == rs["iteration_number"]
+    assert st["local_optimization_number"] == rs["local_optimization_number"]
+    assert st["graph_cut_number"] == rs["graph_cut_number"]
+    assert st["slots"] == rs["slots"]
+    assert st["hypotheses"] == rs["hypotheses"]
+    assert bits(st["score"]) == bits(rs["score"])
+    if ref["num_inliers"] == 0:
+        assert H is None and model is None
+        return st
+    m = ref["model"]
+    got = [model.x0, model.y0, model.s, model.h7, model.h8, model.alpha]
+    exp = [m["x0"], m["y0"], m["s"], m["h7"], m["h8"], m["alpha"]]
+    if kind == N.SOLVER_SIFT22:
+        got.append(model.phi)
+        exp.append(m["phi"])
+    assert np.array_equal(bits(got), bits(exp))
+    assert np.array_equal(bits(H), bits(ref["H"]))
+    return st
+
+
+@pytest.mark.parametrize("kind,n,seed", [
+    (N.SOLVER_SCALE3, 50, 1), (N.SOLVER_SCALE3, 500, 2), (N.SOLVER_SCALE3, 2000, 3),
+    (N.SOLVER_SCALE3_ORIGINAL, 500, 4), (N.SOLVER_SCALE3_ORIGINAL, 2000, 5),
+    (N.SOLVER_SIFT22, 60, 6), (N.SOLVER_SIFT22, 500, 7), (N.SOLVER_SIFT22, 1500, 8),
+])
+def test_end_to_end_matches_oracle(kind, n, seed):
+    f0, f1, thr0, thr1 = _problem_data(kind, n, seed=100 + seed)
+    _assert_same(kind, f0, f1, thr0, thr1, seed=seed)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_adaptive_termination_matches_oracle(kind):
+    f0, f1, thr0, thr1 = _problem_data(kind, 1000, seed=55 + kind)
+    st = _assert_same(kind, f0, f1, thr0, thr1, seed=3, min_iteration_number=0, max_iteration_number=1_000_000,
+                      confidence=0.99)
+    assert st["iteration_number"] < 10_000
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_results_independent_of_batch_size(kind):
+    f0, f1, thr0, thr1 = _problem_data(kind, 600, seed=77 + kind)
+    outs = []
+    for b in (1, 37, 4096):
+        H, masks, model, st = _run_product(kind, f0, f1, thr0, thr1, seed=9, batch_slots=b,
+                                           min_iteration_number=3000, max_iteration_number=3000)
+        outs.append((bits(H).tolist(), [m.tolist() for m in masks], st["iteration_number"], bits(st["score"])))
+    assert outs[0] == outs[1] == outs[2]
+
+
+def test_spatial_coherence_labeling_path_matches_oracle():
+    f0, f1, thr0, thr1 = _problem_data(N.SOLVER_SCALE3, 700, seed=5)
+    _assert_same(N.SOLVER_SCALE3, f0, f1, thr0, thr1, seed=2, spatial_coherence_weight=0.35)
+
+
+@pytest.mark.parametrize("lo", [0, 1, 5])
+def test_lo_trial_budget_matches_oracle(lo):
+    f0, f1, thr0, thr1 = _problem_data(N.SOLVER_SIFT22, 400, seed=9)
+    _assert_same(N.SOLVER_SIFT22, f0, f1, thr0, thr1, seed=4, max_local_optimization_number=lo)
+
+
+# ------------------------------------------------------------- edge cases ---
+def test_minimum_sizes_match_oracle():
+    rng = np.random.default_rng(0)
+    for seed in range(4):
+        f = np.column_stack([rng.uniform(0, 100, 3), rng.uniform(0, 100, 3), rng.uniform(1, 5, 3)])
+        _assert_same(N.SOLVER_SCALE3, f, None, 0.05, 0.0, seed=seed, min_iteration_number=200,
+                     max_iteration_number=200)
+        fs = np.column_stack([rng.uniform(0, 100, 2), rng.uniform(0, 100, 2), rng.uniform(1, 5, 2)])
+        fo = np.column_stack([rng.uniform(0, 100, 2), rng.uniform(0, 100, 2), rng.uniform(0, 6, 2)])
+        _assert_same(N.SOLVER_SIFT22, fs, fo, 0.05, 0.02, seed=seed, min_iteration_number=200,
+                     max_iteration_number=200)
+
+
+def test_pure_outliers_and_degenerate_inputs_match_oracle():
+    rng = np.random.default_rng(1)
+    f = np.column_stack([rng.uniform(0, 1368, 300), rng.uniform(0, 1824, 300), np.exp(rng.uniform(0, 4, 300))])
+    _assert_same(N.SOLVER_SCALE3, f, None, 0.01, 0.0, seed=1, min_iteration_number=500, max_iteration_number=500)
+    same = np.tile([[10.0, 20.0, 3.0]], (20, 1))          # every point identical
+    _assert_same(N.SOLVER_SCALE3, same, None, 0.05, 0.0, seed=1, min_iteration_number=300,
+                 max_iteration_number=300)
+    line = np.column_stack([np.arange(30.0), 2 * np.arange(30.0), np.full(30, 4.0)])   # collinear
+    _assert_same(N.SOLVER_SCALE3, line, None, 0.05, 0.0, seed=1, min_iteration_number=300,
+                 max_iteration_number=300)
+    bad = f.copy()
+    bad[::7, 2] = np.nan
+    bad[::11, 0] = np.inf
+    _assert_same(N.SOLVER_SCALE3, bad, None, 0.05, 0.0, seed=1, min_iteration_number=500,
+                 max_iteration_number=500)
+
+
+def test_full_size_m1_and_m2_match_oracle_and_ground_truth():
+    f, truth, thr = S.problem_m1(10_000)
+    H, masks, model, st = _run_product(N.SOLVER_SCALE3, f, None, thr, 0.0, seed=0)
+    gt = S.GroundTruth()
+    assert abs(model.h7 - gt.h7) < 2e-6 and abs(model.h8 - gt.h8) < 2e-6 and abs(model.alpha - gt.alpha) < 1e-3
+    assert (masks[0] == truth).mean() > 0.95
+    _assert_same(N.SOLVER_SCALE3, f, None, thr, 0.0, seed=0)
+    fs, fo, ts, to, a, b = S.problem_m2(5000, 5000)
+    H, masks, model, st = _run_product(N.SOLVER_SIFT22, fs, fo, a, b, seed=0)
+    assert abs(model.phi - gt.phi) < math.radians(0.5) or abs(model.phi - gt.phi - math.pi / 2) < math.radians(0.5)
+    _assert_same(N.SOLVER_SIFT22, fs, fo, a, b, seed=0)
