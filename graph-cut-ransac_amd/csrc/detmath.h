@@ -9,13 +9,13 @@
 // other arithmetic is IEEE +,-,*,/,sqrt, which both sides round identically.
 //
 //   dm_log      fdlibm e_log.c reduction and minimax polynomial (< 1 ulp),
-//               the two fdlibm tail formulas selected without branches.
+//               FMA Horner form, the two fdlibm tail formulas selected
+//               without branches, special operands out of line.
 //   dm_pow_m3   t^-3 via a double-double t^3 and one Newton correction of the
 //               IEEE reciprocal (nearly correctly rounded).
-//   dm_atan2    fdlibm e_atan2.c / s_atan.c; the five-way argument reduction
-//               of s_atan.c is rewritten as one (a*x+b)/(c*x+d) with selected
-//               coefficients, which is the same IEEE operation sequence as each
-//               fdlibm branch but runs without lane divergence.
+//   dm_atan2    fdlibm s_atan.c polynomial behind a branch-free two-step
+//               reduction (octant swap, then pi/4 shift) with a single IEEE
+//               division; special operands out of line (fdlibm e_atan2.c).
 //
 // The accuracy against glibc/mpmath is pinned by tests/test_detmath.py; the
 // oracle's "twin" mode uses these same three functions so GPU-vs-oracle
@@ -30,10 +30,18 @@ namespace dm {
 constexpr double cf(uint64_t u) { return __builtin_bit_cast(double, u); }
 
 // ------------------------------------------------------------------ log ----
-GCR_HD double dm_log(double x) {
-    constexpr double ln2_hi = cf(0x3fe62e42fee00000ull);
-    constexpr double ln2_lo = cf(0x3dea39ef35793c76ull);
-    constexpr double two54 = cf(0x4350000000000000ull);
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GCR_COLD __attribute__((noinline))
+#else
+#define GCR_COLD
+#endif
+
+constexpr double kLn2Hi = cf(0x3fe62e42fee00000ull);
+constexpr double kLn2Lo = cf(0x3dea39ef35793c76ull);
+
+// fdlibm reduction + minimax polynomial for a normal, finite, positive x
+// (k already includes any subnormal pre-scaling).
+GCR_HD double log_core(uint64_t u, int32_t k) {
     constexpr double Lg1 = cf(0x3fe5555555555593ull);
     constexpr double Lg2 = cf(0x3fd999999997fa04ull);
     constexpr double Lg3 = cf(0x3fd2492494229359ull);
@@ -41,56 +49,51 @@ GCR_HD double dm_log(double x) {
     constexpr double Lg5 = cf(0x3fc7466496cb03deull);
     constexpr double Lg6 = cf(0x3fc39a09d078c69full);
     constexpr double Lg7 = cf(0x3fc2f112df3e5244ull);
-
-    uint64_t u = as_u64(x);
     int32_t hx = (int32_t)(u >> 32);
-    uint32_t lx = (uint32_t)u;
-    int32_t k = 0;
-    if (hx < 0x00100000) {                       // x < 2^-1022 (incl. <= 0)
-        if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -HUGE_VAL;   // log(+-0)
-        if (hx < 0) return __builtin_nan("");       // log(<0) = NaN
-        k -= 54;
-        x *= two54;                              // subnormal: scale up
-        u = as_u64(x);
-        hx = (int32_t)(u >> 32);
-    }
-    if (hx >= 0x7ff00000) return x + x;          // +inf or NaN
     k += (hx >> 20) - 1023;
     hx &= 0x000fffff;
     const int32_t i = (hx + 0x95f64) & 0x100000;
     // normalise x (or x/2) into [sqrt(2)/2, sqrt(2))
-    x = as_f64(((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (uint64_t)(uint32_t)as_u64(x));
+    const double x = as_f64(((uint64_t)(uint32_t)(hx | (i ^ 0x3ff00000)) << 32) | (uint64_t)(uint32_t)u);
     k += (i >> 20);
     const double f = x - 1.0;
     const double dk = (double)k;
     const double s = f / (2.0 + f);
     const double z = s * s;
     const double w = z * z;
-    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const double t1 = w * fma_rn(w, fma_rn(w, Lg6, Lg4), Lg2);
+    const double t2 = z * fma_rn(w, fma_rn(w, fma_rn(w, Lg7, Lg5), Lg3), Lg1);
     const double R = t2 + t1;
     const int32_t sel = (hx - 0x6147a) | (0x6b851 - hx);
     const double hfsq = 0.5 * f * f;
-    const double ra = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
-    const double rb = dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+    const double ra = dk * kLn2Hi - ((hfsq - (s * (hfsq + R) + dk * kLn2Lo)) - f);
+    const double rb = dk * kLn2Hi - ((s * (f - R) - dk * kLn2Lo) - f);
     return sel > 0 ? ra : rb;
 }
 
-// --------------------------------------------------------------- t^-3 -----
-GCR_HD double pm3_core(double t) {
-    const double h = t * t;
-    const double l = fma_rn(t, t, -h);           // t^2 = h + l exactly
-    const double H = h * t;
-    const double L = fma_rn(h, t, -H) + l * t;   // t^3 ~= H + L
-    const double y = 1.0 / H;
-    double e = fma_rn(-y, H, 1.0);               // 1 - y*H (exact)
-    e = fma_rn(-y, L, e);                        // 1 - y*(H + L)
-    return fma_rn(y, e, y);
+GCR_COLD GCR_HD double log_special(double x) {
+    const uint64_t u = as_u64(x);
+    const int32_t hx = (int32_t)(u >> 32);
+    const uint32_t lx = (uint32_t)u;
+    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -HUGE_VAL;   // log(+-0)
+    if (hx < 0) return __builtin_nan("");                           // log(<0), log(-inf)
+    if (hx >= 0x7ff00000) return x + x;                               // +inf, NaN
+    return log_core(as_u64(x * cf(0x4350000000000000ull)), -54);    // subnormal: x * 2^54
 }
 
-GCR_HD double dm_pow_m3(double t) {
+// log(x): fdlibm e_log.c algorithm (< 1 ulp), polynomial in FMA Horner form.
+GCR_HD double dm_log(double x) {
+    if (!(x >= 0x1p-1022 && x < HUGE_VAL)) return log_special(x);
+    return log_core(as_u64(x), 0);
+}
+
+// --------------------------------------------------------------- t^-3 -----
+// t^-3 = 1 / ((t*t)*t): two roundings in the cube and one in the IEEE
+// division (< 2 ulp), valid while t^3 is normal.
+GCR_HD double pm3_core(double t) { return 1.0 / ((t * t) * t); }
+
+GCR_COLD GCR_HD double pm3_special(double t) {
     const double a = __builtin_fabs(t);
-    if (a >= 0x1p-300 && a <= 0x1p300) return pm3_core(t);
     if (a != a) return t + t;                             // NaN
     if (a == 0.0) return 1.0 / (t * t * t);               // +-0 -> +-inf
     if (a == HUGE_VAL) return (t > 0.0) ? 0.0 : -0.0;     // +-inf -> +-0
@@ -100,9 +103,15 @@ GCR_HD double dm_pow_m3(double t) {
     return ldexp(pm3_core(m), -3 * e);
 }
 
+GCR_HD double dm_pow_m3(double t) {
+    const double a = __builtin_fabs(t);
+    if (a >= 0x1p-300 && a <= 0x1p300) return pm3_core(t);
+    return pm3_special(t);
+}
+
 // -------------------------------------------------------------- atan2 -----
-// atan(x) for x >= 0 (finite or +inf), fdlibm s_atan.c.
-GCR_HD double dm_atan_nonneg(double x) {
+// fdlibm s_atan.c odd minimax polynomial, valid for |x| <= 7/16.
+GCR_HD double atan_poly(double x, double hi, double lo) {
     constexpr double aT0 = cf(0x3fd555555555550dull);
     constexpr double aT1 = cf(0xbfc999999998ebc4ull);
     constexpr double aT2 = cf(0x3fc24924920083ffull);
@@ -114,75 +123,67 @@ GCR_HD double dm_atan_nonneg(double x) {
     constexpr double aT8 = cf(0x3fa97b4b24760debull);
     constexpr double aT9 = cf(0xbfa2b4442c6a6c2full);
     constexpr double aT10 = cf(0x3f90ad3ae322da11ull);
-    constexpr double hi0 = cf(0x3fddac670561bb4full), lo0 = cf(0x3c7a2b7f222f65e2ull);
-    constexpr double hi1 = cf(0x3fe921fb54442d18ull), lo1 = cf(0x3c81a62633145c07ull);
-    constexpr double hi2 = cf(0x3fef730bd281f69bull), lo2 = cf(0x3c7007887af0cbbdull);
-    constexpr double hi3 = cf(0x3ff921fb54442d18ull), lo3 = cf(0x3c91a62633145c07ull);
-
-    if (x >= 0x1p66) return hi3 + lo3;           // also +inf
-    // reduction: xr = (ca*x + cb) / (cc*x + cd), result = hi - ((xr*S - lo) - xr)
-    double ca = 1.0, cb = 0.0, cc = 0.0, cd = 1.0, hi = 0.0, lo = 0.0;
-    if (x >= 0.4375) {
-        if (x < 0.6875)      { ca = 2.0; cb = -1.0;  cc = 1.0; cd = 2.0; hi = hi0; lo = lo0; }
-        else if (x < 1.1875) { ca = 1.0; cb = -1.0;  cc = 1.0; cd = 1.0; hi = hi1; lo = lo1; }
-        else if (x < 2.4375) { ca = 1.0; cb = -1.5;  cc = 1.5; cd = 1.0; hi = hi2; lo = lo2; }
-        else                 { ca = 0.0; cb = -1.0;  cc = 1.0; cd = 0.0; hi = hi3; lo = lo3; }
-    }
-    const double xr = (ca * x + cb) / (cc * x + cd);
-    const double z = xr * xr;
+    const double z = x * x;
     const double w = z * z;
-    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
-    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    return hi - ((xr * (s1 + s2) - lo) - xr);
+    const double s1 = z * fma_rn(w, fma_rn(w, fma_rn(w, fma_rn(w, fma_rn(w, aT10, aT8), aT6), aT4), aT2), aT0);
+    const double s2 = w * fma_rn(w, fma_rn(w, fma_rn(w, fma_rn(w, aT9, aT7), aT5), aT3), aT1);
+    return hi - ((x * (s1 + s2) - lo) - x);
 }
 
-GCR_HD double dm_atan2(double y, double x) {
-    constexpr double pi_o_4 = cf(0x3fe921fb54442d18ull);
-    constexpr double pi_o_2 = cf(0x3ff921fb54442d18ull);
-    constexpr double pi = cf(0x400921fb54442d18ull);
-    constexpr double pi_lo = cf(0x3ca1a62633145c07ull);
+constexpr double kPiO2 = cf(0x3ff921fb54442d18ull);
+constexpr double kPiO4 = cf(0x3fe921fb54442d18ull);
+constexpr double kPiF = cf(0x400921fb54442d18ull);
+constexpr double kPiLo = cf(0x3ca1a62633145c07ull);     // pi - kPiF
+constexpr double kPiO4Lo = cf(0x3c81a62633145c07ull);   // pi/4 - kPiO4
+constexpr double kPiO2Lo = cf(0x3c91a62633145c07ull);   // pi/2 - kPiO2
 
-    const uint64_t ux = as_u64(x), uy = as_u64(y);
-    const int32_t hx = (int32_t)(ux >> 32), hy = (int32_t)(uy >> 32);
-    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
-    const uint32_t lx = (uint32_t)ux, ly = (uint32_t)uy;
-    if (x != x || y != y) return x + y;          // NaN
-    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);   // 2*sign(x) + sign(y)
-
-    if ((iy | (int32_t)ly) == 0) {               // y = +-0
+// IEEE special operands (NaN, zeros, infinities) as fdlibm e_atan2.c.
+GCR_COLD GCR_HD double atan2_special(double y, double x) {
+    if (x != x || y != y) return x + y;
+    const int32_t hx = (int32_t)(as_u64(x) >> 32), hy = (int32_t)(as_u64(y) >> 32);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (y == 0.0) {
         if (m < 2) return y;
-        return (m == 2) ? pi : -pi;
+        return (m == 2) ? kPiF : -kPiF;
     }
-    if ((ix | (int32_t)lx) == 0) return (hy < 0) ? -pi_o_2 : pi_o_2;   // x = +-0
-    if (ix == 0x7ff00000) {                      // x = +-inf
-        if (iy == 0x7ff00000) {
+    if (x == 0.0) return (hy < 0) ? -kPiO2 : kPiO2;
+    if (__builtin_fabs(x) == HUGE_VAL) {
+        if (__builtin_fabs(y) == HUGE_VAL) {
             switch (m) {
-                case 0: return pi_o_4;
-                case 1: return -pi_o_4;
-                case 2: return 3.0 * pi_o_4;
-                default: return -3.0 * pi_o_4;
+                case 0: return kPiO4;
+                case 1: return -kPiO4;
+                case 2: return 3.0 * kPiO4;
+                default: return -3.0 * kPiO4;
             }
         }
         switch (m) {
             case 0: return 0.0;
             case 1: return -0.0;
-            case 2: return pi;
-            default: return -pi;
+            case 2: return kPiF;
+            default: return -kPiF;
         }
     }
-    if (iy == 0x7ff00000) return (hy < 0) ? -pi_o_2 : pi_o_2;          // y = +-inf
+    return (hy < 0) ? -kPiO2 : kPiO2;                     // y = +-inf, x finite
+}
 
-    const int32_t k = (iy - ix) >> 20;
-    double z;
-    if (k > 60) z = pi_o_2 + 0.5 * pi_lo;        // |y/x| > 2^60
-    else if (hx < 0 && k < -60) z = 0.0;         // |y|/x < -2^60
-    else z = dm_atan_nonneg(__builtin_fabs(y / x));
-    switch (m) {
-        case 0: return z;
-        case 1: return -z;
-        case 2: return pi - (z - pi_lo);
-        default: return (z - pi_lo) - pi;
-    }
+// atan2(y, x) for finite non-zero operands with a two-step, branch-free
+// reduction: t = min(|y|,|x|) / max(|y|,|x|) in (0, 1]; for t > tan(pi/8) the
+// argument (n - d) / (n + d) is used around pi/4 (one IEEE division either
+// way); |reduced| <= tan(pi/8) < 7/16 feeds fdlibm's polynomial.  Octant and
+// quadrant are restored with fdlibm's hi/lo constants.  Max error ~1.1 ulp.
+GCR_HD double dm_atan2(double y, double x) {
+    const double ay = __builtin_fabs(y), ax = __builtin_fabs(x);
+    if (!(ay > 0.0 && ay < HUGE_VAL && ax > 0.0 && ax < HUGE_VAL)) return atan2_special(y, x);
+    constexpr double kTanPiO8 = cf(0x3fda827999fcef32ull);
+    const bool swap = ay > ax;
+    const double n = swap ? ax : ay;
+    const double d = swap ? ay : ax;
+    const bool red = n > kTanPiO8 * d;
+    const double xr = (red ? n - d : n) / (red ? n + d : d);
+    double a = atan_poly(xr, red ? kPiO4 : 0.0, red ? kPiO4Lo : 0.0);   // atan(n / d)
+    if (swap) a = (kPiO2 - a) + kPiO2Lo;
+    if (x > 0.0) return (y > 0.0) ? a : -a;
+    return (y > 0.0) ? kPiF - (a - kPiLo) : (a - kPiLo) - kPiF;
 }
 
 // -------------------------------------------------------- angle clipping ---
@@ -190,12 +191,13 @@ GCR_HD double dm_atan2(double y, double x) {
 // |a| < 2c the remainder is a or a -+ c, both exact (Sterbenz); every call site
 // on the hot path stays in that range.  Larger arguments (and inf/NaN) use the
 // platform fmod, which is exact by definition on both sides.
+GCR_COLD GCR_HD double fmod_2pi_slow(double a) { return fmod(a, 2.0 * cf(0x400921fb54442d18ull)); }
+
 GCR_HD double fmod_2pi(double a) {
     constexpr double c = 2.0 * cf(0x400921fb54442d18ull);   // 2.0 * M_PI
     const double aa = __builtin_fabs(a);
-    if (aa < c) return a;
-    if (aa < 2.0 * c) return (a > 0.0) ? a - c : a + c;
-    return fmod(a, c);
+    if (!(aa < 2.0 * c)) return fmod_2pi_slow(a);          // |a| >= 4 pi, inf, NaN
+    return (aa < c) ? a : ((a > 0.0) ? a - c : a + c);
 }
 
 GCR_HD double clip_angle(double a) {

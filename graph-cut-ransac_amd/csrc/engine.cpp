@@ -167,6 +167,40 @@ struct gcr_problem {
 namespace {
 
 // ------------------------------------------------------------- problem ----
+// Host SoA copy plus the per-feature constants, evaluated with glibc exactly as
+// the reference evaluates them inside its solvers and residuals:
+//   scale:       pow(s, kScalePower)   (three_sift.hpp:89/172, two_sift.hpp:224)
+//   orientation: cos(theta), sin(theta) (math_utils.hpp:104-109, model.h:158-159)
+//                as ONE glibc sincos(theta): the reference is built with GCC,
+//                which fuses those adjacent cos/sin calls into sincos, and
+//                sincos differs from separate sin/cos in ~0.1% of arguments.
+void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1, size_t n1, HostClass* hc) {
+    const int K = solver == 2 ? 2 : 1;
+    const double kScalePower = (solver == 1) ? (-1.0 / 3.0) : (1.0 / 3.0);
+    const double* src[2] = {f0, f1};
+    const size_t ns[2] = {n0, K == 2 ? n1 : 0};
+    for (int c = 0; c < K; ++c) {
+        HostClass& h = hc[c];
+        const size_t n = ns[c];
+        h.n = n;
+        h.x.resize(n); h.y.resize(n); h.a.resize(n); h.c0.resize(n); h.c1.resize(n);
+        for (size_t i = 0; i < n; ++i) {
+            h.x[i] = src[c][3 * i];
+            h.y[i] = src[c][3 * i + 1];
+            h.a[i] = src[c][3 * i + 2];
+            if (c == 0) {
+                h.c0[i] = std::pow(h.a[i], kScalePower);
+                h.c1[i] = 0.0;
+            } else {
+                double sn, cs;
+                ::sincos(h.a[i], &sn, &cs);
+                h.c0[i] = cs;
+                h.c1[i] = sn;
+            }
+        }
+    }
+}
+
 int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
                  gcr_problem** out) {
     if (!ctx || !out) return set_err(GCR_EINVAL, "null context or output pointer");
@@ -182,27 +216,8 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     P->ctx = ctx;
     P->solver = solver;
     P->K = K;
-    const double kScalePower = (solver == 1) ? (-1.0 / 3.0) : (1.0 / 3.0);
-    const double* src[2] = {f0, f1};
     const size_t ns[2] = {n0, K == 2 ? n1 : 0};
-    for (int c = 0; c < K; ++c) {
-        HostClass& h = P->hc[c];
-        const size_t n = ns[c];
-        h.n = n;
-        h.x.resize(n); h.y.resize(n); h.a.resize(n); h.c0.resize(n); h.c1.resize(n);
-        for (size_t i = 0; i < n; ++i) {
-            h.x[i] = src[c][3 * i];
-            h.y[i] = src[c][3 * i + 1];
-            h.a[i] = src[c][3 * i + 2];
-            if (c == 0) {            // scale: pow(s, kScalePower) exactly as the solvers call it
-                h.c0[i] = std::pow(h.a[i], kScalePower);
-                h.c1[i] = 0.0;
-            } else {                 // orientation: lineFromPointAndAngle's cos / sin
-                h.c0[i] = std::cos(h.a[i]);
-                h.c1[i] = std::sin(h.a[i]);
-            }
-        }
-    }
+    fill_host_classes(solver, f0, n0, f1, n1, P->hc);
     const size_t total = 5 * (ns[0] + ns[1]);
     HIPC(hipSetDevice(ctx->device));
     HIPC(hipMalloc(reinterpret_cast<void**>(&P->dmem), total * sizeof(double)));
@@ -839,6 +854,31 @@ int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_m
         HIPC(hipStreamSynchronize(s));
         return GCR_OK;
     });
+}
+
+int gcr_host_fit_nonminimal(int solver, const double* f0, size_t n0, const double* f1, size_t n1, const uint32_t* idx0,
+                            size_t k0, const uint32_t* idx1, size_t k1, gcr_rect_model* model_out) {
+    if (solver < 0 || solver > 2 || !f0 || !idx0 || !model_out || (solver == 2 && (!f1 || !idx1)))
+        return set_err(GCR_EINVAL, "bad arguments");
+    return guard([&]() -> int {
+        HostClass hc[2];
+        fill_host_classes(solver, f0, n0, f1, n1, hc);
+        std::vector<uint32_t> lists[2];
+        lists[0].assign(idx0, idx0 + k0);
+        if (solver == 2) lists[1].assign(idx1, idx1 + k1);
+        for (int c = 0; c < (solver == 2 ? 2 : 1); ++c)
+            for (uint32_t i : lists[c])
+                if (i >= hc[c].n) return set_err(GCR_EINVAL, "index out of range");
+        RectModel m;
+        if (!fit_nonminimal(solver, hc, lists, m)) return 0;
+        *model_out = gcr_rect_model{m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi};
+        return 1;
+    });
+}
+
+void gcr_host_homography(const gcr_rect_model* m, double* H_out) {
+    if (!m || !H_out) return;
+    homography_of(RectModel{m->x0, m->y0, m->s, m->h7, m->h8, m->alpha, m->phi}, H_out);
 }
 
 double gcr_host_log(double x) { return dm::dm_log(x); }

@@ -15,6 +15,8 @@
 #include "kernels.h"
 #include "philox.h"
 
+#include <cstdlib>
+
 namespace gcr {
 
 namespace {
@@ -128,6 +130,119 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, 
     out.tot[h] = tot;
 }
 
+// ------------------------------------------------------- split scoring ----
+// Exact MSAC with the feature loop split over a 1024-thread workgroup.
+//
+// A workgroup owns H hypotheses and walks the features in rounds of R.  Waves
+// 0..14 (960 threads) evaluate the H x R residuals of round r (thread t ->
+// hypothesis t % H, features t / H + k * 960 / H) and store -r^2 for inliers or
+// +0.0 for outliers into LDS tile r % 2; in the same interval wave 15 folds
+// tile (r-1) % 2 into H running sums, one lane per hypothesis, in feature
+// order.  One barrier per round separates producer and consumer.  Adding +0.0
+// never changes a sum that starts at +0.0, so every chain is bit-identical to
+// the reference's sequential loop (MSAC_scoring_function.hpp:73-85,
+// score.hpp:45-50) for any H and R; the class-1 chain continues the class-0
+// running total exactly as Score::increment_value does.
+constexpr int kSplitThreads = 1024;
+constexpr int kComputeThreads = 960;
+
+template <int KIND, int H, int R>
+__global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, double T0, double T1,
+                                                               const RectModel* __restrict__ models,
+                                                               const uint8_t* __restrict__ inc, uint32_t nh,
+                                                               ScoreOut out) {
+    static_assert((H * R) % kComputeThreads == 0 && kComputeThreads % H == 0, "tile shape");
+    constexpr int kPer = H * R / kComputeThreads;    // residuals per compute thread per round
+    constexpr int kStride = kComputeThreads / H;     // feature stride between a thread's residuals
+    __shared__ double tile[2][H * R];
+    __shared__ uint32_t cnt_sh[2][H];
+
+    const int t = threadIdx.x;
+    const bool chain_wave = t >= kComputeThreads;
+    const int h = chain_wave ? (t - kComputeThreads) : (t % H);
+    const int fsub = t / H;
+    const uint32_t hg = blockIdx.x * H + h;
+    const bool valid_h = h < H && hg < nh && (inc == nullptr || inc[hg] <= 101);
+    const bool live = !chain_wave && valid_h;
+    const RectModel m = live ? models[hg] : default_model();
+    const double ac = alpha_cube(m);
+    OrientConst oc{0.0, 0.0};
+    if constexpr (KIND == 2) oc = orient_const(m);
+    if (t < 2 * H) cnt_sh[t / H][t % H] = 0;
+
+    const uint32_t n0 = p.cls[0].n;
+    const uint32_t n1 = (KIND == 2) ? p.cls[1].n : 0;
+    const uint32_t r0 = (n0 + R - 1) / R;
+    const uint32_t rounds = r0 + (n1 + R - 1) / R;
+    uint32_t cnt0 = 0, cnt1 = 0;
+    double acc0 = 0.0, acc1 = 0.0, tot = 0.0;
+
+    for (uint32_t r = 0; r <= rounds; ++r) {
+        if (!chain_wave) {
+            if (r < rounds) {
+                double* tl = tile[r & 1];
+                if (r < r0) {
+                    const DevClass c = p.cls[0];
+                    const uint32_t base = r * R;
+#pragma unroll 2
+                    for (int k = 0; k < kPer; ++k) {
+                        const uint32_t il = fsub + k * kStride;
+                        const uint32_t i = base + il;
+                        double v = 0.0;
+                        if (live && i < n0) {
+                            const double r2 = scale_sq_residual<KIND == 1, true>(c.x[i], c.y[i], c.a[i], m, ac);
+                            if (r2 <= T0) { v = -r2; cnt0 += 1; }
+                        }
+                        tl[il * H + h] = v;
+                    }
+                } else if constexpr (KIND == 2) {
+                    const DevClass c = p.cls[1];
+                    const uint32_t base = (r - r0) * R;
+#pragma unroll 2
+                    for (int k = 0; k < kPer; ++k) {
+                        const uint32_t il = fsub + k * kStride;
+                        const uint32_t i = base + il;
+                        double v = 0.0;
+                        if (live && i < n1) {
+                            const double r2 = orient_sq_residual<true>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, oc);
+                            if (r2 <= T1) { v = -r2; cnt1 += 1; }
+                        }
+                        tl[il * H + h] = v;
+                    }
+                }
+            }
+        } else if (r > 0 && h < H) {
+            const uint32_t q = r - 1;
+            const double* tl = tile[q & 1];
+            if (q < r0) {
+                const uint32_t len = min((uint32_t)R, n0 - q * R);
+                for (uint32_t il = 0; il < len; ++il) acc0 += tl[il * H + h];
+                tot = acc0;
+            } else {
+                const uint32_t len = min((uint32_t)R, n1 - (q - r0) * R);
+                for (uint32_t il = 0; il < len; ++il) {
+                    const double v = tl[il * H + h];
+                    acc1 += v;
+                    tot += v;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!chain_wave) {
+        atomicAdd(&cnt_sh[0][h], cnt0);
+        if constexpr (KIND == 2) atomicAdd(&cnt_sh[1][h], cnt1);
+    }
+    __syncthreads();
+    if (chain_wave && h < H && hg < nh) {
+        out.n0[hg] = valid_h ? cnt_sh[0][h] : 0;
+        out.n1[hg] = valid_h ? cnt_sh[1][h] : 0;
+        out.v0[hg] = valid_h ? acc0 : 0.0;
+        out.v1[hg] = valid_h ? acc1 : 0.0;
+        out.tot[hg] = valid_h ? tot : 0.0;
+    }
+}
+
 // ----------------------------------------------------------------- mask ----
 template <int KIND>
 __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, RectModel m, int rule, double T,
@@ -196,11 +311,33 @@ void launch_score_t(const DevProblem& p, const double T[2], const RectModel* mod
     }
 }
 
+template <int H, int R>
+void launch_split_t(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc, uint32_t nh,
+                    const ScoreOut& out, hipStream_t stream) {
+    const dim3 grid((nh + H - 1) / H), block(kSplitThreads);
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL((k_score_split<0, H, R>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
+        case 1: hipLaunchKernelGGL((k_score_split<1, H, R>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
+        default: hipLaunchKernelGGL((k_score_split<2, H, R>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
+    }
+}
+
+int score_mode() {
+    static int mode = -1;
+    if (mode < 0) {
+        const char* e = getenv("GCR_SCORE_KERNEL");
+        mode = (e && e[0] == 'n') ? 1 : 0;   // "naive" -> lane-per-hypothesis kernel
+    }
+    return mode;
+}
+
 hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc,
                         uint32_t nh, bool identity, const ScoreOut& out, hipStream_t stream) {
     if (nh == 0) return hipSuccess;
-    if (identity) launch_score_t<true>(p, T, models, inc, nh, out, stream);
-    else launch_score_t<false>(p, T, models, inc, nh, out, stream);
+    if (!identity) launch_score_t<false>(p, T, models, inc, nh, out, stream);
+    else if (score_mode() == 1) launch_score_t<true>(p, T, models, inc, nh, out, stream);
+    else if (nh >= 8192) launch_split_t<16, 480>(p, T, models, inc, nh, out, stream);
+    else launch_split_t<4, 1920>(p, T, models, inc, nh, out, stream);
     return hipGetLastError();
 }
 

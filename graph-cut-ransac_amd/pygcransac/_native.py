@@ -114,6 +114,10 @@ def _load():
     L.gcr_host_sample.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
                                   C.c_uint32, u32p]
     L.gcr_debug_math.argtypes = [vp, C.c_int, dp, dp, C.c_size_t, dp]
+    L.gcr_host_fit_nonminimal.argtypes = [C.c_int, dp, C.c_size_t, dp, C.c_size_t, u32p, C.c_size_t, u32p,
+                                          C.c_size_t, C.POINTER(RectModel)]
+    L.gcr_host_homography.argtypes = [C.POINTER(RectModel), dp]
+    L.gcr_host_homography.restype = None
     return L
 
 

@@ -52,9 +52,8 @@ class _F64:
 
 
 def _cpow(x, y):
-    """C pow() semantics (inf/nan instead of Python exceptions)."""
-    with np.errstate(all="ignore"):
-        return float(np.power(np.float64(x), np.float64(y)))
+    """glibc pow() itself (numpy's SIMD power is not glibc, math.pow raises)."""
+    return _libm.pow(x, y)
 
 
 def _clip_angle(a):
@@ -69,6 +68,22 @@ def _clip_angle(a):
 
 def _atan2(y, x):
     return math.atan2(y, x)
+
+
+_libm = C.CDLL("libm.so.6")
+_libm.pow.argtypes = [C.c_double, C.c_double]
+_libm.pow.restype = C.c_double
+_libm.sincos.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+_libm.sincos.restype = None
+
+
+def _sincos(t):
+    """glibc sincos: the reference (GCC -O3) fuses model.h's adjacent
+    std::cos/std::sin calls into sincos, which differs from separate sin/cos
+    in ~0.1% of arguments."""
+    s, c = C.c_double(), C.c_double()
+    _libm.sincos(t, C.byref(s), C.byref(c))
+    return s.value, c.value
 
 
 class NormalizingTransform:
@@ -113,14 +128,14 @@ class RectifyingHomography(NormalizingTransform):
 
     def rectifiedAngle(self, x, y, angle):
         x, y, angle = float(x), float(y), float(angle)
-        ct, st = math.cos(angle), math.sin(angle)
+        st, ct = _sincos(angle)
         numer = (-x * st + y * ct) * self.h7 + st
         denom = (x * st - y * ct) * self.h8 + ct
         return _clip_angle(_atan2(numer, denom))
 
     def unrectifiedAngle(self, x, y, angle):
         x, y, angle = float(x), float(y), float(angle)
-        ct, st = math.cos(angle), math.sin(angle)
+        st, ct = _sincos(angle)
         numer = (x * st - y * ct) * self.h7 + st
         denom = (-x * st + y * ct) * self.h8 + ct
         return _clip_angle(_atan2(numer, denom))

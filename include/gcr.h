@@ -145,6 +145,14 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
  * ((1.5 thr)^2), 2 = 1-class graph-cut labeling */
 int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* model, int cls, int rule,
                    uint8_t* mask_out);
+/* host-only (no GPU): the LO / final-refit least-squares fit of the given index
+ * lists (RectifyingHomographyEstimator::estimateModelNonminimal,
+ * rectifying_homography_estimator.h:164-227); returns 1 and the model, 0 if the
+ * fit is rejected, < 0 on error */
+int gcr_host_fit_nonminimal(int solver, const double* f0, size_t n0, const double* f1, size_t n1, const uint32_t* idx0,
+                            size_t k0, const uint32_t* idx1, size_t k1, gcr_rect_model* model_out);
+/* host-only: RectifyingHomography::getHomography (model.h:211-226), row-major */
+void gcr_host_homography(const gcr_rect_model* model, double* H_out);
 /* host-only (no GPU): deterministic math and sampler used on both sides */
 double gcr_host_log(double x);
 double gcr_host_pow_m3(double t);

@@ -77,8 +77,16 @@ static inline double linesAnglesDiff(double a1, double a2) {
     return std::fmin(d1, d2);
 }
 struct V3 { double v[3]; double& operator[](int i) { return v[i]; } double operator[](int i) const { return v[i]; } };
+// The reference is built with GCC (-O3, Release), which fuses the adjacent
+// std::cos(t) / std::sin(t) calls of lineFromPointAndAngle and
+// rectifiedAngle / unrectifiedAngle into one glibc sincos(t) call; sincos
+// differs from separate sin/cos in ~0.1% of arguments, so it is called
+// explicitly here (and by the product's host precompute).
+static inline void sincos_ref(double t, double* s, double* c) { ::sincos(t, s, c); }
+
 static inline V3 lineFromPointAndAngle(double x, double y, double theta) {
-    const double c = std::cos(theta), s = std::sin(theta);
+    double s, c;
+    sincos_ref(theta, &s, &c);
     return V3{{s, -c, y * c - x * s}};
 }
 static inline V3 cross(const V3& a, const V3& b) {
@@ -181,10 +189,13 @@ struct Model {
         return clipAngle(m_atan2(numer, denom));
     }
     double rectifiedAngle(double x, double y, double angle) const {
-        return rectifiedAngleCS(x, y, std::cos(angle), std::sin(angle));
+        double st, ct;
+        sincos_ref(angle, &st, &ct);
+        return rectifiedAngleCS(x, y, ct, st);
     }
     double unrectifiedAngle(double x, double y, double angle) const {
-        const double ct = std::cos(angle), st = std::sin(angle);
+        double st, ct;
+        sincos_ref(angle, &st, &ct);
         const double numer = (x * st - y * ct) * h7 + st;
         const double denom = (-x * st + y * ct) * h8 + ct;
         return clipAngle(std::atan2(numer, denom));

@@ -19,6 +19,8 @@ for s in $STEPS; do
     smoke) run smoke 300 python __graft_entry__.py ;;
     tests) run tests 1200 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    sweep) i=0; while IFS= read -r line; do [ -z "$line" ] && continue; i=$((i+1));
+             run "sweep$i" 300 env $line ; done < "${SWEEP_FILE:-tools/sweep.txt}" ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
            run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --no-latency ${BENCH_ARGS:-} ;;
   esac
