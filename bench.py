@@ -6,13 +6,16 @@ N=10k corrs 50% outliers".  Workload (BASELINE.json configs[1], the hybrid
 rectification path on one MI355X): synthetic M2 problem,
 N_s = 5000 scale + N_o = 5000 orientation features, 50 % outliers each, fp64.
 
-One step = one pass of the hot path over one batch: `--slots` outer-iteration
-slots are drawn (Philox), validated and solved (k_generate), every resulting
-model is MSAC-scored against all 10 000 features (k_score), and the batch's
-first strict best (the reference's update rule) is selected on the host.
-Features are uploaded once before timing (HBM-resident).  `value` is the
-whole-job hypotheses/s; the end-to-end latency of a full estimator call at
-confidence 0.99 (including LO and the final refit) is reported beside it.
+One step = one pass of the hot path over one batch: `--slots` (default 4096,
+configs[1]) outer-iteration slots are drawn (Philox), validated and solved
+(k_generate), every resulting model is MSAC-scored against all 10 000 features
+(k_score_split), and the batch's first strict best (the reference's update
+rule, GCRANSAC.h:440-446) is selected on the device (k_select).  The K timed
+steps are queued back to back on one HIP stream (gcr_problem_verify_batches)
+and bracketed by device synchronisation.  Features are uploaded once before
+timing (HBM-resident).  `value` is the whole-job hypotheses/s; the end-to-end
+latency of a full estimator call at confidence 0.99 (including LO and the
+final refit) is reported beside it.
 
 Multi-GPU (torchrun): one process per GPU, each rank solves its own image
 pair (weak scaling, no data-path collective); the final per-rank best models
@@ -34,13 +37,39 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector fp64 spec
 
 
+def score_kernel_name(kind, slots):
+    """The split-scorer instantiation launch_score picks (kernels.hip split_h)."""
+    if os.environ.get("GCR_SCORE_KERNEL", "").startswith("n"):
+        return f"k_score<{kind}, true>"
+    h = int(os.environ.get("GCR_SPLIT_H", "0") or 0)
+    if h not in (64, 16, 4):
+        h = 64 if slots >= 16384 else 16 if slots >= 2048 else 4
+    return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 360), (4, 960)])[h]}>"
+
+
+def traffic_per_launch(kernel, slots):
+    """HBM bytes per launch of `kernel` at this batch size from the committed
+    rocprofv3 PMC summary (profiles/pmc_traffic.json, written by
+    tools/pmc_summary.py from separate --pmc passes: 2 x FETCH_SIZE + WRITE_SIZE
+    per dispatch, the gfx950 correction of MI355X_MICROARCH.md); None if that
+    kernel/batch was not profiled."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            table = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ent = table.get(f"{kernel}@{slots}")
+    return None if ent is None else ent.get("hbm_bytes_per_launch")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--workload", choices=["m2", "m1"], default="m2")
-    ap.add_argument("--slots", type=int, default=65536, help="outer-iteration slots (hypotheses) per launch")
+    ap.add_argument("--slots", type=int, default=4096, help="outer-iteration slots (hypotheses) per launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-latency", action="store_true")
     return ap.parse_args()
@@ -89,20 +118,20 @@ def main():
     p.orientation_residual_thresh = thr1
     p.seed = seed
 
-    def step(k, st_acc):
-        res = N.BatchResult()
+    def steps(k0, n, st_acc):
+        res = (N.BatchResult * n)()
         st = N.Stats()
-        N.check(N.lib.gcr_problem_verify_batch(prob, C.byref(p), k * args.slots, args.slots, C.byref(res),
-                                               C.byref(st)))
+        N.check(N.lib.gcr_problem_verify_batches(prob, C.byref(p), k0 * args.slots, args.slots, n, res,
+                                                 C.byref(st)))
         if st_acc is not None:
-            st_acc["models"] += res.models
             st_acc["kernel_ms"] += st.ms_score_kernel
-            st_acc["launches"] += 1
-            if res.best_slot >= 0 and res.best_score > st_acc["best_score"]:
-                st_acc["best_score"] = res.best_score
-                st_acc["best_model"] = (res.best_model.h7, res.best_model.h8, res.best_model.alpha,
-                                        res.best_model.phi)
-        return res
+            st_acc["launches"] += n
+            for r in res:           # first strict best over the batches, in slot order
+                st_acc["models"] += r.models
+                if r.best_slot >= 0 and r.best_score > st_acc["best_score"]:
+                    st_acc["best_score"] = r.best_score
+                    st_acc["best_model"] = (r.best_model.h7, r.best_model.h8, r.best_model.alpha,
+                                            r.best_model.phi)
 
     def barrier():
         N.check(N.lib.gcr_synchronize(ctx))
@@ -112,13 +141,12 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    for k in range(args.warmup):
-        step(k, None)
+    if args.warmup:
+        steps(0, args.warmup, None)
     acc = dict(models=0, kernel_ms=0.0, launches=0, best_score=-1.0, best_model=(0.0, 0.0, 0.0, 0.0))
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k, acc)
+    steps(args.warmup, args.steps, acc)
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -141,6 +169,8 @@ def main():
         gathered = len(outs)
 
     value = models_total / elapsed
+    kind = 2 if solver == N.SOLVER_SIFT22 else 0
+    kernel_name = score_kernel_name(kind, args.slots)
     avg_kernel_s = acc["kernel_ms"] / max(1, acc["launches"]) / 1e3
     models_per_launch = acc["models"] / max(1, acc["launches"])
     bytes_per_launch = models_per_launch * 24.0 * n_total
@@ -171,7 +201,6 @@ def main():
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_ffi as O
 
-        kind = 2 if solver == N.SOLVER_SIFT22 else 0
         n_cal, s_cal, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, 64)
         rate = n_cal / max(s_cal, 1e-6)
         nslots = max(64, int(rate * args.cpu_seconds))
@@ -208,8 +237,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
-                "kernel": "k_score",
+                "traffic": traffic_per_launch(kernel_name, args.slots),
+                "kernel": kernel_name,
                 "bytes_per_hypothesis": 24 * n_total,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "hypotheses_per_launch": models_per_launch,

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -161,7 +162,12 @@ struct gcr_problem {
     ScoreBufs lo_sb;
     DevBuf<uint8_t> mask[2];
     PinBuf<uint8_t> h_mask[2];
-    ~gcr_problem() { if (dmem) (void)hipFree(dmem); }
+    DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
+    std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
+    ~gcr_problem() {
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+        if (dmem) (void)hipFree(dmem);
+    }
 };
 
 namespace {
@@ -218,9 +224,13 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     P->K = K;
     const size_t ns[2] = {n0, K == 2 ? n1 : 0};
     fill_host_classes(solver, f0, n0, f1, n1, P->hc);
-    const size_t total = 5 * (ns[0] + ns[1]);
+    // SoA, every array padded to an even length (zeros) so that 16-byte
+    // LDS-DMA strips (k_score_split staging) are aligned and in bounds
+    const size_t np[2] = {(ns[0] + 1) & ~size_t(1), (ns[1] + 1) & ~size_t(1)};
+    const size_t total = 5 * (np[0] + np[1]);
     HIPC(hipSetDevice(ctx->device));
     HIPC(hipMalloc(reinterpret_cast<void**>(&P->dmem), total * sizeof(double)));
+    HIPC(hipMemsetAsync(P->dmem, 0, total * sizeof(double), ctx->stream));
     double* cur = P->dmem;
     P->dp.solver = solver;
     for (int c = 0; c < 2; ++c) {
@@ -232,7 +242,7 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
         for (int q = 0; q < 5; ++q) {
             HIPC(hipMemcpyAsync(cur, arrs[q]->data(), ns[c] * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
             *dst[q] = cur;
-            cur += ns[c];
+            cur += np[c];
         }
     }
     HIPC(hipStreamSynchronize(ctx->stream));
@@ -383,48 +393,40 @@ public:
     gcr_stats stats() const { return st_; }
 
     // One hot-path batch (bench): generate + score + first strict maximum.
-    void verify_batch(uint64_t slot0, uint32_t nslots, gcr_batch_result* out) {
+    // `nb` back-to-back batches of `nslots` slots starting at slot0, each
+    // generated, scored and reduced to its first strict best on the device
+    // (k_select); one host synchronisation at the end.
+    void verify_batches(uint64_t slot0, uint32_t nslots, uint32_t nb, gcr_batch_result* out) {
+        static_assert(sizeof(BatchRecord) == sizeof(gcr_batch_result), "record layout");
+        static_assert(offsetof(BatchRecord, best_model) == offsetof(gcr_batch_result, best_model), "record layout");
         const auto t0 = Clock::now();
         P_->inc.ensure(nslots); P_->models.ensure(nslots); P_->sb.ensure(nslots);
-        P_->h_inc.ensure(nslots); P_->h_models.ensure(nslots);
-        HIPC(launch_generate(P_->dp, prm_.seed, slot0, nslots, P_->inc.p, P_->models.p, s_));
-        HIPC(hipEventRecord(P_->ctx->ev0, s_));
-        HIPC(launch_score(P_->dp, Tm_, P_->models.p, P_->inc.p, nslots, true, P_->sb.dev(), s_));
-        HIPC(hipEventRecord(P_->ctx->ev1, s_));
-        P_->sb.d2h(nslots, s_);
-        HIPC(hipMemcpyAsync(P_->h_inc.p, P_->inc.p, nslots, hipMemcpyDeviceToHost, s_));
-        HIPC(hipMemcpyAsync(P_->h_models.p, P_->models.p, nslots * sizeof(RectModel), hipMemcpyDeviceToHost, s_));
+        P_->recs.ensure(nb);
+        while (P_->evs.size() < 2 * (size_t)nb) {
+            hipEvent_t ev;
+            HIPC(hipEventCreate(&ev));
+            P_->evs.push_back(ev);
+        }
+        const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint64_t s0 = slot0 + (uint64_t)b * nslots;
+            HIPC(launch_generate(P_->dp, prm_.seed, s0, nslots, P_->inc.p, P_->models.p, s_));
+            HIPC(hipEventRecord(P_->evs[2 * b], s_));
+            HIPC(launch_score(P_->dp, Tm_, P_->models.p, P_->inc.p, nslots, true, P_->sb.dev(), s_));
+            HIPC(hipEventRecord(P_->evs[2 * b + 1], s_));
+            HIPC(launch_select(P_->solver, P_->sb.dev(), P_->inc.p, P_->models.p, nslots, s0, m32, Tm_,
+                               P_->recs.p + b, s_));
+        }
+        HIPC(hipMemcpyAsync(out, P_->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
-        float kms = 0;
-        HIPC(hipEventElapsedTime(&kms, P_->ctx->ev0, P_->ctx->ev1));
-        st_.ms_score_kernel += kms;
-        st_.launches += 2;
-        out->models = 0;
-        out->iterations = 0;
-        out->best_slot = -1;
-        out->best_score = 0.0;
-        out->best_inliers[0] = out->best_inliers[1] = 0;
-        HScore best;
-        int64_t bj = -1;
-        for (uint32_t j = 0; j < nslots; ++j) {
-            const uint8_t inc = P_->h_inc.p[j];
-            out->iterations += inc;
-            if (inc > 101) continue;
-            ++out->models;
-            const uint32_t rn[2] = {P_->sb.hn0.p[j], P_->sb.hn1.p[j]};
-            const HScore cur = finish(rn, P_->sb.hv0.p[j], P_->sb.hv1.p[j], P_->sb.htot.p[j]);
-            if (best.sum < cur.sum && valid_model(P_->h_models.p[j])) { best = cur; bj = j; }
+        for (uint32_t b = 0; b < nb; ++b) {
+            float kms = 0;
+            HIPC(hipEventElapsedTime(&kms, P_->evs[2 * b], P_->evs[2 * b + 1]));
+            st_.ms_score_kernel += kms;
+            st_.hypotheses += out[b].models;
         }
-        if (bj >= 0) {
-            const RectModel& bm = P_->h_models.p[bj];
-            out->best_model = gcr_rect_model{bm.x0, bm.y0, bm.s, bm.h7, bm.h8, bm.alpha, bm.phi};
-            out->best_slot = (int64_t)(slot0 + (uint64_t)bj);
-            out->best_score = best.sum;
-            out->best_inliers[0] = best.n[0];
-            out->best_inliers[1] = best.n[1];
-        }
-        st_.hypotheses += out->models;
-        st_.hypotheses_computed += nslots;
+        st_.launches += 3 * nb;
+        st_.hypotheses_computed += (uint64_t)nslots * nb;
         st_.ms_total += ms_since(t0);
     }
 
@@ -740,18 +742,24 @@ int gcr_problem_run(gcr_problem* prob, const gcr_params* params, uint8_t* mask0_
     });
 }
 
-int gcr_problem_verify_batch(gcr_problem* prob, const gcr_params* params, uint64_t slot0, uint32_t nslots,
-                             gcr_batch_result* out, gcr_stats* stats_out) {
+int gcr_problem_verify_batches(gcr_problem* prob, const gcr_params* params, uint64_t slot0, uint32_t nslots,
+                               uint32_t nbatches, gcr_batch_result* out, gcr_stats* stats_out) {
     if (!prob || !out) return set_err(GCR_EINVAL, "null problem or output");
     if (int e = check_params(params, prob->solver)) return e;
-    if (nslots == 0) return set_err(GCR_EINVAL, "nslots must be > 0");
+    if (nslots == 0 || nbatches == 0) return set_err(GCR_EINVAL, "nslots and nbatches must be > 0");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
         Runner r(prob, *params);
-        r.verify_batch(slot0, nslots, out);
+        r.verify_batches(slot0, nslots, nbatches, out);
         fill_stats(stats_out, r.stats());
-        return (int)out->models;
+        return GCR_OK;
     });
+}
+
+int gcr_problem_verify_batch(gcr_problem* prob, const gcr_params* params, uint64_t slot0, uint32_t nslots,
+                             gcr_batch_result* out, gcr_stats* stats_out) {
+    const int rc = gcr_problem_verify_batches(prob, params, slot0, nslots, 1, out, stats_out);
+    return rc < 0 ? rc : (int)out->models;
 }
 
 static int run_oneshot(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,

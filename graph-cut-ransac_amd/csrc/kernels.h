@@ -49,6 +49,26 @@ hipError_t launch_generate(const DevProblem& p, uint64_t seed, uint64_t slot0, u
 hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc,
                         uint32_t nh, bool identity, const ScoreOut& out, hipStream_t stream);
 
+// One batch's verdict, layout-identical to gcr_batch_result (include/gcr.h).
+struct BatchRecord {
+    uint64_t models;
+    uint64_t iterations;
+    int64_t best_slot;
+    double best_score;
+    uint64_t best_inliers[2];
+    RectModel best_model;
+};
+
+// First strict best of a scored batch, on the device: each slot's score is
+// finished as MSACScoringFunction::getScore does (MSAC_scoring_function.hpp:
+// 108-127: zero if some n_c < m_c, else v_c / T_c + n_c folded into the running
+// sum), and the reference's update rule `best < score && isValidModel`
+// (GCRANSAC.h:440-446) applied over the slots in order is the maximum score
+// > 0 among valid models with the lowest slot index.
+hipError_t launch_select(int solver, const ScoreOut& sc, const uint8_t* inc, const RectModel* models,
+                         uint32_t nslots, uint64_t slot0, const uint32_t m[2], const double Tm[2], BatchRecord* out,
+                         hipStream_t stream);
+
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)
 // rule 2: 1-class graph-cut labeling with weight lambda, T = (1.5 thr)^2

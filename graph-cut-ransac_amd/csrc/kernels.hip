@@ -1,8 +1,9 @@
 // kernels.hip -- gfx950 kernels of the hypothesize-and-verify hot path.
 //
-//   k_generate   one lane per outer-iteration slot: up to 101 attempts of
-//                Philox sample -> sample validity -> 3x4 Gauss minimal solve,
-//                all in fp64 registers (GCRANSAC.h:296-339, solvers' minimal fits)
+//   k_generate   G lanes per outer-iteration slot evaluate its up-to-101
+//                attempts (Philox sample -> sample validity -> 3x4 Gauss
+//                minimal solve, fp64 registers) G at a time and keep the lowest
+//                success (GCRANSAC.h:296-339, solvers' minimal fits)
 //   k_score      one lane per hypothesis, features streamed in index order
 //                through the scalar unit (uniform addresses), exact sequential
 //                MSAC accumulation (MSAC_scoring_function.hpp:53-130): the
@@ -22,69 +23,92 @@ namespace gcr {
 
 namespace {
 
+typedef __attribute__((address_space(1))) void gvoid;   // global
+typedef __attribute__((address_space(3))) void lvoid;   // LDS
+
 constexpr int kGenBlock = 256;
 constexpr int kScoreBlock = 256;
 constexpr int kMaskBlock = 256;
 
 // ------------------------------------------------------------- generate ----
+// One attempt of one outer-iteration slot: Philox sample -> sample validity ->
+// minimal solve.  Attempts of a slot are independent draws (the counter RNG is
+// keyed by (slot, attempt)), so they may be evaluated in any order/parallel.
 template <int KIND>
+GCR_DEVICE bool attempt(const DevProblem& p, uint64_t seed, uint64_t slot, uint32_t a, RectModel& m) {
+    if constexpr (KIND != 2) {
+        const DevClass& c = p.cls[0];
+        uint32_t idx[3];
+        WordStream ws(seed, slot, a, kStreamMain, 0);
+        if (!sample_distinct<3>(ws, c.n, 3, idx)) return false;
+        double x[3], y[3], pw[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            x[j] = c.x[idx[j]];
+            y[j] = c.y[idx[j]];
+            pw[j] = c.c0[idx[j]];
+        }
+        // areAllPointsCollinear on the single consecutive triplet
+        if (are_collinear(x[0], y[0], x[1], y[1], x[2], y[2], 1.0)) return false;
+        return (KIND == 1) ? solve_scale3<true>(x, y, pw, m) : solve_scale3<false>(x, y, pw, m);
+    } else {
+        const DevClass& sc = p.cls[0];
+        const DevClass& oc = p.cls[1];
+        uint32_t si[2], oi[2];
+        WordStream ws0(seed, slot, a, kStreamMain, 0);
+        if (!sample_distinct<2>(ws0, sc.n, 2, si)) return false;
+        WordStream ws1(seed, slot, a, kStreamMain, 1);
+        if (!sample_distinct<2>(ws1, oc.n, 2, oi)) return false;
+        double sx[2], sy[2], sp[2], ox[2], oy[2], oco[2], osi[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            sx[j] = sc.x[si[j]];
+            sy[j] = sc.y[si[j]];
+            sp[j] = sc.c0[si[j]];
+            ox[j] = oc.x[oi[j]];
+            oy[j] = oc.y[oi[j]];
+            oco[j] = oc.c0[oi[j]];
+            osi[j] = oc.c1[oi[j]];
+        }
+        if (!valid_sample_sift22(sx, sy, ox, oy, oco, osi)) return false;
+        return solve_sift22(sx, sy, sp, ox, oy, oco, osi, m);
+    }
+}
+
+// G lanes per slot (G | 64, groups aligned inside a wave).  Round r evaluates
+// attempts r*G .. r*G+G-1 in parallel; the slot's result is the lowest
+// successful attempt, exactly the first success of the reference's sequential
+// retry loop (GCRANSAC.h:296-339).  inc = attempt + 1, or 102 if all 101 fail.
+template <int KIND, int G>
 __global__ __launch_bounds__(kGenBlock) void k_generate(DevProblem p, uint64_t seed, uint64_t slot0,
                                                         uint32_t nslots, uint8_t* __restrict__ inc,
                                                         RectModel* __restrict__ models) {
-    const uint32_t s = blockIdx.x * kGenBlock + threadIdx.x;
-    if (s >= nslots) return;
+    static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "group size");
+    const uint32_t tid = blockIdx.x * kGenBlock + threadIdx.x;
+    const uint32_t s = tid / G;
+    const uint32_t g = tid % G;
+    if (s >= nslots) return;                 // whole groups exit together
     const uint64_t slot = slot0 + s;
-    RectModel m = default_model();
-    for (uint32_t a = 0; a < 101; ++a) {
-        if constexpr (KIND != 2) {
-            const DevClass& c = p.cls[0];
-            uint32_t idx[3];
-            WordStream ws(seed, slot, a, kStreamMain, 0);
-            if (!sample_distinct<3>(ws, c.n, 3, idx)) continue;
-            double x[3], y[3], pw[3];
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                x[j] = c.x[idx[j]];
-                y[j] = c.y[idx[j]];
-                pw[j] = c.c0[idx[j]];
-            }
-            // areAllPointsCollinear on the single consecutive triplet
-            if (are_collinear(x[0], y[0], x[1], y[1], x[2], y[2], 1.0)) continue;
-            const bool ok = (KIND == 1) ? solve_scale3<true>(x, y, pw, m) : solve_scale3<false>(x, y, pw, m);
-            if (ok) {
+    const int lane = threadIdx.x & 63;
+    const int gbase = lane & ~(G - 1);
+    for (uint32_t r = 0; r * G < 101; ++r) {
+        const uint32_t a = r * G + g;
+        RectModel m = default_model();
+        const bool ok = a < 101 && attempt<KIND>(p, seed, slot, a, m);
+        const uint64_t mask = __ballot(ok);
+        const uint64_t grp = G == 64 ? mask : (mask >> gbase) & ((1ull << G) - 1ull);
+        if (grp) {
+            if (g == (uint32_t)__builtin_ctzll(grp)) {
                 models[s] = m;
                 inc[s] = (uint8_t)(a + 1);
-                return;
             }
-        } else {
-            const DevClass& sc = p.cls[0];
-            const DevClass& oc = p.cls[1];
-            uint32_t si[2], oi[2];
-            WordStream ws0(seed, slot, a, kStreamMain, 0);
-            if (!sample_distinct<2>(ws0, sc.n, 2, si)) continue;
-            WordStream ws1(seed, slot, a, kStreamMain, 1);
-            if (!sample_distinct<2>(ws1, oc.n, 2, oi)) continue;
-            double sx[2], sy[2], sp[2], ox[2], oy[2], oco[2], osi[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                sx[j] = sc.x[si[j]];
-                sy[j] = sc.y[si[j]];
-                sp[j] = sc.c0[si[j]];
-                ox[j] = oc.x[oi[j]];
-                oy[j] = oc.y[oi[j]];
-                oco[j] = oc.c0[oi[j]];
-                osi[j] = oc.c1[oi[j]];
-            }
-            if (!valid_sample_sift22(sx, sy, ox, oy, oco, osi)) continue;
-            if (solve_sift22(sx, sy, sp, ox, oy, oco, osi, m)) {
-                models[s] = m;
-                inc[s] = (uint8_t)(a + 1);
-                return;
-            }
+            return;
         }
     }
-    models[s] = default_model();
-    inc[s] = 102;
+    if (g == 0) {
+        models[s] = default_model();
+        inc[s] = 102;
+    }
 }
 
 // ---------------------------------------------------------------- score ----
@@ -189,8 +213,17 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     static_assert(H * R <= 65536, "queue entries are 16-bit tile indices");
     constexpr int kPer = H * R / kComputeThreads;    // pairs per compute thread per round
     constexpr int kStride = kComputeThreads / H;     // feature stride between a thread's pairs
-    __shared__ double tile[2][H * R];                // -r^2 / +0.0 per (feature, hypothesis)
-    __shared__ double fbuf[2][4][R];                 // staged features of a round: x, y, s|cos, sin
+    // orientation rounds feed two sequential sums (class sum and total): with
+    // H <= 32 they run on two lane groups of the chain wave, else both in-lane
+    constexpr bool kSplitTot = KIND == 2 && 2 * H <= 64;
+    constexpr bool kDual = KIND == 2 && !kSplitTot;
+    // tile: hypothesis-major columns, -r^2 per inlier pair, +0.0 otherwise; the
+    // +2 pad keeps 16-byte column alignment and spreads the chain lanes'
+    // 16-byte reads over distinct banks
+    constexpr int kRP = R + 2;
+    __shared__ double tile[2][H * kRP];
+    constexpr int kRp = (R + 127) / 128 * 128;       // fbuf row: whole 128-feature DMA strips
+    __shared__ double fbuf[2][4][kRp];               // staged features of a round: x, y, s|cos, sin
     __shared__ uint16_t queue[kComputeWaves][kPer * 64];
     __shared__ HypConst hyp[H];
     __shared__ uint32_t cnt_sh[2][H];
@@ -199,10 +232,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     const int wave = t >> 6;
     const int lane = t & 63;
     const bool chain_wave = t >= kComputeThreads;
-    const int h = chain_wave ? (t - kComputeThreads) : (t % H);
+    const int h = chain_wave ? (lane % H) : (t % H);
+    const int role = (chain_wave && kSplitTot) ? lane / H : 0;   // 0: class sums, 1: total
+    const bool chain_lane = chain_wave && lane < (kSplitTot ? 2 * H : H);
     const int fsub = t / H;
     const uint32_t hg = blockIdx.x * H + h;
-    const bool valid_h = h < H && hg < nh && (inc == nullptr || inc[hg] <= 101);
+    const bool valid_h = hg < nh && (inc == nullptr || inc[hg] <= 101);
     const bool live = !chain_wave && valid_h;
 
     const uint32_t n0 = p.cls[0].n;
@@ -226,6 +261,26 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                     fbuf[buf][2][e] = c.c0[i];
                     fbuf[buf][3][e] = c.c1[i];
                 }
+            }
+        }
+    };
+    // chain-wave staging by LDS-DMA (global_load_lds, 16 B = 2 features per
+    // lane): issued before the fold, retired by the round's barrier, so the
+    // global latency hides behind the fold and no registers are spent.
+    // Device arrays are padded to even length; strips past the end re-read the
+    // last pair (never consumed).
+    auto stage_dma = [&](uint32_t rr, int buf) {
+        const int cls = (rr < r0) ? 0 : 1;
+        const DevClass& c = p.cls[cls];
+        const uint32_t base = (cls == 0 ? rr : rr - r0) * R;
+        const uint32_t last = ((c.n + 1u) & ~1u) - 2u;
+        const double* src[4] = {c.x, c.y, cls == 0 ? c.a : c.c0, c.c1};
+        const int nf = cls == 0 ? 3 : 4;
+        for (int f = 0; f < nf; ++f) {
+#pragma unroll
+            for (int q = 0; q < kRp / 128; ++q) {
+                const uint32_t i = min(base + q * 128 + 2 * lane, last);
+                __builtin_amdgcn_global_load_lds((const gvoid*)(src[f] + i), (lvoid*)&fbuf[buf][f][q * 128], 16, 0, 0);
             }
         }
     };
@@ -253,19 +308,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     stage(0, 0, t, kSplitThreads);
     __syncthreads();
 
-    double acc0 = 0.0, acc1 = 0.0, tot = 0.0;
+    // chain-lane state: `run` is the running sum this lane extends; `hold`
+    // keeps the finished class-0 sum; `tot2` the in-lane total (kDual)
+    double run = 0.0, hold = 0.0, tot2 = 0.0;
+    if (chain_wave) __builtin_amdgcn_s_setprio(3);   // latency-bound: issue ahead of the compute waves
     HypConst mine{};
     if (live) mine = hyp[h];
 
     for (uint32_t r = 0; r <= rounds; ++r) {
         if (!chain_wave) {
             if (r < rounds) {
-                double* tl = tile[r & 1];
-                const double(*fb)[R] = fbuf[r & 1];
+                const int b = r & 1;
+                double* tl = tile[b];
+                const double(*fb)[kRp] = fbuf[b];
                 const int cls = (r < r0) ? 0 : 1;
                 const uint32_t base = (cls == 0 ? r : r - r0) * R;
                 const uint32_t nc = cls == 0 ? n0 : n1;
-                // 1) band test + default +0.0
+                // 1) conservative band test
                 uint32_t bits = 0;
 #pragma unroll
                 for (int k = 0; k < kPer; ++k) {
@@ -275,7 +334,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         if (cls == 0) cand = scale_band<KIND>(fb[0][il], fb[1][il], fb[2][il], mine);
                         else if constexpr (KIND == 2) cand = orient_band(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine, tan_tau1);
                     }
-                    tl[il * H + h] = 0.0;
+                    tl[h * kRP + il] = 0.0;
                     bits |= (uint32_t)cand << k;
                 }
                 // 2) wave-level compaction of the surviving pairs
@@ -313,57 +372,147 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         inl = r2 <= T1;
                     }
                     if (inl) {
-                        tl[idx] = -r2;
+                        tl[hh * kRP + il] = -r2;
                         atomicAdd(&cnt_sh[cls][hh], 1u);
                     }
                 }
             }
         } else {
-            // chain wave: stage round r+1's features, then fold tile r-1
-            if (r + 1 < rounds) stage(r + 1, (r + 1) & 1, lane, 64);
-            if (r > 0 && h < H) {
-                // sequential fold of one tile column; LDS reads issued 8 ahead so
-                // only the dependent fp64 adds remain on the critical path
+            // chain wave: stage round r+1's features around the fold of
+            // tile r-1, which extends the sums in feature order (outliers
+            // hold +0.0: an exact no-op)
+            if (r + 1 < rounds) stage_dma(r + 1, (r + 1) & 1);
+            if (r > 0 && chain_lane) {
                 const uint32_t qr = r - 1;
-                const double* col = tile[qr & 1] + h;
-                if (qr < r0) {
-                    const uint32_t len = min((uint32_t)R, n0 - qr * R);
-                    uint32_t il = 0;
-                    for (; il + 8 <= len; il += 8) {
-                        double v[8];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) v[u] = col[(il + u) * H];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) acc0 += v[u];
-                    }
-                    for (; il < len; ++il) acc0 += col[il * H];
-                    tot = acc0;
-                } else {
-                    const uint32_t len = min((uint32_t)R, n1 - (qr - r0) * R);
-                    uint32_t il = 0;
-                    for (; il + 8 <= len; il += 8) {
-                        double v[8];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) v[u] = col[(il + u) * H];
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) { acc1 += v[u]; tot += v[u]; }
-                    }
-                    for (; il < len; ++il) {
-                        const double v = col[il * H];
-                        acc1 += v;
-                        tot += v;
-                    }
+                const bool cls0 = qr < r0;
+                if (KIND == 2 && qr == r0 && role == 0) {   // first orientation round
+                    hold = run;
+                    tot2 = run;
+                    run = 0.0;
                 }
+                const double2* col = reinterpret_cast<const double2*>(tile[qr & 1] + h * kRP);
+                const uint32_t len = cls0 ? min((uint32_t)R, n0 - qr * R) : min((uint32_t)R, n1 - (qr - r0) * R);
+                // entries in [len, kRP) are +0.0, so the fold may run to an even
+                // length; 16-byte reads, one batch ahead of the adds
+                const uint32_t np = (len + 1) >> 1;
+                const bool dual = kDual && !cls0;
+                uint32_t j = 0;
+                auto fold2 = [&](const double2& v) {
+                    run += v.x;
+                    if (dual) tot2 += v.x;
+                    run += v.y;
+                    if (dual) tot2 += v.y;
+                };
+                constexpr int kB = KIND == 2 ? 4 : 8;        // 16-byte reads per batch
+                if (np >= kB) {
+                    double2 v[kB];
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) v[u] = col[u];
+                    for (j = kB; j + kB <= np; j += kB) {
+                        double2 w[kB];
+#pragma unroll
+                        for (int u = 0; u < kB; ++u) w[u] = col[j + u];
+#pragma unroll
+                        for (int u = 0; u < kB; ++u) fold2(v[u]);
+#pragma unroll
+                        for (int u = 0; u < kB; ++u) v[u] = w[u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) fold2(v[u]);
+                }
+                for (; j < np; ++j) fold2(col[j]);
             }
         }
         __syncthreads();
     }
-    if (chain_wave && h < H && hg < nh) {
-        out.n0[hg] = valid_h ? cnt_sh[0][h] : 0;
-        out.n1[hg] = valid_h ? cnt_sh[1][h] : 0;
-        out.v0[hg] = valid_h ? acc0 : 0.0;
-        out.v1[hg] = valid_h ? acc1 : 0.0;
-        out.tot[hg] = valid_h ? tot : 0.0;
+    if (chain_wave) {
+        double tot;
+        if constexpr (kSplitTot) tot = __shfl(run, (lane + H) & 63);
+        else if constexpr (kDual) tot = tot2;
+        else tot = run;
+        if (lane < H && hg < nh) {
+            const double acc0 = KIND == 2 ? hold : run;
+            const double acc1 = KIND == 2 ? run : 0.0;
+            out.n0[hg] = valid_h ? cnt_sh[0][h] : 0;
+            out.n1[hg] = valid_h ? cnt_sh[1][h] : 0;
+            out.v0[hg] = valid_h ? acc0 : 0.0;
+            out.v1[hg] = valid_h ? acc1 : 0.0;
+            out.tot[hg] = valid_h ? tot : 0.0;
+        }
+    }
+}
+
+// --------------------------------------------------------------- select ----
+constexpr int kSelectThreads = 1024;
+
+__global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut sc, const uint8_t* __restrict__ inc,
+                                                           const RectModel* __restrict__ models, uint32_t n,
+                                                           uint64_t slot0, uint32_t m0, uint32_t m1, double Tm0,
+                                                           double Tm1, BatchRecord* out) {
+    __shared__ double s_val[kSelectThreads];
+    __shared__ uint32_t s_idx[kSelectThreads];
+    __shared__ unsigned long long s_models[kSelectThreads], s_its[kSelectThreads];
+    const int t = threadIdx.x;
+    const int K = solver == 2 ? 2 : 1;
+    double best = 0.0;
+    uint32_t bi = 0xffffffffu;
+    unsigned long long nm = 0, its = 0;
+    for (uint32_t j = t; j < n; j += kSelectThreads) {
+        const uint32_t in = inc[j];
+        its += in;
+        if (in > 101) continue;
+        ++nm;
+        double sum = sc.tot[j];
+        bool zero = false;
+        for (int c = 0; c < K; ++c) {
+            const uint32_t nc = c == 0 ? sc.n0[j] : sc.n1[j];
+            if (nc < (c == 0 ? m0 : m1)) { zero = true; break; }
+            const double v = c == 0 ? sc.v0[j] : sc.v1[j];
+            const double msac = v / (c == 0 ? Tm0 : Tm1) + static_cast<double>(nc);
+            sum -= v;
+            sum += msac;
+        }
+        if (zero) sum = 0.0;
+        if (best < sum && (solver != 2 || valid_model_sift22(models[j]))) {
+            best = sum;
+            bi = j;
+        }
+    }
+    s_val[t] = best;
+    s_idx[t] = bi;
+    s_models[t] = nm;
+    s_its[t] = its;
+    __syncthreads();
+    for (int w = kSelectThreads / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            const uint32_t ia = s_idx[t], ib = s_idx[t + w];
+            const double va = s_val[t], vb = s_val[t + w];
+            if (ib != 0xffffffffu && (ia == 0xffffffffu || vb > va || (vb == va && ib < ia))) {
+                s_idx[t] = ib;
+                s_val[t] = vb;
+            }
+            s_models[t] += s_models[t + w];
+            s_its[t] += s_its[t + w];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        BatchRecord r;
+        r.models = s_models[0];
+        r.iterations = s_its[0];
+        r.best_slot = -1;
+        r.best_score = 0.0;
+        r.best_inliers[0] = r.best_inliers[1] = 0;
+        r.best_model = default_model();
+        const uint32_t j = s_idx[0];
+        if (j != 0xffffffffu) {
+            r.best_slot = static_cast<int64_t>(slot0 + j);
+            r.best_score = s_val[0];
+            r.best_inliers[0] = sc.n0[j];
+            r.best_inliers[1] = K == 2 ? sc.n1[j] : 0;
+            r.best_model = models[j];
+        }
+        *out = r;
     }
 }
 
@@ -412,15 +561,27 @@ inline unsigned blocks_for(size_t n, int bs) { return (unsigned)((n + bs - 1) / 
 
 }  // namespace
 
+template <int G>
+void launch_generate_g(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
+                       RectModel* models, hipStream_t stream) {
+    const dim3 grid(blocks_for((size_t)nslots * G, kGenBlock)), block(kGenBlock);
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL((k_generate<0, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
+        case 1: hipLaunchKernelGGL((k_generate<1, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
+        default: hipLaunchKernelGGL((k_generate<2, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
+    }
+}
+
 hipError_t launch_generate(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
                            RectModel* models, hipStream_t stream) {
     if (nslots == 0) return hipSuccess;
-    const dim3 grid(blocks_for(nslots, kGenBlock)), block(kGenBlock);
-    switch (p.solver) {
-        case 0: hipLaunchKernelGGL(k_generate<0>, grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
-        case 1: hipLaunchKernelGGL(k_generate<1>, grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
-        default: hipLaunchKernelGGL(k_generate<2>, grid, block, 0, stream, p, seed, slot0, nslots, inc, models); break;
-    }
+    // lanes per slot: enough lanes in flight to cover the chip (~128k), at
+    // most 16 parallel attempts per slot
+    if (nslots <= 8192) launch_generate_g<16>(p, seed, slot0, nslots, inc, models, stream);
+    else if (nslots <= 16384) launch_generate_g<8>(p, seed, slot0, nslots, inc, models, stream);
+    else if (nslots <= 32768) launch_generate_g<4>(p, seed, slot0, nslots, inc, models, stream);
+    else if (nslots <= 65536) launch_generate_g<2>(p, seed, slot0, nslots, inc, models, stream);
+    else launch_generate_g<1>(p, seed, slot0, nslots, inc, models, stream);
     return hipGetLastError();
 }
 
@@ -460,14 +621,38 @@ int score_mode() {
     return mode;
 }
 
+// GCR_SPLIT_H=64|16|4 pins the split-scorer variant (tuning sweeps); default:
+// by batch size, so that the grid still covers the 256 CUs.
+int split_h(uint32_t nh) {
+    static int forced = -1;
+    if (forced < 0) {
+        const char* e = getenv("GCR_SPLIT_H");
+        const int v = e ? atoi(e) : 0;
+        forced = (v == 64 || v == 16 || v == 4) ? v : 0;
+    }
+    if (forced) return forced;
+    return nh >= 16384 ? 64 : nh >= 2048 ? 16 : 4;
+}
+
+hipError_t launch_select(int solver, const ScoreOut& sc, const uint8_t* inc, const RectModel* models,
+                         uint32_t nslots, uint64_t slot0, const uint32_t m[2], const double Tm[2], BatchRecord* out,
+                         hipStream_t stream) {
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelectThreads), 0, stream, solver, sc, inc, models, nslots, slot0,
+                       m[0], m[1], Tm[0], Tm[1], out);
+    return hipGetLastError();
+}
+
 hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc,
                         uint32_t nh, bool identity, const ScoreOut& out, hipStream_t stream) {
     if (nh == 0) return hipSuccess;
     if (!identity) launch_score_t<false>(p, T, models, inc, nh, out, stream);
     else if (score_mode() == 1) launch_score_t<true>(p, T, models, inc, nh, out, stream);
-    else if (nh >= 16384) launch_split_t<64, 120>(p, T, models, inc, nh, out, stream);
-    else if (nh >= 2048) launch_split_t<16, 360>(p, T, models, inc, nh, out, stream);
-    else launch_split_t<4, 960>(p, T, models, inc, nh, out, stream);
+    else {
+        const int h = split_h(nh);
+        if (h == 64) launch_split_t<64, 120>(p, T, models, inc, nh, out, stream);
+        else if (h == 16) launch_split_t<16, 360>(p, T, models, inc, nh, out, stream);
+        else launch_split_t<4, 960>(p, T, models, inc, nh, out, stream);
+    }
     return hipGetLastError();
 }
 

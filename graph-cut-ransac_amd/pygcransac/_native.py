@@ -102,6 +102,8 @@ def _load():
     L.gcr_problem_run.argtypes = [vp, C.POINTER(Params), u8p, u8p, dp, C.POINTER(RectModel), C.POINTER(Stats)]
     L.gcr_problem_verify_batch.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.POINTER(BatchResult),
                                            C.POINTER(Stats)]
+    L.gcr_problem_verify_batches.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.c_uint32,
+                                             C.POINTER(BatchResult), C.POINTER(Stats)]
     L.gcr_debug_generate.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, u8p, C.POINTER(RectModel)]
     L.gcr_debug_score.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_uint32, u32p, u32p, dp, dp, dp]
     L.gcr_debug_mask.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_int, C.c_int, u8p]

@@ -133,6 +133,12 @@ typedef struct gcr_batch_result {
 } gcr_batch_result;
 int gcr_problem_verify_batch(gcr_problem* prob, const gcr_params* params, uint64_t slot0, uint32_t nslots,
                              gcr_batch_result* out, gcr_stats* stats_out);
+/* `nbatches` consecutive batches of `nslots` slots (batch b covers slots
+ * slot0 + b*nslots ...), queued back to back on the device with the per-batch
+ * selection done on the GPU; out[] holds one result per batch.  One host
+ * synchronisation per call.  Returns GCR_OK or an error code. */
+int gcr_problem_verify_batches(gcr_problem* prob, const gcr_params* params, uint64_t slot0, uint32_t nslots,
+                               uint32_t nbatches, gcr_batch_result* out, gcr_stats* stats_out);
 
 /* ---- parity / debug hooks (used by tests; GPU required unless noted) ---- */
 /* inc[i] in 1..101 (attempt of success) or 102 (no model), models[i] */

@@ -117,6 +117,63 @@ def test_score_kernel_matches_oracle_bitwise(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("nh", [300, 2048, 16384])
+def test_every_split_variant_matches_oracle_bitwise(kind, nh):
+    # launch_score picks H = 4 / 16 / 64 hypotheses per workgroup by batch size
+    # (kernels.hip split_h); tile 96 distinct models up to nh so each variant,
+    # its ragged last workgroup and its round tails are exercised
+    f0, f1, thr0, thr1 = _problem_data(kind, 1337, seed=91 + kind)
+    prob = Problem(kind, f0, f1)
+    inc, models = prob.generate(17, 0, 256)
+    uniq = models[inc <= 101][:96]
+    tiled = np.resize(uniq, (nh, 7))
+    n0, n1, v0, v1, tot = prob.score_raw(tiled, thr0, thr1)
+    refs = [O.score(kind, f0, f1, m, thr0, thr1) for m in uniq]
+    for i in range(nh):
+        ref = refs[i % len(uniq)]
+        got = finish_score(kind, n0[i], n1[i], v0[i], v1[i], tot[i], thr0, thr1)
+        assert got["counts"] == [int(c) for c in ref["counts"]], i
+        assert bits(got["value"]) == bits(ref["value"]), i
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_device_batch_selection_matches_host_replay(kind):
+    # gcr_problem_verify_batches: k_select's first strict best per batch equals
+    # the reference update rule replayed on the host over generate + score
+    f0, f1, thr0, thr1 = _problem_data(kind, 900, seed=44 + kind)
+    prob = Problem(kind, f0, f1)
+    p = N.default_params()
+    p.scale_residual_thresh, p.orientation_residual_thresh, p.seed = thr0, thr1, 123
+    nslots, nb = 1500, 3
+    res = (N.BatchResult * nb)()
+    st = N.Stats()
+    N.check(N.lib.gcr_problem_verify_batches(prob.h, C.byref(p), 7, nslots, nb, res, C.byref(st)))
+    for b in range(nb):
+        inc, models = prob.generate(123, 7 + b * nslots, nslots)
+        ok = inc <= 101
+        n0, n1, v0, v1, tot = prob.score_raw(models[ok], thr0, thr1)
+        best, bj, k = 0.0, -1, 0
+        for j in np.flatnonzero(ok):
+            sc = finish_score(kind, n0[k], n1[k], v0[k], v1[k], tot[k], thr0, thr1)
+            k += 1
+            valid = kind != N.SOLVER_SIFT22 or max(abs(models[j][3]), abs(models[j][4])) < 1e-3
+            if best < sc["value"] and valid:
+                best, bj, cnt = sc["value"], j, sc["counts"]
+        r = res[b]
+        assert r.models == int(ok.sum()) and r.iterations == int(inc.astype(np.int64).sum())
+        assert r.best_slot == (7 + b * nslots + bj if bj >= 0 else -1)
+        if bj >= 0:
+            assert bits(r.best_score) == bits(best)
+            assert [r.best_inliers[0], r.best_inliers[1]] == cnt
+            got = [r.best_model.x0, r.best_model.y0, r.best_model.s, r.best_model.h7, r.best_model.h8,
+                   r.best_model.alpha, r.best_model.phi]
+            assert np.array_equal(bits(got), bits(models[bj]))
+    one = N.BatchResult()
+    assert N.lib.gcr_problem_verify_batch(prob.h, C.byref(p), 7, nslots, C.byref(one), C.byref(st)) == res[0].models
+    assert one.best_slot == res[0].best_slot and bits(one.best_score) == bits(res[0].best_score)
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_mask_kernel_matches_oracle(kind):
     f0, f1, thr0, thr1 = _problem_data(kind, 800, seed=31 + kind)
     prob = Problem(kind, f0, f1)
