@@ -22,6 +22,6 @@ for s in $STEPS; do
     sweep) i=0; while IFS= read -r line; do [ -z "$line" ] && continue; i=$((i+1));
              run "sweep$i" 300 env $line ; done < "${SWEEP_FILE:-tools/sweep.txt}" ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-           run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --no-latency ${BENCH_ARGS:-} ;;
+           run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --no-latency ${BENCH_ARGS:-} ;;
   esac
 done
