@@ -1,0 +1,133 @@
+"""Independent problems across the GPUs of a node.
+
+One process per GPU (torchrun); problems are independent GCRANSAC runs, so the
+data path needs no collective at all: each rank solves its share on its own
+device, and the final models (a fixed-size record per problem, a few hundred
+bytes) are gathered with ONE all_gather -- RCCL over xGMI on the "nccl"
+backend, gloo on CPU.  Inlier masks stay with the rank that computed them.
+
+Extension module: the reference has no batch entry point
+(bindings.cpp:315-399 binds single problems only).
+"""
+from __future__ import annotations
+
+import heapq
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+
+# record layout: [valid, num_inliers, H (9), model x0 y0 s h7 h8 alpha phi (7),
+#                 iteration_number, hypotheses]
+RECORD = 20
+
+
+def problem_cost(problem: dict) -> float:
+    """Estimated cost of a problem: feature count x hypotheses budget."""
+    n = sum(np.asarray(problem[k]).shape[0] for k in ("features", "scale_features", "orientation_features")
+            if k in problem and problem[k] is not None)
+    return float(n) * float(problem.get("max_iteration_number", 10000))
+
+
+def assign_lpt(costs: Sequence[float], world: int) -> list[list[int]]:
+    """Longest-processing-time-first assignment of problems to `world` ranks.
+
+    Deterministic (ties by problem index, then rank), every problem appears
+    exactly once, and each rank's list is in increasing problem order."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    heap = [(0.0, r) for r in range(world)]
+    shares: list[list[int]] = [[] for _ in range(world)]
+    for i in sorted(range(len(costs)), key=lambda i: (-float(costs[i]), i)):
+        load, r = heapq.heappop(heap)
+        shares[r].append(i)
+        heapq.heappush(heap, (load + float(costs[i]), r))
+    return [sorted(s) for s in shares]
+
+
+def encode_result(result) -> np.ndarray:
+    """Fixed-size float64 record of one estimator result (see RECORD)."""
+    rec = np.zeros(RECORD)
+    if result is None:
+        return rec
+    H, model, num_inliers, stats = result.get("H"), result.get("model"), result.get("num_inliers", 0), \
+        result.get("stats") or {}
+    rec[0] = 1.0
+    rec[1] = float(num_inliers)
+    if H is not None:
+        rec[2:11] = np.asarray(H, dtype=np.float64).ravel()
+    if model is not None:
+        rec[11:18] = [float(getattr(model, k, 0.0)) for k in ("x0", "y0", "s", "h7", "h8", "alpha", "phi")]
+    rec[18] = float(stats.get("iteration_number", 0))
+    rec[19] = float(stats.get("hypotheses", 0))
+    return rec
+
+
+def decode_record(rec: np.ndarray) -> Optional[dict]:
+    if rec[0] == 0.0:
+        return None
+    return dict(num_inliers=int(rec[1]), H=None if not np.any(rec[2:11]) else rec[2:11].reshape(3, 3).copy(),
+                model=dict(zip(("x0", "y0", "s", "h7", "h8", "alpha", "phi"), rec[11:18].tolist())),
+                iteration_number=int(rec[18]), hypotheses=int(rec[19]))
+
+
+def solve_sharded(problems: Sequence[dict], solve: Callable[[dict], dict], rank: int = 0, world: int = 1,
+                  dist=None, device=None) -> tuple[list[Optional[dict]], dict]:
+    """Solve this rank's LPT share with `solve(problem) -> result dict`
+    (keys H, model, num_inliers, stats, plus anything rank-local such as masks),
+    then gather every problem's record to every rank with one all_gather.
+
+    Returns (records in problem order -- all ranks, local results by index)."""
+    shares = assign_lpt([problem_cost(p) for p in problems], world)
+    mine = shares[rank]
+    local = {i: solve(problems[i]) for i in mine}
+    cap = max(1, max(len(s) for s in shares))
+    buf = np.zeros((cap, RECORD))
+    for j, i in enumerate(mine):
+        buf[j] = encode_result(local[i])
+    if world == 1 or dist is None:
+        gathered = [buf]
+    else:
+        import torch
+
+        t = torch.from_numpy(buf)
+        if device is not None:
+            t = t.to(device)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)                  # the only collective
+        gathered = [o.cpu().numpy() for o in outs]
+    records: list[Optional[dict]] = [None] * len(problems)
+    for r, share in enumerate(shares):
+        for j, i in enumerate(share):
+            records[i] = decode_record(gathered[r][j])
+    return records, local
+
+
+def gpu_solver(device: int) -> Callable[[dict], dict]:
+    """solve() for solve_sharded that runs the MI355X engine on `device`.
+
+    A problem is a dict with kind "sift" (scale_features, orientation_features,
+    scale_residual_thresh, orientation_residual_thresh) or "scale_only" /
+    "scale_only_original" (features, scale_residual_thresh), plus optional
+    spatial_coherence_weight, min/max_iteration_number,
+    max_local_optimization_number, seed, confidence."""
+    from . import pygcransac as P
+
+    def solve(pr: dict) -> dict:
+        common = [pr.get("spatial_coherence_weight", 0.0), pr.get("min_iteration_number", 10000),
+                  pr.get("max_iteration_number", 10000), pr.get("max_local_optimization_number", 50)]
+        kw = dict(seed=pr.get("seed", 0), confidence=pr.get("confidence", 0.95), device=device, return_stats=True)
+        if pr["kind"] == "sift":
+            out = P.findRectifyingHomographySIFT(pr["scale_features"], pr["orientation_features"],
+                                                 pr["scale_residual_thresh"], pr["orientation_residual_thresh"],
+                                                 *common, **kw)
+            H, sm, om, model, stats = out
+            return dict(H=H, model=model, num_inliers=int(sm.sum() + om.sum()), stats=stats, masks=(sm, om))
+        fn = P.findRectifyingHomographyScaleOnlyOriginal if pr["kind"] == "scale_only_original" \
+            else P.findRectifyingHomographyScaleOnly
+        out = fn(pr["features"], pr["scale_residual_thresh"], *common, **kw)
+        if len(out) == 3:          # (None, inliers, stats) on failure
+            return dict(H=None, model=None, num_inliers=0, stats=out[-1], masks=(out[1],))
+        H, m, model, stats = out
+        return dict(H=H, model=model, num_inliers=int(m.sum()), stats=stats, masks=(m,))
+
+    return solve

@@ -326,3 +326,32 @@ def test_full_size_m1_and_m2_match_oracle_and_ground_truth():
     H, masks, model, st = _run_product(N.SOLVER_SIFT22, fs, fo, a, b, seed=0)
     assert abs(model.phi - gt.phi) < math.radians(0.5) or abs(model.phi - gt.phi - math.pi / 2) < math.radians(0.5)
     _assert_same(N.SOLVER_SIFT22, fs, fo, a, b, seed=0)
+
+
+# ----------------------------------------------------- problem sharding ----
+def test_gpu_solver_records_match_direct_calls():
+    from pygcransac import distributed as D
+
+    probs = []
+    for i in range(3):
+        fs, fo, _, _, ts, to = S.problem_m2(300 + 50 * i, 250 + 40 * i, seed=300 + i)
+        probs.append(dict(kind="sift", scale_features=fs, orientation_features=fo, scale_residual_thresh=ts,
+                          orientation_residual_thresh=to, max_iteration_number=2000, min_iteration_number=200,
+                          seed=i))
+    f, _, thr = S.problem_m1(400, seed=310)
+    probs.append(dict(kind="scale_only", features=f, scale_residual_thresh=thr, seed=9,
+                      min_iteration_number=200, max_iteration_number=2000))
+    recs, local = D.solve_sharded(probs, D.gpu_solver(0))
+    for i, pr in enumerate(probs):
+        if pr["kind"] == "sift":
+            H, sm, om, model = pygcransac.findRectifyingHomographySIFT(
+                pr["scale_features"], pr["orientation_features"], pr["scale_residual_thresh"],
+                pr["orientation_residual_thresh"], 0.0, 200, 2000, 50, seed=pr["seed"])
+            n = int(sm.sum() + om.sum())
+        else:
+            H, m, model = pygcransac.findRectifyingHomographyScaleOnly(pr["features"], pr["scale_residual_thresh"],
+                                                                       0.0, 200, 2000, 50, seed=pr["seed"])
+            n = int(m.sum())
+        assert recs[i]["num_inliers"] == n
+        assert np.array_equal(recs[i]["H"], H)
+        assert recs[i]["model"]["h7"] == model.h7 and recs[i]["model"]["h8"] == model.h8
