@@ -40,6 +40,7 @@
 #include "host_fit.h"
 #include "kernels.h"
 #include "philox.h"
+#include "qr3.h"
 
 using namespace gcr;
 
@@ -163,6 +164,10 @@ struct gcr_problem {
     DevBuf<uint8_t> mask[2];
     PinBuf<uint8_t> h_mask[2];
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
+    DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
+    DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
+    DevBuf<double> rf_part;             // GPU refit: reduction block partials
+    PinBuf<double> rf_hpart;
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
     ~gcr_problem() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
@@ -171,6 +176,77 @@ struct gcr_problem {
 };
 
 namespace {
+
+// --------------------------------------------------------- GPU refit ----
+// qr3.h storage backend in HBM: element-wise steps are kernels, reductions are
+// per-block partials (k_qr_partials, row order inside a block) summed here in
+// block order -- blocked_sum's order exactly, so results equal the host's.
+struct DevQRStore {
+    double* col[4];
+    hipStream_t s;
+    gcr_problem* P;
+    double dot(int a, int c, size_t lo, size_t hi) {
+        if (hi <= lo) return 0.0;
+        size_t nb = (hi - 1) / kSumBlock - lo / kSumBlock + 1;
+        P->rf_part.ensure(nb);
+        P->rf_hpart.ensure(nb);
+        HIPC(launch_qr_partials(col[a], col[c], lo, hi, P->rf_part.p, &nb, s));
+        HIPC(hipMemcpyAsync(P->rf_hpart.p, P->rf_part.p, nb * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        double total = 0.0;
+        for (size_t b = 0; b < nb; ++b) total += P->rf_hpart.p[b];
+        return total;
+    }
+    double sumsq(int c, size_t lo, size_t hi) { return dot(c, c, lo, hi); }
+    double get(int c, size_t i) {
+        HIPC(hipMemcpyAsync(P->rf_hpart.p, col[c] + i, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        return P->rf_hpart.p[0];
+    }
+    void set(int c, size_t i, double v) {
+        HIPC(hipStreamSynchronize(s));          // staging slot may still feed a copy
+        P->rf_hpart.p[0] = v;
+        HIPC(hipMemcpyAsync(col[c] + i, P->rf_hpart.p, sizeof(double), hipMemcpyHostToDevice, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    void scale(int c, size_t lo, size_t hi, double den) { HIPC(launch_qr_scale(col[c], lo, hi, den, s)); }
+    void zero(int c, size_t lo, size_t hi) { HIPC(launch_qr_zero(col[c], lo, hi, s)); }
+    void update(int c, int e, size_t lo, size_t hi, double tau, double t) {
+        HIPC(launch_qr_update(col[c], col[e], lo, hi, tau, t, s));
+    }
+};
+
+// The hybrid final refit's least-squares system on the GPU: rows built in HBM
+// (k_sift_rows, same arithmetic as sift_rows_host), solved by qr3_solve.
+struct GpuSiftSolver final : SiftSystemSolver {
+    explicit GpuSiftSolver(gcr_problem* p) : P(p) {}
+    gcr_problem* P;
+    void solve(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows, double x[3]) override {
+        hipStream_t s = P->ctx->stream;
+        const size_t ns = si.size(), no = oi.size();
+        P->rf_idx.ensure(ns + no);
+        P->rf_hpart.ensure(1);
+        HIPC(hipMemcpyAsync(P->rf_idx.p, si.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIPC(hipMemcpyAsync(P->rf_idx.p + ns, oi.data(), no * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        P->rf_A.ensure(4 * rows);
+        double* A = P->rf_A.p;
+        HIPC(launch_sift_rows(P->dp.cls[0], P->dp.cls[1], P->rf_idx.p, (uint32_t)ns, P->rf_idx.p + ns, (uint32_t)no,
+                              rows, A, A + rows, A + 2 * rows, A + 3 * rows, s));
+        HIPC(hipStreamSynchronize(s));          // index lists are pageable host vectors
+        DevQRStore st{{A, A + rows, A + 2 * rows, A + 3 * rows}, s, P};
+        qr3_solve(st, rows, x);
+    }
+};
+
+// hybrid systems at least this tall are solved on the GPU (the host QR costs
+// ~15 ns/row; the GPU path ~0.3 ms + ~15 synchronisations)
+size_t gpu_refit_rows() {
+    static size_t v = [] {
+        const char* e = getenv("GCR_GPU_REFIT_ROWS");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)32768;
+    }();
+    return v;
+}
 
 // ------------------------------------------------------------- problem ----
 // Host SoA copy plus the per-feature constants, evaluated with glibc exactly as
@@ -359,7 +435,8 @@ public:
             std::vector<uint32_t> lists[2];
             inlier_lists(bufs_[off_].model, Tm_, 0, lists);
             RectModel refit;
-            if (fit_nonminimal(P_->solver, P_->hc, lists, refit)) {
+            GpuSiftSolver gpu(P_);
+            if (fit_nonminimal(P_->solver, P_->hc, lists, refit, &gpu, gpu_refit_rows())) {
                 HScore s;
                 uint32_t rn[2];
                 score_models(&refit, 1, &s, rn);
@@ -879,6 +956,25 @@ int gcr_host_fit_nonminimal(int solver, const double* f0, size_t n0, const doubl
                 if (i >= hc[c].n) return set_err(GCR_EINVAL, "index out of range");
         RectModel m;
         if (!fit_nonminimal(solver, hc, lists, m)) return 0;
+        *model_out = gcr_rect_model{m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi};
+        return 1;
+    });
+}
+
+int gcr_debug_fit_nonminimal(gcr_problem* prob, const uint32_t* idx0, size_t k0, const uint32_t* idx1, size_t k1,
+                              int use_gpu, gcr_rect_model* model_out) {
+    if (!prob || !idx0 || !model_out || (prob->solver == 2 && !idx1)) return set_err(GCR_EINVAL, "bad arguments");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        std::vector<uint32_t> lists[2];
+        lists[0].assign(idx0, idx0 + k0);
+        if (prob->solver == 2) lists[1].assign(idx1, idx1 + k1);
+        for (int c = 0; c < prob->K; ++c)
+            for (uint32_t i : lists[c])
+                if (i >= prob->hc[c].n) return set_err(GCR_EINVAL, "index out of range");
+        RectModel m;
+        GpuSiftSolver gpu(prob);
+        if (!fit_nonminimal(prob->solver, prob->hc, lists, m, use_gpu ? &gpu : nullptr, 0)) return 0;
         *model_out = gcr_rect_model{m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi};
         return 1;
     });

@@ -7,6 +7,7 @@
 // transform is reset to identity), and Eigen's ColPivHouseholderQR for the
 // least-squares solve.  Weights are always empty on the Python path, i.e. 1.0.
 #include "host_fit.h"
+#include "qr3.h"
 
 #include <algorithm>
 #include <cmath>
@@ -15,109 +16,9 @@
 
 namespace gcr {
 
-namespace {
-
-inline double sq(double v) { return v * v; }
-
-// Householder reflector applied from the left to one column (rows k..m-1),
-// essential part stored in column k of A below the diagonal.
-inline void apply_reflector(const double* ess_col, size_t k, size_t m, double tau, double* col) {
-    if (m - k == 1) {
-        col[k] *= (1.0 - tau);
-        return;
-    }
-    if (tau == 0.0) return;
-    double t = 0;
-    for (size_t i = k + 1; i < m; ++i) t += ess_col[i] * col[i];
-    t += col[k];
-    col[k] -= tau * t;
-    for (size_t i = k + 1; i < m; ++i) col[i] -= (tau * ess_col[i]) * t;
-}
-
-}  // namespace
-
 void colpiv_qr_solve3(std::vector<double>& A, size_t m, std::vector<double>& b, double x[3]) {
-    constexpr size_t cols = 3;
-    const size_t size = std::min(m, cols);
-    double* col[3] = {A.data(), A.data() + m, A.data() + 2 * m};
-    double tau_k[3] = {0, 0, 0};
-    size_t transp[3] = {0, 1, 2};
-    double nu[3], nd[3];
-    for (size_t k = 0; k < cols; ++k) {
-        double s = 0;
-        for (size_t i = 0; i < m; ++i) s += col[k][i] * col[k][i];
-        nd[k] = std::sqrt(s);
-        nu[k] = nd[k];
-    }
-    const double eps = std::numeric_limits<double>::epsilon();
-    double maxn = nu[0];
-    for (size_t k = 1; k < cols; ++k)
-        if (maxn < nu[k]) maxn = nu[k];
-    const double thr_helper = sq(maxn * eps) / (double)m;
-    const double downdate_thr = std::sqrt(eps);
-    size_t nonzero = size;
-    for (size_t k = 0; k < size; ++k) {
-        size_t big = k;
-        double bign = nu[k];
-        for (size_t j = k + 1; j < cols; ++j)
-            if (bign < nu[j]) { bign = nu[j]; big = j; }
-        if (nonzero == size && sq(bign) < thr_helper * (double)(m - k)) nonzero = k;
-        transp[k] = big;
-        if (k != big) {
-            std::swap(col[k], col[big]);   // swap column storage
-            std::swap(nu[k], nu[big]);
-            std::swap(nd[k], nd[big]);
-        }
-        double* ck = col[k];
-        double tail = 0;
-        for (size_t i = k + 1; i < m; ++i) tail += ck[i] * ck[i];
-        const double c0 = ck[k];
-        double tau, beta;
-        if (tail <= std::numeric_limits<double>::min()) {
-            tau = 0.0;
-            beta = c0;
-            for (size_t i = k + 1; i < m; ++i) ck[i] = 0.0;
-        } else {
-            beta = std::sqrt(c0 * c0 + tail);
-            if (c0 >= 0.0) beta = -beta;
-            const double den = c0 - beta;
-            for (size_t i = k + 1; i < m; ++i) ck[i] = ck[i] / den;
-            tau = (beta - c0) / beta;
-        }
-        tau_k[k] = tau;
-        ck[k] = beta;
-        for (size_t j = k + 1; j < cols; ++j) apply_reflector(ck, k, m, tau, col[j]);
-        for (size_t j = k + 1; j < cols; ++j) {
-            if (nu[j] != 0.0) {
-                double temp = std::fabs(col[j][k]) / nu[j];
-                temp = (1.0 + temp) * (1.0 - temp);
-                temp = temp < 0.0 ? 0.0 : temp;
-                const double temp2 = temp * sq(nu[j] / nd[j]);
-                if (temp2 <= downdate_thr) {
-                    double s = 0;
-                    for (size_t i = k + 1; i < m; ++i) s += col[j][i] * col[j][i];
-                    nd[j] = std::sqrt(s);
-                    nu[j] = nd[j];
-                } else {
-                    nu[j] *= std::sqrt(temp);
-                }
-            }
-        }
-    }
-    size_t perm[3] = {0, 1, 2};
-    for (size_t k = 0; k < size; ++k) std::swap(perm[k], perm[transp[k]]);
-    if (nonzero == 0) {
-        x[0] = x[1] = x[2] = 0.0;
-        return;
-    }
-    for (size_t k = 0; k < nonzero; ++k) apply_reflector(col[k], k, m, tau_k[k], b.data());
-    double c[3] = {b[0], m > 1 ? b[1] : 0.0, m > 2 ? b[2] : 0.0};
-    for (size_t jj = nonzero; jj-- > 0;) {
-        c[jj] = c[jj] / col[jj][jj];
-        for (size_t i = 0; i < jj; ++i) c[i] -= c[jj] * col[jj][i];
-    }
-    for (size_t i = 0; i < nonzero; ++i) x[perm[i]] = c[i];
-    for (size_t i = nonzero; i < cols; ++i) x[perm[i]] = 0.0;
+    HostQRStore st{{A.data(), A.data() + m, A.data() + 2 * m, b.data()}};
+    qr3_solve(st, m, x);
 }
 
 double weighted_mode(const std::vector<double>& angles, const std::vector<double>& weights, double bin_width) {
@@ -213,7 +114,37 @@ bool fit_scale3(bool original, const HostClass& c, const std::vector<uint32_t>& 
     return finish_model(sol, out);
 }
 
-bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out) {
+// Rows of the hybrid system (assembly two_sift.hpp:474-509): scale rows
+// (setScaleConstraint :228-236: w x, w y, w s^(1/3) | w), then one row per orientation
+// pair i < j in index order.  Column-major A (rows x 3) and b.
+void sift_rows_host(const HostClass& sc, const HostClass& oc, const std::vector<uint32_t>& si,
+                    const std::vector<uint32_t>& oi, size_t rows, double* A, double* b) {
+    const size_t ns = si.size(), no = oi.size();
+    size_t r = 0;
+    for (size_t i = 0; i < ns; ++i, ++r) {
+        const uint32_t j = si[i];
+        const double w = 1.0;
+        A[r] = w * sc.x[j];
+        A[rows + r] = w * sc.y[j];
+        A[2 * rows + r] = w * sc.c0[j];
+        b[r] = w;
+    }
+    for (size_t i = 0; i + 1 < no; ++i) {
+        const uint32_t p = oi[i];
+        for (size_t j = i + 1; j < no; ++j, ++r) {
+            const uint32_t q = oi[j];
+            double row[4];
+            sift_pair_row(oc.x[p], oc.y[p], oc.c0[p], oc.c1[p], oc.x[q], oc.y[q], oc.c0[q], oc.c1[q], row);
+            A[r] = row[0];
+            A[rows + r] = row[1];
+            A[2 * rows + r] = row[2];
+            b[r] = row[3];
+        }
+    }
+}
+
+bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out, SiftSystemSolver* big,
+                size_t big_rows) {
     const HostClass& sc = cls[0];
     const HostClass& oc = cls[1];
     const std::vector<uint32_t>& si = idx[0];
@@ -229,37 +160,14 @@ bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectMode
         return solve_sift22(sx, sy, sp, ox, oy, ocs, osn, out);
     }
     const size_t rows = ns + npairs;
-    std::vector<double> A(rows * 3), b(rows);
-    size_t r = 0;
-    for (size_t i = 0; i < ns; ++i, ++r) {
-        const uint32_t j = si[i];
-        const double w = 1.0;
-        A[r] = w * sc.x[j];
-        A[rows + r] = w * sc.y[j];
-        A[2 * rows + r] = w * sc.c0[j];
-        b[r] = w;
-    }
-    for (size_t i = 0; i + 1 < no; ++i) {
-        double l1[3];
-        line_from(oc.x[oi[i]], oc.y[oi[i]], oc.c0[oi[i]], oc.c1[oi[i]], l1);
-        for (size_t j = i + 1; j < no; ++j, ++r) {
-            const double w = 1.0 * 1.0;
-            double l2[3], vp[3];
-            line_from(oc.x[oi[j]], oc.y[oi[j]], oc.c0[oi[j]], oc.c1[oi[j]], l2);
-            cross3(l1, l2, vp);
-            const double a0 = std::fabs(vp[0]), a1 = std::fabs(vp[1]), a2 = std::fabs(vp[2]);
-            double mx = (a0 < a1) ? a1 : a0;
-            mx = (mx < a2) ? a2 : mx;
-            if (mx > 1.0)
-                for (int q = 0; q < 3; ++q) vp[q] = vp[q] / mx;
-            A[r] = w * vp[0];
-            A[rows + r] = w * vp[1];
-            A[2 * rows + r] = 0.0;
-            b[r] = w * vp[2];
-        }
-    }
     double sol[3];
-    colpiv_qr_solve3(A, rows, b, sol);
+    if (big && rows >= big_rows) {
+        big->solve(si, oi, rows, sol);
+    } else {
+        std::vector<double> A(rows * 3), b(rows);
+        sift_rows_host(sc, oc, si, oi, rows, A.data(), b.data());
+        colpiv_qr_solve3(A, rows, b, sol);
+    }
     if (!finish_model(sol, out)) return false;
     std::vector<double> ang(no), wts(no);
     double wsum = 0;
@@ -280,14 +188,15 @@ bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectMode
 
 }  // namespace
 
-bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out) {
+bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out,
+                    SiftSystemSolver* big, size_t big_rows) {
     const int K = (solver == 2) ? 2 : 1;
     const size_t m[2] = {solver == 2 ? 2u : 3u, 2u};
     for (int c = 0; c < K; ++c)
         if (idx[c].size() < m[c]) return false;
     if (!normalize_ok(K, cls, idx)) return false;
     bool ok;
-    if (solver == 2) ok = fit_sift22(cls, idx, out);
+    if (solver == 2) ok = fit_sift22(cls, idx, out, big, big_rows);
     else ok = fit_scale3(solver == 1, cls[0], idx[0], out);
     if (ok) { out.x0 = 0.0; out.y0 = 0.0; out.s = 1.0; }
     return ok;

@@ -22,13 +22,25 @@ struct HostClass {
 };
 
 // Eigen ColPivHouseholderQR<MatrixX3d>::compute(A).solve(b) restated for an
-// m x 3 column-major matrix (A and b are overwritten).
+// m x 3 column-major matrix (A and b are overwritten); qr3.h, blocked sums.
 void colpiv_qr_solve3(std::vector<double>& A, size_t m, std::vector<double>& b, double x[3]);
+
+// Another backend for the hybrid fit's least-squares system (the GPU refit):
+// builds the ns scale rows + C(no, 2) vanishing-point pair rows of the index
+// lists itself and solves them with qr3_solve; must be op-identical to the
+// host path (rows as in fit_sift22, blocked sums).
+struct SiftSystemSolver {
+    virtual ~SiftSystemSolver() = default;
+    virtual void solve(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows,
+                       double x[3]) = 0;
+};
 
 // RectifyingHomographyEstimator::estimateModelNonminimal for the three solvers
 // (rectifying_homography_estimator.h:164-227): normalisation check, then the
 // minimal solver when the subset is exactly minimal, else weighted LS (+ mode).
-bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out);
+// Hybrid systems with at least `big_rows` rows go to `big` when given.
+bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out,
+                    SiftSystemSolver* big = nullptr, size_t big_rows = 0);
 
 // findWeightedMode (two_sift.hpp:354-394), libstdc++ unordered_map order.
 double weighted_mode(const std::vector<double>& angles, const std::vector<double>& weights, double bin_width);

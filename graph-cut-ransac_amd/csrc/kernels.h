@@ -69,6 +69,24 @@ hipError_t launch_select(int solver, const ScoreOut& sc, const uint8_t* inc, con
                          uint32_t nslots, uint64_t slot0, const uint32_t m[2], const double Tm[2], BatchRecord* out,
                          hipStream_t stream);
 
+// ---- GPU least-squares refit (qr3.h backend) ----
+// Rows of the hybrid non-minimal system for scale inliers si[ns] and
+// orientation inliers oi[no]: ns scale rows then C(no, 2) pair rows (i < j,
+// index order), written to column arrays A0, A1, A2, b of length `rows`.
+hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns,
+                            const uint32_t* oi, uint32_t no, size_t rows, double* A0, double* A1, double* A2,
+                            double* b, hipStream_t stream);
+// Block partials of sum_{i in [lo, hi)} a[i] * c[i] for the aligned blocks of
+// kSumBlock (qr3.h) rows that intersect [lo, hi), each summed in row order;
+// partials[0 .. nblocks) in block order.  Returns the block count via nblocks.
+hipError_t launch_qr_partials(const double* a, const double* c, size_t lo, size_t hi, double* partials,
+                              size_t* nblocks, hipStream_t stream);
+// element-wise updates on [lo, hi): c = c / den; c = 0; c -= (tau * e) * t
+hipError_t launch_qr_scale(double* c, size_t lo, size_t hi, double den, hipStream_t stream);
+hipError_t launch_qr_zero(double* c, size_t lo, size_t hi, hipStream_t stream);
+hipError_t launch_qr_update(double* c, const double* e, size_t lo, size_t hi, double tau, double t,
+                            hipStream_t stream);
+
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)
 // rule 2: 1-class graph-cut labeling with weight lambda, T = (1.5 thr)^2

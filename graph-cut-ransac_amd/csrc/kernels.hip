@@ -15,6 +15,7 @@
 // the host restatement.
 #include "kernels.h"
 #include "philox.h"
+#include "qr3.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -516,6 +517,97 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
     }
 }
 
+// ---------------------------------------------------------------- refit ----
+constexpr int kRowBlock = 256;
+
+// thread per row; pair p = r - ns maps to (i, j), i < j, row-major over i:
+// off(i) = i * (2 no - i - 1) / 2 pairs precede row i
+__global__ __launch_bounds__(kRowBlock) void k_sift_rows(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
+                                                         uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no,
+                                                         uint64_t rows, double* A0, double* A1, double* A2,
+                                                         double* b) {
+    const uint64_t r = (uint64_t)blockIdx.x * kRowBlock + threadIdx.x;
+    if (r >= rows) return;
+    if (r < ns) {
+        const uint32_t j = si[r];
+        const double w = 1.0;
+        A0[r] = w * sc.x[j];
+        A1[r] = w * sc.y[j];
+        A2[r] = w * sc.c0[j];
+        b[r] = w;
+        return;
+    }
+    const uint64_t p = r - ns;
+    const uint64_t n = no;
+    auto off = [n](uint64_t i) { return i * (2 * n - i - 1) / 2; };
+    const double q = (double)(2 * n - 1);
+    int64_t i = (int64_t)((q - sqrt(q * q - 8.0 * (double)p)) * 0.5);
+    if (i < 0) i = 0;
+    if (i > (int64_t)n - 2) i = (int64_t)n - 2;
+    while (i > 0 && off((uint64_t)i) > p) --i;
+    while ((uint64_t)i + 2 < n && off((uint64_t)i + 1) <= p) ++i;
+    const uint64_t j = p - off((uint64_t)i) + (uint64_t)i + 1;
+    const uint32_t a = oi[i], c = oi[j];
+    double row[4];
+    sift_pair_row(oc.x[a], oc.y[a], oc.c0[a], oc.c1[a], oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], row);
+    A0[r] = row[0];
+    A1[r] = row[1];
+    A2[r] = row[2];
+    b[r] = row[3];
+}
+
+// one wave per aligned block of kSumBlock rows: coalesced products into LDS,
+// then lane 0 folds them in row order (16-byte reads, 8 in flight)
+constexpr int kPartWaves = 4;
+__global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* __restrict__ a,
+                                                                 const double* __restrict__ c, uint64_t lo,
+                                                                 uint64_t hi, uint64_t blk0, uint64_t nblk,
+                                                                 double* __restrict__ partials) {
+    __shared__ double prod[kPartWaves][kSumBlock];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t blk = (uint64_t)blockIdx.x * kPartWaves + wave;
+    if (blk >= nblk) return;
+    const uint64_t base = (blk0 + blk) * kSumBlock;
+    const uint64_t b0 = base < lo ? lo : base;
+    const uint64_t b1 = base + kSumBlock < hi ? base + kSumBlock : hi;
+    double* pw = prod[wave];
+    for (uint64_t i = base + lane; i < base + kSumBlock; i += 64)
+        pw[i - base] = (i >= b0 && i < b1) ? a[i] * c[i] : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (lane == 0) {
+        // products outside [b0, b1) are +0.0 but still must not be added
+        // (0.0 + -x differs from -x only in the sign of zero: skip them)
+        double part = 0.0;
+        const double2* p2 = reinterpret_cast<const double2*>(pw);
+        const uint64_t e0 = b0 - base, e1 = b1 - base;
+        uint64_t e = e0;
+        if (e & 1) { part += pw[e]; ++e; }
+        for (; e + 16 <= e1; e += 16) {
+            double2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = p2[(e >> 1) + u];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { part += v[u].x; part += v[u].y; }
+        }
+        for (; e < e1; ++e) part += pw[e];
+        partials[blk] = part;
+    }
+}
+
+__global__ void k_qr_scale(double* c, uint64_t lo, uint64_t hi, double den) {
+    const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < hi) c[i] = c[i] / den;
+}
+__global__ void k_qr_zero(double* c, uint64_t lo, uint64_t hi) {
+    const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < hi) c[i] = 0.0;
+}
+__global__ void k_qr_update(double* c, const double* e, uint64_t lo, uint64_t hi, double tau, double t) {
+    const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < hi) c[i] -= (tau * e[i]) * t;
+}
+
 // ----------------------------------------------------------------- mask ----
 template <int KIND>
 __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, RectModel m, int rule, double T,
@@ -653,6 +745,48 @@ hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel*
         else if (h == 16) launch_split_t<16, 360>(p, T, models, inc, nh, out, stream);
         else launch_split_t<4, 960>(p, T, models, inc, nh, out, stream);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns,
+                            const uint32_t* oi, uint32_t no, size_t rows, double* A0, double* A1, double* A2,
+                            double* b, hipStream_t stream) {
+    if (rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sift_rows, dim3((unsigned)((rows + kRowBlock - 1) / kRowBlock)), dim3(kRowBlock), 0, stream,
+                       sc, oc, si, ns, oi, no, (uint64_t)rows, A0, A1, A2, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_qr_partials(const double* a, const double* c, size_t lo, size_t hi, double* partials,
+                              size_t* nblocks, hipStream_t stream) {
+    *nblocks = 0;
+    if (hi <= lo) return hipSuccess;
+    const uint64_t blk0 = lo / kSumBlock, nblk = (hi - 1) / kSumBlock - blk0 + 1;
+    *nblocks = nblk;
+    hipLaunchKernelGGL(k_qr_partials, dim3((unsigned)((nblk + kPartWaves - 1) / kPartWaves)), dim3(64 * kPartWaves),
+                       0, stream, a, c, (uint64_t)lo, (uint64_t)hi, blk0, nblk, partials);
+    return hipGetLastError();
+}
+
+hipError_t launch_qr_scale(double* c, size_t lo, size_t hi, double den, hipStream_t stream) {
+    if (hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(k_qr_scale, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, stream, c, (uint64_t)lo,
+                       (uint64_t)hi, den);
+    return hipGetLastError();
+}
+
+hipError_t launch_qr_zero(double* c, size_t lo, size_t hi, hipStream_t stream) {
+    if (hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(k_qr_zero, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, stream, c, (uint64_t)lo,
+                       (uint64_t)hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_qr_update(double* c, const double* e, size_t lo, size_t hi, double tau, double t,
+                            hipStream_t stream) {
+    if (hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(k_qr_update, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, stream, c, e,
+                       (uint64_t)lo, (uint64_t)hi, tau, t);
     return hipGetLastError();
 }
 

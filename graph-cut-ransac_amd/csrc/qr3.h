@@ -1,0 +1,166 @@
+// qr3.h -- least-squares solve of an m x 3 system by column-pivoted Householder
+// QR (Eigen ColPivHouseholderQR<MatrixX3d>::compute(A).solve(b), the solve the
+// reference's non-minimal fits call: three_sift.hpp:237, two_sift.hpp:524),
+// written once against a storage backend so that the host (LO fits, small
+// systems) and the GPU (the hybrid final refit's ~n_o^2/2 pair rows) run the
+// same control flow and the same per-element arithmetic.
+//
+// Reductions use ONE fixed order, blocked_sum: sequential inside aligned blocks
+// of kSumBlock rows, then the block partials sequentially.  Eigen's own order
+// is packet-vectorised and unpinned (no Eigen here); for m <= kSumBlock the
+// blocked order is plain sequential summation.  The oracle restates the same
+// order (oracle/gcr_oracle.cpp), so host, GPU and oracle agree bitwise.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstddef>
+#include <limits>
+#include <utility>
+
+namespace gcr {
+
+constexpr size_t kSumBlock = 1024;
+
+// sum_{i in [lo, hi)} f(i) in blocked order
+template <class F>
+inline double blocked_sum(size_t lo, size_t hi, F f) {
+    double total = 0.0;
+    size_t i = lo;
+    while (i < hi) {
+        const size_t end = std::min(hi, (i / kSumBlock + 1) * kSumBlock);
+        double part = 0.0;
+        for (; i < end; ++i) part += f(i);
+        total += part;
+    }
+    return total;
+}
+
+// Backend S stores 4 columns of length m: 0..2 = A, 3 = b, and provides
+//   double sumsq(c, lo, hi)             blocked sum of col[c][i]^2
+//   double dot(a, c, lo, hi)            blocked sum of col[a][i] * col[c][i]
+//   double get(c, i); void set(c, i, v)
+//   void scale(c, lo, hi, den)          col[c][i] = col[c][i] / den
+//   void zero(c, lo, hi)
+//   void update(c, e, lo, hi, tau, t)   col[c][i] -= (tau * col[e][i]) * t
+template <class S>
+void qr3_solve(S& st, size_t m, double x[3]) {
+    constexpr size_t cols = 3;
+    auto sq = [](double v) { return v * v; };
+    const size_t size = std::min(m, cols);
+    int pc[3] = {0, 1, 2};                 // logical -> stored column (pivot swaps)
+    double tau_k[3] = {0, 0, 0};
+    size_t transp[3] = {0, 1, 2};
+    double nu[3], nd[3];
+    for (size_t k = 0; k < cols; ++k) {
+        nd[k] = std::sqrt(st.sumsq(pc[k], 0, m));
+        nu[k] = nd[k];
+    }
+    const double eps = std::numeric_limits<double>::epsilon();
+    double maxn = nu[0];
+    for (size_t k = 1; k < cols; ++k)
+        if (maxn < nu[k]) maxn = nu[k];
+    const double thr_helper = sq(maxn * eps) / (double)m;
+    const double downdate_thr = std::sqrt(eps);
+    size_t nonzero = size;
+
+    // H_k = I - tau v v^T applied to stored column c; v = (1, ess[k+1..m))
+    auto apply_reflector = [&](int ess, size_t k, double tau, int c) {
+        if (m - k == 1) {
+            st.set(c, k, st.get(c, k) * (1.0 - tau));
+            return;
+        }
+        if (tau == 0.0) return;
+        double t = st.dot(ess, c, k + 1, m);
+        const double ck = st.get(c, k);
+        t += ck;
+        st.set(c, k, ck - tau * t);
+        st.update(c, ess, k + 1, m, tau, t);
+    };
+
+    for (size_t k = 0; k < size; ++k) {
+        size_t big = k;
+        double bign = nu[k];
+        for (size_t j = k + 1; j < cols; ++j)
+            if (bign < nu[j]) { bign = nu[j]; big = j; }
+        if (nonzero == size && sq(bign) < thr_helper * (double)(m - k)) nonzero = k;
+        transp[k] = big;
+        if (k != big) {
+            std::swap(pc[k], pc[big]);
+            std::swap(nu[k], nu[big]);
+            std::swap(nd[k], nd[big]);
+        }
+        const int ck = pc[k];
+        const double tail = st.sumsq(ck, k + 1, m);
+        const double c0 = st.get(ck, k);
+        double tau, beta;
+        if (tail <= std::numeric_limits<double>::min()) {
+            tau = 0.0;
+            beta = c0;
+            st.zero(ck, k + 1, m);
+        } else {
+            beta = std::sqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            st.scale(ck, k + 1, m, c0 - beta);
+            tau = (beta - c0) / beta;
+        }
+        tau_k[k] = tau;
+        st.set(ck, k, beta);
+        for (size_t j = k + 1; j < cols; ++j) apply_reflector(ck, k, tau, pc[j]);
+        for (size_t j = k + 1; j < cols; ++j) {
+            if (nu[j] != 0.0) {
+                double temp = std::fabs(st.get(pc[j], k)) / nu[j];
+                temp = (1.0 + temp) * (1.0 - temp);
+                temp = temp < 0.0 ? 0.0 : temp;
+                const double temp2 = temp * sq(nu[j] / nd[j]);
+                if (temp2 <= downdate_thr) {
+                    nd[j] = std::sqrt(st.sumsq(pc[j], k + 1, m));
+                    nu[j] = nd[j];
+                } else {
+                    nu[j] *= std::sqrt(temp);
+                }
+            }
+        }
+    }
+    size_t perm[3] = {0, 1, 2};
+    for (size_t k = 0; k < size; ++k) std::swap(perm[k], perm[transp[k]]);
+    if (nonzero == 0) {
+        x[0] = x[1] = x[2] = 0.0;
+        return;
+    }
+    for (size_t k = 0; k < nonzero; ++k) apply_reflector(pc[k], k, tau_k[k], 3);
+    double c[3] = {st.get(3, 0), m > 1 ? st.get(3, 1) : 0.0, m > 2 ? st.get(3, 2) : 0.0};
+    for (size_t jj = nonzero; jj-- > 0;) {
+        c[jj] = c[jj] / st.get(pc[jj], jj);
+        for (size_t i = 0; i < jj; ++i) c[i] -= c[jj] * st.get(pc[jj], i);
+    }
+    for (size_t i = 0; i < nonzero; ++i) x[perm[i]] = c[i];
+    for (size_t i = nonzero; i < cols; ++i) x[perm[i]] = 0.0;
+}
+
+// Host storage: four column pointers of length m.
+struct HostQRStore {
+    double* col[4];
+    double sumsq(int c, size_t lo, size_t hi) const {
+        const double* p = col[c];
+        return blocked_sum(lo, hi, [p](size_t i) { return p[i] * p[i]; });
+    }
+    double dot(int a, int c, size_t lo, size_t hi) const {
+        const double* p = col[a];
+        const double* q = col[c];
+        return blocked_sum(lo, hi, [p, q](size_t i) { return p[i] * q[i]; });
+    }
+    double get(int c, size_t i) const { return col[c][i]; }
+    void set(int c, size_t i, double v) { col[c][i] = v; }
+    void scale(int c, size_t lo, size_t hi, double den) {
+        for (size_t i = lo; i < hi; ++i) col[c][i] = col[c][i] / den;
+    }
+    void zero(int c, size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) col[c][i] = 0.0;
+    }
+    void update(int c, int e, size_t lo, size_t hi, double tau, double t) {
+        for (size_t i = lo; i < hi; ++i) col[c][i] -= (tau * col[e][i]) * t;
+    }
+};
+
+}  // namespace gcr

@@ -207,6 +207,28 @@ GCR_HD void cross3(const double a[3], const double b[3], double o[3]) {
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+// One orientation-pair row of the hybrid non-minimal system
+// (setOrientationConstraint, two_sift.hpp:238-258): vp = l_i x l_j scaled by
+// 1 / max|vp| when that exceeds 1 (cwiseAbs().maxCoeff(), left fold), weight
+// w_i * w_j = 1 on the Python path; row (w vp0, w vp1, 0 | w vp2).
+GCR_HD void sift_pair_row(double xi, double yi, double ci, double si, double xj, double yj, double cj, double sj,
+                          double row[4]) {
+    double l1[3], l2[3], vp[3];
+    line_from(xi, yi, ci, si, l1);
+    line_from(xj, yj, cj, sj, l2);
+    cross3(l1, l2, vp);
+    const double a0 = __builtin_fabs(vp[0]), a1 = __builtin_fabs(vp[1]), a2 = __builtin_fabs(vp[2]);
+    double mx = (a0 < a1) ? a1 : a0;
+    mx = (mx < a2) ? a2 : mx;
+    if (mx > 1.0)
+        for (int q = 0; q < 3; ++q) vp[q] = vp[q] / mx;
+    const double w = 1.0 * 1.0;
+    row[0] = w * vp[0];
+    row[1] = w * vp[1];
+    row[2] = 0.0;
+    row[3] = w * vp[2];
+}
+
 // ------------------------------------------------------- minimal solvers ---
 // 3-SIFT minimal fit.  p[i] = pow(s_i, kScalePower) precomputed with glibc
 // (+1/3 for the new solver, -1/3 for the original one).

@@ -118,6 +118,7 @@ def _load():
     L.gcr_debug_math.argtypes = [vp, C.c_int, dp, dp, C.c_size_t, dp]
     L.gcr_host_fit_nonminimal.argtypes = [C.c_int, dp, C.c_size_t, dp, C.c_size_t, u32p, C.c_size_t, u32p,
                                           C.c_size_t, C.POINTER(RectModel)]
+    L.gcr_debug_fit_nonminimal.argtypes = [vp, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.POINTER(RectModel)]
     L.gcr_host_homography.argtypes = [C.POINTER(RectModel), dp]
     L.gcr_host_homography.restype = None
     return L

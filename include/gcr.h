@@ -151,6 +151,12 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
  * ((1.5 thr)^2), 2 = 1-class graph-cut labeling */
 int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* model, int cls, int rule,
                    uint8_t* mask_out);
+/* the LO / final-refit fit of the given index lists on the problem's features;
+ * use_gpu = 1 solves the hybrid least-squares system with the GPU refit path
+ * (k_sift_rows + device QR), 0 on the host; both are bit-identical.  Returns 1
+ * and the model, 0 if the fit is rejected, < 0 on error */
+int gcr_debug_fit_nonminimal(gcr_problem* prob, const uint32_t* idx0, size_t k0, const uint32_t* idx1, size_t k1,
+                             int use_gpu, gcr_rect_model* model_out);
 /* host-only (no GPU): the LO / final-refit least-squares fit of the given index
  * lists (RectifyingHomographyEstimator::estimateModelNonminimal,
  * rectifying_homography_estimator.h:164-227); returns 1 and the model, 0 if the

@@ -293,7 +293,25 @@ static bool faithful_subset(const std::vector<size_t>& indices, size_t N, std::v
 
 // ---------------------------------------------- ColPivHouseholderQR (Eigen) ----
 // Restatement of Eigen::ColPivHouseholderQR<MatrixX3d>::compute + solve for an
-// m x 3 column-major matrix; sums run in plain sequential order.
+// m x 3 column-major matrix.  Eigen reduces with packet-vectorised partial sums
+// (an order that cannot be pinned without Eigen); every reduction here uses the
+// engine's fixed blocked order instead: sequential within aligned blocks of
+// 1024 rows, then the block partials sequentially -- plain sequential order
+// for m <= 1024 (all LO fits), and what the GPU refit reproduces bitwise.
+static constexpr size_t kSumBlockRows = 1024;
+template <class F>
+static double bsum(size_t lo, size_t hi, F f) {
+    double total = 0.0;
+    for (size_t b0 = lo; b0 < hi;) {
+        const size_t b1 = std::min(hi, (b0 / kSumBlockRows + 1) * kSumBlockRows);
+        double part = 0.0;
+        for (size_t i = b0; i < b1; ++i) part += f(i);
+        total += part;
+        b0 = b1;
+    }
+    return total;
+}
+
 static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_t m, std::vector<double>& b,
                              double x[3]) {
     const size_t cols = 3, rows = m, size = std::min(rows, cols);
@@ -302,8 +320,7 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
     size_t transp[3] = {0, 1, 2};
     double normsU[3], normsD[3];
     for (size_t k = 0; k < cols; ++k) {
-        double s = 0;
-        for (size_t i = 0; i < rows; ++i) s += at(i, k) * at(i, k);
+        const double s = bsum(0, rows, [&](size_t i) { return at(i, k) * at(i, k); });
         normsD[k] = std::sqrt(s);
         normsU[k] = normsD[k];
     }
@@ -326,8 +343,7 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
             std::swap(normsD[k], normsD[big]);
         }
         // makeHouseholderInPlace on column k, rows k..m-1
-        double tail = 0;
-        for (size_t i = k + 1; i < rows; ++i) tail += at(i, k) * at(i, k);
+        const double tail = bsum(k + 1, rows, [&](size_t i) { return at(i, k) * at(i, k); });
         const double c0 = at(k, k);
         double tau, beta;
         const double tol = std::numeric_limits<double>::min();
@@ -349,8 +365,7 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
             for (size_t j = k + 1; j < cols; ++j) at(k, j) *= (1.0 - tau);
         } else if (tau != 0.0) {
             for (size_t j = k + 1; j < cols; ++j) {
-                double t = 0;
-                for (size_t i = k + 1; i < rows; ++i) t += at(i, k) * at(i, j);
+                double t = bsum(k + 1, rows, [&](size_t i) { return at(i, k) * at(i, j); });
                 t += at(k, j);
                 at(k, j) -= tau * t;
                 for (size_t i = k + 1; i < rows; ++i) at(i, j) -= (tau * at(i, k)) * t;
@@ -363,8 +378,7 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
                 temp = temp < 0.0 ? 0.0 : temp;
                 double temp2 = temp * sqr(normsU[j] / normsD[j]);
                 if (temp2 <= norm_downdate_threshold) {
-                    double s = 0;
-                    for (size_t i = k + 1; i < rows; ++i) s += at(i, j) * at(i, j);
+                    const double s = bsum(k + 1, rows, [&](size_t i) { return at(i, j) * at(i, j); });
                     normsD[j] = std::sqrt(s);
                     normsU[j] = normsD[j];
                 } else {
@@ -381,8 +395,7 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
         const double tau = hc[k];
         if (rows - k == 1) { b[k] *= (1.0 - tau); continue; }
         if (tau == 0.0) continue;
-        double t = 0;
-        for (size_t i = k + 1; i < rows; ++i) t += at(i, k) * b[i];
+        double t = bsum(k + 1, rows, [&](size_t i) { return at(i, k) * b[i]; });
         t += b[k];
         b[k] -= tau * t;
         for (size_t i = k + 1; i < rows; ++i) b[i] -= (tau * at(i, k)) * t;

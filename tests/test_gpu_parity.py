@@ -355,3 +355,27 @@ def test_gpu_solver_records_match_direct_calls():
         assert recs[i]["num_inliers"] == n
         assert np.array_equal(recs[i]["H"], H)
         assert recs[i]["model"]["h7"] == model.h7 and recs[i]["model"]["h8"] == model.h8
+
+
+# ------------------------------------------------------------ GPU refit ----
+@pytest.mark.parametrize("ks,ko", [(40, 46), (800, 120), (2000, 260), (2500, 2500)])
+def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko):
+    # the hybrid least-squares system (ns + C(no,2) rows, up to 3.1 M) built and
+    # solved on the GPU equals the host path and the oracle bit for bit
+    fs, fo, ts, to, _, _ = S.problem_m2(5000, 5000, seed=ks + 3 * ko)
+    rng = np.random.default_rng(ks + ko)
+    i0 = np.sort(rng.choice(np.flatnonzero(ts), size=ks, replace=False)).astype(np.uint32)
+    i1 = np.sort(rng.choice(np.flatnonzero(to), size=ko, replace=False)).astype(np.uint32)
+    prob = Problem(N.SOLVER_SIFT22, fs, fo)
+    u32 = C.POINTER(C.c_uint32)
+    out = []
+    for use_gpu in (1, 0):
+        m = N.RectModel()
+        rc = N.lib.gcr_debug_fit_nonminimal(prob.h, i0.ctypes.data_as(u32), len(i0), i1.ctypes.data_as(u32),
+                                            len(i1), use_gpu, C.byref(m))
+        assert rc == 1
+        out.append(np.array([m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi]))
+    assert np.array_equal(bits(out[0]), bits(out[1]))
+    if ko <= 260:
+        exp = O.fit_nonminimal(N.SOLVER_SIFT22, fs, fo, i0, i1)
+        assert np.array_equal(bits(out[0]), bits(exp))
