@@ -140,20 +140,11 @@ struct Buffer {              // one of temp_inner_inliers[2]
 
 }  // namespace
 
-struct gcr_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-};
-
-struct gcr_problem {
-    gcr_ctx* ctx = nullptr;
-    int solver = 0;
-    int K = 1;
-    HostClass hc[2];
-    double* dmem = nullptr;
-    DevProblem dp{};
-    // work buffers
+// Device and pinned work buffers of a problem.  A context keeps one shared
+// workspace that the one-shot entry points (gcr_rect_*) reuse call after call:
+// allocating and freeing pinned memory per call costs milliseconds.
+struct Workspace {
+    DevBuf<double> feat;                // feature SoA (make_problem)
     DevBuf<uint8_t> inc;
     DevBuf<RectModel> models;
     PinBuf<uint8_t> h_inc;
@@ -169,10 +160,26 @@ struct gcr_problem {
     DevBuf<double> rf_part;             // GPU refit: reduction block partials
     PinBuf<double> rf_hpart;
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
-    ~gcr_problem() {
+    ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
-        if (dmem) (void)hipFree(dmem);
     }
+};
+
+struct gcr_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    Workspace shared;                   // reused by the gcr_rect_* calls
+};
+
+struct gcr_problem {
+    gcr_ctx* ctx = nullptr;
+    int solver = 0;
+    int K = 1;
+    HostClass hc[2];
+    DevProblem dp{};
+    std::unique_ptr<Workspace> own;     // gcr_problem_create: private buffers
+    Workspace* w = nullptr;             // own.get() or &ctx->shared
 };
 
 namespace {
@@ -188,25 +195,25 @@ struct DevQRStore {
     double dot(int a, int c, size_t lo, size_t hi) {
         if (hi <= lo) return 0.0;
         size_t nb = (hi - 1) / kSumBlock - lo / kSumBlock + 1;
-        P->rf_part.ensure(nb);
-        P->rf_hpart.ensure(nb);
-        HIPC(launch_qr_partials(col[a], col[c], lo, hi, P->rf_part.p, &nb, s));
-        HIPC(hipMemcpyAsync(P->rf_hpart.p, P->rf_part.p, nb * sizeof(double), hipMemcpyDeviceToHost, s));
+        P->w->rf_part.ensure(nb);
+        P->w->rf_hpart.ensure(nb);
+        HIPC(launch_qr_partials(col[a], col[c], lo, hi, P->w->rf_part.p, &nb, s));
+        HIPC(hipMemcpyAsync(P->w->rf_hpart.p, P->w->rf_part.p, nb * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
         double total = 0.0;
-        for (size_t b = 0; b < nb; ++b) total += P->rf_hpart.p[b];
+        for (size_t b = 0; b < nb; ++b) total += P->w->rf_hpart.p[b];
         return total;
     }
     double sumsq(int c, size_t lo, size_t hi) { return dot(c, c, lo, hi); }
     double get(int c, size_t i) {
-        HIPC(hipMemcpyAsync(P->rf_hpart.p, col[c] + i, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(P->w->rf_hpart.p, col[c] + i, sizeof(double), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
-        return P->rf_hpart.p[0];
+        return P->w->rf_hpart.p[0];
     }
     void set(int c, size_t i, double v) {
         HIPC(hipStreamSynchronize(s));          // staging slot may still feed a copy
-        P->rf_hpart.p[0] = v;
-        HIPC(hipMemcpyAsync(col[c] + i, P->rf_hpart.p, sizeof(double), hipMemcpyHostToDevice, s));
+        P->w->rf_hpart.p[0] = v;
+        HIPC(hipMemcpyAsync(col[c] + i, P->w->rf_hpart.p, sizeof(double), hipMemcpyHostToDevice, s));
         HIPC(hipStreamSynchronize(s));
     }
     void scale(int c, size_t lo, size_t hi, double den) { HIPC(launch_qr_scale(col[c], lo, hi, den, s)); }
@@ -224,13 +231,13 @@ struct GpuSiftSolver final : SiftSystemSolver {
     void solve(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows, double x[3]) override {
         hipStream_t s = P->ctx->stream;
         const size_t ns = si.size(), no = oi.size();
-        P->rf_idx.ensure(ns + no);
-        P->rf_hpart.ensure(1);
-        HIPC(hipMemcpyAsync(P->rf_idx.p, si.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        HIPC(hipMemcpyAsync(P->rf_idx.p + ns, oi.data(), no * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        P->rf_A.ensure(4 * rows);
-        double* A = P->rf_A.p;
-        HIPC(launch_sift_rows(P->dp.cls[0], P->dp.cls[1], P->rf_idx.p, (uint32_t)ns, P->rf_idx.p + ns, (uint32_t)no,
+        P->w->rf_idx.ensure(ns + no);
+        P->w->rf_hpart.ensure(1);
+        HIPC(hipMemcpyAsync(P->w->rf_idx.p, si.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIPC(hipMemcpyAsync(P->w->rf_idx.p + ns, oi.data(), no * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        P->w->rf_A.ensure(4 * rows);
+        double* A = P->w->rf_A.p;
+        HIPC(launch_sift_rows(P->dp.cls[0], P->dp.cls[1], P->w->rf_idx.p, (uint32_t)ns, P->w->rf_idx.p + ns, (uint32_t)no,
                               rows, A, A + rows, A + 2 * rows, A + 3 * rows, s));
         HIPC(hipStreamSynchronize(s));          // index lists are pageable host vectors
         DevQRStore st{{A, A + rows, A + 2 * rows, A + 3 * rows}, s, P};
@@ -284,7 +291,7 @@ void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1
 }
 
 int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
-                 gcr_problem** out) {
+                 gcr_problem** out, bool shared_workspace = false) {
     if (!ctx || !out) return set_err(GCR_EINVAL, "null context or output pointer");
     if (solver < 0 || solver > 2) return set_err(GCR_EINVAL, "unknown solver %d", solver);
     const int K = solver == 2 ? 2 : 1;
@@ -305,9 +312,15 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     const size_t np[2] = {(ns[0] + 1) & ~size_t(1), (ns[1] + 1) & ~size_t(1)};
     const size_t total = 5 * (np[0] + np[1]);
     HIPC(hipSetDevice(ctx->device));
-    HIPC(hipMalloc(reinterpret_cast<void**>(&P->dmem), total * sizeof(double)));
-    HIPC(hipMemsetAsync(P->dmem, 0, total * sizeof(double), ctx->stream));
-    double* cur = P->dmem;
+    if (shared_workspace) {
+        P->w = &ctx->shared;
+    } else {
+        P->own.reset(new Workspace());
+        P->w = P->own.get();
+    }
+    P->w->feat.ensure(total);
+    HIPC(hipMemsetAsync(P->w->feat.p, 0, total * sizeof(double), ctx->stream));
+    double* cur = P->w->feat.p;
     P->dp.solver = solver;
     for (int c = 0; c < 2; ++c) {
         DevClass& d = P->dp.cls[c];
@@ -375,13 +388,13 @@ public:
             const size_t j = slot - chunk_begin;
             bool do_lo = false;
             ++it_;
-            const uint8_t inc = P_->h_inc.p[j];
+            const uint8_t inc = P_->w->h_inc.p[j];
             it_ += (uint64_t)inc - 1;
             ++slot;
             if (inc <= 101) {
-                const RectModel& model = P_->h_models.p[j];
-                const uint32_t rn[2] = {P_->sb.hn0.p[j], P_->sb.hn1.p[j]};
-                const HScore cur = finish(rn, P_->sb.hv0.p[j], P_->sb.hv1.p[j], P_->sb.htot.p[j]);
+                const RectModel& model = P_->w->h_models.p[j];
+                const uint32_t rn[2] = {P_->w->sb.hn0.p[j], P_->w->sb.hn1.p[j]};
+                const HScore cur = finish(rn, P_->w->sb.hv0.p[j], P_->w->sb.hv1.p[j], P_->w->sb.htot.p[j]);
                 bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
                 ++st_.hypotheses;
                 if (best_.sum < cur.sum && valid_model(model)) {
@@ -477,28 +490,28 @@ public:
         static_assert(sizeof(BatchRecord) == sizeof(gcr_batch_result), "record layout");
         static_assert(offsetof(BatchRecord, best_model) == offsetof(gcr_batch_result, best_model), "record layout");
         const auto t0 = Clock::now();
-        P_->inc.ensure(nslots); P_->models.ensure(nslots); P_->sb.ensure(nslots);
-        P_->recs.ensure(nb);
-        while (P_->evs.size() < 2 * (size_t)nb) {
+        P_->w->inc.ensure(nslots); P_->w->models.ensure(nslots); P_->w->sb.ensure(nslots);
+        P_->w->recs.ensure(nb);
+        while (P_->w->evs.size() < 2 * (size_t)nb) {
             hipEvent_t ev;
             HIPC(hipEventCreate(&ev));
-            P_->evs.push_back(ev);
+            P_->w->evs.push_back(ev);
         }
         const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t s0 = slot0 + (uint64_t)b * nslots;
-            HIPC(launch_generate(P_->dp, prm_.seed, s0, nslots, P_->inc.p, P_->models.p, s_));
-            HIPC(hipEventRecord(P_->evs[2 * b], s_));
-            HIPC(launch_score(P_->dp, Tm_, P_->models.p, P_->inc.p, nslots, true, P_->sb.dev(), s_));
-            HIPC(hipEventRecord(P_->evs[2 * b + 1], s_));
-            HIPC(launch_select(P_->solver, P_->sb.dev(), P_->inc.p, P_->models.p, nslots, s0, m32, Tm_,
-                               P_->recs.p + b, s_));
+            HIPC(launch_generate(P_->dp, prm_.seed, s0, nslots, P_->w->inc.p, P_->w->models.p, s_));
+            HIPC(hipEventRecord(P_->w->evs[2 * b], s_));
+            HIPC(launch_score(P_->dp, Tm_, P_->w->models.p, P_->w->inc.p, nslots, true, P_->w->sb.dev(), s_));
+            HIPC(hipEventRecord(P_->w->evs[2 * b + 1], s_));
+            HIPC(launch_select(P_->solver, P_->w->sb.dev(), P_->w->inc.p, P_->w->models.p, nslots, s0, m32, Tm_,
+                               P_->w->recs.p + b, s_));
         }
-        HIPC(hipMemcpyAsync(out, P_->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
+        HIPC(hipMemcpyAsync(out, P_->w->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
         for (uint32_t b = 0; b < nb; ++b) {
             float kms = 0;
-            HIPC(hipEventElapsedTime(&kms, P_->evs[2 * b], P_->evs[2 * b + 1]));
+            HIPC(hipEventElapsedTime(&kms, P_->w->evs[2 * b], P_->w->evs[2 * b + 1]));
             st_.ms_score_kernel += kms;
             st_.hypotheses += out[b].models;
         }
@@ -562,22 +575,22 @@ private:
     // Generate [s0, s0+B), then score only the slots the loop can still reach
     // (iterations can never pass max(min_it, max_it)).  Returns slots scored.
     uint64_t fetch_chunk(uint64_t s0, uint32_t B, uint64_t L) {
-        P_->inc.ensure(B); P_->models.ensure(B); P_->sb.ensure(B);
-        P_->h_inc.ensure(B); P_->h_models.ensure(B);
+        P_->w->inc.ensure(B); P_->w->models.ensure(B); P_->w->sb.ensure(B);
+        P_->w->h_inc.ensure(B); P_->w->h_models.ensure(B);
         auto t0 = Clock::now();
-        HIPC(launch_generate(P_->dp, prm_.seed, s0, B, P_->inc.p, P_->models.p, s_));
-        HIPC(hipMemcpyAsync(P_->h_inc.p, P_->inc.p, B, hipMemcpyDeviceToHost, s_));
+        HIPC(launch_generate(P_->dp, prm_.seed, s0, B, P_->w->inc.p, P_->w->models.p, s_));
+        HIPC(hipMemcpyAsync(P_->w->h_inc.p, P_->w->inc.p, B, hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
         st_.ms_generate += ms_since(t0);
         uint64_t itp = it_, cnt = 0;
-        while (cnt < B && itp < L) itp += P_->h_inc.p[cnt++];
+        while (cnt < B && itp < L) itp += P_->w->h_inc.p[cnt++];
         if (cnt == 0) cnt = 1;
         t0 = Clock::now();
         HIPC(hipEventRecord(P_->ctx->ev0, s_));
-        HIPC(launch_score(P_->dp, Tm_, P_->models.p, P_->inc.p, (uint32_t)cnt, true, P_->sb.dev(), s_));
+        HIPC(launch_score(P_->dp, Tm_, P_->w->models.p, P_->w->inc.p, (uint32_t)cnt, true, P_->w->sb.dev(), s_));
         HIPC(hipEventRecord(P_->ctx->ev1, s_));
-        P_->sb.d2h(cnt, s_);
-        HIPC(hipMemcpyAsync(P_->h_models.p, P_->models.p, cnt * sizeof(RectModel), hipMemcpyDeviceToHost, s_));
+        P_->w->sb.d2h(cnt, s_);
+        HIPC(hipMemcpyAsync(P_->w->h_models.p, P_->w->models.p, cnt * sizeof(RectModel), hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
         float kms = 0;
         HIPC(hipEventElapsedTime(&kms, P_->ctx->ev0, P_->ctx->ev1));
@@ -590,18 +603,18 @@ private:
 
     // Score explicit host models on the GPU (LO trials, refit, reconcile).
     void score_models(const RectModel* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */) {
-        P_->lo_models.ensure(n);
-        P_->lo_sb.ensure(n);
+        P_->w->lo_models.ensure(n);
+        P_->w->lo_sb.ensure(n);
         bool identity = true;
         for (uint32_t i = 0; i < n; ++i) identity = identity && identity_norm(models[i]);
-        HIPC(hipMemcpyAsync(P_->lo_models.p, models, n * sizeof(RectModel), hipMemcpyHostToDevice, s_));
-        HIPC(launch_score(P_->dp, Tm_, P_->lo_models.p, nullptr, n, identity, P_->lo_sb.dev(), s_));
-        P_->lo_sb.d2h(n, s_);
+        HIPC(hipMemcpyAsync(P_->w->lo_models.p, models, n * sizeof(RectModel), hipMemcpyHostToDevice, s_));
+        HIPC(launch_score(P_->dp, Tm_, P_->w->lo_models.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
+        P_->w->lo_sb.d2h(n, s_);
         HIPC(hipStreamSynchronize(s_));
         st_.launches += 1;
         for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t rn[2] = {P_->lo_sb.hn0.p[i], P_->lo_sb.hn1.p[i]};
-            out[i] = finish(rn, P_->lo_sb.hv0.p[i], P_->lo_sb.hv1.p[i], P_->lo_sb.htot.p[i]);
+            const uint32_t rn[2] = {P_->w->lo_sb.hn0.p[i], P_->w->lo_sb.hn1.p[i]};
+            out[i] = finish(rn, P_->w->lo_sb.hv0.p[i], P_->w->lo_sb.hv1.p[i], P_->w->lo_sb.htot.p[i]);
             raw_n[2 * i] = rn[0];
             raw_n[2 * i + 1] = K_ == 2 ? rn[1] : 0;
         }
@@ -611,17 +624,17 @@ private:
     // LO) the graph-cut labeling (rule 2).
     void inlier_lists(const RectModel& model, const double T[2], int rule, std::vector<uint32_t> lists[2]) {
         for (int c = 0; c < K_; ++c) {
-            P_->mask[c].ensure(N_[c]);
-            P_->h_mask[c].ensure(N_[c]);
-            HIPC(launch_mask(P_->dp, c, model, rule, T[c], prm_.spatial_coherence_weight, P_->mask[c].p, s_));
-            HIPC(hipMemcpyAsync(P_->h_mask[c].p, P_->mask[c].p, N_[c], hipMemcpyDeviceToHost, s_));
+            P_->w->mask[c].ensure(N_[c]);
+            P_->w->h_mask[c].ensure(N_[c]);
+            HIPC(launch_mask(P_->dp, c, model, rule, T[c], prm_.spatial_coherence_weight, P_->w->mask[c].p, s_));
+            HIPC(hipMemcpyAsync(P_->w->h_mask[c].p, P_->w->mask[c].p, N_[c], hipMemcpyDeviceToHost, s_));
         }
         HIPC(hipStreamSynchronize(s_));
         st_.launches += K_;
         for (int c = 0; c < 2; ++c) {
             lists[c].clear();
             if (c >= K_) continue;
-            const uint8_t* mk = P_->h_mask[c].p;
+            const uint8_t* mk = P_->w->h_mask[c].p;
             for (uint64_t i = 0; i < N_[c]; ++i)
                 if (mk[i]) lists[c].push_back((uint32_t)i);
         }
@@ -846,7 +859,7 @@ static int run_oneshot(gcr_ctx* ctx, int solver, const double* f0, size_t n0, co
     if (int e = check_params(params, solver)) return e;
     const auto t0 = Clock::now();
     gcr_problem* prob = nullptr;
-    int rc = gcr_problem_create(ctx, solver, f0, n0, f1, n1, &prob);
+    int rc = guard([&]() { return make_problem(ctx, solver, f0, n0, f1, n1, &prob, true); });
     if (rc != GCR_OK) return rc;
     const double setup = ms_since(t0);
     rc = gcr_problem_run(prob, params, m0, m1, H, model, stats);
@@ -877,12 +890,12 @@ int gcr_debug_generate(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_
     if (!prob || !inc_out || !models_out) return set_err(GCR_EINVAL, "null argument");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
-        prob->inc.ensure(nslots);
-        prob->models.ensure(nslots);
+        prob->w->inc.ensure(nslots);
+        prob->w->models.ensure(nslots);
         hipStream_t s = prob->ctx->stream;
-        HIPC(launch_generate(prob->dp, seed, slot0, nslots, prob->inc.p, prob->models.p, s));
-        HIPC(hipMemcpyAsync(inc_out, prob->inc.p, nslots, hipMemcpyDeviceToHost, s));
-        HIPC(hipMemcpyAsync(models_out, prob->models.p, nslots * sizeof(RectModel), hipMemcpyDeviceToHost, s));
+        HIPC(launch_generate(prob->dp, seed, slot0, nslots, prob->w->inc.p, prob->w->models.p, s));
+        HIPC(hipMemcpyAsync(inc_out, prob->w->inc.p, nslots, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(models_out, prob->w->models.p, nslots * sizeof(RectModel), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
         return GCR_OK;
     });
@@ -904,17 +917,17 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
                               models[i].phi};
             identity = identity && identity_norm(hm[i]);
         }
-        prob->lo_models.ensure(nmodels);
-        prob->lo_sb.ensure(nmodels);
-        HIPC(hipMemcpyAsync(prob->lo_models.p, hm.data(), nmodels * sizeof(RectModel), hipMemcpyHostToDevice, s));
-        HIPC(launch_score(prob->dp, T, prob->lo_models.p, nullptr, nmodels, identity, prob->lo_sb.dev(), s));
-        prob->lo_sb.d2h(nmodels, s);
+        prob->w->lo_models.ensure(nmodels);
+        prob->w->lo_sb.ensure(nmodels);
+        HIPC(hipMemcpyAsync(prob->w->lo_models.p, hm.data(), nmodels * sizeof(RectModel), hipMemcpyHostToDevice, s));
+        HIPC(launch_score(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, identity, prob->w->lo_sb.dev(), s));
+        prob->w->lo_sb.d2h(nmodels, s);
         HIPC(hipStreamSynchronize(s));
-        std::memcpy(n0, prob->lo_sb.hn0.p, nmodels * sizeof(uint32_t));
-        std::memcpy(n1, prob->lo_sb.hn1.p, nmodels * sizeof(uint32_t));
-        std::memcpy(v0, prob->lo_sb.hv0.p, nmodels * sizeof(double));
-        std::memcpy(v1, prob->lo_sb.hv1.p, nmodels * sizeof(double));
-        std::memcpy(tot, prob->lo_sb.htot.p, nmodels * sizeof(double));
+        std::memcpy(n0, prob->w->lo_sb.hn0.p, nmodels * sizeof(uint32_t));
+        std::memcpy(n1, prob->w->lo_sb.hn1.p, nmodels * sizeof(uint32_t));
+        std::memcpy(v0, prob->w->lo_sb.hv0.p, nmodels * sizeof(double));
+        std::memcpy(v1, prob->w->lo_sb.hv1.p, nmodels * sizeof(double));
+        std::memcpy(tot, prob->w->lo_sb.htot.p, nmodels * sizeof(double));
         return GCR_OK;
     });
 }
@@ -932,10 +945,10 @@ int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_m
         else { const double t = 1.5 * thr; T = t * t; }
         const RectModel m{model->x0, model->y0, model->s, model->h7, model->h8, model->alpha, model->phi};
         const size_t n = prob->hc[cls].n;
-        prob->mask[cls].ensure(n);
+        prob->w->mask[cls].ensure(n);
         HIPC(launch_mask(prob->dp, cls, m, rule == 2 ? 2 : 0, T, params->spatial_coherence_weight,
-                         prob->mask[cls].p, s));
-        HIPC(hipMemcpyAsync(mask_out, prob->mask[cls].p, n, hipMemcpyDeviceToHost, s));
+                         prob->w->mask[cls].p, s));
+        HIPC(hipMemcpyAsync(mask_out, prob->w->mask[cls].p, n, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
         return GCR_OK;
     });

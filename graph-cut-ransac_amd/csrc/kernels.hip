@@ -571,8 +571,18 @@ __global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* _
     const uint64_t b0 = base < lo ? lo : base;
     const uint64_t b1 = base + kSumBlock < hi ? base + kSumBlock : hi;
     double* pw = prod[wave];
-    for (uint64_t i = base + lane; i < base + kSumBlock; i += 64)
-        pw[i - base] = (i >= b0 && i < b1) ? a[i] * c[i] : 0.0;
+    // all 2 x 16 loads of the lane in flight before any product is stored
+    constexpr int kPerLane = kSumBlock / 64;
+    double av[kPerLane], cv[kPerLane];
+#pragma unroll
+    for (int q = 0; q < kPerLane; ++q) {
+        const uint64_t i = base + lane + 64 * q;
+        const uint64_t ii = (i >= b0 && i < b1) ? i : b0;
+        av[q] = a[ii];
+        cv[q] = c[ii];
+    }
+#pragma unroll
+    for (int q = 0; q < kPerLane; ++q) pw[lane + 64 * q] = av[q] * cv[q];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (lane == 0) {
