@@ -404,20 +404,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                     run += v.y;
                     if (dual) tot2 += v.y;
                 };
-                constexpr int kB = KIND == 2 ? 4 : 8;        // 16-byte reads per batch
-                if (np >= kB) {
+                // batches of kB 16-byte reads all in flight, then 2 kB adds:
+                // the fold is bound by LDS latency under the compute waves' load
+                constexpr int kB = KIND == 2 ? 10 : 12;
+                for (; j + kB <= np; j += kB) {
                     double2 v[kB];
 #pragma unroll
-                    for (int u = 0; u < kB; ++u) v[u] = col[u];
-                    for (j = kB; j + kB <= np; j += kB) {
-                        double2 w[kB];
-#pragma unroll
-                        for (int u = 0; u < kB; ++u) w[u] = col[j + u];
-#pragma unroll
-                        for (int u = 0; u < kB; ++u) fold2(v[u]);
-#pragma unroll
-                        for (int u = 0; u < kB; ++u) v[u] = w[u];
-                    }
+                    for (int u = 0; u < kB; ++u) v[u] = col[j + u];
 #pragma unroll
                     for (int u = 0; u < kB; ++u) fold2(v[u]);
                 }
@@ -698,15 +691,21 @@ void launch_score_t(const DevProblem& p, const double T[2], const RectModel* mod
     }
 }
 
+// band constants of the conservative prefilters: exp(1.5 thr) bounds the
+// rectified log-scale residual, tan(1.5 thr) the rectified angular one (host
+// libm; the in-kernel tests widen them further)
+void band_consts(const double T[2], double& band0, double& tan_tau1) {
+    band0 = exp(sqrt(T[0] / 2.25) * 1.5) * (1.0 + 1e-9);
+    const double tau1 = sqrt(T[1]);
+    tan_tau1 = (tau1 < 0.7) ? tan(tau1) * (1.0 + 1e-6) + 1e-300 : HUGE_VAL;
+}
+
 template <int H, int R>
 void launch_split_t(const DevProblem& p, const double T[2], const RectModel* models, const uint8_t* inc, uint32_t nh,
                     const ScoreOut& out, hipStream_t stream) {
     const dim3 grid((nh + H - 1) / H), block(kSplitThreads);
-    // band constants: exp(1.5 thr) bounds the rectified log-scale residual,
-    // tan(1.5 thr) the rectified angular one (host libm; margins in-kernel)
-    const double band0 = exp(sqrt(T[0] / 2.25) * 1.5) * (1.0 + 1e-9);
-    const double tau1 = sqrt(T[1]);
-    const double tan_tau1 = (tau1 < 0.7) ? tan(tau1) * (1.0 + 1e-6) + 1e-300 : HUGE_VAL;
+    double band0, tan_tau1;
+    band_consts(T, band0, tan_tau1);
     switch (p.solver) {
         case 0: hipLaunchKernelGGL((k_score_split<0, H, R>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out); break;
         case 1: hipLaunchKernelGGL((k_score_split<1, H, R>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out); break;
