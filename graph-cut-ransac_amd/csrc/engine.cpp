@@ -155,6 +155,7 @@ struct Workspace {
     DevBuf<uint8_t> mask[2];
     PinBuf<uint8_t> h_mask[2];
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
+    DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
     DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
     DevBuf<double> rf_part;             // GPU refit: reduction block partials
@@ -484,8 +485,8 @@ public:
 
     // One hot-path batch (bench): generate + score + first strict maximum.
     // `nb` back-to-back batches of `nslots` slots starting at slot0, each
-    // generated, scored and reduced to its first strict best on the device
-    // (k_select); one host synchronisation at the end.
+    // generated, scored and reduced to its first strict best on the device by
+    // the fused scorer (launch_verify_fused); one host synchronisation at the end.
     void verify_batches(uint64_t slot0, uint32_t nslots, uint32_t nb, gcr_batch_result* out) {
         static_assert(sizeof(BatchRecord) == sizeof(gcr_batch_result), "record layout");
         static_assert(offsetof(BatchRecord, best_model) == offsetof(gcr_batch_result, best_model), "record layout");
@@ -498,14 +499,13 @@ public:
             P_->w->evs.push_back(ev);
         }
         const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
+        const size_t wg_cap = (nslots + 3) / 4;
+        P_->w->wg.ensure(wg_cap);
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t s0 = slot0 + (uint64_t)b * nslots;
-            HIPC(launch_generate(P_->dp, prm_.seed, s0, nslots, P_->w->inc.p, P_->w->models.p, s_));
-            HIPC(hipEventRecord(P_->w->evs[2 * b], s_));
-            HIPC(launch_score(P_->dp, Tm_, P_->w->models.p, P_->w->inc.p, nslots, true, P_->w->sb.dev(), s_));
-            HIPC(hipEventRecord(P_->w->evs[2 * b + 1], s_));
-            HIPC(launch_select(P_->solver, P_->w->sb.dev(), P_->w->inc.p, P_->w->models.p, nslots, s0, m32, Tm_,
-                               P_->w->recs.p + b, s_));
+            HIPC(launch_verify_fused(P_->dp, Tm_, prm_.seed, s0, nslots, m32, P_->w->inc.p, P_->w->models.p,
+                                     P_->w->sb.dev(), P_->w->wg.p, wg_cap, P_->w->recs.p + b, P_->w->evs[2 * b],
+                                     P_->w->evs[2 * b + 1], s_));
         }
         HIPC(hipMemcpyAsync(out, P_->w->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
@@ -515,7 +515,7 @@ public:
             st_.ms_score_kernel += kms;
             st_.hypotheses += out[b].models;
         }
-        st_.launches += 3 * nb;
+        st_.launches += 2 * nb;
         st_.hypotheses_computed += (uint64_t)nslots * nb;
         st_.ms_total += ms_since(t0);
     }

@@ -87,6 +87,23 @@ hipError_t launch_qr_zero(double* c, size_t lo, size_t hi, hipStream_t stream);
 hipError_t launch_qr_update(double* c, const double* e, size_t lo, size_t hi, double tau, double t,
                             hipStream_t stream);
 
+// Fused verify step (gcr_problem_verify_batches): the scorer generates its own
+// hypotheses (slots slot0 .. slot0 + nslots) in a prologue -- exactly
+// k_generate's lowest-successful-attempt rule -- writes inc / models / raw
+// scores like the separate kernels, and each workgroup reduces its slots to
+// their first strict best (WgBest); k_select_wg then reduces the workgroups.
+struct WgBest {
+    double score;        // finished MSAC score of the best slot (0 if none)
+    int32_t slot;        // slot offset in the batch, -1 if none
+    uint32_t n0, n1;     // its raw inlier counts
+    uint32_t models;     // slots of the workgroup with a model (inc <= 101)
+    uint64_t iterations; // sum of the workgroup's inc
+};
+hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t seed, uint64_t slot0,
+                               uint32_t nslots, const uint32_t m[2], uint8_t* inc, RectModel* models,
+                               const ScoreOut& out, WgBest* wg, size_t wg_cap, BatchRecord* rec,
+                               hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)
 // rule 2: 1-class graph-cut labeling with weight lambda, T = (1.5 thr)^2

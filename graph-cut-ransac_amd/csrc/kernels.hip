@@ -205,11 +205,20 @@ __device__ __forceinline__ bool orient_band(double x, double y, double ct, doubl
     return !(__builtin_fmin(u, v) > tan_tau * __builtin_fmax(u, v));
 }
 
-template <int KIND, int H, int R>
+// in-kernel generation + per-workgroup selection (kGen), see kernels.h
+struct GenArgs {
+    uint64_t seed, slot0;
+    uint8_t* inc;
+    RectModel* models;
+    WgBest* wg;
+    uint32_t m0, m1;
+};
+
+template <int KIND, int H, int R, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, double T0, double T1, double band0,
                                                                double tan_tau1, const RectModel* __restrict__ models,
                                                                const uint8_t* __restrict__ inc, uint32_t nh,
-                                                               ScoreOut out) {
+                                                               ScoreOut out, GenArgs gen) {
     static_assert((H * R) % kComputeThreads == 0 && kComputeThreads % H == 0, "tile shape");
     static_assert(H * R <= 65536, "queue entries are 16-bit tile indices");
     constexpr int kPer = H * R / kComputeThreads;    // pairs per compute thread per round
@@ -238,8 +247,6 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     const bool chain_lane = chain_wave && lane < (kSplitTot ? 2 * H : H);
     const int fsub = t / H;
     const uint32_t hg = blockIdx.x * H + h;
-    const bool valid_h = hg < nh && (inc == nullptr || inc[hg] <= 101);
-    const bool live = !chain_wave && valid_h;
 
     const uint32_t n0 = p.cls[0].n;
     const uint32_t n1 = (KIND == 2) ? p.cls[1].n : 0;
@@ -286,9 +293,41 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
         }
     };
 
+    // kGen: draw this workgroup's H slots, G = 1024 / H lanes per slot trying
+    // attempts r*G + g in parallel; the lowest success wins (k_generate's rule)
+    __shared__ int gen_a[kGen ? H : 1];
+    __shared__ RectModel gen_m[kGen ? H : 1];
+    if constexpr (kGen) {
+        constexpr int G = kSplitThreads / H;
+        if (t < H) gen_a[t] = 127;
+        __syncthreads();
+        const int gh = t / G, g = t % G;
+        const uint32_t gs = blockIdx.x * H + gh;
+        for (uint32_t rr = 0; rr * G < 101; ++rr) {
+            const uint32_t a = rr * G + g;
+            RectModel m = default_model();
+            bool ok = false;
+            if (gs < nh && a < 101 && gen_a[gh] == 127) ok = attempt<KIND>(p, gen.seed, gen.slot0 + gs, a, m);
+            if (ok) atomicMin(&gen_a[gh], (int)a);
+            __syncthreads();
+            if (ok && gen_a[gh] == (int)a) gen_m[gh] = m;
+            bool all = true;
+            for (int q = 0; q < H; ++q) all = all && (gen_a[q] != 127 || blockIdx.x * H + q >= nh);
+            __syncthreads();
+            if (all) break;
+        }
+        if (t < H && hg < nh) {
+            const int a = gen_a[t];
+            gen.inc[hg] = (uint8_t)(a == 127 ? 102 : a + 1);
+            gen.models[hg] = a == 127 ? default_model() : gen_m[t];
+        }
+    }
+    const bool valid_h = hg < nh && (kGen ? gen_a[h] != 127 : (inc == nullptr || inc[hg] <= 101));
+    const bool live = !chain_wave && valid_h;
+
     if (t < H) {
-        const bool v = hg < nh && (inc == nullptr || inc[hg] <= 101);
-        const RectModel m = v ? models[hg] : default_model();
+        const bool v = valid_h;
+        const RectModel m = v ? (kGen ? gen_m[h] : models[hg]) : default_model();
         HypConst q;
         q.h7 = m.h7;
         q.h8 = m.h8;
@@ -419,6 +458,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
         }
         __syncthreads();
     }
+    __shared__ double fin_sh[kGen ? H : 1];
     if (chain_wave) {
         double tot;
         if constexpr (kSplitTot) tot = __shfl(run, (lane + H) & 63);
@@ -427,11 +467,52 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
         if (lane < H && hg < nh) {
             const double acc0 = KIND == 2 ? hold : run;
             const double acc1 = KIND == 2 ? run : 0.0;
-            out.n0[hg] = valid_h ? cnt_sh[0][h] : 0;
-            out.n1[hg] = valid_h ? cnt_sh[1][h] : 0;
+            const uint32_t c0 = valid_h ? cnt_sh[0][h] : 0, c1 = valid_h ? cnt_sh[1][h] : 0;
+            out.n0[hg] = c0;
+            out.n1[hg] = c1;
             out.v0[hg] = valid_h ? acc0 : 0.0;
             out.v1[hg] = valid_h ? acc1 : 0.0;
             out.tot[hg] = valid_h ? tot : 0.0;
+            if constexpr (kGen) {
+                // MSACScoringFunction::getScore finish (MSAC_scoring_function.hpp:108-127)
+                double sum = 0.0;
+                if (valid_h && c0 >= gen.m0 && (KIND != 2 || c1 >= gen.m1)) {
+                    sum = tot;
+                    const double ms0 = acc0 / T0 + static_cast<double>(c0);
+                    sum -= acc0;
+                    sum += ms0;
+                    if (KIND == 2) {
+                        const double ms1 = acc1 / T1 + static_cast<double>(c1);
+                        sum -= acc1;
+                        sum += ms1;
+                    }
+                }
+                // candidates of the update rule: score > 0 and a valid model
+                const bool cand = valid_h && sum > 0.0 && (KIND != 2 || valid_model_sift22(gen_m[h]));
+                fin_sh[h] = cand ? sum : -1.0;
+            }
+        }
+        if constexpr (kGen) {
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                // the workgroup's first strict best, slots in order
+                WgBest b{0.0, -1, 0, 0, 0, 0};
+                for (int q = 0; q < H; ++q) {
+                    const uint32_t gq = blockIdx.x * H + q;
+                    if (gq >= nh) break;
+                    const int a = gen_a[q];
+                    b.iterations += (uint64_t)(a == 127 ? 102 : a + 1);
+                    if (a != 127) ++b.models;
+                    const double s = fin_sh[q];
+                    if (s > 0.0 && b.score < s) {
+                        b.score = s;
+                        b.slot = (int32_t)gq;
+                        b.n0 = cnt_sh[0][q];
+                        b.n1 = KIND == 2 ? cnt_sh[1][q] : 0;
+                    }
+                }
+                gen.wg[blockIdx.x] = b;
+            }
         }
     }
 }
@@ -611,6 +692,59 @@ __global__ void k_qr_update(double* c, const double* e, uint64_t lo, uint64_t hi
     if (i < hi) c[i] -= (tau * e[i]) * t;
 }
 
+// workgroup records -> one BatchRecord: first strict best over workgroups in
+// order (= slots in order), ties to the lower slot
+__global__ __launch_bounds__(kSelectThreads) void k_select_wg(const WgBest* __restrict__ wg, uint32_t nwg,
+                                                              const RectModel* __restrict__ models, uint64_t slot0,
+                                                              BatchRecord* out) {
+    __shared__ double s_val[kSelectThreads];
+    __shared__ int32_t s_slot[kSelectThreads];
+    __shared__ uint32_t s_n0[kSelectThreads], s_n1[kSelectThreads];
+    __shared__ unsigned long long s_models[kSelectThreads], s_its[kSelectThreads];
+    const int t = threadIdx.x;
+    double best = 0.0;
+    int32_t bs = -1;
+    uint32_t b0 = 0, b1 = 0;
+    unsigned long long nm = 0, its = 0;
+    for (uint32_t j = t; j < nwg; j += kSelectThreads) {
+        const WgBest w = wg[j];
+        nm += w.models;
+        its += w.iterations;
+        if (w.slot >= 0 && best < w.score) { best = w.score; bs = w.slot; b0 = w.n0; b1 = w.n1; }
+    }
+    s_val[t] = best; s_slot[t] = bs; s_n0[t] = b0; s_n1[t] = b1; s_models[t] = nm; s_its[t] = its;
+    __syncthreads();
+    for (int w = kSelectThreads / 2; w > 0; w >>= 1) {
+        if (t < w) {
+            const int32_t ia = s_slot[t], ib = s_slot[t + w];
+            const double va = s_val[t], vb = s_val[t + w];
+            if (ib >= 0 && (ia < 0 || vb > va || (vb == va && ib < ia))) {
+                s_slot[t] = ib; s_val[t] = vb; s_n0[t] = s_n0[t + w]; s_n1[t] = s_n1[t + w];
+            }
+            s_models[t] += s_models[t + w];
+            s_its[t] += s_its[t + w];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        BatchRecord r;
+        r.models = s_models[0];
+        r.iterations = s_its[0];
+        r.best_slot = -1;
+        r.best_score = 0.0;
+        r.best_inliers[0] = r.best_inliers[1] = 0;
+        r.best_model = default_model();
+        if (s_slot[0] >= 0) {
+            r.best_slot = (int64_t)(slot0 + (uint64_t)s_slot[0]);
+            r.best_score = s_val[0];
+            r.best_inliers[0] = s_n0[0];
+            r.best_inliers[1] = s_n1[0];
+            r.best_model = models[s_slot[0]];
+        }
+        *out = r;
+    }
+}
+
 // ----------------------------------------------------------------- mask ----
 template <int KIND>
 __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, RectModel m, int rule, double T,
@@ -707,9 +841,9 @@ void launch_split_t(const DevProblem& p, const double T[2], const RectModel* mod
     double band0, tan_tau1;
     band_consts(T, band0, tan_tau1);
     switch (p.solver) {
-        case 0: hipLaunchKernelGGL((k_score_split<0, H, R>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out); break;
-        case 1: hipLaunchKernelGGL((k_score_split<1, H, R>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out); break;
-        default: hipLaunchKernelGGL((k_score_split<2, H, R>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out); break;
+        case 0: hipLaunchKernelGGL((k_score_split<0, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, GenArgs{}); break;
+        case 1: hipLaunchKernelGGL((k_score_split<1, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, GenArgs{}); break;
+        default: hipLaunchKernelGGL((k_score_split<2, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, GenArgs{}); break;
     }
 }
 
@@ -796,6 +930,37 @@ hipError_t launch_qr_update(double* c, const double* e, size_t lo, size_t hi, do
     if (hi <= lo) return hipSuccess;
     hipLaunchKernelGGL(k_qr_update, dim3((unsigned)((hi - lo + 255) / 256)), dim3(256), 0, stream, c, e,
                        (uint64_t)lo, (uint64_t)hi, tau, t);
+    return hipGetLastError();
+}
+
+template <int H, int R>
+void launch_fused_t(const DevProblem& p, const double T[2], uint32_t nh, const ScoreOut& out, const GenArgs& g,
+                    hipStream_t stream) {
+    const dim3 grid((nh + H - 1) / H), block(kSplitThreads);
+    double band0, tan_tau1;
+    band_consts(T, band0, tan_tau1);
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL((k_score_split<0, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, nullptr, nullptr, nh, out, g); break;
+        case 1: hipLaunchKernelGGL((k_score_split<1, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, nullptr, nullptr, nh, out, g); break;
+        default: hipLaunchKernelGGL((k_score_split<2, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, nullptr, nullptr, nh, out, g); break;
+    }
+}
+
+hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t seed, uint64_t slot0,
+                               uint32_t nslots, const uint32_t m[2], uint8_t* inc, RectModel* models,
+                               const ScoreOut& out, WgBest* wg, size_t wg_cap, BatchRecord* rec,
+                               hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {
+    if (nslots == 0) return hipErrorInvalidValue;
+    const int h = split_h(nslots);
+    const uint32_t nwg = (nslots + h - 1) / h;
+    if (nwg > wg_cap) return hipErrorInvalidValue;
+    const GenArgs g{seed, slot0, inc, models, wg, m[0], m[1]};
+    if (ev0) (void)hipEventRecord(ev0, stream);
+    if (h == 64) launch_fused_t<64, 120>(p, T, nslots, out, g, stream);
+    else if (h == 16) launch_fused_t<16, 360>(p, T, nslots, out, g, stream);
+    else launch_fused_t<4, 960>(p, T, nslots, out, g, stream);
+    if (ev1) (void)hipEventRecord(ev1, stream);
+    hipLaunchKernelGGL(k_select_wg, dim3(1), dim3(kSelectThreads), 0, stream, wg, nwg, models, slot0, rec);
     return hipGetLastError();
 }
 
