@@ -7,11 +7,12 @@ rectification path on one MI355X): synthetic M2 problem,
 N_s = 5000 scale + N_o = 5000 orientation features, 50 % outliers each, fp64.
 
 One step = one pass of the hot path over one batch: `--slots` (default 4096,
-configs[1]) outer-iteration slots are drawn (Philox), validated and solved
-(k_generate), every resulting model is MSAC-scored against all 10 000 features
-(k_score_split), and the batch's first strict best (the reference's update
-rule, GCRANSAC.h:440-446) is selected on the device (k_select).  The K timed
-steps are queued back to back on one HIP stream (gcr_problem_verify_batches)
+configs[1]) outer-iteration slots are drawn (Philox), validated and solved,
+every resulting model is MSAC-scored against all 10 000 features, and the
+batch's first strict best (the reference's update rule, GCRANSAC.h:440-446) is
+selected -- all on the device: one fused kernel (k_score_split<..., true>:
+in-kernel generation, exact MSAC sums, per-workgroup best) plus k_select_wg.
+The K timed steps are queued back to back on one HIP stream (gcr_problem_verify_batches)
 and bracketed by device synchronisation.  Features are uploaded once before
 timing (HBM-resident).  `value` is the whole-job hypotheses/s; the end-to-end
 latency of a full estimator call at confidence 0.99 (including LO and the
@@ -38,13 +39,12 @@ FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector fp64 spec
 
 
 def score_kernel_name(kind, slots):
-    """The split-scorer instantiation launch_score picks (kernels.hip split_h)."""
-    if os.environ.get("GCR_SCORE_KERNEL", "").startswith("n"):
-        return f"k_score<{kind}, true>"
+    """The fused generate+score instantiation launch_verify_fused picks
+    (kernels.hip split_h); the bench's step launches it plus k_select_wg."""
     h = int(os.environ.get("GCR_SPLIT_H", "0") or 0)
     if h not in (64, 16, 4):
         h = 64 if slots >= 16384 else 16 if slots >= 2048 else 4
-    return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 360), (4, 960)])[h]}>"
+    return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 360), (4, 960)])[h]}, true>"
 
 
 def traffic_per_launch(kernel, slots):

@@ -246,6 +246,17 @@ struct GpuSiftSolver final : SiftSystemSolver {
     }
 };
 
+// verify_batches records kernel-timing events on every n-th batch
+// (GCR_TIMING_STRIDE, default 1 = every batch)
+uint32_t timing_stride() {
+    static uint32_t v = [] {
+        const char* e = getenv("GCR_TIMING_STRIDE");
+        const long n = e ? atol(e) : 1;
+        return (uint32_t)(n < 1 ? 1 : n);
+    }();
+    return v;
+}
+
 // hybrid systems at least this tall are solved on the GPU (the host QR costs
 // ~15 ns/row; the GPU path ~0.3 ms + ~15 synchronisations)
 size_t gpu_refit_rows() {
@@ -501,20 +512,29 @@ public:
         const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
         const size_t wg_cap = (nslots + 3) / 4;
         P_->w->wg.ensure(wg_cap);
+        // score-kernel timing events on every `stride`-th batch
+        // (GCR_TIMING_STRIDE; default every batch)
+        const uint32_t stride = timing_stride();
+        uint32_t timed = 0;
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t s0 = slot0 + (uint64_t)b * nslots;
+            const bool t = b % stride == 0;
             HIPC(launch_verify_fused(P_->dp, Tm_, prm_.seed, s0, nslots, m32, P_->w->inc.p, P_->w->models.p,
-                                     P_->w->sb.dev(), P_->w->wg.p, wg_cap, P_->w->recs.p + b, P_->w->evs[2 * b],
-                                     P_->w->evs[2 * b + 1], s_));
+                                     P_->w->sb.dev(), P_->w->wg.p, wg_cap, P_->w->recs.p + b,
+                                     t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr,
+                                     s_));
+            timed += t;
         }
         HIPC(hipMemcpyAsync(out, P_->w->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
-        for (uint32_t b = 0; b < nb; ++b) {
+        float kms_sum = 0;
+        for (uint32_t q = 0; q < timed; ++q) {
             float kms = 0;
-            HIPC(hipEventElapsedTime(&kms, P_->w->evs[2 * b], P_->w->evs[2 * b + 1]));
-            st_.ms_score_kernel += kms;
-            st_.hypotheses += out[b].models;
+            HIPC(hipEventElapsedTime(&kms, P_->w->evs[2 * q], P_->w->evs[2 * q + 1]));
+            kms_sum += kms;
         }
+        st_.ms_score_kernel += timed ? kms_sum * (double)nb / (double)timed : 0.0;   // scaled to all batches
+        for (uint32_t b = 0; b < nb; ++b) st_.hypotheses += out[b].models;
         st_.launches += 2 * nb;
         st_.hypotheses_computed += (uint64_t)nslots * nb;
         st_.ms_total += ms_since(t0);

@@ -379,3 +379,62 @@ def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko):
     if ko <= 260:
         exp = O.fit_nonminimal(N.SOLVER_SIFT22, fs, fo, i0, i1)
         assert np.array_equal(bits(out[0]), bits(exp))
+
+
+# --------------------------------------------- band prefilter, adversarial ----
+def _boundary_problem(kind, rng, anchors, per=160, eps=(-1e-6, -1e-7, 0.0, 1e-7, 1e-6)):
+    """Features placed at the inlier boundary (+-1.5 thr relative offsets eps)
+    of each anchor model, at large coordinates; thresholds 0.05 / 1 degree."""
+    thr0, thr1 = 0.05, math.radians(1.0)
+    tau0, tau1 = 1.5 * thr0, 1.5 * thr1
+    fs, fo = [], []
+    for m in anchors:
+        h7, h8, alpha, phi = m[3], m[4], m[5], m[6]
+        ac = alpha ** 3
+        for _ in range(per):
+            x, y = rng.uniform(-5000, 5000, size=2)
+            t = 1.0 - h7 * x - h8 * y
+            e = eps[rng.integers(len(eps))] * rng.choice([-1, 1])
+            sgn = rng.choice([-1.0, 1.0])
+            if t > 0:
+                k = math.exp(sgn * tau0 * (1.0 + e))
+                s = t ** 3 * (ac * k if kind == N.SOLVER_SCALE3_ORIGINAL else k / ac)
+            else:
+                s = rng.uniform(0.5, 50)
+            fs.append((x, y, s))
+            if kind == N.SOLVER_SIFT22:
+                rm = pygcransac.RectifyingHomography()
+                rm.h7, rm.h8 = h7, h8
+                u, v = rng.uniform(-3000, 3000, size=2)
+                xo, yo = rm.unrectifiedPoint(u, v)
+                base = phi + (math.pi / 2 if rng.random() < 0.5 else 0.0)
+                th = rm.unrectifiedAngle(u, v, base + sgn * tau1 * (1.0 + e))
+                fo.append((xo, yo, th))
+    f0 = np.array(fs)
+    f1 = np.array(fo) if fo else None
+    return f0, f1, thr0, thr1
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_band_prefilter_is_conservative_at_the_threshold(kind):
+    # every split variant (fp32 band at H=64/16, fp64 band at H=4) must keep
+    # each pair the exact residual would accept: counts and running sums equal
+    # the oracle's bitwise on features placed within 1e-7 of the threshold
+    rng = np.random.default_rng(1000 + kind)
+    anchors = []
+    for i in range(12):
+        big = 2e-3 if i % 3 == 0 else 2e-4
+        anchors.append(np.array([0.0, 0.0, 1.0, *rng.uniform(-big, big, size=2), rng.uniform(0.3, 3.0),
+                                 rng.uniform(0, math.pi)]))
+    f0, f1, thr0, thr1 = _boundary_problem(kind, rng, anchors)
+    prob = Problem(kind, f0, f1)
+    refs = [O.score(kind, f0, f1, m, thr0, thr1) for m in anchors]
+    assert sum(r["counts"][0] for r in refs) > 100          # the boundary is populated
+    for nh in (300, 2048, 16384):
+        tiled = np.resize(np.array(anchors), (nh, 7))
+        n0, n1, v0, v1, tot = prob.score_raw(tiled, thr0, thr1)
+        for i in range(nh):
+            ref = refs[i % len(anchors)]
+            got = finish_score(kind, n0[i], n1[i], v0[i], v1[i], tot[i], thr0, thr1)
+            assert got["counts"] == [int(c) for c in ref["counts"]], (nh, i)
+            assert bits(got["value"]) == bits(ref["value"]), (nh, i)
