@@ -80,21 +80,32 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # "nccl" is RCCL on ROCm; GCR_DIST_BACKEND=gloo rehearses the multi-rank
+    # path on fewer GPUs than ranks (host tensors, ranks share devices)
+    backend = os.environ.get("GCR_DIST_BACKEND", "nccl")
     dist = None
+    coll_dev = None
+    from pygcransac import _native as N
+
+    ndev = max(1, N.lib.gcr_device_count())
+    device = local_rank % ndev
     if world > 1:
         import torch
         import torch.distributed as tdist
 
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(device)
+            coll_dev = torch.device("cuda", device)
+        else:
+            coll_dev = torch.device("cpu")
+        tdist.init_process_group(backend)
         dist = tdist
 
     import numpy as np
     import pygcransac
-    from pygcransac import _native as N
     from pygcransac import synthetic as S
 
-    ctx = N.context(local_rank)
+    ctx = N.context(device)
     seed = 20251121 + rank
     if args.workload == "m2":
         f0, f1, _, _, thr0, thr1 = S.problem_m2(5000, 5000, seed=seed)
@@ -138,7 +149,8 @@ def main():
         if dist is not None:
             import torch
 
-            torch.cuda.synchronize()
+            if backend == "nccl":
+                torch.cuda.synchronize()
             dist.barrier()
 
     if args.warmup:
@@ -155,7 +167,7 @@ def main():
     if dist is not None:
         import torch
 
-        dev = torch.device("cuda", local_rank)
+        dev = coll_dev
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -184,10 +196,10 @@ def main():
             t1 = time.perf_counter()
             if solver == N.SOLVER_SIFT22:
                 out = pygcransac.findRectifyingHomographySIFT(f0, f1, thr0, thr1, 0.0, 0, 10**7, 50, seed=100 + r,
-                                                              confidence=0.99, device=local_rank, return_stats=True)
+                                                              confidence=0.99, device=device, return_stats=True)
             else:
                 out = pygcransac.findRectifyingHomographyScaleOnly(f0, thr0, 0.0, 0, 10**7, 50, seed=100 + r,
-                                                                   confidence=0.99, device=local_rank,
+                                                                   confidence=0.99, device=device,
                                                                    return_stats=True)
             lat.append((time.perf_counter() - t1) * 1e3)
             last_stats = out[-1]
@@ -250,6 +262,7 @@ def main():
         print(json.dumps(line))
     N.lib.gcr_problem_destroy(prob)
     if dist is not None:
+        dist.barrier()          # rank 0's latency / CPU legs finish before teardown
         dist.destroy_process_group()
 
 
