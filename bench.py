@@ -44,7 +44,7 @@ def score_kernel_name(kind, slots):
     h = int(os.environ.get("GCR_SPLIT_H", "0") or 0)
     if h not in (64, 16, 4):
         h = 64 if slots >= 16384 else 16 if slots >= 2048 else 4
-    return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 360), (4, 960)])[h]}, true>"
+    return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, true>"
 
 
 def traffic_per_launch(kernel, slots):

@@ -885,7 +885,7 @@ hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel*
     else {
         const int h = split_h(nh);
         if (h == 64) launch_split_t<64, 120>(p, T, models, inc, nh, out, stream);
-        else if (h == 16) launch_split_t<16, 360>(p, T, models, inc, nh, out, stream);
+        else if (h == 16) launch_split_t<16, 420>(p, T, models, inc, nh, out, stream);
         else launch_split_t<4, 960>(p, T, models, inc, nh, out, stream);
     }
     return hipGetLastError();
@@ -957,7 +957,7 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
     const GenArgs g{seed, slot0, inc, models, wg, m[0], m[1]};
     if (ev0) (void)hipEventRecord(ev0, stream);
     if (h == 64) launch_fused_t<64, 120>(p, T, nslots, out, g, stream);
-    else if (h == 16) launch_fused_t<16, 360>(p, T, nslots, out, g, stream);
+    else if (h == 16) launch_fused_t<16, 420>(p, T, nslots, out, g, stream);
     else launch_fused_t<4, 960>(p, T, nslots, out, g, stream);
     if (ev1) (void)hipEventRecord(ev1, stream);
     hipLaunchKernelGGL(k_select_wg, dim3(1), dim3(kSelectThreads), 0, stream, wg, nwg, models, slot0, rec);
