@@ -44,7 +44,9 @@ def score_kernel_name(kind, slots):
     h = int(os.environ.get("GCR_SPLIT_H", "0") or 0)
     if h not in (64, 16, 4):
         h = 64 if slots >= 16384 else 16 if slots >= 2048 else 4
-    return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, true>"
+    # the homography path generates in k_generate<3, G> and scores unfused
+    fused = "false" if kind == 3 else "true"
+    return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, {fused}>"
 
 
 def traffic_per_launch(kernel, slots):
@@ -68,7 +70,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", choices=["m2", "m1"], default="m2")
+    ap.add_argument("--workload", choices=["m2", "m1", "h"], default="m2",
+                    help="m2: configs[1] hybrid rectification (headline); m1: scale-only; "
+                         "h: configs[2] 4-pt homography, N=5000, 50%% outliers")
     ap.add_argument("--slots", type=int, default=4096, help="outer-iteration slots (hypotheses) per launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-latency", action="store_true")
@@ -111,6 +115,11 @@ def main():
         f0, f1, _, _, thr0, thr1 = S.problem_m2(5000, 5000, seed=seed)
         solver = N.SOLVER_SIFT22
         workload = "M2 hybrid 2+2-SIFT rectification (findRectifyingHomographySIFT), 5000 scale + 5000 orientation"
+    elif args.workload == "h":
+        f0, _, _, thr0 = S.problem_h(5000, 0.5, seed=seed)
+        f1, thr1 = None, 0.0
+        solver = N.SOLVER_HOMOGRAPHY4
+        workload = "H 4-point homography (findHomography), 5000 correspondences"
     else:
         f0, _, thr0 = S.problem_m1(10_000, seed=seed)
         f1, thr1 = None, 0.0
@@ -181,11 +190,15 @@ def main():
         gathered = len(outs)
 
     value = models_total / elapsed
-    kind = 2 if solver == N.SOLVER_SIFT22 else 0
+    kind = {N.SOLVER_SIFT22: 2, N.SOLVER_HOMOGRAPHY4: 3}.get(solver, 0)
     kernel_name = score_kernel_name(kind, args.slots)
     avg_kernel_s = acc["kernel_ms"] / max(1, acc["launches"]) / 1e3
     models_per_launch = acc["models"] / max(1, acc["launches"])
-    bytes_per_launch = models_per_launch * 24.0 * n_total
+    # algorithmic bytes per hypothesis: one pass over the feature SoA the
+    # residual reads -- 3 doubles per rectification feature, 4 per
+    # correspondence (x1, y1, x2, y2)
+    bytes_per_feature = 32.0 if kind == 3 else 24.0
+    bytes_per_launch = models_per_launch * bytes_per_feature * n_total
     achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
 
     # wall time to 0.99 confidence: full estimator call (incl. upload, LO, refit)
@@ -194,7 +207,11 @@ def main():
         lat = []
         for r in range(3):
             t1 = time.perf_counter()
-            if solver == N.SOLVER_SIFT22:
+            if solver == N.SOLVER_HOMOGRAPHY4:
+                out = pygcransac.findHomography(f0, 960, 1280, 960, 1280, threshold=thr0, conf=0.99,
+                                                min_iters=0, max_iters=10**7, seed=100 + r, device=device,
+                                                return_stats=True)
+            elif solver == N.SOLVER_SIFT22:
                 out = pygcransac.findRectifyingHomographySIFT(f0, f1, thr0, thr1, 0.0, 0, 10**7, 50, seed=100 + r,
                                                               confidence=0.99, device=device, return_stats=True)
             else:
@@ -213,14 +230,19 @@ def main():
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_ffi as O
 
-        n_cal, s_cal, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, 64)
+        # rectification: the reference's own sampler (random_device + mt19937 +
+        # shuffle); homography (no reference, finding 0.1): the cheaper Philox
+        # draw, i.e. the stronger CPU baseline
+        smp = O.SAMPLER_PHILOX if kind == 3 else O.SAMPLER_FAITHFUL
+        smp_text = ("Philox counter sampler" if kind == 3
+                    else "reference-faithful random_device+mt19937+shuffle sampler")
+        n_cal, s_cal, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, 64, sampler=smp)
         rate = n_cal / max(s_cal, 1e-6)
         nslots = max(64, int(rate * args.cpu_seconds))
-        n_cpu, s_cpu, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, nslots)
+        n_cpu, s_cpu, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, nslots, sampler=smp)
         cpu = dict(value=n_cpu / s_cpu, unit="hypotheses/s", cores=1, kind="port",
                    sample=f"{nslots} outer-iteration slots of the same workload, CPU oracle (glibc math, "
-                          f"reference-faithful random_device+mt19937+shuffle sampler, -O2), single thread, "
-                          f"{s_cpu:.1f} s")
+                          f"{smp_text}, -O2), single thread, {s_cpu:.1f} s")
 
     if rank == 0:
         line = {
@@ -251,7 +273,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic_per_launch(kernel_name, args.slots),
                 "kernel": kernel_name,
-                "bytes_per_hypothesis": 24 * n_total,
+                "bytes_per_hypothesis": bytes_per_feature * n_total,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
                 "hypotheses_per_launch": models_per_launch,
             },

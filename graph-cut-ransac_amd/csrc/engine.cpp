@@ -132,9 +132,10 @@ struct HScore {
     double sum = 0.0;
 };
 
-struct Buffer {              // one of temp_inner_inliers[2]
+template <class M>
+struct BufferT {             // one of temp_inner_inliers[2]
     bool has = false;
-    RectModel model{};
+    M model{};
     uint64_t n[2] = {0, 0};  // list sizes (raw inlier counts of `model`)
 };
 
@@ -151,6 +152,8 @@ struct Workspace {
     PinBuf<RectModel> h_models;
     ScoreBufs sb;
     DevBuf<RectModel> lo_models;
+    DevBuf<GeoModel> gmodels, lo_gmodels;     // homography (solver 3)
+    PinBuf<GeoModel> h_gmodels;
     ScoreBufs lo_sb;
     DevBuf<uint8_t> mask[2];
     PinBuf<uint8_t> h_mask[2];
@@ -276,6 +279,19 @@ size_t gpu_refit_rows() {
 //                which fuses those adjacent cos/sin calls into sincos, and
 //                sincos differs from separate sin/cos in ~0.1% of arguments.
 void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1, size_t n1, HostClass* hc) {
+    if (solver == 3) {                       // correspondences (x1, y1, x2, y2)
+        HostClass& h = hc[0];
+        h.n = n0;
+        h.x.resize(n0); h.y.resize(n0); h.a.resize(n0); h.c0.resize(n0); h.c1.assign(n0, 0.0);
+        for (size_t i = 0; i < n0; ++i) {
+            h.x[i] = f0[4 * i];
+            h.y[i] = f0[4 * i + 1];
+            h.a[i] = f0[4 * i + 2];
+            h.c0[i] = f0[4 * i + 3];
+        }
+        hc[1] = HostClass{};
+        return;
+    }
     const int K = solver == 2 ? 2 : 1;
     const double kScalePower = (solver == 1) ? (-1.0 / 3.0) : (1.0 / 3.0);
     const double* src[2] = {f0, f1};
@@ -305,9 +321,9 @@ void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1
 int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
                  gcr_problem** out, bool shared_workspace = false) {
     if (!ctx || !out) return set_err(GCR_EINVAL, "null context or output pointer");
-    if (solver < 0 || solver > 2) return set_err(GCR_EINVAL, "unknown solver %d", solver);
+    if (solver < 0 || solver > 3) return set_err(GCR_EINVAL, "unknown solver %d", solver);
     const int K = solver == 2 ? 2 : 1;
-    const size_t m0 = solver == 2 ? 2 : 3;
+    const size_t m0 = solver == 2 ? 2 : solver == 3 ? 4 : 3;
     if (!f0 || (K == 2 && !f1)) return set_err(GCR_EINVAL, "null feature pointer");
     if (n0 < m0 || (K == 2 && n1 < 2))
         return set_err(GCR_EINTERNAL, "Data set smaller than minimal sample size for corresponding data type");
@@ -352,11 +368,93 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
 }
 
 // ---------------------------------------------------------------- runner ----
-class Runner {
+// Estimator traits of the host engine: model type, kernels and host fits of
+// the rectification solvers (0-2) and the homography (3).
+struct RectTraits {
+    using Model = RectModel;
+    static Model def() { return default_model(); }
+    static DevBuf<Model>& dmodels(Workspace* w) { return w->models; }
+    static PinBuf<Model>& hmodels(Workspace* w) { return w->h_models; }
+    static DevBuf<Model>& lomodels(Workspace* w) { return w->lo_models; }
+    static bool identity(const Model& m) { return identity_norm(m); }
+    static bool valid(int solver, const Model& m) { return solver == 2 ? valid_model_sift22(m) : true; }
+    static hipError_t generate(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, uint8_t* inc, Model* m,
+                               hipStream_t s) {
+        return launch_generate(P->dp, seed, s0, n, inc, m, s);
+    }
+    static hipError_t score(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t n,
+                            bool identity, const ScoreOut& out, hipStream_t s) {
+        return launch_score(P->dp, T, m, inc, n, identity, out, s);
+    }
+    static hipError_t mask(gcr_problem* P, int cls, const Model& m, int rule, double T, double lambda, uint8_t* mk,
+                           hipStream_t s) {
+        return launch_mask(P->dp, cls, m, rule, T, lambda, mk, s);
+    }
+    static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
+                             const uint32_t m[2], size_t wg_cap, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
+                             hipStream_t s) {
+        return launch_verify_fused(P->dp, Tm, seed, s0, n, m, P->w->inc.p, P->w->models.p, P->w->sb.dev(),
+                                   P->w->wg.p, wg_cap, rec, e0, e1, s);
+    }
+    // LO fits on the host; the final hybrid refit solves big systems on the GPU
+    static bool fit(gcr_problem* P, const std::vector<uint32_t>* lists, Model& out, bool final_refit) {
+        if (!final_refit) return fit_nonminimal(P->solver, P->hc, lists, out);
+        GpuSiftSolver gpu(P);
+        return fit_nonminimal(P->solver, P->hc, lists, out, &gpu, gpu_refit_rows());
+    }
+    static void output(const Model& m, double* H, gcr_rect_model* model_out) {
+        homography_of(m, H);
+        if (model_out) *model_out = gcr_rect_model{m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi};
+    }
+};
+
+struct GeoTraits {
+    using Model = GeoModel;
+    static Model def() { return default_geo(); }
+    static DevBuf<Model>& dmodels(Workspace* w) { return w->gmodels; }
+    static PinBuf<Model>& hmodels(Workspace* w) { return w->h_gmodels; }
+    static DevBuf<Model>& lomodels(Workspace* w) { return w->lo_gmodels; }
+    static bool identity(const Model&) { return true; }
+    static bool valid(int, const Model&) { return true; }
+    static hipError_t generate(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, uint8_t* inc, Model* m,
+                               hipStream_t s) {
+        return launch_generate_geo(P->dp, seed, s0, n, inc, m, s);
+    }
+    static hipError_t score(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t n, bool,
+                            const ScoreOut& out, hipStream_t s) {
+        return launch_score_geo(P->dp, T[0], m, inc, n, out, s);
+    }
+    static hipError_t mask(gcr_problem* P, int, const Model& m, int rule, double T, double lambda, uint8_t* mk,
+                           hipStream_t s) {
+        return launch_mask_geo(P->dp, m, rule, T, lambda, mk, s);
+    }
+    static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
+                             const uint32_t m[2], size_t, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
+                             hipStream_t s) {
+        hipError_t e = launch_generate_geo(P->dp, seed, s0, n, P->w->inc.p, P->w->gmodels.p, s);
+        if (e != hipSuccess) return e;
+        if (e0) (void)hipEventRecord(e0, s);
+        e = launch_score_geo(P->dp, Tm[0], P->w->gmodels.p, P->w->inc.p, n, P->w->sb.dev(), s);
+        if (e != hipSuccess) return e;
+        if (e1) (void)hipEventRecord(e1, s);
+        return launch_select_geo(P->w->sb.dev(), P->w->inc.p, n, s0, m[0], Tm[0], rec, s);
+    }
+    static bool fit(gcr_problem* P, const std::vector<uint32_t>* lists, Model& out, bool) {
+        return fit_h4_nonminimal(P->hc[0], lists[0], out);
+    }
+    static void output(const Model& m, double* H, gcr_rect_model*) {
+        for (int k = 0; k < 9; ++k) H[k] = m.h[k];
+    }
+};
+
+template <class Tr>
+class RunnerT {
 public:
-    Runner(gcr_problem* P, const gcr_params& prm) : P_(P), prm_(prm), s_(P->ctx->stream) {
+    using Model = typename Tr::Model;
+    using Buffer = BufferT<Model>;
+    RunnerT(gcr_problem* P, const gcr_params& prm) : P_(P), prm_(prm), s_(P->ctx->stream) {
         K_ = P->K;
-        m_[0] = P->solver == 2 ? 2 : 3;
+        m_[0] = P->solver == 2 ? 2 : P->solver == 3 ? 4 : 3;
         m_[1] = 2;
         thr_[0] = prm.scale_residual_thresh;
         thr_[1] = prm.orientation_residual_thresh;
@@ -404,7 +502,7 @@ public:
             it_ += (uint64_t)inc - 1;
             ++slot;
             if (inc <= 101) {
-                const RectModel& model = P_->w->h_models.p[j];
+                const Model& model = Tr::hmodels(P_->w).p[j];
                 const uint32_t rn[2] = {P_->w->sb.hn0.p[j], P_->w->sb.hn1.p[j]};
                 const HScore cur = finish(rn, P_->w->sb.hv0.p[j], P_->w->sb.hv1.p[j], P_->w->sb.htot.p[j]);
                 bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
@@ -432,7 +530,7 @@ public:
         st_.ms_replay = replay_ms;
 
         int total = 0;
-        RectModel out_model = default_model();
+        Model out_model = Tr::def();
         std::memset(mask0, 0, N_[0]);
         if (K_ == 2 && mask1) std::memset(mask1, 0, N_[1]);
         bool minimal = true;
@@ -459,9 +557,8 @@ public:
             // one non-minimal fit on the buffer's inliers, kept if strictly better.
             std::vector<uint32_t> lists[2];
             inlier_lists(bufs_[off_].model, Tm_, 0, lists);
-            RectModel refit;
-            GpuSiftSolver gpu(P_);
-            if (fit_nonminimal(P_->solver, P_->hc, lists, refit, &gpu, gpu_refit_rows())) {
+            Model refit;
+            if (Tr::fit(P_, lists, refit, true)) {
                 HScore s;
                 uint32_t rn[2];
                 score_models(&refit, 1, &s, rn);
@@ -480,11 +577,7 @@ public:
             st_.score = best_.sum;
             st_.ms_refit = ms_since(t_ref);
         }
-        homography_of(out_model, H);
-        if (model_out) {
-            *model_out = gcr_rect_model{out_model.x0, out_model.y0, out_model.s, out_model.h7,
-                                        out_model.h8, out_model.alpha, out_model.phi};
-        }
+        Tr::output(out_model, H, model_out);
         st_.iteration_number = it_;
         st_.local_optimization_number = lo_number_;
         st_.graph_cut_number = gc_number_;
@@ -502,7 +595,7 @@ public:
         static_assert(sizeof(BatchRecord) == sizeof(gcr_batch_result), "record layout");
         static_assert(offsetof(BatchRecord, best_model) == offsetof(gcr_batch_result, best_model), "record layout");
         const auto t0 = Clock::now();
-        P_->w->inc.ensure(nslots); P_->w->models.ensure(nslots); P_->w->sb.ensure(nslots);
+        P_->w->inc.ensure(nslots); Tr::dmodels(P_->w).ensure(nslots); P_->w->sb.ensure(nslots);
         P_->w->recs.ensure(nb);
         while (P_->w->evs.size() < 2 * (size_t)nb) {
             hipEvent_t ev;
@@ -519,10 +612,8 @@ public:
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t s0 = slot0 + (uint64_t)b * nslots;
             const bool t = b % stride == 0;
-            HIPC(launch_verify_fused(P_->dp, Tm_, prm_.seed, s0, nslots, m32, P_->w->inc.p, P_->w->models.p,
-                                     P_->w->sb.dev(), P_->w->wg.p, wg_cap, P_->w->recs.p + b,
-                                     t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr,
-                                     s_));
+            HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, P_->w->recs.p + b,
+                            t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr, s_));
             timed += t;
         }
         HIPC(hipMemcpyAsync(out, P_->w->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
@@ -554,12 +645,12 @@ private:
 
     uint64_t it_ = 0;
     HScore best_{};
-    RectModel best_model_ = default_model();
+    Model best_model_ = Tr::def();
     Buffer bufs_[2];
     int off_ = 0;
     uint64_t lo_number_ = 0, gc_number_ = 0;
 
-    bool valid_model(const RectModel& m) const { return P_->solver == 2 ? valid_model_sift22(m) : true; }
+    bool valid_model(const Model& m) const { return Tr::valid(P_->solver, m); }
 
     HScore finish(const uint32_t rn[2], double v0, double v1, double tot) const {
         HScore s;
@@ -595,10 +686,10 @@ private:
     // Generate [s0, s0+B), then score only the slots the loop can still reach
     // (iterations can never pass max(min_it, max_it)).  Returns slots scored.
     uint64_t fetch_chunk(uint64_t s0, uint32_t B, uint64_t L) {
-        P_->w->inc.ensure(B); P_->w->models.ensure(B); P_->w->sb.ensure(B);
-        P_->w->h_inc.ensure(B); P_->w->h_models.ensure(B);
+        P_->w->inc.ensure(B); Tr::dmodels(P_->w).ensure(B); P_->w->sb.ensure(B);
+        P_->w->h_inc.ensure(B); Tr::hmodels(P_->w).ensure(B);
         auto t0 = Clock::now();
-        HIPC(launch_generate(P_->dp, prm_.seed, s0, B, P_->w->inc.p, P_->w->models.p, s_));
+        HIPC(Tr::generate(P_, prm_.seed, s0, B, P_->w->inc.p, Tr::dmodels(P_->w).p, s_));
         HIPC(hipMemcpyAsync(P_->w->h_inc.p, P_->w->inc.p, B, hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
         st_.ms_generate += ms_since(t0);
@@ -607,10 +698,11 @@ private:
         if (cnt == 0) cnt = 1;
         t0 = Clock::now();
         HIPC(hipEventRecord(P_->ctx->ev0, s_));
-        HIPC(launch_score(P_->dp, Tm_, P_->w->models.p, P_->w->inc.p, (uint32_t)cnt, true, P_->w->sb.dev(), s_));
+        HIPC(Tr::score(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)cnt, true, P_->w->sb.dev(), s_));
         HIPC(hipEventRecord(P_->ctx->ev1, s_));
         P_->w->sb.d2h(cnt, s_);
-        HIPC(hipMemcpyAsync(P_->w->h_models.p, P_->w->models.p, cnt * sizeof(RectModel), hipMemcpyDeviceToHost, s_));
+        HIPC(hipMemcpyAsync(Tr::hmodels(P_->w).p, Tr::dmodels(P_->w).p, cnt * sizeof(Model), hipMemcpyDeviceToHost,
+                            s_));
         HIPC(hipStreamSynchronize(s_));
         float kms = 0;
         HIPC(hipEventElapsedTime(&kms, P_->ctx->ev0, P_->ctx->ev1));
@@ -622,13 +714,14 @@ private:
     }
 
     // Score explicit host models on the GPU (LO trials, refit, reconcile).
-    void score_models(const RectModel* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */) {
-        P_->w->lo_models.ensure(n);
+    void score_models(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */) {
+        auto& lm = Tr::lomodels(P_->w);
+        lm.ensure(n);
         P_->w->lo_sb.ensure(n);
         bool identity = true;
-        for (uint32_t i = 0; i < n; ++i) identity = identity && identity_norm(models[i]);
-        HIPC(hipMemcpyAsync(P_->w->lo_models.p, models, n * sizeof(RectModel), hipMemcpyHostToDevice, s_));
-        HIPC(launch_score(P_->dp, Tm_, P_->w->lo_models.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
+        for (uint32_t i = 0; i < n; ++i) identity = identity && Tr::identity(models[i]);
+        HIPC(hipMemcpyAsync(lm.p, models, n * sizeof(Model), hipMemcpyHostToDevice, s_));
+        HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
         P_->w->lo_sb.d2h(n, s_);
         HIPC(hipStreamSynchronize(s_));
         st_.launches += 1;
@@ -642,11 +735,11 @@ private:
 
     // Inlier index lists of one model: rule 0 with thresholds T, or (1-class
     // LO) the graph-cut labeling (rule 2).
-    void inlier_lists(const RectModel& model, const double T[2], int rule, std::vector<uint32_t> lists[2]) {
+    void inlier_lists(const Model& model, const double T[2], int rule, std::vector<uint32_t> lists[2]) {
         for (int c = 0; c < K_; ++c) {
             P_->w->mask[c].ensure(N_[c]);
             P_->w->h_mask[c].ensure(N_[c]);
-            HIPC(launch_mask(P_->dp, c, model, rule, T[c], prm_.spatial_coherence_weight, P_->w->mask[c].p, s_));
+            HIPC(Tr::mask(P_, c, model, rule, T[c], prm_.spatial_coherence_weight, P_->w->mask[c].p, s_));
             HIPC(hipMemcpyAsync(P_->w->h_mask[c].p, P_->w->mask[c].p, N_[c], hipMemcpyDeviceToHost, s_));
         }
         HIPC(hipStreamSynchronize(s_));
@@ -664,12 +757,13 @@ private:
     bool local_optimization(Buffer& sfb_buf) {
         const auto t0 = Clock::now();
         HScore max_score = best_;
-        RectModel lo_model = best_model_;
+        Model lo_model = best_model_;
         Buffer lo_buf;
         const uint64_t limit[2] = {7 * m_[0], 7 * m_[1]};
+
         ++lo_number_;
         std::vector<uint32_t> inl[2], sample[2];
-        std::vector<RectModel> trial_models;
+        std::vector<Model> trial_models;
         std::vector<HScore> trial_scores;
         std::vector<uint32_t> trial_raw;
         const uint64_t T = prm_.max_local_optimization_number;
@@ -703,8 +797,8 @@ private:
                     }
                 }
                 if (!ok) break;
-                RectModel fm;
-                if (!fit_nonminimal(P_->solver, P_->hc, sample, fm)) continue;
+                Model fm;
+                if (!Tr::fit(P_, sample, fm, false)) continue;
                 trial_models.push_back(fm);
             }
             if (!trial_models.empty()) {
@@ -734,6 +828,9 @@ private:
         return false;
     }
 };
+
+using Runner = RunnerT<RectTraits>;
+using GeoRunner = RunnerT<GeoTraits>;
 
 }  // namespace
 
@@ -845,10 +942,12 @@ int gcr_problem_run(gcr_problem* prob, const gcr_params* params, uint8_t* mask0_
     if (!mask0_out || !H_out || (prob->K == 2 && !mask1_out)) return set_err(GCR_EINVAL, "null output buffer");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
-        Runner r(prob, *params);
-        const int total = r.run(mask0_out, mask1_out, H_out, model_out);
-        fill_stats(stats_out, r.stats());
-        return total;
+        auto go = [&](auto&& r) {
+            const int total = r.run(mask0_out, mask1_out, H_out, model_out);
+            fill_stats(stats_out, r.stats());
+            return total;
+        };
+        return prob->solver == GCR_SOLVER_HOMOGRAPHY4 ? go(GeoRunner(prob, *params)) : go(Runner(prob, *params));
     });
 }
 
@@ -859,10 +958,12 @@ int gcr_problem_verify_batches(gcr_problem* prob, const gcr_params* params, uint
     if (nslots == 0 || nbatches == 0) return set_err(GCR_EINVAL, "nslots and nbatches must be > 0");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
-        Runner r(prob, *params);
-        r.verify_batches(slot0, nslots, nbatches, out);
-        fill_stats(stats_out, r.stats());
-        return GCR_OK;
+        auto go = [&](auto&& r) {
+            r.verify_batches(slot0, nslots, nbatches, out);
+            fill_stats(stats_out, r.stats());
+            return GCR_OK;
+        };
+        return prob->solver == GCR_SOLVER_HOMOGRAPHY4 ? go(GeoRunner(prob, *params)) : go(Runner(prob, *params));
     });
 }
 
@@ -902,6 +1003,89 @@ int gcr_rect_sift(gcr_ctx* ctx, const double* scale_features, size_t n_scale, co
                   uint8_t* orientation_mask_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out) {
     return run_oneshot(ctx, GCR_SOLVER_SIFT22, scale_features, n_scale, orientation_features, n_orientation, params,
                        scale_mask_out, orientation_mask_out, H_out, model_out, stats_out);
+}
+
+int gcr_find_homography(gcr_ctx* ctx, const double* correspondences, size_t n, const gcr_params* params,
+                        uint8_t* mask_out, double* H_out, gcr_stats* stats_out) {
+    return run_oneshot(ctx, GCR_SOLVER_HOMOGRAPHY4, correspondences, n, nullptr, 0, params, mask_out, nullptr, H_out,
+                       nullptr, stats_out);
+}
+
+// ------------------------------------------------------- homography debug ----
+int gcr_debug_generate_h(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc_out,
+                         double* H_out) {
+    if (!prob || !inc_out || !H_out) return set_err(GCR_EINVAL, "null argument");
+    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4) return set_err(GCR_EINVAL, "not a homography problem");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        prob->w->inc.ensure(nslots);
+        prob->w->gmodels.ensure(nslots);
+        hipStream_t s = prob->ctx->stream;
+        HIPC(launch_generate_geo(prob->dp, seed, slot0, nslots, prob->w->inc.p, prob->w->gmodels.p, s));
+        HIPC(hipMemcpyAsync(inc_out, prob->w->inc.p, nslots, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(H_out, prob->w->gmodels.p, nslots * sizeof(GeoModel), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        return GCR_OK;
+    });
+}
+
+int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double* H, uint32_t nmodels, uint32_t* n0,
+                      double* v0, double* tot) {
+    if (!prob || !params || !H || !n0 || !v0 || !tot) return set_err(GCR_EINVAL, "null argument");
+    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4) return set_err(GCR_EINVAL, "not a homography problem");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        hipStream_t s = prob->ctx->stream;
+        const double thr = params->scale_residual_thresh;
+        const double T = (2.25 * thr) * thr;
+        prob->w->lo_gmodels.ensure(nmodels);
+        prob->w->lo_sb.ensure(nmodels);
+        HIPC(hipMemcpyAsync(prob->w->lo_gmodels.p, H, nmodels * sizeof(GeoModel), hipMemcpyHostToDevice, s));
+        HIPC(launch_score_geo(prob->dp, T, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(), s));
+        prob->w->lo_sb.d2h(nmodels, s);
+        HIPC(hipStreamSynchronize(s));
+        std::memcpy(n0, prob->w->lo_sb.hn0.p, nmodels * sizeof(uint32_t));
+        std::memcpy(v0, prob->w->lo_sb.hv0.p, nmodels * sizeof(double));
+        std::memcpy(tot, prob->w->lo_sb.htot.p, nmodels * sizeof(double));
+        return GCR_OK;
+    });
+}
+
+int gcr_debug_mask_h(gcr_problem* prob, const gcr_params* params, const double* H, int rule, uint8_t* mask_out) {
+    if (!prob || !params || !H || !mask_out) return set_err(GCR_EINVAL, "null argument");
+    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4) return set_err(GCR_EINVAL, "not a homography problem");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        hipStream_t s = prob->ctx->stream;
+        const double thr = params->scale_residual_thresh;
+        double T;
+        if (rule == 0) T = (2.25 * thr) * thr;
+        else { const double t = 1.5 * thr; T = t * t; }
+        GeoModel m;
+        for (int k = 0; k < 9; ++k) m.h[k] = H[k];
+        const size_t n = prob->hc[0].n;
+        prob->w->mask[0].ensure(n);
+        HIPC(launch_mask_geo(prob->dp, m, rule == 2 ? 2 : 0, T, params->spatial_coherence_weight, prob->w->mask[0].p,
+                             s));
+        HIPC(hipMemcpyAsync(mask_out, prob->w->mask[0].p, n, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        return GCR_OK;
+    });
+}
+
+int gcr_host_fit_h(const double* correspondences, size_t n, const uint32_t* idx, size_t k, double* H_out) {
+    if (!correspondences || !idx || !H_out) return set_err(GCR_EINVAL, "bad arguments");
+    return guard([&]() -> int {
+        HostClass hc[2];
+        fill_host_classes(GCR_SOLVER_HOMOGRAPHY4, correspondences, n, nullptr, 0, hc);
+        std::vector<uint32_t> list(idx, idx + k);
+        for (uint32_t i : list)
+            if (i >= n) return set_err(GCR_EINVAL, "index out of range");
+        GeoModel m;
+        if (!fit_h4_nonminimal(hc[0], list, m)) return 0;
+        for (int q = 0; q < 9; ++q) H_out[q] = m.h[q];
+        return 1;
+    });
 }
 
 // ---------------------------------------------------------------- debug ----

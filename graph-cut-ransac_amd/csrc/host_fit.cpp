@@ -202,4 +202,68 @@ bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t
     return ok;
 }
 
+bool fit_h4_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, GeoModel& out) {
+    const size_t n = idx.size();
+    if (n < 4) return false;
+    if (n == 4) {
+        double x1[4], y1[4], x2[4], y2[4];
+        for (int i = 0; i < 4; ++i) {
+            x1[i] = c.x[idx[i]]; y1[i] = c.y[idx[i]]; x2[i] = c.a[idx[i]]; y2[i] = c.c0[idx[i]];
+        }
+        return solve_h4(x1, y1, x2, y2, out);
+    }
+    // Hartley normalisation of both point sets (blocked-order sums)
+    const double inv_n = 1.0 / static_cast<double>(n);
+    const double mx1 = blocked_sum(0, n, [&](size_t i) { return c.x[idx[i]]; }) * inv_n;
+    const double my1 = blocked_sum(0, n, [&](size_t i) { return c.y[idx[i]]; }) * inv_n;
+    const double mx2 = blocked_sum(0, n, [&](size_t i) { return c.a[idx[i]]; }) * inv_n;
+    const double my2 = blocked_sum(0, n, [&](size_t i) { return c.c0[idx[i]]; }) * inv_n;
+    const double d1 = blocked_sum(0, n, [&](size_t i) {
+        const double dx = c.x[idx[i]] - mx1, dy = c.y[idx[i]] - my1;
+        return std::sqrt(dx * dx + dy * dy);
+    }) * inv_n;
+    const double d2 = blocked_sum(0, n, [&](size_t i) {
+        const double dx = c.a[idx[i]] - mx2, dy = c.c0[idx[i]] - my2;
+        return std::sqrt(dx * dx + dy * dy);
+    }) * inv_n;
+    if (!(d1 > 1e-12) || !(d2 > 1e-12)) return false;
+    const double s1 = std::sqrt(2.0) / d1, s2 = std::sqrt(2.0) / d2;
+    // 2n x 8 system (column-major) and right-hand side
+    const size_t m = 2 * n;
+    std::vector<double> A(9 * m);
+    double* col[9];
+    for (int k = 0; k < 9; ++k) col[k] = A.data() + k * m;
+    for (size_t i = 0; i < n; ++i) {
+        const double u1 = (c.x[idx[i]] - mx1) * s1, v1 = (c.y[idx[i]] - my1) * s1;
+        const double u2 = (c.a[idx[i]] - mx2) * s2, v2 = (c.c0[idx[i]] - my2) * s2;
+        const size_t r0 = 2 * i, r1 = 2 * i + 1;
+        col[0][r0] = u1; col[1][r0] = v1; col[2][r0] = 1.0; col[3][r0] = 0.0; col[4][r0] = 0.0; col[5][r0] = 0.0;
+        col[6][r0] = -u2 * u1; col[7][r0] = -u2 * v1; col[8][r0] = u2;
+        col[0][r1] = 0.0; col[1][r1] = 0.0; col[2][r1] = 0.0; col[3][r1] = u1; col[4][r1] = v1; col[5][r1] = 1.0;
+        col[6][r1] = -v2 * u1; col[7][r1] = -v2 * v1; col[8][r1] = v2;
+    }
+    HostQRStoreN<8> st;
+    for (int k = 0; k < 9; ++k) st.col[k] = col[k];
+    double hn[8];
+    qr_solve<8>(st, m, hn);
+    const double Hn[9] = {hn[0], hn[1], hn[2], hn[3], hn[4], hn[5], hn[6], hn[7], 1.0};
+    // H = T2^-1 * Hn * T1, T1 = [s1 0 -s1 mx1; 0 s1 -s1 my1; 0 0 1],
+    // T2^-1 = [1/s2 0 mx2; 0 1/s2 my2; 0 0 1]
+    const double T1[9] = {s1, 0.0, -s1 * mx1, 0.0, s1, -s1 * my1, 0.0, 0.0, 1.0};
+    const double T2i[9] = {1.0 / s2, 0.0, mx2, 0.0, 1.0 / s2, my2, 0.0, 0.0, 1.0};
+    double M[9], H[9];
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q)
+            M[r * 3 + q] = (Hn[r * 3] * T1[q] + Hn[r * 3 + 1] * T1[3 + q]) + Hn[r * 3 + 2] * T1[6 + q];
+    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < 3; ++q)
+            H[r * 3 + q] = (T2i[r * 3] * M[q] + T2i[r * 3 + 1] * M[3 + q]) + T2i[r * 3 + 2] * M[6 + q];
+    if (!(std::fabs(H[8]) > 1e-300)) return false;
+    for (int k = 0; k < 9; ++k) {
+        out.h[k] = H[k] / H[8];
+        if (std::isnan(out.h[k])) return false;
+    }
+    return true;
+}
+
 }  // namespace gcr

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "geo.h"
 #include "rect.h"
 
 namespace gcr {
@@ -41,6 +42,12 @@ struct SiftSystemSolver {
 // Hybrid systems with at least `big_rows` rows go to `big` when given.
 bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out,
                     SiftSystemSolver* big = nullptr, size_t big_rows = 0);
+
+// Non-minimal homography fit (LO and final refit; geo.h): exactly 4 points ->
+// the minimal solver; more -> Hartley-normalised DLT, h33 = 1, solved by the
+// 8-column pivoted QR of qr3.h, denormalised and scaled to h33 = 1.
+// Correspondences: c.x = x1, c.y = y1, c.a = x2, c.c0 = y2.
+bool fit_h4_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, GeoModel& out);
 
 // findWeightedMode (two_sift.hpp:354-394), libstdc++ unordered_map order.
 double weighted_mode(const std::vector<double>& angles, const std::vector<double>& weights, double bin_width);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "geo.h"
 #include "rect.h"
 
 namespace gcr {
@@ -20,6 +21,20 @@ struct DevClass {
     uint32_t n;
 };
 
+// model type per estimator: rectification solvers 0-2, homography 3
+template <int KIND>
+struct ModelOf {
+    using type = RectModel;
+    static GCR_HD type def() { return default_model(); }
+};
+template <>
+struct ModelOf<3> {
+    using type = GeoModel;
+    static GCR_HD type def() { return default_geo(); }
+};
+
+// solver 3 (homography): class 0 holds correspondences, x = x1, y = y1,
+// a = x2, c0 = y2
 struct DevProblem {
     int solver;     // GCR_SOLVER_*
     DevClass cls[2];
@@ -103,6 +118,17 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
                                uint32_t nslots, const uint32_t m[2], uint8_t* inc, RectModel* models,
                                const ScoreOut& out, WgBest* wg, size_t wg_cap, BatchRecord* rec,
                                hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+
+// homography (solver 3) counterparts of launch_generate / launch_score /
+// launch_mask / launch_select
+hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
+                               GeoModel* models, hipStream_t stream);
+hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
+                            const ScoreOut& out, hipStream_t stream);
+hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule, double T, double lambda,
+                           uint8_t* mask, hipStream_t stream);
+hipError_t launch_select_geo(const ScoreOut& sc, const uint8_t* inc, uint32_t nslots, uint64_t slot0, uint32_t m,
+                             double Tm, BatchRecord* out, hipStream_t stream);
 
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)

@@ -19,6 +19,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 namespace gcr {
 
@@ -36,8 +37,25 @@ constexpr int kMaskBlock = 256;
 // minimal solve.  Attempts of a slot are independent draws (the counter RNG is
 // keyed by (slot, attempt)), so they may be evaluated in any order/parallel.
 template <int KIND>
-GCR_DEVICE bool attempt(const DevProblem& p, uint64_t seed, uint64_t slot, uint32_t a, RectModel& m) {
-    if constexpr (KIND != 2) {
+GCR_DEVICE bool attempt(const DevProblem& p, uint64_t seed, uint64_t slot, uint32_t a,
+                        typename ModelOf<KIND>::type& m) {
+    if constexpr (KIND == 3) {
+        // homography: 4 correspondences, orientation check, 4-point DLT (geo.h)
+        const DevClass& c = p.cls[0];
+        uint32_t idx[4];
+        WordStream ws(seed, slot, a, kStreamMain, 0);
+        if (!sample_distinct<4>(ws, c.n, 4, idx)) return false;
+        double x1[4], y1[4], x2[4], y2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            x1[j] = c.x[idx[j]];
+            y1[j] = c.y[idx[j]];
+            x2[j] = c.a[idx[j]];
+            y2[j] = c.c0[idx[j]];
+        }
+        if (!valid_sample_h4(x1, y1, x2, y2)) return false;
+        return solve_h4(x1, y1, x2, y2, m);
+    } else if constexpr (KIND != 2) {
         const DevClass& c = p.cls[0];
         uint32_t idx[3];
         WordStream ws(seed, slot, a, kStreamMain, 0);
@@ -83,7 +101,7 @@ GCR_DEVICE bool attempt(const DevProblem& p, uint64_t seed, uint64_t slot, uint3
 template <int KIND, int G>
 __global__ __launch_bounds__(kGenBlock) void k_generate(DevProblem p, uint64_t seed, uint64_t slot0,
                                                         uint32_t nslots, uint8_t* __restrict__ inc,
-                                                        RectModel* __restrict__ models) {
+                                                        typename ModelOf<KIND>::type* __restrict__ models) {
     static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "group size");
     const uint32_t tid = blockIdx.x * kGenBlock + threadIdx.x;
     const uint32_t s = tid / G;
@@ -94,7 +112,7 @@ __global__ __launch_bounds__(kGenBlock) void k_generate(DevProblem p, uint64_t s
     const int gbase = lane & ~(G - 1);
     for (uint32_t r = 0; r * G < 101; ++r) {
         const uint32_t a = r * G + g;
-        RectModel m = default_model();
+        typename ModelOf<KIND>::type m = ModelOf<KIND>::def();
         const bool ok = a < 101 && attempt<KIND>(p, seed, slot, a, m);
         const uint64_t mask = __ballot(ok);
         const uint64_t grp = G == 64 ? mask : (mask >> gbase) & ((1ull << G) - 1ull);
@@ -107,7 +125,7 @@ __global__ __launch_bounds__(kGenBlock) void k_generate(DevProblem p, uint64_t s
         }
     }
     if (g == 0) {
-        models[s] = default_model();
+        models[s] = ModelOf<KIND>::def();
         inc[s] = 102;
     }
 }
@@ -181,11 +199,16 @@ constexpr int kSplitThreads = 1024;
 constexpr int kComputeThreads = 960;
 constexpr int kComputeWaves = 15;
 
-struct HypConst {       // per-hypothesis constants of the exact and band tests
-    double h7, h8, ac;  // scale: model, alpha^3
-    double lo, hi;      // scale band on s / t^3 (ac-adjusted)
-    double cphi, cphi2; // orientation: clipped phi, clip(clip(phi + pi/2))
-    double cf, sf;      // orientation: cos(phi), sin(phi) (band test only)
+struct HypConst {           // per-hypothesis constants of the exact and band tests
+    union {
+        struct {
+            double h7, h8, ac;  // scale: model, alpha^3
+            double lo, hi;      // scale band on s / t^3 (ac-adjusted)
+            double cphi, cphi2; // orientation: clipped phi, clip(clip(phi + pi/2))
+            double cf, sf;      // orientation: cos(phi), sin(phi) (band test only)
+        };
+        double g[9];            // homography (KIND 3), row-major
+    };
 };
 
 template <int KIND>
@@ -216,7 +239,8 @@ struct GenArgs {
 
 template <int KIND, int H, int R, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, double T0, double T1, double band0,
-                                                               double tan_tau1, const RectModel* __restrict__ models,
+                                                               double tan_tau1,
+                                                               const typename ModelOf<KIND>::type* __restrict__ models,
                                                                const uint8_t* __restrict__ inc, uint32_t nh,
                                                                ScoreOut out, GenArgs gen) {
     static_assert((H * R) % kComputeThreads == 0 && kComputeThreads % H == 0, "tile shape");
@@ -265,6 +289,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                 fbuf[buf][1][e] = c.y[i];
                 if (cls == 0) {
                     fbuf[buf][2][e] = c.a[i];
+                    if constexpr (KIND == 3) fbuf[buf][3][e] = c.c0[i];
                 } else {
                     fbuf[buf][2][e] = c.c0[i];
                     fbuf[buf][3][e] = c.c1[i];
@@ -282,8 +307,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
         const DevClass& c = p.cls[cls];
         const uint32_t base = (cls == 0 ? rr : rr - r0) * R;
         const uint32_t last = ((c.n + 1u) & ~1u) - 2u;
-        const double* src[4] = {c.x, c.y, cls == 0 ? c.a : c.c0, c.c1};
-        const int nf = cls == 0 ? 3 : 4;
+        const double* src[4] = {c.x, c.y, cls == 0 ? c.a : c.c0, cls == 0 ? c.c0 : c.c1};
+        const int nf = (cls == 0 && KIND != 3) ? 3 : 4;
         for (int f = 0; f < nf; ++f) {
 #pragma unroll
             for (int q = 0; q < kRp / 128; ++q) {
@@ -325,9 +350,17 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     const bool valid_h = hg < nh && (kGen ? gen_a[h] != 127 : (inc == nullptr || inc[hg] <= 101));
     const bool live = !chain_wave && valid_h;
 
-    if (t < H) {
+    if (KIND == 3 && t < H) {
+        if constexpr (KIND == 3) {
+            const GeoModel m = valid_h ? models[hg] : default_geo();
+            HypConst q;
+            for (int j = 0; j < 9; ++j) q.g[j] = m.h[j];
+            hyp[h] = q;
+        }
+    } else if (t < H) {
         const bool v = valid_h;
-        const RectModel m = v ? (kGen ? gen_m[h] : models[hg]) : default_model();
+        RectModel m = default_model();
+        if constexpr (KIND != 3) m = v ? (kGen ? gen_m[h] : models[hg]) : default_model();
         HypConst q;
         q.h7 = m.h7;
         q.h8 = m.h8;
@@ -364,6 +397,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                 const int cls = (r < r0) ? 0 : 1;
                 const uint32_t base = (cls == 0 ? r : r - r0) * R;
                 const uint32_t nc = cls == 0 ? n0 : n1;
+                if constexpr (KIND == 3) {
+                    // homography: the exact residual is cheap, every pair is
+                    // evaluated directly (no band, no queue)
+#pragma unroll
+                    for (int k = 0; k < kPer; ++k) {
+                        const uint32_t il = fsub + k * kStride;
+                        double v = 0.0;
+                        if (live && base + il < nc) {
+                            const double r2 = h_sq_residual(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine.g);
+                            if (r2 <= T0) {
+                                v = -r2;
+                                atomicAdd(&cnt_sh[0][h], 1u);
+                            }
+                        }
+                        tl[h * kRP + il] = v;
+                    }
+                } else {
                 // 1) conservative band test
                 uint32_t bits = 0;
 #pragma unroll
@@ -416,6 +466,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         atomicAdd(&cnt_sh[cls][hh], 1u);
                     }
                 }
+                }   // KIND != 3
             }
         } else {
             // chain wave: stage round r+1's features around the fold of
@@ -520,8 +571,9 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
 // --------------------------------------------------------------- select ----
 constexpr int kSelectThreads = 1024;
 
+template <class M>
 __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut sc, const uint8_t* __restrict__ inc,
-                                                           const RectModel* __restrict__ models, uint32_t n,
+                                                           const M* __restrict__ models, uint32_t n,
                                                            uint64_t slot0, uint32_t m0, uint32_t m1, double Tm0,
                                                            double Tm1, BatchRecord* out) {
     __shared__ double s_val[kSelectThreads];
@@ -548,7 +600,9 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
             sum += msac;
         }
         if (zero) sum = 0.0;
-        if (best < sum && (solver != 2 || valid_model_sift22(models[j]))) {
+        bool valid = true;
+        if constexpr (std::is_same<M, RectModel>::value) valid = solver != 2 || valid_model_sift22(models[j]);
+        if (best < sum && valid) {
             best = sum;
             bi = j;
         }
@@ -585,7 +639,7 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
             r.best_score = s_val[0];
             r.best_inliers[0] = sc.n0[j];
             r.best_inliers[1] = K == 2 ? sc.n1[j] : 0;
-            r.best_model = models[j];
+            if constexpr (std::is_same<M, RectModel>::value) r.best_model = models[j];
         }
         *out = r;
     }
@@ -747,12 +801,13 @@ __global__ __launch_bounds__(kSelectThreads) void k_select_wg(const WgBest* __re
 
 // ----------------------------------------------------------------- mask ----
 template <int KIND>
-__global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, RectModel m, int rule, double T,
-                                                     double lambda, uint8_t* __restrict__ mask) {
+__global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, typename ModelOf<KIND>::type m, int rule,
+                                                     double T, double lambda, uint8_t* __restrict__ mask) {
     const uint32_t i = blockIdx.x * kMaskBlock + threadIdx.x;
     if (i >= c.n) return;
     double r2;
-    if (cls == 0) r2 = scale_sq_residual<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
+    if constexpr (KIND == 3) r2 = h_sq_residual(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
+    else if (cls == 0) r2 = scale_sq_residual<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
     else r2 = orient_sq_residual<false>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
     bool inl;
     if (rule == 2) {
@@ -872,8 +927,8 @@ int split_h(uint32_t nh) {
 hipError_t launch_select(int solver, const ScoreOut& sc, const uint8_t* inc, const RectModel* models,
                          uint32_t nslots, uint64_t slot0, const uint32_t m[2], const double Tm[2], BatchRecord* out,
                          hipStream_t stream) {
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelectThreads), 0, stream, solver, sc, inc, models, nslots, slot0,
-                       m[0], m[1], Tm[0], Tm[1], out);
+    hipLaunchKernelGGL(k_select<RectModel>, dim3(1), dim3(kSelectThreads), 0, stream, solver, sc, inc, models,
+                       nslots, slot0, m[0], m[1], Tm[0], Tm[1], out);
     return hipGetLastError();
 }
 
@@ -980,6 +1035,52 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
 hipError_t launch_math(int op, const double* a, const double* b, size_t n, double* out, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_math, dim3(blocks_for(n, 256)), dim3(256), 0, stream, op, a, b, n, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------- homography (3) ----
+hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
+                               GeoModel* models, hipStream_t stream) {
+    if (nslots == 0) return hipSuccess;
+    auto go = [&](auto gtag) {
+        constexpr int G = decltype(gtag)::value;
+        const dim3 grid(blocks_for((size_t)nslots * G, kGenBlock)), block(kGenBlock);
+        hipLaunchKernelGGL((k_generate<3, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+    };
+    if (nslots <= 8192) go(std::integral_constant<int, 16>{});
+    else if (nslots <= 32768) go(std::integral_constant<int, 4>{});
+    else go(std::integral_constant<int, 1>{});
+    return hipGetLastError();
+}
+
+hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
+                            const ScoreOut& out, hipStream_t stream) {
+    if (nh == 0) return hipSuccess;
+    auto go = [&](auto htag, auto rtag) {
+        constexpr int H = decltype(htag)::value, R = decltype(rtag)::value;
+        hipLaunchKernelGGL((k_score_split<3, H, R, false>), dim3((nh + H - 1) / H), dim3(kSplitThreads), 0, stream,
+                           p, T, 0.0, 0.0, 0.0, models, inc, nh, out, GenArgs{});
+    };
+    const int h = split_h(nh);
+    if (h == 64) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 120>{});
+    else if (h == 16) go(std::integral_constant<int, 16>{}, std::integral_constant<int, 420>{});
+    else go(std::integral_constant<int, 4>{}, std::integral_constant<int, 960>{});
+    return hipGetLastError();
+}
+
+hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule, double T, double lambda,
+                           uint8_t* mask, hipStream_t stream) {
+    const DevClass& c = p.cls[0];
+    if (c.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_mask<3>, dim3(blocks_for(c.n, kMaskBlock)), dim3(kMaskBlock), 0, stream, c, 0, model, rule,
+                       T, lambda, mask);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_geo(const ScoreOut& sc, const uint8_t* inc, uint32_t nslots, uint64_t slot0, uint32_t m,
+                             double Tm, BatchRecord* out, hipStream_t stream) {
+    hipLaunchKernelGGL(k_select<GeoModel>, dim3(1), dim3(kSelectThreads), 0, stream, 3, sc, inc,
+                       (const GeoModel*)nullptr, nslots, slot0, m, 0u, Tm, 0.0, out);
     return hipGetLastError();
 }
 

@@ -36,22 +36,24 @@ inline double blocked_sum(size_t lo, size_t hi, F f) {
     return total;
 }
 
-// Backend S stores 4 columns of length m: 0..2 = A, 3 = b, and provides
+// Backend S stores C + 1 columns of length m: 0..C-1 = A, C = b, and provides
 //   double sumsq(c, lo, hi)             blocked sum of col[c][i]^2
 //   double dot(a, c, lo, hi)            blocked sum of col[a][i] * col[c][i]
 //   double get(c, i); void set(c, i, v)
 //   void scale(c, lo, hi, den)          col[c][i] = col[c][i] / den
 //   void zero(c, lo, hi)
 //   void update(c, e, lo, hi, tau, t)   col[c][i] -= (tau * col[e][i]) * t
-template <class S>
-void qr3_solve(S& st, size_t m, double x[3]) {
-    constexpr size_t cols = 3;
+template <int C, class S>
+void qr_solve(S& st, size_t m, double x[C]) {
+    constexpr size_t cols = C;
+    constexpr int kB = C;                  // stored column of b
     auto sq = [](double v) { return v * v; };
     const size_t size = std::min(m, cols);
-    int pc[3] = {0, 1, 2};                 // logical -> stored column (pivot swaps)
-    double tau_k[3] = {0, 0, 0};
-    size_t transp[3] = {0, 1, 2};
-    double nu[3], nd[3];
+    int pc[C];                             // logical -> stored column (pivot swaps)
+    double tau_k[C];
+    size_t transp[C];
+    double nu[C], nd[C];
+    for (int k = 0; k < C; ++k) { pc[k] = k; tau_k[k] = 0.0; transp[k] = k; }
     for (size_t k = 0; k < cols; ++k) {
         nd[k] = std::sqrt(st.sumsq(pc[k], 0, m));
         nu[k] = nd[k];
@@ -122,14 +124,16 @@ void qr3_solve(S& st, size_t m, double x[3]) {
             }
         }
     }
-    size_t perm[3] = {0, 1, 2};
+    size_t perm[C];
+    for (int k = 0; k < C; ++k) perm[k] = k;
     for (size_t k = 0; k < size; ++k) std::swap(perm[k], perm[transp[k]]);
     if (nonzero == 0) {
-        x[0] = x[1] = x[2] = 0.0;
+        for (int k = 0; k < C; ++k) x[k] = 0.0;
         return;
     }
-    for (size_t k = 0; k < nonzero; ++k) apply_reflector(pc[k], k, tau_k[k], 3);
-    double c[3] = {st.get(3, 0), m > 1 ? st.get(3, 1) : 0.0, m > 2 ? st.get(3, 2) : 0.0};
+    for (size_t k = 0; k < nonzero; ++k) apply_reflector(pc[k], k, tau_k[k], kB);
+    double c[C];
+    for (int k = 0; k < C; ++k) c[k] = m > (size_t)k ? st.get(kB, k) : 0.0;
     for (size_t jj = nonzero; jj-- > 0;) {
         c[jj] = c[jj] / st.get(pc[jj], jj);
         for (size_t i = 0; i < jj; ++i) c[i] -= c[jj] * st.get(pc[jj], i);
@@ -138,9 +142,13 @@ void qr3_solve(S& st, size_t m, double x[3]) {
     for (size_t i = nonzero; i < cols; ++i) x[perm[i]] = 0.0;
 }
 
-// Host storage: four column pointers of length m.
-struct HostQRStore {
-    double* col[4];
+template <class S>
+void qr3_solve(S& st, size_t m, double x[3]) { qr_solve<3>(st, m, x); }
+
+// Host storage: C + 1 column pointers of length m (C = 3 unless given).
+template <int C = 3>
+struct HostQRStoreN {
+    double* col[C + 1];
     double sumsq(int c, size_t lo, size_t hi) const {
         const double* p = col[c];
         return blocked_sum(lo, hi, [p](size_t i) { return p[i] * p[i]; });
@@ -162,5 +170,7 @@ struct HostQRStore {
         for (size_t i = lo; i < hi; ++i) col[c][i] -= (tau * col[e][i]) * t;
     }
 };
+
+using HostQRStore = HostQRStoreN<3>;
 
 }  // namespace gcr

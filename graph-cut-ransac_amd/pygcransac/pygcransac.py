@@ -28,6 +28,7 @@ __all__ = [
     "findRectifyingHomographyScaleOnly",
     "findRectifyingHomographyScaleOnlyOriginal",
     "findRectifyingHomographySIFT",
+    "findHomography",
 ]
 
 _TWO_PI = 2.0 * math.pi
@@ -363,3 +364,47 @@ def findRectifyingHomographySIFT(scale_features, orientation_features, scale_res
         return (None, s_in, o_in, None) + extra
     model = _fill(SIFTRectifyingHomography(), m, sift=True)
     return (H.reshape(3, 3), s_in, o_in, model) + extra
+
+
+def findHomography(correspondences, h1, w1, h2, w2, probabilities=None, threshold=1.0, conf=0.99,
+                   spatial_coherence_weight=0.975, max_iters=10000, min_iters=50, sampler=0, lo_number=50, *,
+                   seed=0, device=None, batch_slots=0, return_stats=False):
+    """4-point homography with graph-cut LO -- an EXTENSION (SURVEY.md §8(f)
+    row 3): this fork has no homography estimator (finding 0.1); the argument
+    names and order follow upstream pygcransac's findHomography.
+
+    ``correspondences`` is (N, 4) float64: x1, y1, x2, y2.  ``h1, w1, h2, w2``
+    (image sizes) are accepted for signature compatibility; they only feed
+    upstream's neighbourhood grid and non-uniform samplers, which are not part
+    of this path: ``sampler`` must be 0 (uniform) and ``probabilities`` empty.
+    ``threshold`` is the inlier threshold in pixels of the second image
+    (MSAC threshold 2.25 * threshold, as the rectification solvers).
+
+    Returns ``(H, inliers)`` with H (3, 3) and H[2, 2] = 1, or ``(None, inliers)``.
+    """
+    for name, v in (("h1", h1), ("w1", w1), ("h2", h2), ("w2", w2)):
+        _as_double(v, name)
+    if probabilities is not None and len(probabilities) != 0:
+        raise ValueError("Only the uniform sampler is supported; probabilities must be empty.")
+    if _as_size_t(sampler, "sampler") != 0:
+        raise ValueError(f"Unsupported sampler {sampler}: only 0 (uniform) is supported.")
+    f = _as_features(correspondences)
+    if f.ndim != 2:
+        raise ValueError("Number of dimensions must be 2.")
+    n, cols = f.shape
+    if n < 4 or cols != 4:
+        raise ValueError(f"Correspondences should be an array with 4 columns and at least 4 rows. "
+                         f"It has {cols} columns and {n} rows.")
+    f = np.ascontiguousarray(f)
+    p = _params(threshold, 2.0, spatial_coherence_weight, min_iters, max_iters, lo_number, seed, conf, batch_slots)
+    mask = np.zeros(n, dtype=np.uint8)
+    H = np.zeros(9, dtype=np.float64)
+    st = N.Stats()
+    ctx = N.context(device)
+    rc = N.lib.gcr_find_homography(ctx, _dp(f), n, C.byref(p), _u8(mask), _dp(H), C.byref(st))
+    num_inliers = N.check(rc)
+    inliers = mask.astype(bool)
+    extra = (st.as_dict(),) if return_stats else ()
+    if num_inliers == 0:
+        return (None, inliers) + extra
+    return (H.reshape(3, 3), inliers) + extra

@@ -94,3 +94,34 @@ def problem_m2(n_scale: int = 5_000, n_orient: int = 5_000, outlier_ratio: float
     fs, ts = scale_features(n_scale, outlier_ratio, seed)
     fo, to = orientation_features(n_orient, outlier_ratio, seed + 1)
     return fs, fo, ts, to, 0.05, math.radians(1.0)
+
+
+# ------------------------------------------------------------ homography ----
+# BASELINE configs[2]: N = 5 000 correspondences, 50 % outliers.  Two views of
+# a plane: inliers are image-1 points mapped by a ground-truth homography plus
+# Gaussian pixel noise; outliers are independent uniform pairs.
+H_GT = np.array([[0.92, -0.08, 35.0],
+                 [0.06, 0.97, -18.0],
+                 [4.0e-5, -3.0e-5, 1.0]])
+IMG_W, IMG_H = 1280.0, 960.0
+
+
+def problem_h(n: int = 5_000, outlier_ratio: float = 0.5, seed: int = DEFAULT_SEED, noise: float = 0.5,
+              H: np.ndarray = H_GT):
+    """Homography problem: correspondences (n, 4) = (x1, y1, x2, y2), inlier
+    truth mask, ground-truth H and the inlier threshold (px)."""
+    rng = np.random.default_rng(seed)
+    n_out = int(round(n * outlier_ratio))
+    n_in = n - n_out
+    x1 = rng.uniform(0, IMG_W, n_in)
+    y1 = rng.uniform(0, IMG_H, n_in)
+    w = H[2, 0] * x1 + H[2, 1] * y1 + H[2, 2]
+    x2 = (H[0, 0] * x1 + H[0, 1] * y1 + H[0, 2]) / w + rng.normal(0, noise, n_in)
+    y2 = (H[1, 0] * x1 + H[1, 1] * y1 + H[1, 2]) / w + rng.normal(0, noise, n_in)
+    inl = np.stack([x1, y1, x2, y2], axis=1)
+    out = np.stack([rng.uniform(0, IMG_W, n_out), rng.uniform(0, IMG_H, n_out),
+                    rng.uniform(0, IMG_W, n_out), rng.uniform(0, IMG_H, n_out)], axis=1)
+    corr = np.concatenate([inl, out])
+    truth = np.concatenate([np.ones(n_in, bool), np.zeros(n_out, bool)])
+    perm = rng.permutation(n)
+    return np.ascontiguousarray(corr[perm]), truth[perm], H.copy(), 2.0

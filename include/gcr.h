@@ -49,6 +49,7 @@ extern "C" {
 #define GCR_SOLVER_SCALE3 0          /* RectifyingHomographyThreeSIFTSolver         */
 #define GCR_SOLVER_SCALE3_ORIGINAL 1 /* RectifyingHomographyThreeSIFTSolverOriginal */
 #define GCR_SOLVER_SIFT22 2          /* RectifyingHomographyTwoSIFTSolver           */
+#define GCR_SOLVER_HOMOGRAPHY4 3     /* 4-point homography (upstream GC-RANSAC)     */
 
 typedef struct gcr_ctx gcr_ctx;
 typedef struct gcr_problem gcr_problem;
@@ -109,6 +110,15 @@ int gcr_rect_sift(gcr_ctx* ctx, const double* scale_features, size_t n_scale, co
                   size_t n_orientation, const gcr_params* params, uint8_t* scale_mask_out,
                   uint8_t* orientation_mask_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
 
+/* 4-point homography (an EXTENSION: this fork has no
+ * homography estimator, finding 0.1 -- the entry point upstream pygcransac's
+ * findHomography would bind).  correspondences: row-major N x 4 float64
+ * (x1, y1, x2, y2); threshold = params->scale_residual_thresh (pixels, second
+ * image); mask_out: N bytes; H_out: row-major 3x3 with H[2][2] = 1.  Returns
+ * the number of inliers (0: no model, H_out untouched) or < 0 on error. */
+int gcr_find_homography(gcr_ctx* ctx, const double* correspondences, size_t n, const gcr_params* params,
+                        uint8_t* mask_out, double* H_out, gcr_stats* stats_out);
+
 /* ---- device-resident problems (benchmarks, problem batches) -------------- */
 /* Uploads the features once; runs reuse the HBM-resident copy.  f1 is the
  * orientation set for GCR_SOLVER_SIFT22 and NULL otherwise. */
@@ -163,6 +173,17 @@ int gcr_debug_fit_nonminimal(gcr_problem* prob, const uint32_t* idx0, size_t k0,
  * fit is rejected, < 0 on error */
 int gcr_host_fit_nonminimal(int solver, const double* f0, size_t n0, const double* f1, size_t n1, const uint32_t* idx0,
                             size_t k0, const uint32_t* idx1, size_t k1, gcr_rect_model* model_out);
+/* homography problems (GCR_SOLVER_HOMOGRAPHY4): models are 9 row-major
+ * doubles.  generate: inc[i] as above, H_out 9 per slot; score: n0 / v0 / tot
+ * per model (MSAC threshold 2.25 thr); mask: rules as gcr_debug_mask */
+int gcr_debug_generate_h(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc_out,
+                         double* H_out);
+int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double* H, uint32_t nmodels, uint32_t* n0,
+                      double* v0, double* tot);
+int gcr_debug_mask_h(gcr_problem* prob, const gcr_params* params, const double* H, int rule, uint8_t* mask_out);
+/* host-only: normalised least-squares homography of the listed
+ * correspondences (the LO / final-refit fit); 1 = fitted, 0 = rejected */
+int gcr_host_fit_h(const double* correspondences, size_t n, const uint32_t* idx, size_t k, double* H_out);
 /* host-only: RectifyingHomography::getHomography (model.h:211-226), row-major */
 void gcr_host_homography(const gcr_rect_model* model, double* H_out);
 /* host-only (no GPU): deterministic math and sampler used on both sides */

@@ -312,13 +312,15 @@ static double bsum(size_t lo, size_t hi, F f) {
     return total;
 }
 
-static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_t m, std::vector<double>& b,
-                             double x[3]) {
-    const size_t cols = 3, rows = m, size = std::min(rows, cols);
+template <size_t C>
+static bool colpiv_qr_solve(std::vector<double>& A /* col-major m x C */, size_t m, std::vector<double>& b,
+                            double x[C]) {
+    const size_t cols = C, rows = m, size = std::min(rows, cols);
     auto at = [&](size_t i, size_t j) -> double& { return A[j * rows + i]; };
-    double hc[3] = {0, 0, 0};
-    size_t transp[3] = {0, 1, 2};
-    double normsU[3], normsD[3];
+    double hc[C];
+    size_t transp[C];
+    for (size_t k = 0; k < C; ++k) { hc[k] = 0.0; transp[k] = k; }
+    double normsU[C], normsD[C];
     for (size_t k = 0; k < cols; ++k) {
         const double s = bsum(0, rows, [&](size_t i) { return at(i, k) * at(i, k); });
         normsD[k] = std::sqrt(s);
@@ -387,9 +389,10 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
             }
         }
     }
-    size_t perm[3] = {0, 1, 2};
+    size_t perm[C];
+    for (size_t k = 0; k < C; ++k) perm[k] = k;
     for (size_t k = 0; k < size; ++k) std::swap(perm[k], perm[transp[k]]);
-    if (nonzero == 0) { x[0] = x[1] = x[2] = 0.0; return true; }
+    if (nonzero == 0) { for (size_t k = 0; k < C; ++k) x[k] = 0.0; return true; }
     // c = Q^T b with the first `nonzero` reflectors (H_0 first)
     for (size_t k = 0; k < nonzero; ++k) {
         const double tau = hc[k];
@@ -401,7 +404,8 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
         for (size_t i = k + 1; i < rows; ++i) b[i] -= (tau * at(i, k)) * t;
     }
     // upper-triangular solve, column oriented (Eigen triangular_solve_vector)
-    double c[3] = {b[0], b[1], b[2]};
+    double c[C];
+    for (size_t k = 0; k < C; ++k) c[k] = k < rows ? b[k] : 0.0;
     for (size_t jj = nonzero; jj-- > 0;) {
         c[jj] = c[jj] / at(jj, jj);
         for (size_t i = 0; i < jj; ++i) c[i] -= c[jj] * at(i, jj);
@@ -410,12 +414,16 @@ static bool colpiv_qr_solve3(std::vector<double>& A /* col-major m x 3 */, size_
     for (size_t i = nonzero; i < cols; ++i) x[perm[i]] = 0.0;
     return true;
 }
+static bool colpiv_qr_solve3(std::vector<double>& A, size_t m, std::vector<double>& b, double x[3]) {
+    return colpiv_qr_solve<3>(A, m, b, x);
+}
 
 // ------------------------------------------------------------- data ----
 struct Features {
-    std::vector<double> d;   // row-major n x 3
+    std::vector<double> d;   // row-major n x cols
     size_t n = 0;
-    double at(size_t i, size_t j) const { return d[i * 3 + j]; }
+    size_t cols = 3;
+    double at(size_t i, size_t j) const { return d[i * cols + j]; }
 };
 
 template <size_t K>
@@ -441,6 +449,7 @@ struct Score {
 // kind 0: ThreeSIFT, 1: ThreeSIFTOriginal, 2: TwoSIFT
 template <int KIND>
 struct Solver {
+    using ModelT = Model;
     static constexpr size_t K = (KIND == 2) ? 2 : 1;
     static constexpr double kScalePower = (KIND == 1) ? (-1.0 / 3.0) : (1.0 / 3.0);
     std::array<size_t, K> sampleSize() const {
@@ -713,10 +722,146 @@ struct Solver {
     }
 };
 
+// ------------------------------------------------------ homography (H4) ----
+// absent from this fork; restated (parity unpinned) as
+// described in graph-cut-ransac_amd/csrc/geo.h.  Correspondences are N x 4
+// rows (x1, y1, x2, y2).
+struct HModel {
+    double h[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+};
+
+// math_utils.hpp:164-221 gaussElimination<_Size> for any size
+template <size_t N>
+static void gaussEliminationN(double m[N][N + 1], double r[N]) {
+    for (size_t i = 0; i < N; i++)
+        for (size_t k = i + 1; k < N; k++)
+            if (std::abs(m[i][i]) < std::abs(m[k][i]))
+                for (size_t j = 0; j <= N; j++) std::swap(m[i][j], m[k][j]);
+    for (size_t i = 0; i < N - 1; i++)
+        for (size_t k = i + 1; k < N; k++) {
+            const double t = m[k][i] / m[i][i];
+            for (size_t j = 0; j <= N; j++) m[k][j] = m[k][j] - t * m[i][j];
+        }
+    for (size_t i = 0; i < N; i++) {
+        const size_t row = N - 1 - i;
+        r[row] = m[row][N];
+        for (size_t col = row + 1; col < N; col++) r[row] = r[row] - m[row][col] * r[col];
+        r[row] = r[row] / m[row][row];
+    }
+}
+
+struct HSolver {
+    using ModelT = HModel;
+    static constexpr size_t K = 1;
+    std::array<size_t, 1> sampleSize() const { return {4}; }
+
+    double squaredResidual(size_t, const Features& f, size_t i, const HModel& m) const {
+        const double x1 = f.at(i, 0), y1 = f.at(i, 1), x2 = f.at(i, 2), y2 = f.at(i, 3);
+        const double* h = m.h;
+        const double w = (h[6] * x1 + h[7] * y1) + h[8];
+        const double du = ((h[0] * x1 + h[1] * y1) + h[2]) / w - x2;
+        const double dv = ((h[3] * x1 + h[4] * y1) + h[5]) / w - y2;
+        return du * du + dv * dv;
+    }
+
+    // orientation of the triangles (0,1,2), (1,2,3), (2,3,0), (3,0,1) agrees
+    bool isValidSample(const Data<1>& data, const Inliers<1>& s) const {
+        const Features& f = *data[0];
+        if (s[0].size() != 4) return false;
+        auto area = [](double ax, double ay, double bx, double by, double cx, double cy) {
+            return (bx - ax) * (cy - ay) - (by - ay) * (cx - ax);
+        };
+        static const int T[4][3] = {{0, 1, 2}, {1, 2, 3}, {2, 3, 0}, {3, 0, 1}};
+        for (const auto& t : T) {
+            const size_t a = s[0][t[0]], b = s[0][t[1]], c = s[0][t[2]];
+            const double s1 = area(f.at(a, 0), f.at(a, 1), f.at(b, 0), f.at(b, 1), f.at(c, 0), f.at(c, 1));
+            const double s2 = area(f.at(a, 2), f.at(a, 3), f.at(b, 2), f.at(b, 3), f.at(c, 2), f.at(c, 3));
+            if (!(s1 * s2 > 0.0)) return false;
+        }
+        return true;
+    }
+    bool isValidModel(const HModel&) const { return true; }
+
+    bool minimal(const Features& f, const std::vector<size_t>& in, std::vector<HModel>& models) const {
+        double a[8][9];
+        for (size_t i = 0; i < 4; ++i) {
+            const double x1 = f.at(in[i], 0), y1 = f.at(in[i], 1), x2 = f.at(in[i], 2), y2 = f.at(in[i], 3);
+            const double r0[9] = {x1, y1, 1.0, 0.0, 0.0, 0.0, -x2 * x1, -x2 * y1, x2};
+            const double r1[9] = {0.0, 0.0, 0.0, x1, y1, 1.0, -y2 * x1, -y2 * y1, y2};
+            for (int j = 0; j < 9; ++j) { a[2 * i][j] = r0[j]; a[2 * i + 1][j] = r1[j]; }
+        }
+        double h[8];
+        gaussEliminationN<8>(a, h);
+        HModel m;
+        for (int k = 0; k < 8; ++k) {
+            if (std::isnan(h[k]) || !(std::fabs(h[k]) < 1e300)) return false;
+            m.h[k] = h[k];
+        }
+        m.h[8] = 1.0;
+        models.push_back(m);
+        return true;
+    }
+
+    // Hartley-normalised DLT, h33 = 1, 8-column pivoted QR, blocked sums
+    bool nonminimal(const Features& f, const std::vector<size_t>& in, std::vector<HModel>& models) const {
+        const size_t n = in.size();
+        const double inv_n = 1.0 / static_cast<double>(n);
+        auto mean = [&](size_t col) { return bsum(0, n, [&](size_t i) { return f.at(in[i], col); }) * inv_n; };
+        const double mx1 = mean(0), my1 = mean(1), mx2 = mean(2), my2 = mean(3);
+        auto spread = [&](size_t cx, size_t cy, double mx, double my) {
+            return bsum(0, n, [&](size_t i) {
+                const double dx = f.at(in[i], cx) - mx, dy = f.at(in[i], cy) - my;
+                return std::sqrt(dx * dx + dy * dy);
+            }) * inv_n;
+        };
+        const double d1 = spread(0, 1, mx1, my1), d2 = spread(2, 3, mx2, my2);
+        if (!(d1 > 1e-12) || !(d2 > 1e-12)) return false;
+        const double s1 = std::sqrt(2.0) / d1, s2 = std::sqrt(2.0) / d2;
+        const size_t rows = 2 * n;
+        std::vector<double> A(8 * rows), b(rows);
+        for (size_t i = 0; i < n; ++i) {
+            const double u1 = (f.at(in[i], 0) - mx1) * s1, v1 = (f.at(in[i], 1) - my1) * s1;
+            const double u2 = (f.at(in[i], 2) - mx2) * s2, v2 = (f.at(in[i], 3) - my2) * s2;
+            const double ra[8] = {u1, v1, 1.0, 0.0, 0.0, 0.0, -u2 * u1, -u2 * v1};
+            const double rb[8] = {0.0, 0.0, 0.0, u1, v1, 1.0, -v2 * u1, -v2 * v1};
+            for (size_t j = 0; j < 8; ++j) { A[j * rows + 2 * i] = ra[j]; A[j * rows + 2 * i + 1] = rb[j]; }
+            b[2 * i] = u2;
+            b[2 * i + 1] = v2;
+        }
+        double x[8];
+        colpiv_qr_solve<8>(A, rows, b, x);
+        const double Hn[3][3] = {{x[0], x[1], x[2]}, {x[3], x[4], x[5]}, {x[6], x[7], 1.0}};
+        const double T1[3][3] = {{s1, 0.0, -s1 * mx1}, {0.0, s1, -s1 * my1}, {0.0, 0.0, 1.0}};
+        const double T2i[3][3] = {{1.0 / s2, 0.0, mx2}, {0.0, 1.0 / s2, my2}, {0.0, 0.0, 1.0}};
+        double M[3][3], H[3][3];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) M[r][c] = (Hn[r][0] * T1[0][c] + Hn[r][1] * T1[1][c]) + Hn[r][2] * T1[2][c];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) H[r][c] = (T2i[r][0] * M[0][c] + T2i[r][1] * M[1][c]) + T2i[r][2] * M[2][c];
+        if (!(std::fabs(H[2][2]) > 1e-300)) return false;
+        HModel m;
+        for (int k = 0; k < 9; ++k) {
+            m.h[k] = H[k / 3][k % 3] / H[2][2];
+            if (std::isnan(m.h[k])) return false;
+        }
+        models.push_back(m);
+        return true;
+    }
+
+    bool estimateModel(const Data<1>& data, const Inliers<1>& in, std::vector<HModel>& models) const {
+        if (in[0].size() < 4) return false;
+        if (in[0].size() == 4) return minimal(*data[0], in[0], models);
+        return nonminimal(*data[0], in[0], models);
+    }
+    bool estimateModelNonminimal(const Data<1>& data, const Inliers<1>& in, std::vector<HModel>& models) const {
+        return estimateModel(data, in, models);
+    }
+};
+
 // --------------------------------------------------------------- MSAC ----
 template <class S>
-static Score<S::K> getScore(const S& solver, const Data<S::K>& data, const Model& m, const double thr[S::K],
-                            Inliers<S::K>& inliers) {
+static Score<S::K> getScore(const S& solver, const Data<S::K>& data, const typename S::ModelT& m,
+                            const double thr[S::K], Inliers<S::K>& inliers) {
     constexpr size_t K = S::K;
     Score<K> score{};
     double T[K];
@@ -767,6 +912,7 @@ struct Statistics {
 template <class S>
 class GCRANSAC {
 public:
+    using Model = typename S::ModelT;
     static constexpr size_t K = S::K;
     Settings settings;
     Statistics stats;
@@ -1006,10 +1152,11 @@ struct oracle_stats {
     double score, seconds;
 };
 
-static Features make_features(const double* p, size_t n) {
+static Features make_features(const double* p, size_t n, size_t cols = 3) {
     Features f;
     f.n = n;
-    f.d.assign(p, p + n * 3);
+    f.cols = cols;
+    f.d.assign(p, p + n * cols);
     return f;
 }
 
@@ -1081,6 +1228,93 @@ int oracle_rect_sift(const double* sfeat, size_t ns, const double* ofeat, size_t
     Features a = make_features(sfeat, ns), b = make_features(ofeat, no);
     uint8_t* masks[2] = {smask, omask};
     return run_generic<2>({&a, &b}, p, masks, H9, model7, st);
+}
+
+// homography: correspondences N x 4, threshold in px
+int oracle_find_homography(const double* corr, size_t n, const oracle_params* p, uint8_t* mask, double* H9,
+                           oracle_stats* st) {
+    g_math = p->math_mode;
+    Features f = make_features(corr, n, 4);
+    GCRANSAC<HSolver> g;
+    g.settings.threshold[0] = p->thr0;
+    g.settings.spatial_coherence_weight = p->spatial_coherence_weight;
+    g.settings.min_iteration_number = p->min_iteration_number;
+    g.settings.max_iteration_number = p->max_iteration_number;
+    g.settings.max_local_optimization_number = p->max_local_optimization_number;
+    g.settings.confidence = p->confidence;
+    g.settings.seed = p->seed;
+    g.settings.sampler = p->sampler;
+    HModel model;
+    try {
+        g.run({&f}, HSolver{}, model);
+    } catch (const std::exception& e) {
+        fprintf(stderr, "oracle: %s\n", e.what());
+        return -1;
+    }
+    std::memcpy(H9, model.h, sizeof(model.h));
+    std::memset(mask, 0, n);
+    for (size_t i : g.final_inliers[0]) mask[i] = 1;
+    if (st) {
+        st->iteration_number = g.stats.iteration_number;
+        st->local_optimization_number = g.stats.local_optimization_number;
+        st->graph_cut_number = g.stats.graph_cut_number;
+        st->slots = g.stats.slots;
+        st->hypotheses = g.stats.hypotheses;
+        st->score = g.stats.score;
+        st->seconds = g.stats.seconds;
+    }
+    return (int)g.final_inliers[0].size();
+}
+
+// homography hooks: one slot (model9), score / residuals of a model9, fit
+int oracle_h_slot(const double* corr, size_t n, uint64_t seed, uint64_t slot, double* model9) {
+    Features f = make_features(corr, n, 4);
+    const Data<1> data{&f};
+    HSolver solver;
+    Inliers<1> smp{};
+    std::vector<HModel> models;
+    size_t umg = 0;
+    uint32_t attempt = 0;
+    while (umg++ <= 100) {
+        const uint32_t at = attempt++;
+        if (!philox_subset(seed, slot, at, 0, 0, n, 4, smp[0])) continue;
+        if (!solver.isValidSample(data, smp)) continue;
+        if (solver.estimateModel(data, smp, models)) break;
+    }
+    if (!models.empty()) std::memcpy(model9, models[0].h, sizeof(models[0].h));
+    return (int)umg;
+}
+
+int oracle_h_score(const double* corr, size_t n, const double* model9, double thr, uint64_t* count, double* value,
+                   uint8_t* mask) {
+    Features f = make_features(corr, n, 4);
+    HModel m;
+    std::memcpy(m.h, model9, sizeof(m.h));
+    const double t[1] = {thr};
+    Inliers<1> in{};
+    auto s = getScore(HSolver{}, Data<1>{&f}, m, t, in);
+    *count = s.n[0];
+    *value = s.value();
+    if (mask) { std::memset(mask, 0, n); for (size_t i : in[0]) mask[i] = 1; }
+    return 0;
+}
+
+int oracle_h_residuals(const double* corr, size_t n, const double* model9, double* r2) {
+    Features f = make_features(corr, n, 4);
+    HModel m;
+    std::memcpy(m.h, model9, sizeof(m.h));
+    for (size_t i = 0; i < n; ++i) r2[i] = HSolver{}.squaredResidual(0, f, i, m);
+    return 0;
+}
+
+int oracle_h_fit(const double* corr, size_t n, const uint64_t* idx, size_t k, double* model9) {
+    Features f = make_features(corr, n, 4);
+    Inliers<1> in{};
+    for (size_t i = 0; i < k; ++i) in[0].push_back(idx[i]);
+    std::vector<HModel> models;
+    if (!HSolver{}.estimateModelNonminimal(Data<1>{&f}, in, models)) return 0;
+    std::memcpy(model9, models[0].h, sizeof(models[0].h));
+    return 1;
 }
 
 // ---- fine-grained hooks used by the parity tests -------------------------
@@ -1192,13 +1426,14 @@ int64_t oracle_hot_batch(int kind, const double* f0, size_t n0, const double* f1
                          uint64_t seed, uint64_t slot0, uint64_t nslots, int sampler, int math_mode, double* seconds,
                          double* best_value) {
     g_math = math_mode;
-    Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
+    // kind 3 (homography): f0 is N x 4 correspondences
+    Features a = make_features(f0, n0, kind == 3 ? 4 : 3), b = f1 ? make_features(f1, n1) : Features{};
     const double thr[2] = {thr0, thr1};
     auto go = [&](auto solver, auto data) -> int64_t {
         constexpr size_t K = decltype(solver)::K;
         Inliers<K> smp{}, pool{}, inl{};
         for (size_t c = 0; c < K; ++c) for (size_t j = 0; j < data[c]->n; ++j) pool[c].push_back(j);
-        std::vector<Model> models;
+        std::vector<typename decltype(solver)::ModelT> models;
         const auto m = solver.sampleSize();
         int64_t scored = 0;
         Score<K> best{};
@@ -1230,6 +1465,7 @@ int64_t oracle_hot_batch(int kind, const double* f0, size_t n0, const double* f1
     };
     if (kind == 0) return go(Solver<0>{}, Data<1>{&a});
     if (kind == 1) return go(Solver<1>{}, Data<1>{&a});
+    if (kind == 3) return go(HSolver{}, Data<1>{&a});
     return go(Solver<2>{}, Data<2>{&a, &b});
 }
 

@@ -68,6 +68,12 @@ def lib():
         L.oracle_hot_batch.argtypes = [C.c_int, dp, C.c_size_t, dp, C.c_size_t, C.c_double, C.c_double, C.c_uint64,
                                        C.c_uint64, C.c_uint64, C.c_int, C.c_int, dp, dp]
         L.oracle_hot_batch.restype = C.c_int64
+        L.oracle_find_homography.argtypes = [dp, C.c_size_t, C.POINTER(OracleParams), u8p, dp,
+                                             C.POINTER(OracleStats)]
+        L.oracle_h_slot.argtypes = [dp, C.c_size_t, C.c_uint64, C.c_uint64, dp]
+        L.oracle_h_score.argtypes = [dp, C.c_size_t, dp, C.c_double, u64p, dp, u8p]
+        L.oracle_h_residuals.argtypes = [dp, C.c_size_t, dp, dp]
+        L.oracle_h_fit.argtypes = [dp, C.c_size_t, u64p, C.c_size_t, dp]
         for name in ["oracle_clip_angle", "oracle_deg2rad", "oracle_rad2deg"]:
             getattr(L, name).argtypes = [C.c_double]
             getattr(L, name).restype = C.c_double
@@ -216,6 +222,55 @@ def fit_nonminimal(kind, f0, f1, idx0, idx1=None, math_mode=MATH_TWIN):
                                      0 if f1 is None else f1.shape[0], i0.ctypes.data_as(u64), len(i0),
                                      i1.ctypes.data_as(u64), len(i1), math_mode, _dp(m))
     return (m if ok else None)
+
+
+def find_homography(corr, thr, **kw):
+    c = _f64(corr)
+    n = c.shape[0]
+    mask = np.zeros(n, dtype=np.uint8)
+    H = np.zeros(9)
+    st = OracleStats()
+    p = params(thr, **kw)
+    r = lib().oracle_find_homography(_dp(c), n, C.byref(p), mask.ctypes.data_as(C.POINTER(C.c_uint8)), _dp(H),
+                                     C.byref(st))
+    if r < 0:
+        raise RuntimeError("oracle failed")
+    return dict(num_inliers=r, mask=mask.astype(bool), H=H.reshape(3, 3), stats=_stats_dict(st))
+
+
+def h_slot(corr, seed, slot):
+    c = _f64(corr)
+    m = np.zeros(9)
+    inc = lib().oracle_h_slot(_dp(c), c.shape[0], seed, slot, _dp(m))
+    return inc, m
+
+
+def h_score(corr, model9, thr, want_mask=False):
+    c = _f64(corr)
+    cnt = C.c_uint64()
+    val = C.c_double()
+    mask = np.zeros(c.shape[0], dtype=np.uint8) if want_mask else None
+    lib().oracle_h_score(_dp(c), c.shape[0], _dp(_f64(model9)), thr, C.byref(cnt), C.byref(val),
+                         mask.ctypes.data_as(C.POINTER(C.c_uint8)) if want_mask else None)
+    out = dict(count=int(cnt.value), value=val.value)
+    if want_mask:
+        out["mask"] = mask.astype(bool)
+    return out
+
+
+def h_residuals(corr, model9):
+    c = _f64(corr)
+    r2 = np.zeros(c.shape[0])
+    lib().oracle_h_residuals(_dp(c), c.shape[0], _dp(_f64(model9)), _dp(r2))
+    return r2
+
+
+def h_fit(corr, idx):
+    c = _f64(corr)
+    i = np.ascontiguousarray(np.asarray(idx, dtype=np.uint64))
+    m = np.zeros(9)
+    ok = lib().oracle_h_fit(_dp(c), c.shape[0], i.ctypes.data_as(C.POINTER(C.c_uint64)), len(i), _dp(m))
+    return m if ok else None
 
 
 def hot_batch(kind, f0, f1, thr0, thr1, seed, slot0, nslots, sampler=SAMPLER_FAITHFUL, math_mode=MATH_GLIBC):
