@@ -45,7 +45,7 @@ def score_kernel_name(kind, slots):
     if h not in (64, 16, 4):
         h = 64 if slots >= 16384 else 16 if slots >= 2048 else 4
     # the homography path generates in k_generate<3, G> and scores unfused
-    fused = "false" if kind == 3 else "true"
+    fused = "false" if kind >= 3 else "true"
     return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, {fused}>"
 
 
@@ -70,9 +70,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", choices=["m2", "m1", "h"], default="m2",
+    ap.add_argument("--workload", choices=["m2", "m1", "h", "f"], default="m2",
                     help="m2: configs[1] hybrid rectification (headline); m1: scale-only; "
-                         "h: configs[2] 4-pt homography, N=5000, 50%% outliers")
+                         "h: configs[2] 4-pt homography, N=5000, 50%% outliers; "
+                         "f: configs[3] 7-pt fundamental matrix, N=10000, 80%% outliers")
     ap.add_argument("--slots", type=int, default=4096, help="outer-iteration slots (hypotheses) per launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-latency", action="store_true")
@@ -120,6 +121,11 @@ def main():
         f1, thr1 = None, 0.0
         solver = N.SOLVER_HOMOGRAPHY4
         workload = "H 4-point homography (findHomography), 5000 correspondences"
+    elif args.workload == "f":
+        f0, _, _, thr0 = S.problem_f(10_000, 0.8, seed=seed)
+        f1, thr1 = None, 0.0
+        solver = N.SOLVER_FUNDAMENTAL7
+        workload = "F 7-point fundamental matrix (findFundamentalMatrix), 10000 correspondences"
     else:
         f0, _, thr0 = S.problem_m1(10_000, seed=seed)
         f1, thr1 = None, 0.0
@@ -190,14 +196,14 @@ def main():
         gathered = len(outs)
 
     value = models_total / elapsed
-    kind = {N.SOLVER_SIFT22: 2, N.SOLVER_HOMOGRAPHY4: 3}.get(solver, 0)
+    kind = {N.SOLVER_SIFT22: 2, N.SOLVER_HOMOGRAPHY4: 3, N.SOLVER_FUNDAMENTAL7: 4}.get(solver, 0)
     kernel_name = score_kernel_name(kind, args.slots)
     avg_kernel_s = acc["kernel_ms"] / max(1, acc["launches"]) / 1e3
     models_per_launch = acc["models"] / max(1, acc["launches"])
     # algorithmic bytes per hypothesis: one pass over the feature SoA the
     # residual reads -- 3 doubles per rectification feature, 4 per
     # correspondence (x1, y1, x2, y2)
-    bytes_per_feature = 32.0 if kind == 3 else 24.0
+    bytes_per_feature = 32.0 if kind >= 3 else 24.0
     bytes_per_launch = models_per_launch * bytes_per_feature * n_total
     achieved = bytes_per_launch / avg_kernel_s / 1e9 if avg_kernel_s > 0 else 0.0
 
@@ -207,7 +213,11 @@ def main():
         lat = []
         for r in range(3):
             t1 = time.perf_counter()
-            if solver == N.SOLVER_HOMOGRAPHY4:
+            if solver == N.SOLVER_FUNDAMENTAL7:
+                out = pygcransac.findFundamentalMatrix(f0, 960, 1280, 960, 1280, threshold=thr0, conf=0.99,
+                                                       min_iters=0, max_iters=10**7, seed=100 + r, device=device,
+                                                       return_stats=True)
+            elif solver == N.SOLVER_HOMOGRAPHY4:
                 out = pygcransac.findHomography(f0, 960, 1280, 960, 1280, threshold=thr0, conf=0.99,
                                                 min_iters=0, max_iters=10**7, seed=100 + r, device=device,
                                                 return_stats=True)
@@ -233,8 +243,8 @@ def main():
         # rectification: the reference's own sampler (random_device + mt19937 +
         # shuffle); homography (no reference, finding 0.1): the cheaper Philox
         # draw, i.e. the stronger CPU baseline
-        smp = O.SAMPLER_PHILOX if kind == 3 else O.SAMPLER_FAITHFUL
-        smp_text = ("Philox counter sampler" if kind == 3
+        smp = O.SAMPLER_PHILOX if kind >= 3 else O.SAMPLER_FAITHFUL
+        smp_text = ("Philox counter sampler" if kind >= 3
                     else "reference-faithful random_device+mt19937+shuffle sampler")
         n_cal, s_cal, _ = O.hot_batch(kind, f0, f1, thr0, thr1, seed, 0, 64, sampler=smp)
         rate = n_cal / max(s_cal, 1e-6)
@@ -261,7 +271,7 @@ def main():
             "config": {
                 "workload": workload,
                 "n_features": n_total,
-                "outlier_ratio": 0.5,
+                "outlier_ratio": 0.8 if kind == 4 else 0.5,
                 "hypotheses_per_launch": args.slots,
                 "parallelism": f"problem-sharded x{world}" if world > 1 else "single GPU",
             },

@@ -279,7 +279,7 @@ size_t gpu_refit_rows() {
 //                which fuses those adjacent cos/sin calls into sincos, and
 //                sincos differs from separate sin/cos in ~0.1% of arguments.
 void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1, size_t n1, HostClass* hc) {
-    if (solver == 3) {                       // correspondences (x1, y1, x2, y2)
+    if (solver == 3 || solver == 4) {        // correspondences (x1, y1, x2, y2)
         HostClass& h = hc[0];
         h.n = n0;
         h.x.resize(n0); h.y.resize(n0); h.a.resize(n0); h.c0.resize(n0); h.c1.assign(n0, 0.0);
@@ -321,9 +321,9 @@ void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1
 int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
                  gcr_problem** out, bool shared_workspace = false) {
     if (!ctx || !out) return set_err(GCR_EINVAL, "null context or output pointer");
-    if (solver < 0 || solver > 3) return set_err(GCR_EINVAL, "unknown solver %d", solver);
+    if (solver < 0 || solver > 4) return set_err(GCR_EINVAL, "unknown solver %d", solver);
     const int K = solver == 2 ? 2 : 1;
-    const size_t m0 = solver == 2 ? 2 : solver == 3 ? 4 : 3;
+    const size_t m0 = solver == 2 ? 2 : solver == 3 ? 4 : solver == 4 ? 7 : 3;
     if (!f0 || (K == 2 && !f1)) return set_err(GCR_EINVAL, "null feature pointer");
     if (n0 < m0 || (K == 2 && n1 < 2))
         return set_err(GCR_EINTERNAL, "Data set smaller than minimal sample size for corresponding data type");
@@ -372,6 +372,7 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
 // the rectification solvers (0-2) and the homography (3).
 struct RectTraits {
     using Model = RectModel;
+    static constexpr size_t kPer = 1;
     static Model def() { return default_model(); }
     static DevBuf<Model>& dmodels(Workspace* w) { return w->models; }
     static PinBuf<Model>& hmodels(Workspace* w) { return w->h_models; }
@@ -408,8 +409,9 @@ struct RectTraits {
     }
 };
 
-struct GeoTraits {
+struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     using Model = GeoModel;
+    static constexpr size_t kPer = 1;
     static Model def() { return default_geo(); }
     static DevBuf<Model>& dmodels(Workspace* w) { return w->gmodels; }
     static PinBuf<Model>& hmodels(Workspace* w) { return w->h_gmodels; }
@@ -434,12 +436,15 @@ struct GeoTraits {
         hipError_t e = launch_generate_geo(P->dp, seed, s0, n, P->w->inc.p, P->w->gmodels.p, s);
         if (e != hipSuccess) return e;
         if (e0) (void)hipEventRecord(e0, s);
-        e = launch_score_geo(P->dp, Tm[0], P->w->gmodels.p, P->w->inc.p, n, P->w->sb.dev(), s);
+        e = launch_score_geo(P->dp, Tm[0], P->w->gmodels.p, P->w->inc.p, n * (uint32_t)per(P), P->w->sb.dev(), s);
         if (e != hipSuccess) return e;
         if (e1) (void)hipEventRecord(e1, s);
-        return launch_select_geo(P->w->sb.dev(), P->w->inc.p, n, s0, m[0], Tm[0], rec, s);
+        return launch_select_geo(P->solver, P->w->sb.dev(), P->w->inc.p, n * (uint32_t)per(P), s0, m[0], Tm[0], rec,
+                                 s);
     }
+    static size_t per(gcr_problem* P) { return P->solver == 4 ? kFModels : 1; }
     static bool fit(gcr_problem* P, const std::vector<uint32_t>* lists, Model& out, bool) {
+        if (P->solver == 4) return fit_f8_nonminimal(P->hc[0], lists[0], out);
         return fit_h4_nonminimal(P->hc[0], lists[0], out);
     }
     static void output(const Model& m, double* H, gcr_rect_model*) {
@@ -447,14 +452,21 @@ struct GeoTraits {
     }
 };
 
+struct FundTraits : GeoTraits {     // up to kFModels models per sample
+    static constexpr size_t kPer = kFModels;
+};
+
+constexpr int kMaxLOSample = 64;     // largest LO sample: 7 x the largest minimal sample (7)
+
 template <class Tr>
 class RunnerT {
 public:
     using Model = typename Tr::Model;
     using Buffer = BufferT<Model>;
+    static constexpr size_t kP = Tr::kPer;           // hypotheses per slot
     RunnerT(gcr_problem* P, const gcr_params& prm) : P_(P), prm_(prm), s_(P->ctx->stream) {
         K_ = P->K;
-        m_[0] = P->solver == 2 ? 2 : P->solver == 3 ? 4 : 3;
+        m_[0] = P->solver == 2 ? 2 : P->solver == 3 ? 4 : P->solver == 4 ? 7 : 3;
         m_[1] = 2;
         thr_[0] = prm.scale_residual_thresh;
         thr_[1] = prm.orientation_residual_thresh;
@@ -498,13 +510,17 @@ public:
             const size_t j = slot - chunk_begin;
             bool do_lo = false;
             ++it_;
-            const uint8_t inc = P_->w->h_inc.p[j];
+            const uint8_t inc = P_->w->h_inc.p[j * kP];
             it_ += (uint64_t)inc - 1;
             ++slot;
-            if (inc <= 101) {
-                const Model& model = Tr::hmodels(P_->w).p[j];
-                const uint32_t rn[2] = {P_->w->sb.hn0.p[j], P_->w->sb.hn1.p[j]};
-                const HScore cur = finish(rn, P_->w->sb.hv0.p[j], P_->w->sb.hv1.p[j], P_->w->sb.htot.p[j]);
+            // the sample's models in solver order (kP > 1: inc 0 marks an
+            // extra model of the same sample, 255 an absent one)
+            for (size_t q = 0; inc <= 101 && q < kP; ++q) {
+                const size_t hj = j * kP + q;
+                if (q > 0 && P_->w->h_inc.p[hj] != 0) break;
+                const Model& model = Tr::hmodels(P_->w).p[hj];
+                const uint32_t rn[2] = {P_->w->sb.hn0.p[hj], P_->w->sb.hn1.p[hj]};
+                const HScore cur = finish(rn, P_->w->sb.hv0.p[hj], P_->w->sb.hv1.p[hj], P_->w->sb.htot.p[hj]);
                 bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
                 ++st_.hypotheses;
                 if (best_.sum < cur.sum && valid_model(model)) {
@@ -595,7 +611,7 @@ public:
         static_assert(sizeof(BatchRecord) == sizeof(gcr_batch_result), "record layout");
         static_assert(offsetof(BatchRecord, best_model) == offsetof(gcr_batch_result, best_model), "record layout");
         const auto t0 = Clock::now();
-        P_->w->inc.ensure(nslots); Tr::dmodels(P_->w).ensure(nslots); P_->w->sb.ensure(nslots);
+        P_->w->inc.ensure(nslots * kP); Tr::dmodels(P_->w).ensure(nslots * kP); P_->w->sb.ensure(nslots * kP);
         P_->w->recs.ensure(nb);
         while (P_->w->evs.size() < 2 * (size_t)nb) {
             hipEvent_t ev;
@@ -627,7 +643,7 @@ public:
         st_.ms_score_kernel += timed ? kms_sum * (double)nb / (double)timed : 0.0;   // scaled to all batches
         for (uint32_t b = 0; b < nb; ++b) st_.hypotheses += out[b].models;
         st_.launches += 2 * nb;
-        st_.hypotheses_computed += (uint64_t)nslots * nb;
+        st_.hypotheses_computed += (uint64_t)nslots * nb * kP;
         st_.ms_total += ms_since(t0);
     }
 
@@ -686,22 +702,24 @@ private:
     // Generate [s0, s0+B), then score only the slots the loop can still reach
     // (iterations can never pass max(min_it, max_it)).  Returns slots scored.
     uint64_t fetch_chunk(uint64_t s0, uint32_t B, uint64_t L) {
-        P_->w->inc.ensure(B); Tr::dmodels(P_->w).ensure(B); P_->w->sb.ensure(B);
-        P_->w->h_inc.ensure(B); Tr::hmodels(P_->w).ensure(B);
+        const size_t BP = (size_t)B * kP;
+        P_->w->inc.ensure(BP); Tr::dmodels(P_->w).ensure(BP); P_->w->sb.ensure(BP);
+        P_->w->h_inc.ensure(BP); Tr::hmodels(P_->w).ensure(BP);
         auto t0 = Clock::now();
         HIPC(Tr::generate(P_, prm_.seed, s0, B, P_->w->inc.p, Tr::dmodels(P_->w).p, s_));
-        HIPC(hipMemcpyAsync(P_->w->h_inc.p, P_->w->inc.p, B, hipMemcpyDeviceToHost, s_));
+        HIPC(hipMemcpyAsync(P_->w->h_inc.p, P_->w->inc.p, BP, hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
         st_.ms_generate += ms_since(t0);
         uint64_t itp = it_, cnt = 0;
-        while (cnt < B && itp < L) itp += P_->w->h_inc.p[cnt++];
+        while (cnt < B && itp < L) itp += P_->w->h_inc.p[kP * cnt++];
         if (cnt == 0) cnt = 1;
+        const size_t nh = cnt * kP;
         t0 = Clock::now();
         HIPC(hipEventRecord(P_->ctx->ev0, s_));
-        HIPC(Tr::score(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)cnt, true, P_->w->sb.dev(), s_));
+        HIPC(Tr::score(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, true, P_->w->sb.dev(), s_));
         HIPC(hipEventRecord(P_->ctx->ev1, s_));
-        P_->w->sb.d2h(cnt, s_);
-        HIPC(hipMemcpyAsync(Tr::hmodels(P_->w).p, Tr::dmodels(P_->w).p, cnt * sizeof(Model), hipMemcpyDeviceToHost,
+        P_->w->sb.d2h(nh, s_);
+        HIPC(hipMemcpyAsync(Tr::hmodels(P_->w).p, Tr::dmodels(P_->w).p, nh * sizeof(Model), hipMemcpyDeviceToHost,
                             s_));
         HIPC(hipStreamSynchronize(s_));
         float kms = 0;
@@ -709,7 +727,7 @@ private:
         st_.ms_score_kernel += kms;
         st_.ms_score += ms_since(t0);
         st_.launches += 2;
-        st_.hypotheses_computed += cnt;
+        st_.hypotheses_computed += nh;
         return cnt;
     }
 
@@ -760,6 +778,7 @@ private:
         Model lo_model = best_model_;
         Buffer lo_buf;
         const uint64_t limit[2] = {7 * m_[0], 7 * m_[1]};
+        static_assert(kMaxLOSample >= 7 * 7, "LO sample buffer");
 
         ++lo_number_;
         std::vector<uint32_t> inl[2], sample[2];
@@ -785,9 +804,13 @@ private:
                 bool ok = true;
                 for (int c = 0; c < K_ && ok; ++c) {
                     if (ssz[c] < inl[c].size()) {
-                        uint32_t pos[32];
+                        // 7 m points: 49 for the 7-point fundamental matrix
+                        uint32_t pos[kMaxLOSample];
                         WordStream ws(prm_.seed, round_id, (uint32_t)trial, kStreamLO, (uint32_t)c);
-                        if (!sample_distinct<32>(ws, inl[c].size(), (int)ssz[c], pos)) { ok = false; break; }
+                        if (!sample_distinct<kMaxLOSample>(ws, inl[c].size(), (int)ssz[c], pos)) {
+                            ok = false;
+                            break;
+                        }
                         sample[c].resize(ssz[c]);
                         for (uint64_t q = 0; q < ssz[c]; ++q) sample[c][q] = inl[c][pos[q]];
                     } else if (m_[c] < inl[c].size()) {
@@ -831,6 +854,7 @@ private:
 
 using Runner = RunnerT<RectTraits>;
 using GeoRunner = RunnerT<GeoTraits>;
+using FundRunner = RunnerT<FundTraits>;
 
 }  // namespace
 
@@ -947,6 +971,7 @@ int gcr_problem_run(gcr_problem* prob, const gcr_params* params, uint8_t* mask0_
             fill_stats(stats_out, r.stats());
             return total;
         };
+        if (prob->solver == GCR_SOLVER_FUNDAMENTAL7) return go(FundRunner(prob, *params));
         return prob->solver == GCR_SOLVER_HOMOGRAPHY4 ? go(GeoRunner(prob, *params)) : go(Runner(prob, *params));
     });
 }
@@ -963,6 +988,7 @@ int gcr_problem_verify_batches(gcr_problem* prob, const gcr_params* params, uint
             fill_stats(stats_out, r.stats());
             return GCR_OK;
         };
+        if (prob->solver == GCR_SOLVER_FUNDAMENTAL7) return go(FundRunner(prob, *params));
         return prob->solver == GCR_SOLVER_HOMOGRAPHY4 ? go(GeoRunner(prob, *params)) : go(Runner(prob, *params));
     });
 }
@@ -1011,19 +1037,42 @@ int gcr_find_homography(gcr_ctx* ctx, const double* correspondences, size_t n, c
                        nullptr, stats_out);
 }
 
+int gcr_find_fundamental_matrix(gcr_ctx* ctx, const double* correspondences, size_t n, const gcr_params* params,
+                                uint8_t* mask_out, double* F_out, gcr_stats* stats_out) {
+    return run_oneshot(ctx, GCR_SOLVER_FUNDAMENTAL7, correspondences, n, nullptr, 0, params, mask_out, nullptr, F_out,
+                       nullptr, stats_out);
+}
+
+int gcr_host_fit_f(const double* correspondences, size_t n, const uint32_t* idx, size_t k, double* F_out) {
+    if (!correspondences || !idx || !F_out) return set_err(GCR_EINVAL, "bad arguments");
+    return guard([&]() -> int {
+        HostClass hc[2];
+        fill_host_classes(GCR_SOLVER_FUNDAMENTAL7, correspondences, n, nullptr, 0, hc);
+        std::vector<uint32_t> list(idx, idx + k);
+        for (uint32_t i : list)
+            if (i >= n) return set_err(GCR_EINVAL, "index out of range");
+        GeoModel m;
+        if (!fit_f8_nonminimal(hc[0], list, m)) return 0;
+        for (int q = 0; q < 9; ++q) F_out[q] = m.h[q];
+        return 1;
+    });
+}
+
 // ------------------------------------------------------- homography debug ----
 int gcr_debug_generate_h(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc_out,
                          double* H_out) {
     if (!prob || !inc_out || !H_out) return set_err(GCR_EINVAL, "null argument");
-    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4) return set_err(GCR_EINVAL, "not a homography problem");
+    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4 && prob->solver != GCR_SOLVER_FUNDAMENTAL7)
+        return set_err(GCR_EINVAL, "not a correspondence (homography / fundamental) problem");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
-        prob->w->inc.ensure(nslots);
-        prob->w->gmodels.ensure(nslots);
+        const size_t nh = (size_t)nslots * GeoTraits::per(prob);
+        prob->w->inc.ensure(nh);
+        prob->w->gmodels.ensure(nh);
         hipStream_t s = prob->ctx->stream;
         HIPC(launch_generate_geo(prob->dp, seed, slot0, nslots, prob->w->inc.p, prob->w->gmodels.p, s));
-        HIPC(hipMemcpyAsync(inc_out, prob->w->inc.p, nslots, hipMemcpyDeviceToHost, s));
-        HIPC(hipMemcpyAsync(H_out, prob->w->gmodels.p, nslots * sizeof(GeoModel), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(inc_out, prob->w->inc.p, nh, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(H_out, prob->w->gmodels.p, nh * sizeof(GeoModel), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
         return GCR_OK;
     });
@@ -1032,7 +1081,8 @@ int gcr_debug_generate_h(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint3
 int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double* H, uint32_t nmodels, uint32_t* n0,
                       double* v0, double* tot) {
     if (!prob || !params || !H || !n0 || !v0 || !tot) return set_err(GCR_EINVAL, "null argument");
-    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4) return set_err(GCR_EINVAL, "not a homography problem");
+    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4 && prob->solver != GCR_SOLVER_FUNDAMENTAL7)
+        return set_err(GCR_EINVAL, "not a correspondence (homography / fundamental) problem");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
         hipStream_t s = prob->ctx->stream;
@@ -1053,7 +1103,8 @@ int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double*
 
 int gcr_debug_mask_h(gcr_problem* prob, const gcr_params* params, const double* H, int rule, uint8_t* mask_out) {
     if (!prob || !params || !H || !mask_out) return set_err(GCR_EINVAL, "null argument");
-    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4) return set_err(GCR_EINVAL, "not a homography problem");
+    if (prob->solver != GCR_SOLVER_HOMOGRAPHY4 && prob->solver != GCR_SOLVER_FUNDAMENTAL7)
+        return set_err(GCR_EINVAL, "not a correspondence (homography / fundamental) problem");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
         hipStream_t s = prob->ctx->stream;

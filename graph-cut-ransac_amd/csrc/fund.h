@@ -1,0 +1,259 @@
+// fund.h -- fundamental-matrix estimator of the hot path (SURVEY.md §8(f)
+// row 3, BASELINE configs[3]), host and device (GCR_HD).
+//
+// Like the homography (geo.h) this estimator is absent from the fork (SURVEY
+// finding 0.1) and upstream GC-RANSAC is not in the container: parity is
+// UNPINNED against any reference and rests on the oracle restatement
+// (oracle/gcr_oracle.cpp FSolver) plus synthetic two-view ground truth.  The
+// structure follows upstream's published 7-point estimator:
+//   * minimal solver: 7 correspondences, Hartley-normalised, the 2-D null space
+//     of the 7 x 9 epipolar system by Gaussian elimination with partial
+//     pivoting, det(F1 + l F2) = 0 as a cubic, up to three real roots -- so a
+//     sample may yield 1..3 models, every one of which is scored;
+//   * model validity: the oriented epipolar constraint on the 7 sample points
+//     (models violating it are dropped by the solver);
+//   * residual: squared Sampson distance;
+//   * non-minimal fit (LO, final refit; host only): normalised 8-point --
+//     smallest eigenvector of A^T A, then rank-2 projection.
+// Everything a device kernel evaluates uses +, -, *, / and sqrt only (all
+// correctly rounded on gfx950 and x86-64 with -ffp-contract=off): the cubic is
+// solved by bracketing between the critical points and bisection, not by
+// Cardano (which would need cbrt / acos / cos twins).
+#pragma once
+
+#include "gcr_hd.h"
+#include "geo.h"
+
+namespace gcr {
+
+constexpr int kFModels = 3;          // real roots of the cubic, models per sample
+
+GCR_HD double det3(const double* m) {
+    return (m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6])) +
+           m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+// ((l + a) l + b) l + c
+GCR_HD double cubic_monic(double a, double b, double c, double l) { return ((l + a) * l + b) * l + c; }
+
+// Real roots of c3 l^3 + c2 l^2 + c1 l + c0 in ascending order (basic ops +
+// sqrt only).  Returns the count.
+GCR_HD int real_roots_cubic(double c3, double c2, double c1, double c0, double r[3]) {
+    const double big = __builtin_fmax(__builtin_fabs(c2), __builtin_fmax(__builtin_fabs(c1), __builtin_fabs(c0)));
+    if (!(__builtin_fabs(c3) > 1e-12 * big)) {
+        // degenerate leading coefficient: quadratic / linear
+        if (c2 != 0.0) {
+            const double disc = c1 * c1 - 4.0 * c2 * c0;
+            if (disc < 0.0) return 0;
+            const double sq = sqrt(disc);
+            double u = (-c1 - sq) / (2.0 * c2), v = (-c1 + sq) / (2.0 * c2);
+            if (v < u) { const double t = u; u = v; v = t; }
+            r[0] = u;
+            if (v == u) return 1;
+            r[1] = v;
+            return 2;
+        }
+        if (c1 != 0.0) {
+            r[0] = -c0 / c1;
+            return 1;
+        }
+        return 0;
+    }
+    const double a = c2 / c3, b = c1 / c3, c = c0 / c3;
+    const double R = 1.0 + __builtin_fmax(__builtin_fabs(a), __builtin_fmax(__builtin_fabs(b), __builtin_fabs(c)));
+    double ends[4];
+    int ne;
+    const double dd = a * a - 3.0 * b;          // discriminant of the derivative / 4
+    if (dd <= 0.0) {
+        ends[0] = -R; ends[1] = R; ne = 2;
+    } else {
+        const double sq = sqrt(dd);
+        ends[0] = -R;
+        ends[1] = (-a - sq) / 3.0;
+        ends[2] = (-a + sq) / 3.0;
+        ends[3] = R;
+        ne = 4;
+    }
+    int n = 0;
+    for (int k = 0; k + 1 < ne; ++k) {
+        double lo = ends[k], hi = ends[k + 1];
+        double flo = cubic_monic(a, b, c, lo);
+        const double fhi = cubic_monic(a, b, c, hi);
+        if (flo == 0.0) {
+            if (n == 0 || r[n - 1] != lo) r[n++] = lo;
+            continue;
+        }
+        if (!((flo < 0.0) != (fhi < 0.0)) || fhi == 0.0) continue;
+        for (int it = 0; it < 256; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            if (!(mid > lo && mid < hi)) break;
+            const double fm = cubic_monic(a, b, c, mid);
+            if (fm == 0.0) { lo = mid; break; }
+            if ((fm < 0.0) == (flo < 0.0)) { lo = mid; flo = fm; }
+            else hi = mid;
+        }
+        r[n++] = lo;
+    }
+    return n;
+}
+
+// Hartley normalisation of n points: centroid, mean distance, s = sqrt(2) / d;
+// normalised u = s * (x - cx).  Sequential sums in index order.
+template <int N>
+GCR_HD bool hartley7(const double* x, const double* y, double& cx, double& cy, double& s) {
+    double sx = 0.0, sy = 0.0;
+    for (int i = 0; i < N; ++i) { sx += x[i]; sy += y[i]; }
+    cx = sx / (double)N;
+    cy = sy / (double)N;
+    double sd = 0.0;
+    for (int i = 0; i < N; ++i) {
+        const double dx = x[i] - cx, dy = y[i] - cy;
+        sd += sqrt(dx * dx + dy * dy);
+    }
+    const double d = sd / (double)N;
+    if (!(d > 0.0)) return false;
+    s = 1.4142135623730951 / d;
+    return true;
+}
+
+// F = T2^T Fn T1 with Ti = [[si, 0, -si cxi], [0, si, -si cyi], [0, 0, 1]],
+// then scaled to unit Frobenius norm.
+GCR_HD bool denormalize_f(const double* fn, double s1, double cx1, double cy1, double s2, double cx2, double cy2,
+                          double* f) {
+    const double tx1 = -s1 * cx1, ty1 = -s1 * cy1, tx2 = -s2 * cx2, ty2 = -s2 * cy2;
+    double m[9];
+    for (int i = 0; i < 3; ++i) {
+        m[3 * i] = fn[3 * i] * s1;
+        m[3 * i + 1] = fn[3 * i + 1] * s1;
+        m[3 * i + 2] = (fn[3 * i] * tx1 + fn[3 * i + 1] * ty1) + fn[3 * i + 2];
+    }
+    for (int j = 0; j < 3; ++j) {
+        f[j] = s2 * m[j];
+        f[3 + j] = s2 * m[3 + j];
+        f[6 + j] = (tx2 * m[j] + ty2 * m[3 + j]) + m[6 + j];
+    }
+    double nn = 0.0;
+    for (int k = 0; k < 9; ++k) nn += f[k] * f[k];
+    const double nrm = sqrt(nn);
+    if (!(nrm > 0.0) || !(nrm < 1e300)) return false;
+    for (int k = 0; k < 9; ++k) f[k] = f[k] / nrm;
+    return true;
+}
+
+// Oriented epipolar constraint (Chum, Werner, Matas 2004): with e2 the
+// epipole of image 2 (F^T e2 = 0), (e2 x x2_i) . (F x1_i) has one sign for
+// every correspondence of the sample.
+template <int N>
+GCR_HD bool oriented_ok(const double* f, const double* x1, const double* y1, const double* x2, const double* y2) {
+    // e2 orthogonal to every column of F: the largest cross product of two columns
+    const double c[3][3] = {{f[0], f[3], f[6]}, {f[1], f[4], f[7]}, {f[2], f[5], f[8]}};
+    const int pa[3] = {0, 0, 1}, pb[3] = {1, 2, 2};
+    double e[3] = {0.0, 0.0, 0.0}, best = -1.0;
+    for (int q = 0; q < 3; ++q) {
+        const double* u = c[pa[q]];
+        const double* v = c[pb[q]];
+        const double w0 = u[1] * v[2] - u[2] * v[1];
+        const double w1 = u[2] * v[0] - u[0] * v[2];
+        const double w2 = u[0] * v[1] - u[1] * v[0];
+        const double nn = (w0 * w0 + w1 * w1) + w2 * w2;
+        if (nn > best) { best = nn; e[0] = w0; e[1] = w1; e[2] = w2; }
+    }
+    if (!(best > 0.0)) return false;
+    int pos = 0, neg = 0;
+    for (int i = 0; i < N; ++i) {
+        const double fx0 = (f[0] * x1[i] + f[1] * y1[i]) + f[2];
+        const double fx1 = (f[3] * x1[i] + f[4] * y1[i]) + f[5];
+        const double fx2 = (f[6] * x1[i] + f[7] * y1[i]) + f[8];
+        // e2 x (x2, y2, 1)
+        const double l0 = e[1] - e[2] * y2[i];
+        const double l1 = e[2] * x2[i] - e[0];
+        const double l2 = e[0] * y2[i] - e[1] * x2[i];
+        const double sgn = (l0 * fx0 + l1 * fx1) + l2 * fx2;
+        pos += sgn > 0.0;
+        neg += sgn < 0.0;
+    }
+    return pos == N || neg == N;
+}
+
+// 7-point solver: up to kFModels oriented-valid models, returned in ascending
+// root order.  0 = the sample yields no model.
+GCR_HD int solve_f7(const double x1[7], const double y1[7], const double x2[7], const double y2[7],
+                    GeoModel out[kFModels]) {
+    double cx1, cy1, s1, cx2, cy2, s2;
+    if (!hartley7<7>(x1, y1, cx1, cy1, s1) || !hartley7<7>(x2, y2, cx2, cy2, s2)) return 0;
+    double a[7][9];
+    for (int i = 0; i < 7; ++i) {
+        const double u1 = s1 * (x1[i] - cx1), v1 = s1 * (y1[i] - cy1);
+        const double u2 = s2 * (x2[i] - cx2), v2 = s2 * (y2[i] - cy2);
+        a[i][0] = u2 * u1; a[i][1] = u2 * v1; a[i][2] = u2;
+        a[i][3] = v2 * u1; a[i][4] = v2 * v1; a[i][5] = v2;
+        a[i][6] = u1;      a[i][7] = v1;      a[i][8] = 1.0;
+    }
+    // forward elimination, partial pivoting on columns 0..6
+    for (int k = 0; k < 7; ++k) {
+        int p = k;
+        double pm = __builtin_fabs(a[k][k]);
+        for (int i = k + 1; i < 7; ++i)
+            if (__builtin_fabs(a[i][k]) > pm) { pm = __builtin_fabs(a[i][k]); p = i; }
+        if (!(pm > 1e-10)) return 0;                 // rank < 7: degenerate sample
+        if (p != k)
+            for (int j = k; j < 9; ++j) { const double t = a[k][j]; a[k][j] = a[p][j]; a[p][j] = t; }
+        for (int i = k + 1; i < 7; ++i) {
+            const double fct = a[i][k] / a[k][k];
+            for (int j = k + 1; j < 9; ++j) a[i][j] = a[i][j] - fct * a[k][j];
+            a[i][k] = 0.0;
+        }
+    }
+    // null-space basis: (f7, f8) = (1, 0) and (0, 1)
+    double F1[9], F2[9];
+    for (int b = 0; b < 2; ++b) {
+        double* f = b == 0 ? F1 : F2;
+        f[7] = b == 0 ? 1.0 : 0.0;
+        f[8] = b == 0 ? 0.0 : 1.0;
+        for (int r = 6; r >= 0; --r) {
+            double acc = a[r][7] * f[7];
+            acc = acc + a[r][8] * f[8];
+            for (int cc = r + 1; cc < 7; ++cc) acc = acc + a[r][cc] * f[cc];
+            f[r] = -acc / a[r][r];
+        }
+    }
+    // det(F1 + l F2) = c3 l^3 + c2 l^2 + c1 l + c0 from four evaluations
+    double P[9], M[9];
+    for (int k = 0; k < 9; ++k) { P[k] = F1[k] + F2[k]; M[k] = F1[k] - F2[k]; }
+    const double c0 = det3(F1), c3 = det3(F2), d1 = det3(P), dm1 = det3(M);
+    const double c2 = (d1 + dm1) * 0.5 - c0;
+    const double c1 = (d1 - dm1) * 0.5 - c3;
+    double roots[3];
+    const int nr = real_roots_cubic(c3, c2, c1, c0, roots);
+    int n = 0;
+    for (int q = 0; q < nr; ++q) {
+        double fn[9], f[9];
+        for (int k = 0; k < 9; ++k) fn[k] = F1[k] + roots[q] * F2[k];
+        if (!denormalize_f(fn, s1, cx1, cy1, s2, cx2, cy2, f)) continue;
+        if (!oriented_ok<7>(f, x1, y1, x2, y2)) continue;
+        for (int k = 0; k < 9; ++k) out[n].h[k] = f[k];
+        ++n;
+    }
+    return n;
+}
+
+// squared Sampson distance of (x1, y1) <-> (x2, y2) under F
+GCR_HD double f_sq_sampson(double x1, double y1, double x2, double y2, const double* h) {
+    const double fx0 = (h[0] * x1 + h[1] * y1) + h[2];
+    const double fx1 = (h[3] * x1 + h[4] * y1) + h[5];
+    const double fx2 = (h[6] * x1 + h[7] * y1) + h[8];
+    const double ft0 = (h[0] * x2 + h[3] * y2) + h[6];
+    const double ft1 = (h[1] * x2 + h[4] * y2) + h[7];
+    const double num = (x2 * fx0 + y2 * fx1) + fx2;
+    const double den = ((fx0 * fx0 + fx1 * fx1) + ft0 * ft0) + ft1 * ft1;
+    return (num * num) / den;
+}
+
+// residual of the correspondence estimators: 3 = homography, 4 = fundamental
+template <int KIND>
+GCR_HD double geo_sq_residual(double x1, double y1, double x2, double y2, const double* h) {
+    if constexpr (KIND == 4) return f_sq_sampson(x1, y1, x2, y2, h);
+    else return h_sq_residual(x1, y1, x2, y2, h);
+}
+
+}  // namespace gcr

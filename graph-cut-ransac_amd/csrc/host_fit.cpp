@@ -266,4 +266,125 @@ bool fit_h4_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, Geo
     return true;
 }
 
+template <int N>
+void jacobi_eigen(double (&a)[N][N], double (&v)[N][N], double (&d)[N]) {
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) v[i][j] = i == j ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 64; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < N; ++p)
+            for (int q = p + 1; q < N; ++q) off += a[p][q] * a[p][q];
+        if (!(off > 0.0)) break;
+        for (int p = 0; p < N; ++p)
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = a[p][q];
+                if (apq == 0.0) continue;
+                const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+                double t = 1.0 / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                if (theta < 0.0) t = -t;
+                const double cs = 1.0 / std::sqrt(t * t + 1.0), sn = t * cs;
+                for (int k = 0; k < N; ++k) {           // columns p, q
+                    const double akp = a[k][p], akq = a[k][q];
+                    a[k][p] = cs * akp - sn * akq;
+                    a[k][q] = sn * akp + cs * akq;
+                }
+                for (int k = 0; k < N; ++k) {           // rows p, q
+                    const double apk = a[p][k], aqk = a[q][k];
+                    a[p][k] = cs * apk - sn * aqk;
+                    a[q][k] = sn * apk + cs * aqk;
+                }
+                a[p][q] = 0.0;
+                a[q][p] = 0.0;
+                for (int k = 0; k < N; ++k) {
+                    const double vkp = v[k][p], vkq = v[k][q];
+                    v[k][p] = cs * vkp - sn * vkq;
+                    v[k][q] = sn * vkp + cs * vkq;
+                }
+            }
+    }
+    for (int k = 0; k < N; ++k) d[k] = a[k][k];
+}
+
+template void jacobi_eigen<3>(double (&)[3][3], double (&)[3][3], double (&)[3]);
+template void jacobi_eigen<9>(double (&)[9][9], double (&)[9][9], double (&)[9]);
+
+namespace {
+// column of v with the smallest eigenvalue (first on ties)
+template <int N>
+int argmin_eig(const double (&d)[N]) {
+    int k = 0;
+    for (int i = 1; i < N; ++i)
+        if (d[i] < d[k]) k = i;
+    return k;
+}
+}  // namespace
+
+bool fit_f8_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, GeoModel& out) {
+    const size_t n = idx.size();
+    if (n < 7) return false;
+    if (n == 7) {
+        double x1[7], y1[7], x2[7], y2[7];
+        for (int i = 0; i < 7; ++i) {
+            x1[i] = c.x[idx[i]]; y1[i] = c.y[idx[i]]; x2[i] = c.a[idx[i]]; y2[i] = c.c0[idx[i]];
+        }
+        GeoModel ms[kFModels];
+        if (solve_f7(x1, y1, x2, y2, ms) == 0) return false;
+        out = ms[0];
+        return true;
+    }
+    const double inv_n = 1.0 / static_cast<double>(n);
+    const double mx1 = blocked_sum(0, n, [&](size_t i) { return c.x[idx[i]]; }) * inv_n;
+    const double my1 = blocked_sum(0, n, [&](size_t i) { return c.y[idx[i]]; }) * inv_n;
+    const double mx2 = blocked_sum(0, n, [&](size_t i) { return c.a[idx[i]]; }) * inv_n;
+    const double my2 = blocked_sum(0, n, [&](size_t i) { return c.c0[idx[i]]; }) * inv_n;
+    const double d1 = blocked_sum(0, n, [&](size_t i) {
+        const double dx = c.x[idx[i]] - mx1, dy = c.y[idx[i]] - my1;
+        return std::sqrt(dx * dx + dy * dy);
+    }) * inv_n;
+    const double d2 = blocked_sum(0, n, [&](size_t i) {
+        const double dx = c.a[idx[i]] - mx2, dy = c.c0[idx[i]] - my2;
+        return std::sqrt(dx * dx + dy * dy);
+    }) * inv_n;
+    if (!(d1 > 1e-12) || !(d2 > 1e-12)) return false;
+    const double s1 = std::sqrt(2.0) / d1, s2 = std::sqrt(2.0) / d2;
+    // A^T A, upper triangle, accumulated in blocked order (all entries in one pass)
+    double ata[9][9] = {};
+    size_t i = 0;
+    while (i < n) {
+        const size_t end = std::min(n, (i / kSumBlock + 1) * kSumBlock);
+        double part[9][9] = {};
+        for (; i < end; ++i) {
+            const double u1 = (c.x[idx[i]] - mx1) * s1, v1 = (c.y[idx[i]] - my1) * s1;
+            const double u2 = (c.a[idx[i]] - mx2) * s2, v2 = (c.c0[idx[i]] - my2) * s2;
+            const double r[9] = {u2 * u1, u2 * v1, u2, v2 * u1, v2 * v1, v2, u1, v1, 1.0};
+            for (int p = 0; p < 9; ++p)
+                for (int q = p; q < 9; ++q) part[p][q] += r[p] * r[q];
+        }
+        for (int p = 0; p < 9; ++p)
+            for (int q = p; q < 9; ++q) ata[p][q] += part[p][q];
+    }
+    for (int p = 0; p < 9; ++p)
+        for (int q = 0; q < p; ++q) ata[p][q] = ata[q][p];
+    double V[9][9], D[9];
+    jacobi_eigen<9>(ata, V, D);
+    const int k9 = argmin_eig<9>(D);
+    double fn[9];
+    for (int k = 0; k < 9; ++k) fn[k] = V[k][k9];
+    // rank 2: Fn (I - v v^T), v the right singular vector of the smallest
+    // singular value (smallest eigenvector of Fn^T Fn)
+    double ftf[3][3];
+    for (int p = 0; p < 3; ++p)
+        for (int q = 0; q < 3; ++q) ftf[p][q] = (fn[p] * fn[q] + fn[3 + p] * fn[3 + q]) + fn[6 + p] * fn[6 + q];
+    double V3[3][3], D3[3];
+    jacobi_eigen<3>(ftf, V3, D3);
+    const int k3 = argmin_eig<3>(D3);
+    const double v[3] = {V3[0][k3], V3[1][k3], V3[2][k3]};
+    double f2[9];
+    for (int r = 0; r < 3; ++r) {
+        const double fv = (fn[3 * r] * v[0] + fn[3 * r + 1] * v[1]) + fn[3 * r + 2] * v[2];
+        for (int q = 0; q < 3; ++q) f2[3 * r + q] = fn[3 * r + q] - fv * v[q];
+    }
+    return denormalize_f(f2, s1, mx1, my1, s2, mx2, my2, out.h);
+}
+
 }  // namespace gcr

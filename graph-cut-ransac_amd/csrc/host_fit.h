@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "fund.h"
 #include "geo.h"
 #include "rect.h"
 
@@ -48,6 +49,17 @@ bool fit_nonminimal(int solver, const HostClass* cls, const std::vector<uint32_t
 // 8-column pivoted QR of qr3.h, denormalised and scaled to h33 = 1.
 // Correspondences: c.x = x1, c.y = y1, c.a = x2, c.c0 = y2.
 bool fit_h4_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, GeoModel& out);
+
+// Non-minimal fundamental-matrix fit (LO and final refit; fund.h): exactly 7
+// points -> the 7-point solver's first model; more -> normalised 8-point
+// (smallest eigenvector of A^T A by cyclic Jacobi, rank-2 projection), unit
+// Frobenius norm.  Blocked-order sums (qr3.h), restated by the oracle.
+bool fit_f8_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, GeoModel& out);
+
+// Cyclic Jacobi eigen-decomposition of a symmetric N x N matrix (a is
+// destroyed); eigenvalues d[k] with eigenvectors in the COLUMNS of v.
+template <int N>
+void jacobi_eigen(double (&a)[N][N], double (&v)[N][N], double (&d)[N]);
 
 // findWeightedMode (two_sift.hpp:354-394), libstdc++ unordered_map order.
 double weighted_mode(const std::vector<double>& angles, const std::vector<double>& weights, double bin_width);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "fund.h"
 #include "geo.h"
 #include "rect.h"
 
@@ -29,6 +30,11 @@ struct ModelOf {
 };
 template <>
 struct ModelOf<3> {
+    using type = GeoModel;
+    static GCR_HD type def() { return default_geo(); }
+};
+template <>
+struct ModelOf<4> {                 // fundamental matrix: same 9-double POD
     using type = GeoModel;
     static GCR_HD type def() { return default_geo(); }
 };
@@ -121,14 +127,17 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
 
 // homography (solver 3) counterparts of launch_generate / launch_score /
 // launch_mask / launch_select
+// solver 3 (homography): one hypothesis per slot; solver 4 (fundamental
+// matrix): kFModels hypotheses per slot (inc / models sized kFModels * nslots,
+// see k_generate_f).  Score / mask / select dispatch on the same solver.
 hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
                                GeoModel* models, hipStream_t stream);
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
                             const ScoreOut& out, hipStream_t stream);
 hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule, double T, double lambda,
                            uint8_t* mask, hipStream_t stream);
-hipError_t launch_select_geo(const ScoreOut& sc, const uint8_t* inc, uint32_t nslots, uint64_t slot0, uint32_t m,
-                             double Tm, BatchRecord* out, hipStream_t stream);
+hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint64_t slot0,
+                             uint32_t m, double Tm, BatchRecord* out, hipStream_t stream);
 
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)

@@ -130,6 +130,67 @@ __global__ __launch_bounds__(kGenBlock) void k_generate(DevProblem p, uint64_t s
     }
 }
 
+// Fundamental matrix: one attempt = Philox sample of 7 correspondences ->
+// 7-point solver (fund.h), 0..3 models.  No sample-validity test beyond the
+// solver's own rank and orientation checks.
+GCR_DEVICE int attempt_f(const DevProblem& p, uint64_t seed, uint64_t slot, uint32_t a, GeoModel (&ms)[kFModels]) {
+    const DevClass& c = p.cls[0];
+    uint32_t idx[7];
+    WordStream ws(seed, slot, a, kStreamMain, 0);
+    if (!sample_distinct<7>(ws, c.n, 7, idx)) return 0;
+    double x1[7], y1[7], x2[7], y2[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+        x1[j] = c.x[idx[j]];
+        y1[j] = c.y[idx[j]];
+        x2[j] = c.a[idx[j]];
+        y2[j] = c.c0[idx[j]];
+    }
+    return solve_f7(x1, y1, x2, y2, ms);
+}
+
+// k_generate for the fundamental matrix: a sample yields up to kFModels
+// models, stored as hypotheses 3s + k.  inc[3s] = attempt + 1 (102: all 101
+// attempts failed); inc[3s + k], k >= 1, = 0 if the k-th model exists (scored,
+// no extra iterations) and 255 if not (skipped).
+template <int G>
+__global__ __launch_bounds__(kGenBlock) void k_generate_f(DevProblem p, uint64_t seed, uint64_t slot0,
+                                                          uint32_t nslots, uint8_t* __restrict__ inc,
+                                                          GeoModel* __restrict__ models) {
+    static_assert(G >= 1 && G <= 64 && (64 % G) == 0, "group size");
+    const uint32_t tid = blockIdx.x * kGenBlock + threadIdx.x;
+    const uint32_t s = tid / G;
+    const uint32_t g = tid % G;
+    if (s >= nslots) return;
+    const uint64_t slot = slot0 + s;
+    const int lane = threadIdx.x & 63;
+    const int gbase = lane & ~(G - 1);
+    for (uint32_t r = 0; r * G < 101; ++r) {
+        const uint32_t a = r * G + g;
+        GeoModel ms[kFModels];
+        const int cnt = a < 101 ? attempt_f(p, seed, slot, a, ms) : 0;
+        const uint64_t mask = __ballot(cnt > 0);
+        const uint64_t grp = G == 64 ? mask : (mask >> gbase) & ((1ull << G) - 1ull);
+        if (grp) {
+            if (g == (uint32_t)__builtin_ctzll(grp)) {
+#pragma unroll
+                for (int q = 0; q < kFModels; ++q) {
+                    models[(size_t)kFModels * s + q] = q < cnt ? ms[q] : default_geo();
+                    inc[(size_t)kFModels * s + q] = q == 0 ? (uint8_t)(a + 1) : (q < cnt ? 0 : 255);
+                }
+            }
+            return;
+        }
+    }
+    if (g == 0) {
+#pragma unroll
+        for (int q = 0; q < kFModels; ++q) {
+            models[(size_t)kFModels * s + q] = default_geo();
+            inc[(size_t)kFModels * s + q] = q == 0 ? 102 : 255;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- score ----
 template <int KIND, bool kIdentity>
 __global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, double T1,
@@ -289,7 +350,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                 fbuf[buf][1][e] = c.y[i];
                 if (cls == 0) {
                     fbuf[buf][2][e] = c.a[i];
-                    if constexpr (KIND == 3) fbuf[buf][3][e] = c.c0[i];
+                    if constexpr (KIND >= 3) fbuf[buf][3][e] = c.c0[i];
                 } else {
                     fbuf[buf][2][e] = c.c0[i];
                     fbuf[buf][3][e] = c.c1[i];
@@ -308,7 +369,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
         const uint32_t base = (cls == 0 ? rr : rr - r0) * R;
         const uint32_t last = ((c.n + 1u) & ~1u) - 2u;
         const double* src[4] = {c.x, c.y, cls == 0 ? c.a : c.c0, cls == 0 ? c.c0 : c.c1};
-        const int nf = (cls == 0 && KIND != 3) ? 3 : 4;
+        const int nf = (cls == 0 && KIND < 3) ? 3 : 4;
         for (int f = 0; f < nf; ++f) {
 #pragma unroll
             for (int q = 0; q < kRp / 128; ++q) {
@@ -350,8 +411,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     const bool valid_h = hg < nh && (kGen ? gen_a[h] != 127 : (inc == nullptr || inc[hg] <= 101));
     const bool live = !chain_wave && valid_h;
 
-    if (KIND == 3 && t < H) {
-        if constexpr (KIND == 3) {
+    if (KIND >= 3 && t < H) {
+        if constexpr (KIND >= 3) {
             const GeoModel m = valid_h ? models[hg] : default_geo();
             HypConst q;
             for (int j = 0; j < 9; ++j) q.g[j] = m.h[j];
@@ -360,7 +421,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     } else if (t < H) {
         const bool v = valid_h;
         RectModel m = default_model();
-        if constexpr (KIND != 3) m = v ? (kGen ? gen_m[h] : models[hg]) : default_model();
+        if constexpr (KIND < 3) m = v ? (kGen ? gen_m[h] : models[hg]) : default_model();
         HypConst q;
         q.h7 = m.h7;
         q.h8 = m.h8;
@@ -397,15 +458,15 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                 const int cls = (r < r0) ? 0 : 1;
                 const uint32_t base = (cls == 0 ? r : r - r0) * R;
                 const uint32_t nc = cls == 0 ? n0 : n1;
-                if constexpr (KIND == 3) {
-                    // homography: the exact residual is cheap, every pair is
-                    // evaluated directly (no band, no queue)
+                if constexpr (KIND >= 3) {
+                    // homography / fundamental matrix: the exact residual is
+                    // cheap, every pair is evaluated directly (no band, no queue)
 #pragma unroll
                     for (int k = 0; k < kPer; ++k) {
                         const uint32_t il = fsub + k * kStride;
                         double v = 0.0;
                         if (live && base + il < nc) {
-                            const double r2 = h_sq_residual(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine.g);
+                            const double r2 = geo_sq_residual<KIND>(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine.g);
                             if (r2 <= T0) {
                                 v = -r2;
                                 atomicAdd(&cnt_sh[0][h], 1u);
@@ -466,7 +527,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         atomicAdd(&cnt_sh[cls][hh], 1u);
                     }
                 }
-                }   // KIND != 3
+                }   // KIND < 3
             }
         } else {
             // chain wave: stage round r+1's features around the fold of
@@ -571,11 +632,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
 // --------------------------------------------------------------- select ----
 constexpr int kSelectThreads = 1024;
 
+// `per` hypotheses per slot (3 for the fundamental matrix: inc 0 = extra
+// model of the slot, 255 = absent, neither adds iterations).
 template <class M>
 __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut sc, const uint8_t* __restrict__ inc,
                                                            const M* __restrict__ models, uint32_t n,
                                                            uint64_t slot0, uint32_t m0, uint32_t m1, double Tm0,
-                                                           double Tm1, BatchRecord* out) {
+                                                           double Tm1, BatchRecord* out, uint32_t per = 1) {
     __shared__ double s_val[kSelectThreads];
     __shared__ uint32_t s_idx[kSelectThreads];
     __shared__ unsigned long long s_models[kSelectThreads], s_its[kSelectThreads];
@@ -586,7 +649,7 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
     unsigned long long nm = 0, its = 0;
     for (uint32_t j = t; j < n; j += kSelectThreads) {
         const uint32_t in = inc[j];
-        its += in;
+        its += in <= 102 ? in : 0;
         if (in > 101) continue;
         ++nm;
         double sum = sc.tot[j];
@@ -635,7 +698,7 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
         r.best_model = default_model();
         const uint32_t j = s_idx[0];
         if (j != 0xffffffffu) {
-            r.best_slot = static_cast<int64_t>(slot0 + j);
+            r.best_slot = static_cast<int64_t>(slot0 + j / per);
             r.best_score = s_val[0];
             r.best_inliers[0] = sc.n0[j];
             r.best_inliers[1] = K == 2 ? sc.n1[j] : 0;
@@ -806,7 +869,7 @@ __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, typena
     const uint32_t i = blockIdx.x * kMaskBlock + threadIdx.x;
     if (i >= c.n) return;
     double r2;
-    if constexpr (KIND == 3) r2 = h_sq_residual(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
+    if constexpr (KIND >= 3) r2 = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
     else if (cls == 0) r2 = scale_sq_residual<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
     else r2 = orient_sq_residual<false>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
     bool inl;
@@ -1038,14 +1101,17 @@ hipError_t launch_math(int op, const double* a, const double* b, size_t n, doubl
     return hipGetLastError();
 }
 
-// ------------------------------------------------------- homography (3) ----
+// ------------------------------------ homography (3) / fundamental (4) ----
 hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
                                GeoModel* models, hipStream_t stream) {
     if (nslots == 0) return hipSuccess;
     auto go = [&](auto gtag) {
         constexpr int G = decltype(gtag)::value;
         const dim3 grid(blocks_for((size_t)nslots * G, kGenBlock)), block(kGenBlock);
-        hipLaunchKernelGGL((k_generate<3, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+        if (p.solver == 4)
+            hipLaunchKernelGGL((k_generate_f<G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+        else
+            hipLaunchKernelGGL((k_generate<3, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
     };
     if (nslots <= 8192) go(std::integral_constant<int, 16>{});
     else if (nslots <= 32768) go(std::integral_constant<int, 4>{});
@@ -1056,15 +1122,19 @@ hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
                             const ScoreOut& out, hipStream_t stream) {
     if (nh == 0) return hipSuccess;
-    auto go = [&](auto htag, auto rtag) {
-        constexpr int H = decltype(htag)::value, R = decltype(rtag)::value;
-        hipLaunchKernelGGL((k_score_split<3, H, R, false>), dim3((nh + H - 1) / H), dim3(kSplitThreads), 0, stream,
-                           p, T, 0.0, 0.0, 0.0, models, inc, nh, out, GenArgs{});
+    auto go = [&](auto ktag, auto htag, auto rtag) {
+        constexpr int KIND = decltype(ktag)::value, H = decltype(htag)::value, R = decltype(rtag)::value;
+        hipLaunchKernelGGL((k_score_split<KIND, H, R, false>), dim3((nh + H - 1) / H), dim3(kSplitThreads), 0,
+                           stream, p, T, 0.0, 0.0, 0.0, models, inc, nh, out, GenArgs{});
     };
-    const int h = split_h(nh);
-    if (h == 64) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 120>{});
-    else if (h == 16) go(std::integral_constant<int, 16>{}, std::integral_constant<int, 420>{});
-    else go(std::integral_constant<int, 4>{}, std::integral_constant<int, 960>{});
+    auto by_h = [&](auto ktag) {
+        const int h = split_h(nh);
+        if (h == 64) go(ktag, std::integral_constant<int, 64>{}, std::integral_constant<int, 120>{});
+        else if (h == 16) go(ktag, std::integral_constant<int, 16>{}, std::integral_constant<int, 420>{});
+        else go(ktag, std::integral_constant<int, 4>{}, std::integral_constant<int, 960>{});
+    };
+    if (p.solver == 4) by_h(std::integral_constant<int, 4>{});
+    else by_h(std::integral_constant<int, 3>{});
     return hipGetLastError();
 }
 
@@ -1072,15 +1142,18 @@ hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule,
                            uint8_t* mask, hipStream_t stream) {
     const DevClass& c = p.cls[0];
     if (c.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mask<3>, dim3(blocks_for(c.n, kMaskBlock)), dim3(kMaskBlock), 0, stream, c, 0, model, rule,
-                       T, lambda, mask);
+    const dim3 grid(blocks_for(c.n, kMaskBlock)), block(kMaskBlock);
+    if (p.solver == 4)
+        hipLaunchKernelGGL(k_mask<4>, grid, block, 0, stream, c, 0, model, rule, T, lambda, mask);
+    else
+        hipLaunchKernelGGL(k_mask<3>, grid, block, 0, stream, c, 0, model, rule, T, lambda, mask);
     return hipGetLastError();
 }
 
-hipError_t launch_select_geo(const ScoreOut& sc, const uint8_t* inc, uint32_t nslots, uint64_t slot0, uint32_t m,
-                             double Tm, BatchRecord* out, hipStream_t stream) {
-    hipLaunchKernelGGL(k_select<GeoModel>, dim3(1), dim3(kSelectThreads), 0, stream, 3, sc, inc,
-                       (const GeoModel*)nullptr, nslots, slot0, m, 0u, Tm, 0.0, out);
+hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint64_t slot0,
+                             uint32_t m, double Tm, BatchRecord* out, hipStream_t stream) {
+    hipLaunchKernelGGL(k_select<GeoModel>, dim3(1), dim3(kSelectThreads), 0, stream, solver, sc, inc,
+                       (const GeoModel*)nullptr, nh, slot0, m, 0u, Tm, 0.0, out, solver == 4 ? kFModels : 1u);
     return hipGetLastError();
 }
 

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libgcr.so")
 GCR_OK = 0
 GCR_EINVAL = -22
 GCR_ENODEV = -19
-SOLVER_SCALE3, SOLVER_SCALE3_ORIGINAL, SOLVER_SIFT22, SOLVER_HOMOGRAPHY4 = 0, 1, 2, 3
+SOLVER_SCALE3, SOLVER_SCALE3_ORIGINAL, SOLVER_SIFT22, SOLVER_HOMOGRAPHY4, SOLVER_FUNDAMENTAL7 = 0, 1, 2, 3, 4
 FLAG_NO_LO = 1
 
 
@@ -124,6 +124,8 @@ def _load():
     L.gcr_debug_score_h.argtypes = [vp, C.POINTER(Params), dp, C.c_uint32, u32p, dp, dp]
     L.gcr_debug_mask_h.argtypes = [vp, C.POINTER(Params), dp, C.c_int, u8p]
     L.gcr_host_fit_h.argtypes = [dp, C.c_size_t, u32p, C.c_size_t, dp]
+    L.gcr_find_fundamental_matrix.argtypes = L.gcr_find_homography.argtypes
+    L.gcr_host_fit_f.argtypes = L.gcr_host_fit_h.argtypes
     L.gcr_host_homography.argtypes = [C.POINTER(RectModel), dp]
     L.gcr_host_homography.restype = None
     return L

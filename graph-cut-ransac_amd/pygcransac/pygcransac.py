@@ -29,6 +29,7 @@ __all__ = [
     "findRectifyingHomographyScaleOnlyOriginal",
     "findRectifyingHomographySIFT",
     "findHomography",
+    "findFundamentalMatrix",
 ]
 
 _TWO_PI = 2.0 * math.pi
@@ -366,6 +367,37 @@ def findRectifyingHomographySIFT(scale_features, orientation_features, scale_res
     return (H.reshape(3, 3), s_in, o_in, model) + extra
 
 
+def _correspondence_call(entry, correspondences, h1, w1, h2, w2, probabilities, threshold, conf,
+                         spatial_coherence_weight, max_iters, min_iters, sampler, lo_number, seed, device,
+                         batch_slots, return_stats, min_rows):
+    for name, v in (("h1", h1), ("w1", w1), ("h2", h2), ("w2", w2)):
+        _as_double(v, name)
+    if probabilities is not None and len(probabilities) != 0:
+        raise ValueError("Only the uniform sampler is supported; probabilities must be empty.")
+    if _as_size_t(sampler, "sampler") != 0:
+        raise ValueError(f"Unsupported sampler {sampler}: only 0 (uniform) is supported.")
+    f = _as_features(correspondences)
+    if f.ndim != 2:
+        raise ValueError("Number of dimensions must be 2.")
+    n, cols = f.shape
+    if n < min_rows or cols != 4:
+        raise ValueError(f"Correspondences should be an array with 4 columns and at least {min_rows} rows. "
+                         f"It has {cols} columns and {n} rows.")
+    f = np.ascontiguousarray(f)
+    p = _params(threshold, 2.0, spatial_coherence_weight, min_iters, max_iters, lo_number, seed, conf, batch_slots)
+    mask = np.zeros(n, dtype=np.uint8)
+    M = np.zeros(9, dtype=np.float64)
+    st = N.Stats()
+    ctx = N.context(device)
+    rc = entry(ctx, _dp(f), n, C.byref(p), _u8(mask), _dp(M), C.byref(st))
+    num_inliers = N.check(rc)
+    inliers = mask.astype(bool)
+    extra = (st.as_dict(),) if return_stats else ()
+    if num_inliers == 0:
+        return (None, inliers) + extra
+    return (M.reshape(3, 3), inliers) + extra
+
+
 def findHomography(correspondences, h1, w1, h2, w2, probabilities=None, threshold=1.0, conf=0.99,
                    spatial_coherence_weight=0.975, max_iters=10000, min_iters=50, sampler=0, lo_number=50, *,
                    seed=0, device=None, batch_slots=0, return_stats=False):
@@ -382,29 +414,22 @@ def findHomography(correspondences, h1, w1, h2, w2, probabilities=None, threshol
 
     Returns ``(H, inliers)`` with H (3, 3) and H[2, 2] = 1, or ``(None, inliers)``.
     """
-    for name, v in (("h1", h1), ("w1", w1), ("h2", h2), ("w2", w2)):
-        _as_double(v, name)
-    if probabilities is not None and len(probabilities) != 0:
-        raise ValueError("Only the uniform sampler is supported; probabilities must be empty.")
-    if _as_size_t(sampler, "sampler") != 0:
-        raise ValueError(f"Unsupported sampler {sampler}: only 0 (uniform) is supported.")
-    f = _as_features(correspondences)
-    if f.ndim != 2:
-        raise ValueError("Number of dimensions must be 2.")
-    n, cols = f.shape
-    if n < 4 or cols != 4:
-        raise ValueError(f"Correspondences should be an array with 4 columns and at least 4 rows. "
-                         f"It has {cols} columns and {n} rows.")
-    f = np.ascontiguousarray(f)
-    p = _params(threshold, 2.0, spatial_coherence_weight, min_iters, max_iters, lo_number, seed, conf, batch_slots)
-    mask = np.zeros(n, dtype=np.uint8)
-    H = np.zeros(9, dtype=np.float64)
-    st = N.Stats()
-    ctx = N.context(device)
-    rc = N.lib.gcr_find_homography(ctx, _dp(f), n, C.byref(p), _u8(mask), _dp(H), C.byref(st))
-    num_inliers = N.check(rc)
-    inliers = mask.astype(bool)
-    extra = (st.as_dict(),) if return_stats else ()
-    if num_inliers == 0:
-        return (None, inliers) + extra
-    return (H.reshape(3, 3), inliers) + extra
+    return _correspondence_call(N.lib.gcr_find_homography, correspondences, h1, w1, h2, w2, probabilities,
+                                threshold, conf, spatial_coherence_weight, max_iters, min_iters, sampler, lo_number,
+                                seed, device, batch_slots, return_stats, 4)
+
+
+def findFundamentalMatrix(correspondences, h1, w1, h2, w2, probabilities=None, threshold=1.0, conf=0.99,
+                          spatial_coherence_weight=0.975, max_iters=10000, min_iters=50, sampler=0, lo_number=50,
+                          *, seed=0, device=None, batch_slots=0, return_stats=False):
+    """7-point fundamental matrix with graph-cut LO -- an EXTENSION like
+    findHomography (same arguments; upstream pygcransac's findFundamentalMatrix
+    order).  The residual is the Sampson distance in pixels; a sample yields up
+    to three models, each scored.
+
+    Returns ``(F, inliers)`` with F (3, 3), unit Frobenius norm and
+    x2^T F x1 = 0, or ``(None, inliers)``.
+    """
+    return _correspondence_call(N.lib.gcr_find_fundamental_matrix, correspondences, h1, w1, h2, w2, probabilities,
+                                threshold, conf, spatial_coherence_weight, max_iters, min_iters, sampler, lo_number,
+                                seed, device, batch_slots, return_stats, 7)

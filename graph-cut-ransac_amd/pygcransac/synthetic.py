@@ -125,3 +125,54 @@ def problem_h(n: int = 5_000, outlier_ratio: float = 0.5, seed: int = DEFAULT_SE
     truth = np.concatenate([np.ones(n_in, bool), np.zeros(n_out, bool)])
     perm = rng.permutation(n)
     return np.ascontiguousarray(corr[perm]), truth[perm], H.copy(), 2.0
+
+
+def _rot(yaw, pitch, roll):
+    cy, sy, cp, sp, cr, sr = (math.cos(yaw), math.sin(yaw), math.cos(pitch), math.sin(pitch), math.cos(roll),
+                              math.sin(roll))
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+    Rz = np.array([[cr, -sr, 0], [sr, cr, 0], [0, 0, 1]])
+    return Rz @ Rx @ Ry
+
+
+def two_view_geometry(focal: float = 1000.0, yaw: float = 0.12, pitch: float = 0.03, roll: float = 0.02,
+                      t=(1.0, 0.1, 0.15)):
+    """Calibration, relative pose and F_gt (x2^T F x1 = 0, unit Frobenius norm)."""
+    K = np.array([[focal, 0, IMG_W / 2], [0, focal, IMG_H / 2], [0, 0, 1.0]])
+    R = _rot(yaw, pitch, roll)
+    t = np.asarray(t, dtype=float)
+    tx = np.array([[0, -t[2], t[1]], [t[2], 0, -t[0]], [-t[1], t[0], 0]])
+    Ki = np.linalg.inv(K)
+    F = Ki.T @ tx @ R @ Ki
+    return K, R, t, F / np.linalg.norm(F)
+
+
+def problem_f(n: int = 10_000, outlier_ratio: float = 0.8, seed: int = DEFAULT_SEED, noise: float = 0.5):
+    """Fundamental-matrix problem (BASELINE configs[3]): a random 3-D scene seen
+    by two calibrated cameras.  Returns correspondences (n, 4) = (x1, y1, x2,
+    y2), inlier truth mask, F_gt and the inlier threshold (px, Sampson)."""
+    rng = np.random.default_rng(seed)
+    K, R, t, F = two_view_geometry()
+    n_out = int(round(n * outlier_ratio))
+    n_in = n - n_out
+    pts = []
+    while sum(len(p) for p in pts) < n_in:
+        m = 2 * n_in
+        X = np.stack([rng.uniform(-5, 5, m), rng.uniform(-4, 4, m), rng.uniform(6, 16, m)], axis=1)
+        p1 = X @ K.T
+        X2 = X @ R.T + t
+        p2 = X2 @ K.T
+        ok = (X2[:, 2] > 0.1)
+        u1, v1 = p1[:, 0] / p1[:, 2], p1[:, 1] / p1[:, 2]
+        u2, v2 = p2[:, 0] / p2[:, 2], p2[:, 1] / p2[:, 2]
+        ok &= (u1 >= 0) & (u1 < IMG_W) & (v1 >= 0) & (v1 < IMG_H) & (u2 >= 0) & (u2 < IMG_W) & (v2 >= 0) & (v2 < IMG_H)
+        pts.append(np.stack([u1, v1, u2, v2], axis=1)[ok])
+    inl = np.concatenate(pts)[:n_in]
+    inl = inl + rng.normal(0, noise, inl.shape)
+    out = np.stack([rng.uniform(0, IMG_W, n_out), rng.uniform(0, IMG_H, n_out),
+                    rng.uniform(0, IMG_W, n_out), rng.uniform(0, IMG_H, n_out)], axis=1)
+    corr = np.concatenate([inl, out])
+    truth = np.concatenate([np.ones(n_in, bool), np.zeros(n_out, bool)])
+    perm = rng.permutation(n)
+    return np.ascontiguousarray(corr[perm]), truth[perm], F, 1.0

@@ -50,6 +50,7 @@ extern "C" {
 #define GCR_SOLVER_SCALE3_ORIGINAL 1 /* RectifyingHomographyThreeSIFTSolverOriginal */
 #define GCR_SOLVER_SIFT22 2          /* RectifyingHomographyTwoSIFTSolver           */
 #define GCR_SOLVER_HOMOGRAPHY4 3     /* 4-point homography (upstream GC-RANSAC)     */
+#define GCR_SOLVER_FUNDAMENTAL7 4    /* 7-point fundamental matrix (upstream)       */
 
 typedef struct gcr_ctx gcr_ctx;
 typedef struct gcr_problem gcr_problem;
@@ -119,6 +120,14 @@ int gcr_rect_sift(gcr_ctx* ctx, const double* scale_features, size_t n_scale, co
 int gcr_find_homography(gcr_ctx* ctx, const double* correspondences, size_t n, const gcr_params* params,
                         uint8_t* mask_out, double* H_out, gcr_stats* stats_out);
 
+/* 7-point fundamental matrix (an EXTENSION like
+ * gcr_find_homography -- what upstream pygcransac's findFundamentalMatrix
+ * would bind).  Same buffers as gcr_find_homography; the residual is the
+ * squared Sampson distance, F_out is row-major 3x3 with unit Frobenius norm
+ * (x2^T F x1 = 0). */
+int gcr_find_fundamental_matrix(gcr_ctx* ctx, const double* correspondences, size_t n, const gcr_params* params,
+                                uint8_t* mask_out, double* F_out, gcr_stats* stats_out);
+
 /* ---- device-resident problems (benchmarks, problem batches) -------------- */
 /* Uploads the features once; runs reuse the HBM-resident copy.  f1 is the
  * orientation set for GCR_SOLVER_SIFT22 and NULL otherwise. */
@@ -173,9 +182,12 @@ int gcr_debug_fit_nonminimal(gcr_problem* prob, const uint32_t* idx0, size_t k0,
  * fit is rejected, < 0 on error */
 int gcr_host_fit_nonminimal(int solver, const double* f0, size_t n0, const double* f1, size_t n1, const uint32_t* idx0,
                             size_t k0, const uint32_t* idx1, size_t k1, gcr_rect_model* model_out);
-/* homography problems (GCR_SOLVER_HOMOGRAPHY4): models are 9 row-major
- * doubles.  generate: inc[i] as above, H_out 9 per slot; score: n0 / v0 / tot
- * per model (MSAC threshold 2.25 thr); mask: rules as gcr_debug_mask */
+/* correspondence problems (GCR_SOLVER_HOMOGRAPHY4 / _FUNDAMENTAL7): models
+ * are 9 row-major doubles.  generate: homography -- inc[i] as above, H_out 9
+ * per slot; fundamental -- 3 hypotheses per slot (inc_out 3 bytes, H_out 27
+ * doubles per slot): inc[3s] as above, inc[3s+k] = 0 if the sample's k-th
+ * model exists, 255 if not.  score: n0 / v0 / tot per model (MSAC threshold
+ * 2.25 thr); mask: rules as gcr_debug_mask */
 int gcr_debug_generate_h(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc_out,
                          double* H_out);
 int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double* H, uint32_t nmodels, uint32_t* n0,
@@ -184,6 +196,9 @@ int gcr_debug_mask_h(gcr_problem* prob, const gcr_params* params, const double* 
 /* host-only: normalised least-squares homography of the listed
  * correspondences (the LO / final-refit fit); 1 = fitted, 0 = rejected */
 int gcr_host_fit_h(const double* correspondences, size_t n, const uint32_t* idx, size_t k, double* H_out);
+/* host-only: the fundamental-matrix LO / refit fit (7 points: 7-point solver's
+ * first model; more: normalised 8-point with rank-2 projection) */
+int gcr_host_fit_f(const double* correspondences, size_t n, const uint32_t* idx, size_t k, double* F_out);
 /* host-only: RectifyingHomography::getHomography (model.h:211-226), row-major */
 void gcr_host_homography(const gcr_rect_model* model, double* H_out);
 /* host-only (no GPU): deterministic math and sampler used on both sides */

@@ -93,3 +93,52 @@ def finish_score(kind, n0, n1, v0, v1, tot, thr0, thr1):
 
 def bits(x):
     return np.asarray(x, dtype=np.float64).view(np.uint64)
+
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+
+
+class CorrProblem:
+    """A device-resident homography / fundamental-matrix problem (C ABI)."""
+
+    def __init__(self, solver, corr):
+        self.solver = solver
+        self.c = np.ascontiguousarray(corr, dtype=np.float64)
+        h = C.c_void_p()
+        N.check(N.lib.gcr_problem_create(N.context(0), solver, dp(self.c), self.c.shape[0], None, 0,
+                                         C.byref(h)))
+        self.h = h.value
+
+    def __del__(self):
+        if self.h:
+            N.lib.gcr_problem_destroy(self.h)
+
+    def generate(self, seed, slot0, n):
+        """homography: inc (n,), models (n, 9); fundamental: (n, 3), (n, 3, 9)"""
+        per = 3 if self.solver == N.SOLVER_FUNDAMENTAL7 else 1
+        inc = np.zeros(n * per, dtype=np.uint8)
+        H = np.zeros((n * per, 9))
+        N.check(N.lib.gcr_debug_generate_h(self.h, seed, slot0, n, inc.ctypes.data_as(u8p), dp(H)))
+        if per == 1:
+            return inc, H
+        return inc.reshape(n, per), H.reshape(n, per, 9)
+
+    def score(self, models, thr):
+        models = np.ascontiguousarray(models, dtype=np.float64)
+        n = len(models)
+        p = N.default_params()
+        p.scale_residual_thresh = thr
+        n0 = np.zeros(n, dtype=np.uint32)
+        v0, tot = np.zeros(n), np.zeros(n)
+        N.check(N.lib.gcr_debug_score_h(self.h, C.byref(p), dp(models), n, n0.ctypes.data_as(u32p), dp(v0), dp(tot)))
+        return n0, v0, tot
+
+    def mask(self, model, rule, thr, lam=0.0):
+        p = N.default_params()
+        p.scale_residual_thresh = thr
+        p.spatial_coherence_weight = lam
+        out = np.zeros(self.c.shape[0], dtype=np.uint8)
+        m = np.ascontiguousarray(model, dtype=np.float64)
+        N.check(N.lib.gcr_debug_mask_h(self.h, C.byref(p), dp(m), rule, out.ctypes.data_as(u8p)))
+        return out.astype(bool)

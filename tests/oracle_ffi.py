@@ -73,6 +73,11 @@ def lib():
         L.oracle_h_slot.argtypes = [dp, C.c_size_t, C.c_uint64, C.c_uint64, dp]
         L.oracle_h_score.argtypes = [dp, C.c_size_t, dp, C.c_double, u64p, dp, u8p]
         L.oracle_h_residuals.argtypes = [dp, C.c_size_t, dp, dp]
+        L.oracle_find_fundamental.argtypes = L.oracle_find_homography.argtypes
+        L.oracle_f_slot.argtypes = [dp, C.c_size_t, C.c_uint64, C.c_uint64, dp, C.POINTER(C.c_int)]
+        L.oracle_f_score.argtypes = L.oracle_h_score.argtypes
+        L.oracle_f_residuals.argtypes = L.oracle_h_residuals.argtypes
+        L.oracle_f_fit.argtypes = L.oracle_h_fit.argtypes
         L.oracle_h_fit.argtypes = [dp, C.c_size_t, u64p, C.c_size_t, dp]
         for name in ["oracle_clip_angle", "oracle_deg2rad", "oracle_rad2deg"]:
             getattr(L, name).argtypes = [C.c_double]
@@ -270,6 +275,57 @@ def h_fit(corr, idx):
     i = np.ascontiguousarray(np.asarray(idx, dtype=np.uint64))
     m = np.zeros(9)
     ok = lib().oracle_h_fit(_dp(c), c.shape[0], i.ctypes.data_as(C.POINTER(C.c_uint64)), len(i), _dp(m))
+    return m if ok else None
+
+
+def find_fundamental(corr, thr, **kw):
+    c = _f64(corr)
+    n = c.shape[0]
+    mask = np.zeros(n, dtype=np.uint8)
+    H = np.zeros(9)
+    st = OracleStats()
+    p = params(thr, **kw)
+    r = lib().oracle_find_fundamental(_dp(c), n, C.byref(p), mask.ctypes.data_as(C.POINTER(C.c_uint8)), _dp(H),
+                                     C.byref(st))
+    if r < 0:
+        raise RuntimeError("oracle failed")
+    return dict(num_inliers=r, mask=mask.astype(bool), H=H.reshape(3, 3), stats=_stats_dict(st))
+
+
+def f_slot(corr, seed, slot):
+    """(inc, models (k, 9)) of one outer-iteration slot of the 7-point solver."""
+    c = _f64(corr)
+    m = np.zeros(27)
+    k = C.c_int()
+    inc = lib().oracle_f_slot(_dp(c), c.shape[0], seed, slot, _dp(m), C.byref(k))
+    return inc, m.reshape(3, 9)[:k.value].copy()
+
+
+def f_score(corr, model9, thr, want_mask=False):
+    c = _f64(corr)
+    cnt = C.c_uint64()
+    val = C.c_double()
+    mask = np.zeros(c.shape[0], dtype=np.uint8) if want_mask else None
+    lib().oracle_f_score(_dp(c), c.shape[0], _dp(_f64(model9)), thr, C.byref(cnt), C.byref(val),
+                         mask.ctypes.data_as(C.POINTER(C.c_uint8)) if want_mask else None)
+    out = dict(count=int(cnt.value), value=val.value)
+    if want_mask:
+        out["mask"] = mask.astype(bool)
+    return out
+
+
+def f_residuals(corr, model9):
+    c = _f64(corr)
+    r2 = np.zeros(c.shape[0])
+    lib().oracle_f_residuals(_dp(c), c.shape[0], _dp(_f64(model9)), _dp(r2))
+    return r2
+
+
+def f_fit(corr, idx):
+    c = _f64(corr)
+    i = np.ascontiguousarray(np.asarray(idx, dtype=np.uint64))
+    m = np.zeros(9)
+    ok = lib().oracle_f_fit(_dp(c), c.shape[0], i.ctypes.data_as(C.POINTER(C.c_uint64)), len(i), _dp(m))
     return m if ok else None
 
 

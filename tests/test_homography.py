@@ -15,7 +15,7 @@ import pytest
 
 import oracle_ffi as O
 import pygcransac
-from gcr_testutil import bits, dp
+from gcr_testutil import CorrProblem, bits, dp
 from pygcransac import _native as N
 from pygcransac import synthetic as S
 
@@ -112,44 +112,6 @@ def test_find_homography_signature_and_errors():
 
 
 # -------------------------------------------------------------- GPU parity --
-class HProblem:
-    def __init__(self, corr):
-        self.c = np.ascontiguousarray(corr, dtype=np.float64)
-        h = C.c_void_p()
-        N.check(N.lib.gcr_problem_create(N.context(0), N.SOLVER_HOMOGRAPHY4, dp(self.c), self.c.shape[0], None, 0,
-                                         C.byref(h)))
-        self.h = h.value
-
-    def __del__(self):
-        if self.h:
-            N.lib.gcr_problem_destroy(self.h)
-
-    def generate(self, seed, slot0, n):
-        inc = np.zeros(n, dtype=np.uint8)
-        H = np.zeros((n, 9))
-        N.check(N.lib.gcr_debug_generate_h(self.h, seed, slot0, n, inc.ctypes.data_as(u8p), dp(H)))
-        return inc, H
-
-    def score(self, models, thr):
-        models = np.ascontiguousarray(models, dtype=np.float64)
-        n = len(models)
-        p = N.default_params()
-        p.scale_residual_thresh = thr
-        n0 = np.zeros(n, dtype=np.uint32)
-        v0, tot = np.zeros(n), np.zeros(n)
-        N.check(N.lib.gcr_debug_score_h(self.h, C.byref(p), dp(models), n, n0.ctypes.data_as(u32p), dp(v0), dp(tot)))
-        return n0, v0, tot
-
-    def mask(self, model, rule, thr, lam=0.0):
-        p = N.default_params()
-        p.scale_residual_thresh = thr
-        p.spatial_coherence_weight = lam
-        out = np.zeros(self.c.shape[0], dtype=np.uint8)
-        m = np.ascontiguousarray(model, dtype=np.float64)
-        N.check(N.lib.gcr_debug_mask_h(self.h, C.byref(p), dp(m), rule, out.ctypes.data_as(u8p)))
-        return out.astype(bool)
-
-
 def _finish(n0, v0, tot, thr):
     """MSACScoringFunction::getScore post-processing for one class, m = 4."""
     if int(n0) < 4:
@@ -169,7 +131,7 @@ def gpu():
 @pytest.mark.gpu
 def test_generate_matches_oracle_slots(gpu):
     corr, _, _, _ = S.problem_h(500, 0.5, seed=21)
-    prob = HProblem(corr)
+    prob = CorrProblem(N.SOLVER_HOMOGRAPHY4, corr)
     inc, H = prob.generate(31, 4000, 512)
     for s in range(512):
         oinc, om = O.h_slot(corr, 31, 4000 + s)
@@ -184,7 +146,7 @@ def test_generate_matches_oracle_slots(gpu):
 def test_score_matches_oracle_bitwise(gpu, nh):
     # covers the H = 4 / 16 / 64 hypotheses-per-workgroup variants
     corr, _, _, thr = S.problem_h(1337, 0.5, seed=22)
-    prob = HProblem(corr)
+    prob = CorrProblem(N.SOLVER_HOMOGRAPHY4, corr)
     inc, H = prob.generate(5, 0, 256)
     uniq = H[inc <= 101][:96]
     tiled = np.resize(uniq, (nh, 9))
@@ -201,7 +163,7 @@ def test_score_matches_oracle_bitwise(gpu, nh):
 @pytest.mark.gpu
 def test_mask_matches_oracle(gpu):
     corr, _, _, thr = S.problem_h(900, 0.5, seed=23)
-    prob = HProblem(corr)
+    prob = CorrProblem(N.SOLVER_HOMOGRAPHY4, corr)
     inc, H = prob.generate(8, 0, 64)
     for m in H[inc <= 101][:16]:
         assert np.array_equal(prob.mask(m, 0, thr), O.h_score(corr, m, thr, want_mask=True)["mask"])
@@ -272,7 +234,7 @@ def test_degenerate_input_returns_none(gpu):
 @pytest.mark.gpu
 def test_verify_batches_best_slot_matches_oracle(gpu):
     corr, _, _, thr = S.problem_h(1000, 0.5, seed=12)
-    prob = HProblem(corr)
+    prob = CorrProblem(N.SOLVER_HOMOGRAPHY4, corr)
     p = N.default_params()
     p.scale_residual_thresh = thr
     p.seed = 77
