@@ -152,7 +152,8 @@ struct Workspace {
     PinBuf<RectModel> h_models;
     ScoreBufs sb;
     DevBuf<RectModel> lo_models;
-    DevBuf<GeoModel> gmodels, lo_gmodels;     // homography (solver 3)
+    DevBuf<GeoModel> gmodels, lo_gmodels;     // homography (solver 3) / fundamental (4)
+    DevBuf<uint32_t> hmap, hcount;            // live-hypothesis compaction (fundamental)
     PinBuf<GeoModel> h_gmodels;
     ScoreBufs lo_sb;
     DevBuf<uint8_t> mask[2];
@@ -391,6 +392,10 @@ struct RectTraits {
                            hipStream_t s) {
         return launch_mask(P->dp, cls, m, rule, T, lambda, mk, s);
     }
+    static hipError_t score_live(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t nh,
+                                 const ScoreOut& out, hipStream_t s) {
+        return launch_score(P->dp, T, m, inc, nh, true, out, s);
+    }
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t wg_cap, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
                              hipStream_t s) {
@@ -433,14 +438,34 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
                              hipStream_t s) {
+        const uint32_t nh = n * (uint32_t)per(P);
         hipError_t e = launch_generate_geo(P->dp, seed, s0, n, P->w->inc.p, P->w->gmodels.p, s);
         if (e != hipSuccess) return e;
+        const uint32_t *map = nullptr, *cnt = nullptr;
+        if (per(P) > 1) {
+            P->w->hmap.ensure(nh);
+            P->w->hcount.ensure(1);
+            map = P->w->hmap.p;
+            cnt = P->w->hcount.p;
+            e = launch_compact(P->w->inc.p, nh, P->w->hmap.p, P->w->hcount.p, s);
+            if (e != hipSuccess) return e;
+        }
         if (e0) (void)hipEventRecord(e0, s);
-        e = launch_score_geo(P->dp, Tm[0], P->w->gmodels.p, P->w->inc.p, n * (uint32_t)per(P), P->w->sb.dev(), s);
+        e = launch_score_geo(P->dp, Tm[0], P->w->gmodels.p, P->w->inc.p, nh, P->w->sb.dev(), s, map, cnt);
         if (e != hipSuccess) return e;
         if (e1) (void)hipEventRecord(e1, s);
-        return launch_select_geo(P->solver, P->w->sb.dev(), P->w->inc.p, n * (uint32_t)per(P), s0, m[0], Tm[0], rec,
-                                 s);
+        return launch_select_geo(P->solver, P->w->sb.dev(), P->w->inc.p, nh, s0, m[0], Tm[0], rec, s, map, cnt);
+    }
+    // replay-path scoring of a fetched chunk: fundamental-matrix launches are
+    // compacted to the live hypotheses (results in hypothesis order)
+    static hipError_t score_live(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t nh,
+                                 const ScoreOut& out, hipStream_t s) {
+        if (per(P) == 1) return launch_score_geo(P->dp, T[0], m, inc, nh, out, s);
+        P->w->hmap.ensure(nh);
+        P->w->hcount.ensure(1);
+        hipError_t e = launch_compact(inc, nh, P->w->hmap.p, P->w->hcount.p, s);
+        if (e != hipSuccess) return e;
+        return launch_score_geo(P->dp, T[0], m, inc, nh, out, s, P->w->hmap.p, P->w->hcount.p);
     }
     static size_t per(gcr_problem* P) { return P->solver == 4 ? kFModels : 1; }
     static bool fit(gcr_problem* P, const std::vector<uint32_t>* lists, Model& out, bool) {
@@ -518,9 +543,11 @@ public:
             for (size_t q = 0; inc <= 101 && q < kP; ++q) {
                 const size_t hj = j * kP + q;
                 if (q > 0 && P_->w->h_inc.p[hj] != 0) break;
+                // multi-model slots are scored compacted: results in order
+                const size_t si = kP > 1 ? cursor_++ : hj;
                 const Model& model = Tr::hmodels(P_->w).p[hj];
-                const uint32_t rn[2] = {P_->w->sb.hn0.p[hj], P_->w->sb.hn1.p[hj]};
-                const HScore cur = finish(rn, P_->w->sb.hv0.p[hj], P_->w->sb.hv1.p[hj], P_->w->sb.htot.p[hj]);
+                const uint32_t rn[2] = {P_->w->sb.hn0.p[si], P_->w->sb.hn1.p[si]};
+                const HScore cur = finish(rn, P_->w->sb.hv0.p[si], P_->w->sb.hv1.p[si], P_->w->sb.htot.p[si]);
                 bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
                 ++st_.hypotheses;
                 if (best_.sum < cur.sum && valid_model(model)) {
@@ -613,17 +640,22 @@ public:
         const auto t0 = Clock::now();
         P_->w->inc.ensure(nslots * kP); Tr::dmodels(P_->w).ensure(nslots * kP); P_->w->sb.ensure(nslots * kP);
         P_->w->recs.ensure(nb);
-        while (P_->w->evs.size() < 2 * (size_t)nb) {
-            hipEvent_t ev;
-            HIPC(hipEventCreate(&ev));
-            P_->w->evs.push_back(ev);
-        }
+
         const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
         const size_t wg_cap = (nslots + 3) / 4;
         P_->w->wg.ensure(wg_cap);
         // score-kernel timing events on every `stride`-th batch
-        // (GCR_TIMING_STRIDE; default every batch)
-        const uint32_t stride = timing_stride();
+        // (GCR_TIMING_STRIDE; default every batch), at most kMaxTimed evenly
+        // spaced batches per call: the event pool is created once and reused
+        // (hipEventCreate inside a long queue costs more than the kernels)
+        constexpr uint32_t kMaxTimed = 64;
+        const uint32_t stride = std::max(timing_stride(), (nb + kMaxTimed - 1) / kMaxTimed);
+        const uint32_t ntimed = (nb + stride - 1) / stride;
+        while (P_->w->evs.size() < 2 * (size_t)std::max(ntimed, kMaxTimed)) {
+            hipEvent_t ev;
+            HIPC(hipEventCreate(&ev));
+            P_->w->evs.push_back(ev);
+        }
         uint32_t timed = 0;
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t s0 = slot0 + (uint64_t)b * nslots;
@@ -660,6 +692,7 @@ private:
     gcr_stats st_;
 
     uint64_t it_ = 0;
+    size_t cursor_ = 0;           // next compacted score of the current chunk
     HScore best_{};
     Model best_model_ = Tr::def();
     Buffer bufs_[2];
@@ -716,7 +749,8 @@ private:
         const size_t nh = cnt * kP;
         t0 = Clock::now();
         HIPC(hipEventRecord(P_->ctx->ev0, s_));
-        HIPC(Tr::score(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, true, P_->w->sb.dev(), s_));
+        HIPC(Tr::score_live(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(), s_));
+        cursor_ = 0;
         HIPC(hipEventRecord(P_->ctx->ev1, s_));
         P_->w->sb.d2h(nh, s_);
         HIPC(hipMemcpyAsync(Tr::hmodels(P_->w).p, Tr::dmodels(P_->w).p, nh * sizeof(Model), hipMemcpyDeviceToHost,

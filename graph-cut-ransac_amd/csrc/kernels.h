@@ -133,11 +133,15 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
 hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
                                GeoModel* models, hipStream_t stream);
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
-                            const ScoreOut& out, hipStream_t stream);
+                            const ScoreOut& out, hipStream_t stream, const uint32_t* hmap = nullptr,
+                            const uint32_t* hcount = nullptr);
 hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule, double T, double lambda,
                            uint8_t* mask, hipStream_t stream);
 hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint64_t slot0,
-                             uint32_t m, double Tm, BatchRecord* out, hipStream_t stream);
+                             uint32_t m, double Tm, BatchRecord* out, hipStream_t stream,
+                             const uint32_t* hmap = nullptr, const uint32_t* hcount = nullptr);
+// order-preserving list of live hypotheses (inc <= 101): map[0 .. *count)
+hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_t* count, hipStream_t stream);
 
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)

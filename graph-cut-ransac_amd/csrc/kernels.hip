@@ -296,15 +296,25 @@ struct GenArgs {
     RectModel* models;
     WgBest* wg;
     uint32_t m0, m1;
+    // correspondence estimators (KIND >= 3): optional compaction map of the
+    // live hypotheses (k_compact) -- hypothesis j of the launch is model
+    // hmap[j], j < *hcount; results are written at j
+    const uint32_t* hmap;
+    const uint32_t* hcount;
 };
 
 template <int KIND, int H, int R, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, double T0, double T1, double band0,
                                                                double tan_tau1,
                                                                const typename ModelOf<KIND>::type* __restrict__ models,
-                                                               const uint8_t* __restrict__ inc, uint32_t nh,
+                                                               const uint8_t* __restrict__ inc, uint32_t nh_in,
                                                                ScoreOut out, GenArgs gen) {
     static_assert((H * R) % kComputeThreads == 0 && kComputeThreads % H == 0, "tile shape");
+    uint32_t nh = nh_in;
+    if constexpr (KIND >= 3) {
+        if (gen.hcount != nullptr) nh = min(nh_in, *gen.hcount);
+        if (blockIdx.x * H >= nh) return;            // whole workgroup, before any barrier
+    }
     static_assert(H * R <= 65536, "queue entries are 16-bit tile indices");
     constexpr int kPer = H * R / kComputeThreads;    // pairs per compute thread per round
     constexpr int kStride = kComputeThreads / H;     // feature stride between a thread's pairs
@@ -332,6 +342,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     const bool chain_lane = chain_wave && lane < (kSplitTot ? 2 * H : H);
     const int fsub = t / H;
     const uint32_t hg = blockIdx.x * H + h;
+    // model / inc index of this hypothesis (compacted launches: the map)
+    const uint32_t mi = (KIND >= 3 && gen.hmap != nullptr && hg < nh) ? gen.hmap[hg] : hg;
 
     const uint32_t n0 = p.cls[0].n;
     const uint32_t n1 = (KIND == 2) ? p.cls[1].n : 0;
@@ -408,12 +420,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
             gen.models[hg] = a == 127 ? default_model() : gen_m[t];
         }
     }
-    const bool valid_h = hg < nh && (kGen ? gen_a[h] != 127 : (inc == nullptr || inc[hg] <= 101));
+    const bool valid_h = hg < nh && (kGen ? gen_a[h] != 127 : (inc == nullptr || inc[mi] <= 101));
     const bool live = !chain_wave && valid_h;
 
     if (KIND >= 3 && t < H) {
         if constexpr (KIND >= 3) {
-            const GeoModel m = valid_h ? models[hg] : default_geo();
+            const GeoModel m = valid_h ? models[mi] : default_geo();
             HypConst q;
             for (int j = 0; j < 9; ++j) q.g[j] = m.h[j];
             hyp[h] = q;
@@ -629,6 +641,35 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     }
 }
 
+// -------------------------------------------------------------- compact ----
+// Order-preserving list of the live hypotheses (inc <= 101) of a launch: one
+// workgroup, contiguous chunks per thread, exclusive scan in LDS.  Used by the
+// fundamental matrix, whose slots carry up to three hypotheses of which on
+// average ~1.1 exist.
+constexpr int kCompactThreads = 1024;
+
+__global__ __launch_bounds__(kCompactThreads) void k_compact(const uint8_t* __restrict__ inc, uint32_t n,
+                                                            uint32_t* __restrict__ map, uint32_t* __restrict__ count) {
+    __shared__ uint32_t part[kCompactThreads];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (n + kCompactThreads - 1) / kCompactThreads;
+    const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
+    uint32_t c = 0;
+    for (uint32_t i = lo; i < hi; ++i) c += inc[i] <= 101;
+    part[t] = c;
+    __syncthreads();
+    for (uint32_t off = 1; off < kCompactThreads; off <<= 1) {     // inclusive Hillis-Steele scan
+        const uint32_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t o = part[t] - c;
+    for (uint32_t i = lo; i < hi; ++i)
+        if (inc[i] <= 101) map[o++] = i;
+    if (t == kCompactThreads - 1) *count = part[t];
+}
+
 // --------------------------------------------------------------- select ----
 constexpr int kSelectThreads = 1024;
 
@@ -638,7 +679,9 @@ template <class M>
 __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut sc, const uint8_t* __restrict__ inc,
                                                            const M* __restrict__ models, uint32_t n,
                                                            uint64_t slot0, uint32_t m0, uint32_t m1, double Tm0,
-                                                           double Tm1, BatchRecord* out, uint32_t per = 1) {
+                                                           double Tm1, BatchRecord* out, uint32_t per = 1,
+                                                           const uint32_t* __restrict__ hmap = nullptr,
+                                                           const uint32_t* __restrict__ hcount = nullptr) {
     __shared__ double s_val[kSelectThreads];
     __shared__ uint32_t s_idx[kSelectThreads];
     __shared__ unsigned long long s_models[kSelectThreads], s_its[kSelectThreads];
@@ -647,10 +690,9 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
     double best = 0.0;
     uint32_t bi = 0xffffffffu;
     unsigned long long nm = 0, its = 0;
-    for (uint32_t j = t; j < n; j += kSelectThreads) {
-        const uint32_t in = inc[j];
-        its += in <= 102 ? in : 0;
-        if (in > 101) continue;
+    // score index j: hypothesis j, or hmap[j] of a compacted launch (the map
+    // is increasing, so the lowest j is still the first hypothesis)
+    auto consider = [&](uint32_t j, uint32_t hyp) {
         ++nm;
         double sum = sc.tot[j];
         bool zero = false;
@@ -664,11 +706,20 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
         }
         if (zero) sum = 0.0;
         bool valid = true;
-        if constexpr (std::is_same<M, RectModel>::value) valid = solver != 2 || valid_model_sift22(models[j]);
+        if constexpr (std::is_same<M, RectModel>::value) valid = solver != 2 || valid_model_sift22(models[hyp]);
         if (best < sum && valid) {
             best = sum;
             bi = j;
         }
+    };
+    for (uint32_t j = t; j < n; j += kSelectThreads) {
+        const uint32_t in = inc[j];
+        its += in <= 102 ? in : 0;
+        if (hmap == nullptr && in <= 101) consider(j, j);
+    }
+    if (hmap != nullptr) {
+        const uint32_t nc = min(n, *hcount);
+        for (uint32_t j = t; j < nc; j += kSelectThreads) consider(j, hmap[j]);
     }
     s_val[t] = best;
     s_idx[t] = bi;
@@ -698,7 +749,7 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
         r.best_model = default_model();
         const uint32_t j = s_idx[0];
         if (j != 0xffffffffu) {
-            r.best_slot = static_cast<int64_t>(slot0 + j / per);
+            r.best_slot = static_cast<int64_t>(slot0 + (hmap != nullptr ? hmap[j] : j) / per);
             r.best_score = s_val[0];
             r.best_inliers[0] = sc.n0[j];
             r.best_inliers[1] = K == 2 ? sc.n1[j] : 0;
@@ -1113,19 +1164,39 @@ hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot
         else
             hipLaunchKernelGGL((k_generate<3, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
     };
-    if (nslots <= 8192) go(std::integral_constant<int, 16>{});
-    else if (nslots <= 32768) go(std::integral_constant<int, 4>{});
-    else go(std::integral_constant<int, 1>{});
+    // GCR_GEN_G overrides the lanes per slot (1 .. 64)
+    static const int env_g = [] {
+        const char* e = getenv("GCR_GEN_G");
+        return e ? atoi(e) : 0;
+    }();
+    // 7-point solver: ~7.7 attempts per slot at 80 % outliers (p99 35), latency-
+    // bound per attempt -> a half wave per slot (measured: G = 8 / 16 / 32 / 64
+    // -> 0.46 / 0.37 / 0.34 / 0.36 ms per 4096-slot step)
+    int g = p.solver == 4 ? (nslots <= 8192 ? 32 : nslots <= 32768 ? 8 : 2)
+                          : (nslots <= 8192 ? 16 : nslots <= 32768 ? 4 : 1);
+    if (env_g == 1 || env_g == 2 || env_g == 4 || env_g == 8 || env_g == 16 || env_g == 32 || env_g == 64) g = env_g;
+    switch (g) {
+        case 64: go(std::integral_constant<int, 64>{}); break;
+        case 32: go(std::integral_constant<int, 32>{}); break;
+        case 16: go(std::integral_constant<int, 16>{}); break;
+        case 8: go(std::integral_constant<int, 8>{}); break;
+        case 4: go(std::integral_constant<int, 4>{}); break;
+        case 2: go(std::integral_constant<int, 2>{}); break;
+        default: go(std::integral_constant<int, 1>{}); break;
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
-                            const ScoreOut& out, hipStream_t stream) {
+                            const ScoreOut& out, hipStream_t stream, const uint32_t* hmap, const uint32_t* hcount) {
     if (nh == 0) return hipSuccess;
+    GenArgs ga{};
+    ga.hmap = hmap;
+    ga.hcount = hcount;
     auto go = [&](auto ktag, auto htag, auto rtag) {
         constexpr int KIND = decltype(ktag)::value, H = decltype(htag)::value, R = decltype(rtag)::value;
         hipLaunchKernelGGL((k_score_split<KIND, H, R, false>), dim3((nh + H - 1) / H), dim3(kSplitThreads), 0,
-                           stream, p, T, 0.0, 0.0, 0.0, models, inc, nh, out, GenArgs{});
+                           stream, p, T, 0.0, 0.0, 0.0, models, inc, nh, out, ga);
     };
     auto by_h = [&](auto ktag) {
         const int h = split_h(nh);
@@ -1151,9 +1222,16 @@ hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule,
 }
 
 hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint64_t slot0,
-                             uint32_t m, double Tm, BatchRecord* out, hipStream_t stream) {
+                             uint32_t m, double Tm, BatchRecord* out, hipStream_t stream, const uint32_t* hmap,
+                             const uint32_t* hcount) {
     hipLaunchKernelGGL(k_select<GeoModel>, dim3(1), dim3(kSelectThreads), 0, stream, solver, sc, inc,
-                       (const GeoModel*)nullptr, nh, slot0, m, 0u, Tm, 0.0, out, solver == 4 ? kFModels : 1u);
+                       (const GeoModel*)nullptr, nh, slot0, m, 0u, Tm, 0.0, out, solver == 4 ? kFModels : 1u, hmap,
+                       hcount);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_t* count, hipStream_t stream) {
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(kCompactThreads), 0, stream, inc, n, map, count);
     return hipGetLastError();
 }
 

@@ -869,6 +869,38 @@ static double det3x3(const double* m) {
            m[2] * (m[3] * m[7] - m[4] * m[6]);
 }
 
+// safeguarded Newton ("rtsafe") inside a sign-change bracket of the monic cubic
+static double cubicRootIn(double a, double b, double c, double lo, double hi, double flo) {
+    auto p = [&](double l) { return ((l + a) * l + b) * l + c; };
+    auto dp = [&](double l) { return (3.0 * l + 2.0 * a) * l + b; };
+    double xl = lo, xh = hi;
+    if (!(flo < 0.0)) std::swap(xl, xh);
+    double x = 0.5 * (lo + hi), dxold = std::fabs(hi - lo), dx = dxold;
+    double f = p(x), df = dp(x);
+    for (int it = 0; it < 100; ++it) {
+        if (f == 0.0) break;
+        const bool bisect = (((x - xh) * df - f) * ((x - xl) * df - f) > 0.0) ||
+                            (std::fabs(2.0 * f) > std::fabs(dxold * df));
+        if (bisect) {
+            dxold = dx;
+            dx = 0.5 * (xh - xl);
+            x = xl + dx;
+            if (xl == x) break;
+        } else {
+            dxold = dx;
+            dx = f / df;
+            const double prev = x;
+            x = x - dx;
+            if (prev == x) break;
+        }
+        if (std::fabs(dx) < 1e-14 * (1.0 + std::fabs(x))) break;
+        f = p(x);
+        df = dp(x);
+        (f < 0.0 ? xl : xh) = x;
+    }
+    return x;
+}
+
 static std::vector<double> cubicRealRoots(double c3, double c2, double c1, double c0) {
     std::vector<double> out;
     const double big = std::fmax(std::fabs(c2), std::fmax(std::fabs(c1), std::fabs(c0)));
@@ -898,22 +930,14 @@ static std::vector<double> cubicRealRoots(double c3, double c2, double c1, doubl
     }
     ends.push_back(R);
     for (size_t k = 0; k + 1 < ends.size(); ++k) {
-        double lo = ends[k], hi = ends[k + 1];
-        double flo = p(lo);
-        const double fhi = p(hi);
+        const double lo = ends[k], hi = ends[k + 1];
+        const double flo = p(lo), fhi = p(hi);
         if (flo == 0.0) {
             if (out.empty() || out.back() != lo) out.push_back(lo);
             continue;
         }
         if ((flo < 0.0) == (fhi < 0.0) || fhi == 0.0) continue;
-        for (int it = 0; it < 256; ++it) {
-            const double mid = 0.5 * (lo + hi);
-            if (!(mid > lo && mid < hi)) break;
-            const double fm = p(mid);
-            if (fm == 0.0) { lo = mid; break; }
-            if ((fm < 0.0) == (flo < 0.0)) { lo = mid; flo = fm; } else hi = mid;
-        }
-        out.push_back(lo);
+        out.push_back(cubicRootIn(a, b, c, lo, hi, flo));
     }
     return out;
 }
