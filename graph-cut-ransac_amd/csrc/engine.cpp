@@ -507,6 +507,15 @@ public:
         std::memset(&st_, 0, sizeof(st_));
     }
 
+    // Shard every fetched chunk over `world` ranks.
+    void set_sharding(int rank, int world, gcr_allgather_fn fn, void* user) {
+        rank_ = rank;
+        world_ = world;
+        xfn_ = fn;
+        xuser_ = user;
+        compact_ = false;         // fixed-size per-hypothesis records cross the exchange
+    }
+
     // Full GCRANSAC::run; fills outputs, returns total inlier count.
     int run(uint8_t* mask0, uint8_t* mask1, double* H, gcr_rect_model* model_out) {
         const auto t_all = Clock::now();
@@ -544,7 +553,7 @@ public:
                 const size_t hj = j * kP + q;
                 if (q > 0 && P_->w->h_inc.p[hj] != 0) break;
                 // multi-model slots are scored compacted: results in order
-                const size_t si = kP > 1 ? cursor_++ : hj;
+                const size_t si = compact_ ? cursor_++ : hj;
                 const Model& model = Tr::hmodels(P_->w).p[hj];
                 const uint32_t rn[2] = {P_->w->sb.hn0.p[si], P_->w->sb.hn1.p[si]};
                 const HScore cur = finish(rn, P_->w->sb.hv0.p[si], P_->w->sb.hv1.p[si], P_->w->sb.htot.p[si]);
@@ -693,6 +702,11 @@ private:
 
     uint64_t it_ = 0;
     size_t cursor_ = 0;           // next compacted score of the current chunk
+    bool compact_ = kP > 1;       // multi-model slots scored compacted (single rank)
+    // one problem over several ranks (gcr_problem_run_sharded)
+    int rank_ = 0, world_ = 1;
+    gcr_allgather_fn xfn_ = nullptr;
+    void* xuser_ = nullptr;
     HScore best_{};
     Model best_model_ = Tr::def();
     Buffer bufs_[2];
@@ -734,7 +748,67 @@ private:
 
     // Generate [s0, s0+B), then score only the slots the loop can still reach
     // (iterations can never pass max(min_it, max_it)).  Returns slots scored.
+    // One hypothesis of a sharded chunk as it crosses the exchange.
+    struct HypRec {
+        Model m;
+        double v0, v1, tot;
+        uint32_t n0, n1;
+        uint32_t inc;
+        uint32_t pad;
+    };
+
+    // Sharded chunk: rank r generates and scores slots [s0 + r per, s0 + (r+1) per)
+    // on its own device; the all-gather gives every rank the whole chunk, so
+    // every rank replays identically.
+    uint64_t fetch_chunk_sharded(uint64_t s0, uint32_t B, uint64_t L) {
+        const uint32_t per = (B + world_ - 1) / world_;
+        const size_t nh = (size_t)per * kP;
+        P_->w->inc.ensure(nh); Tr::dmodels(P_->w).ensure(nh); P_->w->sb.ensure(nh);
+        P_->w->h_inc.ensure(nh); Tr::hmodels(P_->w).ensure(nh);
+        auto t0 = Clock::now();
+        const uint64_t my0 = s0 + (uint64_t)rank_ * per;
+        HIPC(Tr::generate(P_, prm_.seed, my0, per, P_->w->inc.p, Tr::dmodels(P_->w).p, s_));
+        HIPC(hipEventRecord(P_->ctx->ev0, s_));
+        HIPC(Tr::score(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, true, P_->w->sb.dev(), s_));
+        HIPC(hipEventRecord(P_->ctx->ev1, s_));
+        HIPC(hipMemcpyAsync(P_->w->h_inc.p, P_->w->inc.p, nh, hipMemcpyDeviceToHost, s_));
+        P_->w->sb.d2h(nh, s_);
+        HIPC(hipMemcpyAsync(Tr::hmodels(P_->w).p, Tr::dmodels(P_->w).p, nh * sizeof(Model), hipMemcpyDeviceToHost,
+                            s_));
+        HIPC(hipStreamSynchronize(s_));
+        float kms = 0;
+        HIPC(hipEventElapsedTime(&kms, P_->ctx->ev0, P_->ctx->ev1));
+        st_.ms_score_kernel += kms;
+        st_.ms_score += ms_since(t0);
+        st_.launches += 2;
+        st_.hypotheses_computed += nh;
+        std::vector<HypRec> send(nh), recv(nh * (size_t)world_);
+        const ScoreBufs& sb = P_->w->sb;
+        for (size_t i = 0; i < nh; ++i)
+            send[i] = HypRec{Tr::hmodels(P_->w).p[i], sb.hv0.p[i], sb.hv1.p[i], sb.htot.p[i],
+                             sb.hn0.p[i], sb.hn1.p[i], P_->w->h_inc.p[i], 0u};
+        t0 = Clock::now();
+        if (xfn_(xuser_, send.data(), recv.data(), nh * sizeof(HypRec)) != 0)
+            throw std::runtime_error("all-gather callback failed");
+        st_.ms_score += ms_since(t0);            // the exchange is part of verification
+        const size_t total = nh * (size_t)world_;
+        P_->w->h_inc.ensure(total); Tr::hmodels(P_->w).ensure(total); P_->w->sb.ensure(total);
+        for (size_t i = 0; i < total; ++i) {
+            const HypRec& r = recv[i];
+            P_->w->h_inc.p[i] = (uint8_t)r.inc;
+            Tr::hmodels(P_->w).p[i] = r.m;
+            P_->w->sb.hn0.p[i] = r.n0; P_->w->sb.hn1.p[i] = r.n1;
+            P_->w->sb.hv0.p[i] = r.v0; P_->w->sb.hv1.p[i] = r.v1; P_->w->sb.htot.p[i] = r.tot;
+        }
+        const uint64_t Bw = (uint64_t)per * world_;
+        uint64_t itp = it_, cnt = 0;
+        while (cnt < Bw && itp < L) itp += P_->w->h_inc.p[kP * cnt++];
+        if (cnt == 0) cnt = 1;
+        return cnt;
+    }
+
     uint64_t fetch_chunk(uint64_t s0, uint32_t B, uint64_t L) {
+        if (world_ > 1) return fetch_chunk_sharded(s0, B, L);
         const size_t BP = (size_t)B * kP;
         P_->w->inc.ensure(BP); Tr::dmodels(P_->w).ensure(BP); P_->w->sb.ensure(BP);
         P_->w->h_inc.ensure(BP); Tr::hmodels(P_->w).ensure(BP);
@@ -1007,6 +1081,28 @@ int gcr_problem_run(gcr_problem* prob, const gcr_params* params, uint8_t* mask0_
         };
         if (prob->solver == GCR_SOLVER_FUNDAMENTAL7) return go(FundRunner(prob, *params));
         return prob->solver == GCR_SOLVER_HOMOGRAPHY4 ? go(GeoRunner(prob, *params)) : go(Runner(prob, *params));
+    });
+}
+
+int gcr_problem_run_sharded(gcr_problem* prob, const gcr_params* params, int rank, int world,
+                            gcr_allgather_fn allgather, void* user, uint8_t* mask0_out, uint8_t* mask1_out,
+                            double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out) {
+    if (!prob) return set_err(GCR_EINVAL, "null problem");
+    if (int e = check_params(params, prob->solver)) return e;
+    if (world < 1 || rank < 0 || rank >= world || (world > 1 && !allgather))
+        return set_err(GCR_EINVAL, "bad rank/world/allgather");
+    if (!mask0_out || !H_out || (prob->K == 2 && !mask1_out)) return set_err(GCR_EINVAL, "null output buffer");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        auto go = [&](auto&& r) {
+            if (world > 1) r.set_sharding(rank, world, allgather, user);
+            const int total = r.run(mask0_out, mask1_out, H_out, model_out);
+            fill_stats(stats_out, r.stats());
+            return total;
+        };
+        if (prob->solver == GCR_SOLVER_FUNDAMENTAL7) return go(FundRunner(prob, *params));
+        if (prob->solver == GCR_SOLVER_HOMOGRAPHY4) return go(GeoRunner(prob, *params));
+        return go(Runner(prob, *params));
     });
 }
 

@@ -75,6 +75,10 @@ class BatchResult(C.Structure):
     ]
 
 
+# int (*)(void* user, const void* send, void* recv, size_t bytes)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -100,6 +104,8 @@ def _load():
     L.gcr_problem_destroy.argtypes = [vp]
     L.gcr_problem_destroy.restype = None
     L.gcr_problem_run.argtypes = [vp, C.POINTER(Params), u8p, u8p, dp, C.POINTER(RectModel), C.POINTER(Stats)]
+    L.gcr_problem_run_sharded.argtypes = [vp, C.POINTER(Params), C.c_int, C.c_int, ALLGATHER_FN, vp, u8p, u8p, dp,
+                                          C.POINTER(RectModel), C.POINTER(Stats)]
     L.gcr_problem_verify_batch.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.POINTER(BatchResult),
                                            C.POINTER(Stats)]
     L.gcr_problem_verify_batches.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.c_uint32,

@@ -23,7 +23,8 @@ RECORD = 20
 
 def problem_cost(problem: dict) -> float:
     """Estimated cost of a problem: feature count x hypotheses budget."""
-    n = sum(np.asarray(problem[k]).shape[0] for k in ("features", "scale_features", "orientation_features")
+    n = sum(np.asarray(problem[k]).shape[0]
+            for k in ("features", "scale_features", "orientation_features", "correspondences")
             if k in problem and problem[k] is not None)
     return float(n) * float(problem.get("max_iteration_number", 10000))
 
@@ -106,13 +107,23 @@ def gpu_solver(device: int) -> Callable[[dict], dict]:
     """solve() for solve_sharded that runs the MI355X engine on `device`.
 
     A problem is a dict with kind "sift" (scale_features, orientation_features,
-    scale_residual_thresh, orientation_residual_thresh) or "scale_only" /
-    "scale_only_original" (features, scale_residual_thresh), plus optional
+    scale_residual_thresh, orientation_residual_thresh), "scale_only" /
+    "scale_only_original" (features, scale_residual_thresh) or "homography" /
+    "fundamental" (correspondences (N, 4), threshold), plus optional
     spatial_coherence_weight, min/max_iteration_number,
     max_local_optimization_number, seed, confidence."""
     from . import pygcransac as P
 
     def solve(pr: dict) -> dict:
+        if pr["kind"] in ("homography", "fundamental"):
+            fn = P.findHomography if pr["kind"] == "homography" else P.findFundamentalMatrix
+            out = fn(pr["correspondences"], 0, 0, 0, 0, threshold=pr["threshold"],
+                     conf=pr.get("confidence", 0.99), spatial_coherence_weight=pr.get("spatial_coherence_weight", 0.0),
+                     max_iters=pr.get("max_iteration_number", 10000), min_iters=pr.get("min_iteration_number", 50),
+                     lo_number=pr.get("max_local_optimization_number", 50), seed=pr.get("seed", 0), device=device,
+                     return_stats=True)
+            M, mask, stats = out
+            return dict(H=M, model=None, num_inliers=int(mask.sum()), stats=stats, masks=(mask,))
         common = [pr.get("spatial_coherence_weight", 0.0), pr.get("min_iteration_number", 10000),
                   pr.get("max_iteration_number", 10000), pr.get("max_local_optimization_number", 50)]
         kw = dict(seed=pr.get("seed", 0), confidence=pr.get("confidence", 0.95), device=device, return_stats=True)
@@ -131,3 +142,73 @@ def gpu_solver(device: int) -> Callable[[dict], dict]:
         return dict(H=H, model=model, num_inliers=int(m.sum()), stats=stats, masks=(m,))
 
     return solve
+
+
+# ------------------------------------------------ one problem, many ranks ----
+def make_allgather(dist, world: int, device=None):
+    """ctypes all-gather callback for gcr_problem_run_sharded over a
+    torch.distributed group: RCCL (device tensors) on "nccl", gloo on CPU.
+    Keep the returned object alive for the duration of the call."""
+    import ctypes as C
+
+    import torch
+
+    from . import _native as N
+
+    def fn(_user, send, recv, nbytes):
+        try:
+            src = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(send))
+            t = torch.from_numpy(src.copy())
+            if device is not None:
+                t = t.to(device)
+            outs = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(outs, t)
+            o = torch.cat(outs).cpu().numpy()
+            C.memmove(recv, o.ctypes.data, world * nbytes)
+            return 0
+        except Exception:          # noqa: BLE001 -- reported to the engine as a failed exchange
+            return -1
+
+    return N.ALLGATHER_FN(fn)
+
+
+def run_problem_sharded(solver: int, f0, f1=None, params: Optional[dict] = None, rank: int = 0, world: int = 1,
+                        dist=None, device: Optional[int] = None, coll_device=None):
+    """One estimator problem over `world` ranks.
+
+    Every rank calls this with the same inputs; each verifies its block of
+    every chunk of slots on its own GPU and the chunks are all-gathered, so
+    every rank returns the single-rank result bit for bit.  `params` holds
+    gcr_params fields (scale_residual_thresh, confidence, seed, ...).
+    Returns (H (3, 3) or None, masks tuple, stats dict, rect model record)."""
+    import ctypes as C
+
+    from . import _native as N
+
+    f0 = np.ascontiguousarray(f0, dtype=np.float64)
+    f1 = None if f1 is None else np.ascontiguousarray(f1, dtype=np.float64)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    ctx = N.context(device)
+    h = C.c_void_p()
+    N.check(N.lib.gcr_problem_create(ctx, solver, dp(f0), f0.shape[0], dp(f1) if f1 is not None else None,
+                                     0 if f1 is None else f1.shape[0], C.byref(h)))
+    try:
+        p = N.default_params()
+        for k, v in (params or {}).items():
+            setattr(p, k, v)
+        m0 = np.zeros(f0.shape[0], dtype=np.uint8)
+        m1 = np.zeros(0 if f1 is None else f1.shape[0], dtype=np.uint8)
+        H = np.zeros(9)
+        model = N.RectModel()
+        st = N.Stats()
+        cb = make_allgather(dist, world, coll_device) if world > 1 else N.ALLGATHER_FN(0)
+        u8 = C.POINTER(C.c_uint8)
+        rc = N.lib.gcr_problem_run_sharded(h, C.byref(p), rank, world, cb, None, m0.ctypes.data_as(u8),
+                                           m1.ctypes.data_as(u8) if f1 is not None else None, dp(H), C.byref(model),
+                                           C.byref(st))
+        n = N.check(rc)
+    finally:
+        N.lib.gcr_problem_destroy(h)
+    masks = (m0.astype(bool),) if f1 is None else (m0.astype(bool), m1.astype(bool))
+    rec = [model.x0, model.y0, model.s, model.h7, model.h8, model.alpha, model.phi]
+    return (H.reshape(3, 3) if n > 0 else None), masks, st.as_dict(), rec

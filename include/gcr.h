@@ -138,6 +138,19 @@ void gcr_problem_destroy(gcr_problem* prob);
 int gcr_problem_run(gcr_problem* prob, const gcr_params* params, uint8_t* mask0_out, uint8_t* mask1_out,
                     double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
 
+/* One problem over `world` processes: every rank
+ * calls this with the same problem and params.  Each fetched chunk of slots is
+ * split into `world` contiguous blocks; rank r generates and scores block r
+ * on its own device, and `allgather` (host memory: `bytes` from every rank
+ * into recv, rank-major -- e.g. RCCL all_gather over xGMI, or gloo) hands
+ * every rank the whole chunk.  The replay, LO and the final refit then run
+ * identically on every rank, so all ranks return the single-rank result bit
+ * for bit.  The callback returns 0 on success. */
+typedef int (*gcr_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
+int gcr_problem_run_sharded(gcr_problem* prob, const gcr_params* params, int rank, int world,
+                            gcr_allgather_fn allgather, void* user, uint8_t* mask0_out, uint8_t* mask1_out,
+                            double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
+
 /* One pass of the hot path over one batch: draw and solve `nslots`
  * outer-iteration slots starting at `slot0`, MSAC-score every resulting model
  * against all features on the GPU, and return the best-scoring slot (first

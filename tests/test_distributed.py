@@ -96,3 +96,35 @@ def test_solve_sharded_gloo_world2(tmp_path):
     exp = [None if r is None else dict(n=r["num_inliers"], h7=r["model"]["h7"], it=r["iteration_number"])
            for r in ref]
     assert outs[0]["recs"] == exp
+
+
+# --------------------------------------- one problem, many ranks (e row 2) ---
+def _allgather_worker(rank, world, port, outdir):
+    import ctypes as C
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        cb = D.make_allgather(dist, world)
+        nbytes = 1000 + 24 * 7
+        send = (np.arange(nbytes) * (rank + 3) % 251).astype(np.uint8)
+        recv = np.zeros(world * nbytes, dtype=np.uint8)
+        rcs = [cb(None, send.ctypes.data, recv.ctypes.data, nbytes) for _ in range(3)]   # repeated exchanges
+        with open(os.path.join(outdir, f"ag{rank}.json"), "w") as f:
+            json.dump(dict(rcs=rcs, recv=recv.tolist()), f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_allgather_callback_gloo_world2(tmp_path):
+    # the exchange gcr_problem_run_sharded calls through its C function pointer
+    world = 2
+    mp.spawn(_allgather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    nbytes = 1000 + 24 * 7
+    exp = np.concatenate([(np.arange(nbytes) * (r + 3) % 251).astype(np.uint8) for r in range(world)]).tolist()
+    for r in range(world):
+        out = json.load(open(tmp_path / f"ag{r}.json"))
+        assert out["rcs"] == [0, 0, 0]
+        assert out["recv"] == exp

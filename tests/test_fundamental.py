@@ -251,3 +251,30 @@ def test_verify_batches_best_matches_oracle(gpu):
                     best, bslot = v, s
         assert out[b].models == models and out[b].iterations == its
         assert out[b].best_slot == bslot and bits(out[b].best_score) == bits(best)
+
+
+@pytest.mark.gpu
+def test_mixed_batch_records_match_direct_calls(gpu):
+    # BASELINE configs[4] shape (mixed H / F / rectification problems), small
+    from pygcransac import distributed as D
+
+    probs = []
+    for i in range(2):
+        c, _, _, thr = S.problem_h(400 + 100 * i, 0.5, seed=500 + i)
+        probs.append(dict(kind="homography", correspondences=c, threshold=thr, seed=i, min_iteration_number=50,
+                          max_iteration_number=2000))
+        c, _, _, thr = S.problem_f(600 + 100 * i, 0.5, seed=510 + i)
+        probs.append(dict(kind="fundamental", correspondences=c, threshold=thr, seed=i, min_iteration_number=50,
+                          max_iteration_number=5000))
+    f, _, thr = S.problem_m1(400, seed=520)
+    probs.append(dict(kind="scale_only", features=f, scale_residual_thresh=thr, seed=9, min_iteration_number=200,
+                      max_iteration_number=2000))
+    recs, local = D.solve_sharded(probs, D.gpu_solver(0))
+    for i, pr in enumerate(probs):
+        if pr["kind"] == "scale_only":
+            continue
+        fn = pygcransac.findHomography if pr["kind"] == "homography" else pygcransac.findFundamentalMatrix
+        M, mask = fn(pr["correspondences"], 0, 0, 0, 0, threshold=pr["threshold"], conf=0.99,
+                     spatial_coherence_weight=0.0, max_iters=pr["max_iteration_number"], min_iters=50, seed=pr["seed"])
+        assert recs[i]["num_inliers"] == int(mask.sum())
+        assert np.array_equal(bits(recs[i]["H"]), bits(M))
