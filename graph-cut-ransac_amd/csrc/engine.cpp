@@ -35,6 +35,9 @@
 #include <new>
 #include <string>
 #include <vector>
+#include <thread>
+#include <mutex>
+#include <atomic>
 
 #include "gcr.h"
 #include "host_fit.h"
@@ -1146,6 +1149,43 @@ static int run_oneshot(gcr_ctx* ctx, int solver, const double* f0, size_t n0, co
         stats->ms_total += setup;
     }
     return rc;
+}
+
+int gcr_solve_batch(int device, gcr_batch_item* items, size_t n, int concurrency) {
+    if (n > 0 && !items) return set_err(GCR_EINVAL, "null items");
+    if (concurrency < 1) concurrency = 1;
+    if ((size_t)concurrency > n) concurrency = (int)std::max<size_t>(n, 1);
+    std::vector<gcr_ctx*> ctxs((size_t)concurrency, nullptr);
+    for (auto& c : ctxs)
+        if (int rc = gcr_create(device, &c); rc != GCR_OK) {
+            for (auto* d : ctxs) gcr_destroy(d);
+            return rc;
+        }
+    std::atomic<size_t> next{0};
+    std::atomic<int> first_err{GCR_OK};
+    std::mutex err_mu;
+    std::string err_text;
+    auto worker = [&](gcr_ctx* ctx) {
+        for (size_t i; (i = next.fetch_add(1)) < n;) {
+            gcr_batch_item& it = items[i];
+            it.result = run_oneshot(ctx, it.solver, it.f0, it.n0, it.f1, it.n1, &it.params, it.mask0_out,
+                                    it.mask1_out, it.H_out, &it.model_out, &it.stats_out);
+            if (it.result < 0) {
+                int expect = GCR_OK;
+                if (first_err.compare_exchange_strong(expect, it.result)) {
+                    std::lock_guard<std::mutex> lk(err_mu);
+                    err_text = g_err;        // thread-local message of this worker
+                }
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < concurrency; ++t) pool.emplace_back(worker, ctxs[(size_t)t]);
+    worker(ctxs[0]);
+    for (auto& th : pool) th.join();
+    for (auto* c : ctxs) gcr_destroy(c);
+    if (first_err.load() != GCR_OK) return set_err(first_err.load(), "%s", err_text.c_str());
+    return GCR_OK;
 }
 
 int gcr_rect_scale_only(gcr_ctx* ctx, const double* features, size_t n, const gcr_params* params, int original,

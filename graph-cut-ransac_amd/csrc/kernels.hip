@@ -1017,23 +1017,21 @@ void launch_split_t(const DevProblem& p, const double T[2], const RectModel* mod
 }
 
 int score_mode() {
-    static int mode = -1;
-    if (mode < 0) {
+    static const int mode = [] {          // thread-safe one-time init (gcr_solve_batch threads)
         const char* e = getenv("GCR_SCORE_KERNEL");
-        mode = (e && e[0] == 'n') ? 1 : 0;   // "naive" -> lane-per-hypothesis kernel
-    }
+        return (e && e[0] == 'n') ? 1 : 0;   // "naive" -> lane-per-hypothesis kernel
+    }();
     return mode;
 }
 
 // GCR_SPLIT_H=64|16|4 pins the split-scorer variant (tuning sweeps); default:
 // by batch size, so that the grid still covers the 256 CUs.
 int split_h(uint32_t nh) {
-    static int forced = -1;
-    if (forced < 0) {
+    static const int forced = [] {
         const char* e = getenv("GCR_SPLIT_H");
         const int v = e ? atoi(e) : 0;
-        forced = (v == 64 || v == 16 || v == 4) ? v : 0;
-    }
+        return (v == 64 || v == 16 || v == 4) ? v : 0;
+    }();
     if (forced) return forced;
     return nh >= 16384 ? 64 : nh >= 2048 ? 16 : 4;
 }

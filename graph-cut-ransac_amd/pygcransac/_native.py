@@ -75,6 +75,23 @@ class BatchResult(C.Structure):
     ]
 
 
+class BatchItem(C.Structure):
+    _fields_ = [
+        ("solver", C.c_int),
+        ("f0", C.POINTER(C.c_double)),
+        ("n0", C.c_size_t),
+        ("f1", C.POINTER(C.c_double)),
+        ("n1", C.c_size_t),
+        ("params", Params),
+        ("mask0_out", C.POINTER(C.c_uint8)),
+        ("mask1_out", C.POINTER(C.c_uint8)),
+        ("H_out", C.c_double * 9),
+        ("model_out", RectModel),
+        ("stats_out", Stats),
+        ("result", C.c_int),
+    ]
+
+
 # int (*)(void* user, const void* send, void* recv, size_t bytes)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
@@ -106,6 +123,7 @@ def _load():
     L.gcr_problem_run.argtypes = [vp, C.POINTER(Params), u8p, u8p, dp, C.POINTER(RectModel), C.POINTER(Stats)]
     L.gcr_problem_run_sharded.argtypes = [vp, C.POINTER(Params), C.c_int, C.c_int, ALLGATHER_FN, vp, u8p, u8p, dp,
                                           C.POINTER(RectModel), C.POINTER(Stats)]
+    L.gcr_solve_batch.argtypes = [C.c_int, C.POINTER(BatchItem), C.c_size_t, C.c_int]
     L.gcr_problem_verify_batch.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.POINTER(BatchResult),
                                            C.POINTER(Stats)]
     L.gcr_problem_verify_batches.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.c_uint32,

@@ -71,16 +71,22 @@ def decode_record(rec: np.ndarray) -> Optional[dict]:
                 iteration_number=int(rec[18]), hypotheses=int(rec[19]))
 
 
-def solve_sharded(problems: Sequence[dict], solve: Callable[[dict], dict], rank: int = 0, world: int = 1,
-                  dist=None, device=None) -> tuple[list[Optional[dict]], dict]:
+def solve_sharded(problems: Sequence[dict], solve: Optional[Callable[[dict], dict]] = None, rank: int = 0,
+                  world: int = 1, dist=None, device=None,
+                  solve_many: Optional[Callable[[list], list]] = None) -> tuple[list[Optional[dict]], dict]:
     """Solve this rank's LPT share with `solve(problem) -> result dict`
-    (keys H, model, num_inliers, stats, plus anything rank-local such as masks),
-    then gather every problem's record to every rank with one all_gather.
+    (keys H, model, num_inliers, stats, plus anything rank-local such as masks)
+    or, for the whole share at once, `solve_many(problems) -> [result dict]`
+    (e.g. `batch_solver`), then gather every problem's record to every rank
+    with one all_gather.
 
     Returns (records in problem order -- all ranks, local results by index)."""
     shares = assign_lpt([problem_cost(p) for p in problems], world)
     mine = shares[rank]
-    local = {i: solve(problems[i]) for i in mine}
+    if solve_many is not None:
+        local = dict(zip(mine, solve_many([problems[i] for i in mine])))
+    else:
+        local = {i: solve(problems[i]) for i in mine}
     cap = max(1, max(len(s) for s in shares))
     buf = np.zeros((cap, RECORD))
     for j, i in enumerate(mine):
@@ -212,3 +218,63 @@ def run_problem_sharded(solver: int, f0, f1=None, params: Optional[dict] = None,
     masks = (m0.astype(bool),) if f1 is None else (m0.astype(bool), m1.astype(bool))
     rec = [model.x0, model.y0, model.s, model.h7, model.h8, model.alpha, model.phi]
     return (H.reshape(3, 3) if n > 0 else None), masks, st.as_dict(), rec
+
+
+# ------------------------------------------------ native batch (one device) --
+_SOLVERS = {"scale_only": 0, "scale_only_original": 1, "sift": 2, "homography": 3, "fundamental": 4}
+
+
+def batch_solver(device: int = 0, concurrency: int = 4) -> Callable[[list], list]:
+    """solve_many() for solve_sharded: the rank's share in ONE gcr_solve_batch
+    call (`concurrency` host threads, a HIP stream and workspace each, so host
+    phases of one problem overlap kernels of another).  Problem dicts as for
+    gpu_solver."""
+    import ctypes as C
+
+    from . import _native as N
+
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    u8 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))  # noqa: E731
+
+    def solve_many(problems: list) -> list:
+        items = (N.BatchItem * len(problems))()
+        keep = []
+        for it, pr in zip(items, problems):
+            kind = pr["kind"]
+            it.solver = _SOLVERS[kind]
+            if kind == "sift":
+                f0, f1 = pr["scale_features"], pr["orientation_features"]
+                t0, t1 = pr["scale_residual_thresh"], pr["orientation_residual_thresh"]
+            elif kind in ("homography", "fundamental"):
+                f0, f1, t0, t1 = pr["correspondences"], None, pr["threshold"], 2.0
+            else:
+                f0, f1, t0, t1 = pr["features"], None, pr["scale_residual_thresh"], 2.0
+            f0 = np.ascontiguousarray(f0, dtype=np.float64)
+            f1 = None if f1 is None else np.ascontiguousarray(f1, dtype=np.float64)
+            m0 = np.zeros(f0.shape[0], dtype=np.uint8)
+            m1 = None if f1 is None else np.zeros(f1.shape[0], dtype=np.uint8)
+            keep.append((f0, f1, m0, m1))
+            it.f0, it.n0 = dp(f0), f0.shape[0]
+            it.f1, it.n1 = (dp(f1), f1.shape[0]) if f1 is not None else (None, 0)
+            it.mask0_out = u8(m0)
+            it.mask1_out = u8(m1) if m1 is not None else None
+            p = N.default_params()
+            p.scale_residual_thresh, p.orientation_residual_thresh = float(t0), float(t1)
+            p.spatial_coherence_weight = float(pr.get("spatial_coherence_weight", 0.0))
+            p.min_iteration_number = int(pr.get("min_iteration_number", 10000))
+            p.max_iteration_number = int(pr.get("max_iteration_number", 10000))
+            p.max_local_optimization_number = int(pr.get("max_local_optimization_number", 50))
+            p.seed = int(pr.get("seed", 0))
+            p.confidence = float(pr.get("confidence", 0.95))
+            it.params = p
+        N.check(N.lib.gcr_solve_batch(device, items, len(problems), concurrency))
+        out = []
+        for it, (f0, f1, m0, m1) in zip(items, keep):
+            n = int(it.result)
+            masks = (m0.astype(bool),) if m1 is None else (m0.astype(bool), m1.astype(bool))
+            H = np.array(it.H_out[:]).reshape(3, 3) if n > 0 else None
+            out.append(dict(H=H, model=it.model_out if it.solver < 3 and n > 0 else None, num_inliers=n,
+                            stats=it.stats_out.as_dict(), masks=masks))
+        return out
+
+    return solve_many

@@ -128,6 +128,29 @@ int gcr_find_homography(gcr_ctx* ctx, const double* correspondences, size_t n, c
 int gcr_find_fundamental_matrix(gcr_ctx* ctx, const double* correspondences, size_t n, const gcr_params* params,
                                 uint8_t* mask_out, double* F_out, gcr_stats* stats_out);
 
+/* ---- batches of independent problems (SURVEY.md §8(b) gcr_rect_batch,
+ * BASELINE configs[4]) ----------------------------------------------------- */
+typedef struct gcr_batch_item {
+    int solver;                  /* GCR_SOLVER_*                                   */
+    const double* f0;            /* N0 x 3 features, or N0 x 4 correspondences     */
+    size_t n0;
+    const double* f1;            /* orientation features (SIFT22), else NULL       */
+    size_t n1;
+    gcr_params params;
+    uint8_t* mask0_out;          /* caller-owned, n0 bytes                          */
+    uint8_t* mask1_out;          /* caller-owned, n1 bytes (SIFT22), else NULL      */
+    double H_out[9];
+    gcr_rect_model model_out;
+    gcr_stats stats_out;
+    int result;                  /* inlier count (0: no model) or error code        */
+} gcr_batch_item;
+/* Solve n independent problems on one device.  `concurrency` host threads,
+ * each with its own context (HIP stream + workspace), take problems in index
+ * order from a shared counter, so one problem's host phases (replay, LO fits,
+ * refit control) overlap another's kernels.  Results are per item; returns
+ * GCR_OK, or the first error code (message in gcr_last_error()). */
+int gcr_solve_batch(int device, gcr_batch_item* items, size_t n, int concurrency);
+
 /* ---- device-resident problems (benchmarks, problem batches) -------------- */
 /* Uploads the features once; runs reuse the HBM-resident copy.  f1 is the
  * orientation set for GCR_SOLVER_SIFT22 and NULL otherwise. */

@@ -84,3 +84,39 @@ def test_single_rank_entry_equals_public_api():
                                             return_stats=True)
     assert np.array_equal(bits(H), bits(H2)) and np.array_equal(masks[0], m2)
     assert st["iteration_number"] == st2["iteration_number"]
+
+
+def _mixed_problems():
+    probs = []
+    for i in range(3):
+        c, _, _, thr = S.problem_h(500 + 150 * i, 0.5, seed=600 + i)
+        probs.append(dict(kind="homography", correspondences=c, threshold=thr, seed=i, confidence=0.99,
+                          min_iteration_number=50, max_iteration_number=5000, spatial_coherence_weight=0.0))
+        c, _, _, thr = S.problem_f(800 + 200 * i, 0.6, seed=610 + i)
+        probs.append(dict(kind="fundamental", correspondences=c, threshold=thr, seed=i, confidence=0.99,
+                          min_iteration_number=50, max_iteration_number=20000, spatial_coherence_weight=0.0))
+        fs, fo, _, _, ts, to = S.problem_m2(700 + 100 * i, 600, seed=620 + i)
+        probs.append(dict(kind="sift", scale_features=fs, orientation_features=fo, scale_residual_thresh=ts,
+                          orientation_residual_thresh=to, seed=i, min_iteration_number=200,
+                          max_iteration_number=3000))
+        f, _, thr = S.problem_m1(600 + 100 * i, seed=630 + i)
+        probs.append(dict(kind="scale_only", features=f, scale_residual_thresh=thr, seed=i,
+                          min_iteration_number=200, max_iteration_number=3000))
+    return probs
+
+
+@pytest.mark.parametrize("concurrency", [1, 4])
+def test_native_batch_equals_one_by_one(concurrency):
+    # gcr_solve_batch (threads, one context each) == gpu_solver's sequential calls
+    probs = _mixed_problems()
+    many = D.batch_solver(0, concurrency)(probs)
+    one = D.gpu_solver(0)
+    for pr, got in zip(probs, many):
+        exp = one(pr)
+        assert got["num_inliers"] == exp["num_inliers"], pr["kind"]
+        assert (got["H"] is None) == (exp["H"] is None)
+        if exp["H"] is not None:
+            assert np.array_equal(bits(got["H"]), bits(exp["H"])), pr["kind"]
+        for a, b in zip(got["masks"], exp["masks"]):
+            assert np.array_equal(a, b)
+        assert got["stats"]["iteration_number"] == exp["stats"]["iteration_number"]
