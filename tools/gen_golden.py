@@ -10,7 +10,7 @@ both math modes:
 Each file holds the inputs, the parameters and, per mode, the masks, H, the
 model parameters and the run statistics.
 
-usage: python tools/gen_golden.py   (rewrites tests/golden/)
+usage: python tools/gen_golden.py [--corr-only]   (rewrites tests/golden/)
 """
 import os
 import sys
@@ -65,5 +65,30 @@ def main():
         print(name, d["glibc_num_inliers"], d["glibc_stats"])
 
 
+CORR_OUT = os.path.join(OUT, "corr")
+CORR_PARAMS = dict(min_it=50, max_it=5000, lo=50, seed=20251121, confidence=0.99)
+
+
+def main_corr():
+    """Homography / fundamental-matrix fixtures (no reference exists: these pin
+    the oracle restatement and the product against regressions)."""
+    os.makedirs(CORR_OUT, exist_ok=True)
+    for n in (30, 500, 2000):
+        for kind, gen, fn in (("h", S.problem_h, O.find_homography), ("f", S.problem_f, O.find_fundamental)):
+            c, _, _, thr = gen(max(n, 30), 0.5, seed=3000 + n)
+            r = fn(c, thr, **CORR_PARAMS)
+            d = dict(correspondences=c, thr=np.float64(thr),
+                     params=np.array([CORR_PARAMS[k] for k in ("min_it", "max_it", "lo", "seed")]),
+                     confidence=np.float64(CORR_PARAMS["confidence"]), num_inliers=np.int64(r["num_inliers"]),
+                     M=r["H"], mask=np.packbits(r["mask"].astype(np.uint8)),
+                     stats=np.array([r["stats"][k] for k in STAT_KEYS], dtype=np.int64))
+            name = f"{kind}_n{n}.npz"
+            np.savez_compressed(os.path.join(CORR_OUT, name), **d)
+            print(name, d["num_inliers"], d["stats"])
+
+
 if __name__ == "__main__":
-    main()
+    if "--corr-only" not in sys.argv:
+        main()
+    O.build()
+    main_corr()
