@@ -267,6 +267,19 @@ def main():
         cpu = dict(value=n_cpu / s_cpu, unit="hypotheses/s", cores=1, kind="port",
                    sample=f"{nslots} outer-iteration slots of the same workload, CPU oracle (glibc math, "
                           f"{smp_text}, -O2), single thread, {s_cpu:.1f} s")
+        # the same full estimator call to 0.99 confidence on the CPU oracle (one
+        # run; skipped for F at 80 % outliers, ~490k iterations ~ minutes)
+        if latency is not None and kind != 4:
+            t1 = time.perf_counter()
+            kw = dict(min_it=0, max_it=10**7, lo=50, confidence=0.99, seed=100, math_mode=O.MATH_GLIBC, sampler=smp)
+            if kind == 2:
+                O.rect_sift(f0, f1, thr0, thr1, **kw)
+            elif kind == 3:
+                O.find_homography(f0, thr0, **kw)
+            else:
+                O.rect_scale_only(f0, thr0, **kw)
+            latency["cpu_oracle_ms"] = (time.perf_counter() - t1) * 1e3
+            latency["cpu_oracle_note"] = f"CPU oracle, 1 thread, glibc math, {smp_text}, same call"
 
     if rank == 0:
         line = {

@@ -278,3 +278,18 @@ def test_mixed_batch_records_match_direct_calls(gpu):
                      spatial_coherence_weight=0.0, max_iters=pr["max_iteration_number"], min_iters=50, seed=pr["seed"])
         assert recs[i]["num_inliers"] == int(mask.sum())
         assert np.array_equal(bits(recs[i]["H"]), bits(M))
+
+
+@pytest.mark.gpu
+def test_minimum_and_nonfinite_inputs_match_oracle(gpu):
+    rng = np.random.default_rng(6)
+    for seed in range(3):                       # exactly the minimal sample size
+        c = np.column_stack([rng.uniform(0, 1000, (7, 2)), rng.uniform(0, 1000, (7, 2))])
+        _assert_same(c, 1.0, seed, min_it=100, max_it=100)
+    c, _, _, thr = S.problem_f(900, 0.5, seed=78)
+    bad = c.copy()
+    bad[::9, 3] = np.nan
+    bad[::13, 0] = -np.inf
+    _assert_same(bad, thr, 1)
+    pure = np.column_stack([rng.uniform(0, 1280, (400, 2)), rng.uniform(0, 1280, (400, 2))])
+    _assert_same(pure, 1.0, 2, min_it=500, max_it=500)

@@ -254,3 +254,18 @@ def test_verify_batches_best_slot_matches_oracle(gpu):
                 best, bslot = v, s
         assert out[b].models == models and out[b].iterations == its
         assert out[b].best_slot == bslot and bits(out[b].best_score) == bits(best)
+
+
+@pytest.mark.gpu
+def test_minimum_and_nonfinite_inputs_match_oracle(gpu):
+    rng = np.random.default_rng(5)
+    for seed in range(3):                       # exactly the minimal sample size
+        c = np.column_stack([rng.uniform(0, 1000, (4, 2)), rng.uniform(0, 1000, (4, 2))])
+        _assert_same(c, 2.0, seed, min_it=100, max_it=100)
+    c, _, _, thr = S.problem_h(600, 0.5, seed=77)
+    bad = c.copy()
+    bad[::9, 2] = np.nan
+    bad[::13, 1] = np.inf
+    _assert_same(bad, thr, 1)
+    pure = np.column_stack([rng.uniform(0, 1280, (300, 2)), rng.uniform(0, 1280, (300, 2))])
+    _assert_same(pure, 1.0, 2, min_it=500, max_it=500)
