@@ -167,6 +167,7 @@ struct Workspace {
     DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
     DevBuf<double> rf_part;             // GPU refit: reduction block partials
     PinBuf<double> rf_hpart;
+    PinBuf<double> rf_htop;             // GPU refit: top-row mirror + async upload ring
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
@@ -197,9 +198,46 @@ namespace {
 // per-block partials (k_qr_partials, row order inside a block) summed here in
 // block order -- blocked_sum's order exactly, so results equal the host's.
 struct DevQRStore {
+    // qr_solve<3> only ever reads rows 0..2 of a column on the host (pivots,
+    // R entries, the reduced right-hand side).  Those rows are mirrored in a
+    // host cache refreshed inside every reduction's synchronisation, and
+    // writes go out asynchronously from a pinned ring, so the ~50 scalar
+    // round trips of the driver collapse to one synchronisation per reduction.
+    static constexpr int kTop = 3;
+    static constexpr int kRing = 64;
     double* col[4];
     hipStream_t s;
     gcr_problem* P;
+    size_t m = 0;                 // rows
+    double cache[4][kTop] = {};
+    bool valid[4][kTop] = {};
+    int ring_used = 0;
+
+    double* top() { return P->w->rf_htop.p; }             // 4 x kTop staging
+    double* ring() { return P->w->rf_htop.p + 4 * kTop; }
+    void prepare() { P->w->rf_htop.ensure(4 * kTop + kRing); }
+
+    // queue the copies of rows 0..kTop-1 of every column (complete after the
+    // caller's next stream synchronisation)
+    void enqueue_top() {
+        const size_t n = std::min<size_t>(kTop, m);
+        for (int c = 0; c < 4; ++c)
+            HIPC(hipMemcpyAsync(top() + c * kTop, col[c], n * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    void sync_and_take_top() {
+        HIPC(hipStreamSynchronize(s));
+        ring_used = 0;                                    // every queued upload has completed
+        const size_t n = std::min<size_t>(kTop, m);
+        for (int c = 0; c < 4; ++c)
+            for (size_t i = 0; i < (size_t)kTop; ++i) {
+                valid[c][i] = i < n;
+                if (i < n) cache[c][i] = top()[c * kTop + i];
+            }
+    }
+    void invalidate(int c, size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi && i < (size_t)kTop; ++i) valid[c][i] = false;
+    }
+
     double dot(int a, int c, size_t lo, size_t hi) {
         if (hi <= lo) return 0.0;
         size_t nb = (hi - 1) / kSumBlock - lo / kSumBlock + 1;
@@ -207,27 +245,49 @@ struct DevQRStore {
         P->w->rf_hpart.ensure(nb);
         HIPC(launch_qr_partials(col[a], col[c], lo, hi, P->w->rf_part.p, &nb, s));
         HIPC(hipMemcpyAsync(P->w->rf_hpart.p, P->w->rf_part.p, nb * sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        enqueue_top();
+        sync_and_take_top();
         double total = 0.0;
         for (size_t b = 0; b < nb; ++b) total += P->w->rf_hpart.p[b];
         return total;
     }
     double sumsq(int c, size_t lo, size_t hi) { return dot(c, c, lo, hi); }
     double get(int c, size_t i) {
+        if (i < (size_t)kTop && valid[c][i]) return cache[c][i];
+        if (i < (size_t)kTop) {
+            enqueue_top();
+            sync_and_take_top();
+            return cache[c][i];
+        }
         HIPC(hipMemcpyAsync(P->w->rf_hpart.p, col[c] + i, sizeof(double), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
+        ring_used = 0;
         return P->w->rf_hpart.p[0];
     }
     void set(int c, size_t i, double v) {
-        HIPC(hipStreamSynchronize(s));          // staging slot may still feed a copy
-        P->w->rf_hpart.p[0] = v;
-        HIPC(hipMemcpyAsync(col[c] + i, P->w->rf_hpart.p, sizeof(double), hipMemcpyHostToDevice, s));
-        HIPC(hipStreamSynchronize(s));
+        if (ring_used == kRing) {                         // never at C = 3; kept for safety
+            HIPC(hipStreamSynchronize(s));
+            ring_used = 0;
+        }
+        double* slot = ring() + ring_used++;
+        *slot = v;
+        HIPC(hipMemcpyAsync(col[c] + i, slot, sizeof(double), hipMemcpyHostToDevice, s));
+        if (i < (size_t)kTop) {
+            cache[c][i] = v;
+            valid[c][i] = true;
+        }
     }
-    void scale(int c, size_t lo, size_t hi, double den) { HIPC(launch_qr_scale(col[c], lo, hi, den, s)); }
-    void zero(int c, size_t lo, size_t hi) { HIPC(launch_qr_zero(col[c], lo, hi, s)); }
+    void scale(int c, size_t lo, size_t hi, double den) {
+        HIPC(launch_qr_scale(col[c], lo, hi, den, s));
+        invalidate(c, lo, hi);
+    }
+    void zero(int c, size_t lo, size_t hi) {
+        HIPC(launch_qr_zero(col[c], lo, hi, s));
+        invalidate(c, lo, hi);
+    }
     void update(int c, int e, size_t lo, size_t hi, double tau, double t) {
         HIPC(launch_qr_update(col[c], col[e], lo, hi, tau, t, s));
+        invalidate(c, lo, hi);
     }
 };
 
@@ -249,7 +309,10 @@ struct GpuSiftSolver final : SiftSystemSolver {
                               rows, A, A + rows, A + 2 * rows, A + 3 * rows, s));
         HIPC(hipStreamSynchronize(s));          // index lists are pageable host vectors
         DevQRStore st{{A, A + rows, A + 2 * rows, A + 3 * rows}, s, P};
+        st.m = rows;
+        st.prepare();
         qr3_solve(st, rows, x);
+        HIPC(hipStreamSynchronize(s));          // the pinned ring must outlive its uploads
     }
 };
 
