@@ -220,13 +220,37 @@ GCR_HD bool oriented_ok(const double* f, const double* x1, const double* y1, con
     return pos == N || neg == N;
 }
 
-// 7-point solver: up to kFModels oriented-valid models, returned in ascending
-// root order.  0 = the sample yields no model.
-GCR_HD int solve_f7(const double x1[7], const double y1[7], const double x2[7], const double y2[7],
-                    GeoModel out[kFModels]) {
+// The 7-point solver's intermediate state: normalisation, the null-space
+// basis and the real roots of the cubic, with the oriented-valid roots in a
+// bit mask.  Kept in registers; a model is rebuilt from it on demand
+// (f7_model), so the generator never holds three 9-double models per lane.
+struct F7Basis {
+    double F1[9], F2[9];
+    double s1, cx1, cy1, s2, cx2, cy2;
+    double root0, root1, root2;
+    unsigned valid;              // bit q: root q gives an oriented-valid model
+};
+
+GCR_HD double f7_root(const F7Basis& b, int q) { return q == 0 ? b.root0 : (q == 1 ? b.root1 : b.root2); }
+
+// model of root q (false if it does not denormalise)
+GCR_HD bool f7_model(const F7Basis& b, double l, double fm[9]) {
+    double fn[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) fn[k] = b.F1[k] + l * b.F2[k];
+    return denormalize_f(fn, b.s1, b.cx1, b.cy1, b.s2, b.cx2, b.cy2, fm);
+}
+
+// 7-point solver: fills the basis; returns the number of oriented-valid
+// models (0 = the sample yields no model).  Models are in ascending root order.
+GCR_HD int solve_f7_basis(const double x1[7], const double y1[7], const double x2[7], const double y2[7],
+                          F7Basis& out) {
+    out.valid = 0;
     double cx1, cy1, s1, cx2, cy2, s2;
     if (!hartley7<7>(x1, y1, cx1, cy1, s1) || !hartley7<7>(x2, y2, cx2, cy2, s2)) return 0;
+    out.s1 = s1; out.cx1 = cx1; out.cy1 = cy1; out.s2 = s2; out.cx2 = cx2; out.cy2 = cy2;
     double a[7][9];
+#pragma unroll
     for (int i = 0; i < 7; ++i) {
         const double u1 = s1 * (x1[i] - cx1), v1 = s1 * (y1[i] - cy1);
         const double u2 = s2 * (x2[i] - cx2), v2 = s2 * (y2[i] - cy2);
@@ -264,7 +288,6 @@ GCR_HD int solve_f7(const double x1[7], const double y1[7], const double x2[7], 
         }
     }
     // null-space basis: (f7, f8) = (1, 0) and (0, 1)
-    double F1[9], F2[9];
     auto back_substitute = [&](double (&fv)[9], double f7, double f8) {
         fv[7] = f7;
         fv[8] = f8;
@@ -277,35 +300,42 @@ GCR_HD int solve_f7(const double x1[7], const double y1[7], const double x2[7], 
             fv[r] = -acc / a[r][r];
         }
     };
-    back_substitute(F1, 1.0, 0.0);
-    back_substitute(F2, 0.0, 1.0);
+    back_substitute(out.F1, 1.0, 0.0);
+    back_substitute(out.F2, 0.0, 1.0);
     // det(F1 + l F2) = c3 l^3 + c2 l^2 + c1 l + c0 from four evaluations
     double P[9], M[9];
-    for (int k = 0; k < 9; ++k) { P[k] = F1[k] + F2[k]; M[k] = F1[k] - F2[k]; }
-    const double c0 = det3(F1), c3 = det3(F2), d1 = det3(P), dm1 = det3(M);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { P[k] = out.F1[k] + out.F2[k]; M[k] = out.F1[k] - out.F2[k]; }
+    const double c0 = det3(out.F1), c3 = det3(out.F2), d1 = det3(P), dm1 = det3(M);
     const double c2 = (d1 + dm1) * 0.5 - c0;
     const double c1 = (d1 - dm1) * 0.5 - c3;
-    double roots[3];
+    double roots[3] = {0.0, 0.0, 0.0};
     const int nr = real_roots_cubic(c3, c2, c1, c0, roots);
+    out.root0 = roots[0];
+    out.root1 = roots[1];
+    out.root2 = roots[2];
     int n = 0;
-    // one root -> one model; destinations are static (n <= q)
-    auto emit = [&](double l, auto qtag) {
-        constexpr int q = decltype(qtag)::value;
-        double fn[9], fm[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) fn[k] = F1[k] + l * F2[k];
-        if (!denormalize_f(fn, s1, cx1, cy1, s2, cx2, cy2, fm)) return;
-        if (!oriented_ok<7>(fm, x1, y1, x2, y2)) return;
-#pragma unroll
-        for (int d = 0; d <= q; ++d)
-            if (d == n)
-#pragma unroll
-                for (int k = 0; k < 9; ++k) out[d].h[k] = fm[k];
+    for (int q = 0; q < 3; ++q) {
+        if (q >= nr) break;
+        double fm[9];
+        if (!f7_model(out, f7_root(out, q), fm)) continue;
+        if (!oriented_ok<7>(fm, x1, y1, x2, y2)) continue;
+        out.valid |= 1u << q;
         ++n;
-    };
-    if (nr > 0) emit(roots[0], std::integral_constant<int, 0>{});
-    if (nr > 1) emit(roots[1], std::integral_constant<int, 1>{});
-    if (nr > 2) emit(roots[2], std::integral_constant<int, 2>{});
+    }
+    return n;
+}
+
+// 7-point solver, models materialised: up to kFModels oriented-valid models in
+// ascending root order (host paths and tests)
+GCR_HD int solve_f7(const double x1[7], const double y1[7], const double x2[7], const double y2[7],
+                    GeoModel out[kFModels]) {
+    F7Basis b;
+    const int n = solve_f7_basis(x1, y1, x2, y2, b);
+    int k = 0;
+    for (int q = 0; q < 3 && k < n; ++q)
+        if (b.valid & (1u << q)) f7_model(b, f7_root(b, q), out[k++].h);
     return n;
 }
 

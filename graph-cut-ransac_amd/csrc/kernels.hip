@@ -131,9 +131,9 @@ __global__ __launch_bounds__(kGenBlock) void k_generate(DevProblem p, uint64_t s
 }
 
 // Fundamental matrix: one attempt = Philox sample of 7 correspondences ->
-// 7-point solver (fund.h), 0..3 models.  No sample-validity test beyond the
-// solver's own rank and orientation checks.
-GCR_DEVICE int attempt_f(const DevProblem& p, uint64_t seed, uint64_t slot, uint32_t a, GeoModel (&ms)[kFModels]) {
+// 7-point solver (fund.h) into a register-resident basis; 0..3 models.  No
+// sample-validity test beyond the solver's own rank and orientation checks.
+GCR_DEVICE int attempt_f(const DevProblem& p, uint64_t seed, uint64_t slot, uint32_t a, F7Basis& b) {
     const DevClass& c = p.cls[0];
     uint32_t idx[7];
     WordStream ws(seed, slot, a, kStreamMain, 0);
@@ -146,13 +146,14 @@ GCR_DEVICE int attempt_f(const DevProblem& p, uint64_t seed, uint64_t slot, uint
         x2[j] = c.a[idx[j]];
         y2[j] = c.c0[idx[j]];
     }
-    return solve_f7(x1, y1, x2, y2, ms);
+    return solve_f7_basis(x1, y1, x2, y2, b);
 }
 
 // k_generate for the fundamental matrix: a sample yields up to kFModels
 // models, stored as hypotheses 3s + k.  inc[3s] = attempt + 1 (102: all 101
 // attempts failed); inc[3s + k], k >= 1, = 0 if the k-th model exists (scored,
-// no extra iterations) and 255 if not (skipped).
+// no extra iterations) and 255 if not (skipped).  The winning lane rebuilds
+// its models from the basis and writes them straight to global memory.
 template <int G>
 __global__ __launch_bounds__(kGenBlock) void k_generate_f(DevProblem p, uint64_t seed, uint64_t slot0,
                                                           uint32_t nslots, uint8_t* __restrict__ inc,
@@ -167,17 +168,27 @@ __global__ __launch_bounds__(kGenBlock) void k_generate_f(DevProblem p, uint64_t
     const int gbase = lane & ~(G - 1);
     for (uint32_t r = 0; r * G < 101; ++r) {
         const uint32_t a = r * G + g;
-        GeoModel ms[kFModels];
-        const int cnt = a < 101 ? attempt_f(p, seed, slot, a, ms) : 0;
+        F7Basis b;
+        const int cnt = a < 101 ? attempt_f(p, seed, slot, a, b) : 0;
         const uint64_t mask = __ballot(cnt > 0);
         const uint64_t grp = G == 64 ? mask : (mask >> gbase) & ((1ull << G) - 1ull);
         if (grp) {
             if (g == (uint32_t)__builtin_ctzll(grp)) {
+                GeoModel* out = models + (size_t)kFModels * s;
+                uint8_t* oi = inc + (size_t)kFModels * s;
+                int k = 0;
 #pragma unroll
-                for (int q = 0; q < kFModels; ++q) {
-                    models[(size_t)kFModels * s + q] = q < cnt ? ms[q] : default_geo();
-                    inc[(size_t)kFModels * s + q] = q == 0 ? (uint8_t)(a + 1) : (q < cnt ? 0 : 255);
-                }
+                for (int q = 0; q < 3; ++q)
+                    if (b.valid & (1u << q)) {
+                        double fm[9];
+                        f7_model(b, f7_root(b, q), fm);
+                        for (int j = 0; j < 9; ++j) out[k].h[j] = fm[j];
+                        ++k;
+                    }
+                for (int q = k; q < kFModels; ++q) out[q] = default_geo();
+                oi[0] = (uint8_t)(a + 1);
+                oi[1] = cnt > 1 ? 0 : 255;
+                oi[2] = cnt > 2 ? 0 : 255;
             }
             return;
         }
