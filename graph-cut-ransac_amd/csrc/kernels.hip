@@ -291,6 +291,20 @@ __device__ __forceinline__ bool scale_band(double x, double y, double s, const H
     return !(s < q.lo * t3 || s > q.hi * t3);
 }
 
+// Homography band: the transfer error without its two divisions.  With
+// w = h31 x1 + h32 y1 + h33 and e = (h1 . x1 - x2 w, h2 . x1 - y2 w), the
+// exact r^2 is |e|^2 / w^2 (in real arithmetic), so a pair can only be an
+// inlier if |e|^2 <= Tb w^2, Tb = (sqrt(T)(1 + 1e-7) + 1e-7)^2 (1e-7 px of
+// slack against rounding, far above the ~1e-11 px errors at image
+// coordinates).  NaN never rejects (the exact residual decides).
+__device__ __forceinline__ bool h_band(double x1, double y1, double x2, double y2, const double* h, double Tb) {
+    const double w = (h[6] * x1 + h[7] * y1) + h[8];
+    const double tu = (h[0] * x1 + h[1] * y1) + h[2];
+    const double tv = (h[3] * x1 + h[4] * y1) + h[5];
+    const double e1 = tu - x2 * w, e2 = tv - y2 * w;
+    return !(e1 * e1 + e2 * e2 > Tb * (w * w));
+}
+
 __device__ __forceinline__ bool orient_band(double x, double y, double ct, double st, const HypConst& q,
                                             double tan_tau) {
     const double numer = (-x * st + y * ct) * q.h7 + st;
@@ -338,12 +352,13 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     // 16-byte reads over distinct banks
     constexpr int kRP = R + 2;
     // KIND 4: packed in-order inlier segments (sparse chain fold, measured
-    // 220 -> 181 us at 4096 slots); KIND 3 keeps the dense tile (61 vs 90 us)
+    // 220 -> 181 us at 4096 slots); KIND 3 goes through the band + queue path
+    // with the division-free h_band prefilter
     constexpr bool kPack = KIND == 4;
     __shared__ double tile[2][H * kRP];
     constexpr int kRp = (R + 127) / 128 * 128;       // fbuf row: whole 128-feature DMA strips
     __shared__ double fbuf[2][4][kRp];               // staged features of a round: x, y, s|cos, sin
-    __shared__ uint16_t queue[kComputeWaves][KIND >= 3 ? 1 : kPer * 64];
+    __shared__ uint16_t queue[kComputeWaves][kPack ? 1 : kPer * 64];
     __shared__ HypConst hyp[H];
     __shared__ uint32_t cnt_sh[2][H];
     // KIND >= 3: per round buffer, compute wave and hypothesis, the number of
@@ -488,23 +503,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                 const int cls = (r < r0) ? 0 : 1;
                 const uint32_t base = (cls == 0 ? r : r - r0) * R;
                 const uint32_t nc = cls == 0 ? n0 : n1;
-                if constexpr (KIND >= 3 && !kPack) {
-                    // homography: every pair evaluated directly into the dense
-                    // tile (outliers +0.0), counts by LDS atomics
-#pragma unroll
-                    for (int k = 0; k < kPer; ++k) {
-                        const uint32_t il = fsub + k * kStride;
-                        double v = 0.0;
-                        if (live && base + il < nc) {
-                            const double r2 = geo_sq_residual<KIND>(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine.g);
-                            if (r2 <= T0) {
-                                v = -r2;
-                                atomicAdd(&cnt_sh[0][h], 1u);
-                            }
-                        }
-                        tl[h * kRP + il] = v;
-                    }
-                } else if constexpr (KIND >= 3) {
+                if constexpr (kPack) {
                     // fundamental matrix: the exact residual is cheap, every
                     // pair is evaluated directly (no band).  Wave w
                     // owns the contiguous feature segment [w kSeg, (w+1) kSeg)
@@ -550,7 +549,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                     const uint32_t il = fsub + k * kStride;
                     bool cand = false;
                     if (live && base + il < nc) {
-                        if (cls == 0) cand = scale_band<KIND>(fb[0][il], fb[1][il], fb[2][il], mine);
+                        if constexpr (KIND == 3) cand = h_band(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine.g, band0);
+                        else if (cls == 0) cand = scale_band<KIND>(fb[0][il], fb[1][il], fb[2][il], mine);
                         else if constexpr (KIND == 2) cand = orient_band(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine, tan_tau1);
                     }
                     tl[h * kRP + il] = 0.0;
@@ -582,7 +582,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                     m.h8 = q.h8;
                     double r2;
                     bool inl;
-                    if (cls == 0) {
+                    if constexpr (KIND == 3) {
+                        r2 = h_sq_residual(fb[0][il], fb[1][il], fb[2][il], fb[3][il], q.g);
+                        inl = r2 <= T0;
+                    } else if (cls == 0) {
                         r2 = scale_sq_residual<KIND == 1, true>(fb[0][il], fb[1][il], fb[2][il], m, q.ac);
                         inl = r2 <= T0;
                     } else {
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         atomicAdd(&cnt_sh[cls][hh], 1u);
                     }
                 }
-                }   // KIND < 3
+                }   // band path (KIND <= 3)
             }
         } else {
             // chain wave: stage round r+1's features around the fold of
@@ -1274,8 +1277,9 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
     ga.hcount = hcount;
     auto go = [&](auto ktag, auto htag, auto rtag) {
         constexpr int KIND = decltype(ktag)::value, H = decltype(htag)::value, R = decltype(rtag)::value;
+        const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;     // h_band slack
         hipLaunchKernelGGL((k_score_split<KIND, H, R, false>), dim3((nh + H - 1) / H), dim3(kSplitThreads), 0,
-                           stream, p, T, 0.0, 0.0, 0.0, models, inc, nh, out, ga);
+                           stream, p, T, 0.0, sb * sb, 0.0, models, inc, nh, out, ga);
     };
     auto by_h = [&](auto ktag) {
         const int h = split_h(nh);

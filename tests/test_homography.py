@@ -269,3 +269,38 @@ def test_minimum_and_nonfinite_inputs_match_oracle(gpu):
     _assert_same(bad, thr, 1)
     pure = np.column_stack([rng.uniform(0, 1280, (300, 2)), rng.uniform(0, 1280, (300, 2))])
     _assert_same(pure, 1.0, 2, min_it=500, max_it=500)
+
+
+@pytest.mark.gpu
+def test_band_prefilter_is_conservative_at_the_threshold(gpu):
+    # the division-free h_band must keep every pair the exact transfer error
+    # accepts: correspondences placed within a few ulps of sqrt(T) (the MSAC
+    # threshold) of their model's transfer, counts and sums equal the oracle's
+    rng = np.random.default_rng(1234)
+    thr = 2.0
+    T = (2.25 * thr) * thr
+    models = []
+    rows = []
+    for i in range(12):
+        Hm = S.H_GT * (1.0 + rng.normal(0, 1e-3, (3, 3)))
+        Hm = Hm / Hm[2, 2]
+        models.append(Hm.ravel())
+        x1 = rng.uniform(0, 1280, (400, 2))
+        w = (Hm[2, 0] * x1[:, 0] + Hm[2, 1] * x1[:, 1]) + Hm[2, 2]
+        u = ((Hm[0, 0] * x1[:, 0] + Hm[0, 1] * x1[:, 1]) + Hm[0, 2]) / w
+        v = ((Hm[1, 0] * x1[:, 0] + Hm[1, 1] * x1[:, 1]) + Hm[1, 2]) / w
+        th = rng.uniform(0, 2 * np.pi, 400)
+        rad = np.sqrt(T) * (1.0 + rng.integers(-8, 9, 400) * 2.0 ** -52) + rng.choice([0.0, 1e-9, -1e-9], 400)
+        rows.append(np.column_stack([x1, u + rad * np.cos(th), v + rad * np.sin(th)]))
+    corr = np.concatenate(rows)
+    prob = CorrProblem(N.SOLVER_HOMOGRAPHY4, corr)
+    refs = [O.h_score(corr, m, thr) for m in models]
+    assert sum(r["count"] for r in refs) > 500                 # the boundary is populated
+    for nh in (100, 2048, 16384):
+        tiled = np.resize(np.array(models), (nh, 9))
+        n0, v0, tot = prob.score(tiled, thr)
+        for i in range(nh):
+            ref = refs[i % len(models)]
+            cnt, val = _finish(n0[i], v0[i], tot[i], thr)
+            assert cnt == (ref["count"] if ref["count"] >= 4 else 0), (nh, i)
+            assert bits(val) == bits(ref["value"]), (nh, i)
