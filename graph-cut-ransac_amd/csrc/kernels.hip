@@ -911,22 +911,35 @@ __global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* _
     for (int q = 0; q < kPerLane; ++q) pw[lane + 64 * q] = av[q] * cv[q];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (lane == 0) {
-        // products outside [b0, b1) are +0.0 but still must not be added
-        // (0.0 + -x differs from -x only in the sign of zero: skip them)
-        double part = 0.0;
-        const double2* p2 = reinterpret_cast<const double2*>(pw);
-        const uint64_t e0 = b0 - base, e1 = b1 - base;
-        uint64_t e = e0;
-        if (e & 1) { part += pw[e]; ++e; }
-        for (; e + 16 <= e1; e += 16) {
-            double2 v[8];
+    // blocked_sum's order (qr3.h): lane l < 16 folds sub-block l (64 rows,
+    // clipped to [b0, b1)) sequentially, then lane 0 folds the sub-block
+    // partials of the sub-blocks that meet the range, in order
+    constexpr int kSubs = (int)(kSumBlock / kSumSub);
+    __shared__ double subp[kPartWaves][kSubs];
+    const uint64_t e0 = b0 - base, e1 = b1 - base;
+    if (lane < kSubs) {
+        const uint64_t s0 = (uint64_t)lane * kSumSub, s1 = s0 + kSumSub;
+        const uint64_t lo_e = s0 > e0 ? s0 : e0, hi_e = s1 < e1 ? s1 : e1;
+        double sp = 0.0;
+        uint64_t e = lo_e;
+        for (; e + 8 <= hi_e; e += 8) {
+            double v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = p2[(e >> 1) + u];
+            for (int u = 0; u < 8; ++u) v[u] = pw[e + u];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) { part += v[u].x; part += v[u].y; }
+            for (int u = 0; u < 8; ++u) sp += v[u];
         }
-        for (; e < e1; ++e) part += pw[e];
+        for (; e < hi_e; ++e) sp += pw[e];
+        subp[wave][lane] = sp;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (lane == 0) {
+        double part = 0.0;
+        for (int l = 0; l < kSubs; ++l) {
+            const uint64_t s0 = (uint64_t)l * kSumSub, s1 = s0 + kSumSub;
+            if (s1 > e0 && s0 < e1) part += subp[wave][l];
+        }
         partials[blk] = part;
     }
 }

@@ -5,10 +5,11 @@
 // systems) and the GPU (the hybrid final refit's ~n_o^2/2 pair rows) run the
 // same control flow and the same per-element arithmetic.
 //
-// Reductions use ONE fixed order, blocked_sum: sequential inside aligned blocks
-// of kSumBlock rows, then the block partials sequentially.  Eigen's own order
-// is packet-vectorised and unpinned (no Eigen here); for m <= kSumBlock the
-// blocked order is plain sequential summation.  The oracle restates the same
+// Reductions use ONE fixed order, blocked_sum: sequential inside aligned
+// sub-blocks of kSumSub rows, sub-block partials sequentially inside aligned
+// blocks of kSumBlock rows, then the block partials sequentially.  Eigen's own
+// order is packet-vectorised and unpinned (no Eigen here); for m <= kSumSub
+// the blocked order is plain sequential summation.  The oracle restates the same
 // order (oracle/gcr_oracle.cpp), so host, GPU and oracle agree bitwise.
 #pragma once
 
@@ -21,8 +22,13 @@
 namespace gcr {
 
 constexpr size_t kSumBlock = 1024;
+constexpr size_t kSumSub = 64;         // sub-blocks: 16 per block
 
-// sum_{i in [lo, hi)} f(i) in blocked order
+// sum_{i in [lo, hi)} f(i) in blocked order: sequential inside each aligned
+// sub-block of kSumSub rows, the sub-block partials of an aligned block of
+// kSumBlock rows sequentially, then the block partials sequentially.  (The
+// two-level block keeps the GPU's sequential chains at 64 + 16 adds instead
+// of 1024; for m <= 64 it is plain sequential summation.)
 template <class F>
 inline double blocked_sum(size_t lo, size_t hi, F f) {
     double total = 0.0;
@@ -30,7 +36,12 @@ inline double blocked_sum(size_t lo, size_t hi, F f) {
     while (i < hi) {
         const size_t end = std::min(hi, (i / kSumBlock + 1) * kSumBlock);
         double part = 0.0;
-        for (; i < end; ++i) part += f(i);
+        while (i < end) {
+            const size_t send = std::min(end, (i / kSumSub + 1) * kSumSub);
+            double sp = 0.0;
+            for (; i < send; ++i) sp += f(i);
+            part += sp;
+        }
         total += part;
     }
     return total;
