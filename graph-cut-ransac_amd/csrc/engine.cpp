@@ -38,6 +38,9 @@
 #include <thread>
 #include <mutex>
 #include <atomic>
+#include <exception>
+#include <array>
+#include <condition_variable>
 
 #include "gcr.h"
 #include "host_fit.h"
@@ -315,6 +318,96 @@ struct GpuSiftSolver final : SiftSystemSolver {
         HIPC(hipStreamSynchronize(s));          // the pinned ring must outlive its uploads
     }
 };
+
+// A small persistent pool of host threads for the LO trial fits (independent
+// least-squares solves; results land at their trial index, so the outcome
+// does not depend on the scheduling).  Size: GCR_HOST_THREADS, default
+// min(8, hardware threads).
+class HostPool {
+public:
+    explicit HostPool(unsigned n) {
+        for (unsigned t = 1; t < n; ++t) workers_.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& w : workers_) w.join();
+    }
+    // fn(i) for i in [0, n); the calling thread works too
+    void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
+        if (n == 0) return;
+        if (workers_.empty() || n == 1) {
+            for (size_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        std::unique_lock<std::mutex> call(call_mu_);      // one job at a time
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &fn;
+            n_ = n;
+            next_.store(0);
+            pending_ = workers_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        run();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        job_ = nullptr;
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            std::rethrow_exception(e);            // the first failure, on the caller
+        }
+    }
+
+private:
+    void run() {
+        try {
+            for (size_t i; (i = next_.fetch_add(1)) < n_;) (*job_)(i);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(err_mu_);
+            if (!err_) err_ = std::current_exception();
+            next_.store(n_);                      // stop handing out work
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            run();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_, call_mu_, err_mu_;
+    std::exception_ptr err_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)>* job_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    size_t pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+HostPool& host_pool() {
+    static HostPool pool([] {
+        const char* e = getenv("GCR_HOST_THREADS");
+        long n = e ? atol(e) : (long)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        return (unsigned)std::max(1L, std::min(64L, n));
+    }());
+    return pool;
+}
 
 // verify_batches records kernel-timing events on every n-th batch
 // (GCR_TIMING_STRIDE, default 1 = every batch)
@@ -955,7 +1048,10 @@ private:
         static_assert(kMaxLOSample >= 7 * 7, "LO sample buffer");
 
         ++lo_number_;
-        std::vector<uint32_t> inl[2], sample[2];
+        std::vector<uint32_t> inl[2];
+        std::vector<std::array<std::vector<uint32_t>, 2>> trial_samples;
+        std::vector<Model> trial_fit;
+        std::vector<char> trial_ok;
         std::vector<Model> trial_models;
         std::vector<HScore> trial_scores;
         std::vector<uint32_t> trial_raw;
@@ -974,8 +1070,14 @@ private:
             // when every class uses all its inliers each trial refits the same
             // set: one trial decides the round (later ones cannot be strictly better)
             const uint64_t ntrials = all_deterministic ? std::min<uint64_t>(T, 1) : T;
+            // draw the trials' samples in order (a failed draw ends the round,
+            // as in the sequential loop), fit them on the host worker pool,
+            // keep the successful fits in trial order
+            trial_samples.resize(ntrials);
+            uint64_t ndrawn = 0;
             for (uint64_t trial = 0; trial < ntrials; ++trial) {
                 bool ok = true;
+                auto& smp = trial_samples[trial];
                 for (int c = 0; c < K_ && ok; ++c) {
                     if (ssz[c] < inl[c].size()) {
                         // 7 m points: 49 for the 7-point fundamental matrix
@@ -985,19 +1087,24 @@ private:
                             ok = false;
                             break;
                         }
-                        sample[c].resize(ssz[c]);
-                        for (uint64_t q = 0; q < ssz[c]; ++q) sample[c][q] = inl[c][pos[q]];
+                        smp[c].resize(ssz[c]);
+                        for (uint64_t q = 0; q < ssz[c]; ++q) smp[c][q] = inl[c][pos[q]];
                     } else if (m_[c] < inl[c].size()) {
-                        sample[c] = inl[c];
+                        smp[c] = inl[c];
                     } else {
                         ok = false;
                     }
                 }
                 if (!ok) break;
-                Model fm;
-                if (!Tr::fit(P_, sample, fm, false)) continue;
-                trial_models.push_back(fm);
+                ++ndrawn;
             }
+            trial_fit.resize(ndrawn);
+            trial_ok.assign(ndrawn, 0);
+            host_pool().parallel_for(ndrawn, [&](size_t i) {
+                trial_ok[i] = Tr::fit(P_, trial_samples[i].data(), trial_fit[i], false) ? 1 : 0;
+            });
+            for (uint64_t i = 0; i < ndrawn; ++i)
+                if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
             if (!trial_models.empty()) {
                 trial_scores.resize(trial_models.size());
                 trial_raw.resize(2 * trial_models.size());
