@@ -271,13 +271,15 @@ constexpr int kSplitThreads = 1024;
 constexpr int kComputeThreads = 960;
 constexpr int kComputeWaves = 15;
 
-struct HypConst {           // per-hypothesis constants of the exact and band tests
+struct alignas(16) HypConst {   // per-hypothesis constants of the exact and band tests
     union {
         struct {
-            double h7, h8, ac;  // scale: model, alpha^3
+            // band constants first, in 16-byte pairs (ds_read_b128)
+            double h7, h8;      // model
             double lo, hi;      // scale band on s / t^3 (ac-adjusted)
-            double cphi, cphi2; // orientation: clipped phi, clip(clip(phi + pi/2))
             double cf, sf;      // orientation: cos(phi), sin(phi) (band test only)
+            double ac;          // scale: alpha^3
+            double cphi, cphi2; // orientation: clipped phi, clip(clip(phi + pi/2))
         };
         double g[9];            // homography (KIND 3), row-major
     };
@@ -326,6 +328,13 @@ struct GenArgs {
     // hmap[j], j < *hcount; results are written at j
     const uint32_t* hmap;
     const uint32_t* hcount;
+    // kGen prologue: lanes per slot (a power of two dividing 1024 / H; 0 =
+    // 1024 / H, every thread of the workgroup)
+    uint32_t glanes;
+    // timing probes only (GCR_PROBE, results invalid when set): bit 0 skips
+    // the chain fold, bit 1 the exact pass, bit 2 the band test, bit 3 the
+    // prologue's attempts (every slot takes attempt 0's default model)
+    uint32_t probe;
 };
 
 template <int KIND, int H, int R, bool kGen>
@@ -428,16 +437,20 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     __shared__ int gen_a[kGen ? H : 1];
     __shared__ RectModel gen_m[kGen ? H : 1];
     if constexpr (kGen) {
-        constexpr int G = kSplitThreads / H;
+        // G lanes per slot on threads [0, H G): fewer waves contend for the
+        // SIMDs, so one round of attempts finishes sooner
+        const int G = gen.glanes ? (int)gen.glanes : kSplitThreads / H;
+        const bool gact = t < H * G;
         if (t < H) gen_a[t] = 127;
         __syncthreads();
-        const int gh = t / G, g = t % G;
+        const int gh = gact ? t / G : 0, g = t % G;
         const uint32_t gs = blockIdx.x * H + gh;
         for (uint32_t rr = 0; rr * G < 101; ++rr) {
             const uint32_t a = rr * G + g;
             RectModel m = default_model();
             bool ok = false;
-            if (gs < nh && a < 101 && gen_a[gh] == 127) ok = attempt<KIND>(p, gen.seed, gen.slot0 + gs, a, m);
+            if (gact && gs < nh && a < 101 && gen_a[gh] == 127)
+                ok = (gen.probe & 8u) ? a == 0 : attempt<KIND>(p, gen.seed, gen.slot0 + gs, a, m);
             if (ok) atomicMin(&gen_a[gh], (int)a);
             __syncthreads();
             if (ok && gen_a[gh] == (int)a) gen_m[gh] = m;
@@ -548,7 +561,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                 for (int k = 0; k < kPer; ++k) {
                     const uint32_t il = fsub + k * kStride;
                     bool cand = false;
-                    if (live && base + il < nc) {
+                    if (live && base + il < nc && !(gen.probe & 4u)) {
                         if constexpr (KIND == 3) cand = h_band(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine.g, band0);
                         else if (cls == 0) cand = scale_band<KIND>(fb[0][il], fb[1][il], fb[2][il], mine);
                         else if constexpr (KIND == 2) cand = orient_band(fb[0][il], fb[1][il], fb[2][il], fb[3][il], mine, tan_tau1);
@@ -572,6 +585,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                     qn += (uint32_t)__builtin_popcountll(mask);
                 }
                 // 3) exact residuals of the survivors, all lanes busy
+                if (gen.probe & 2u) qn = 0;
                 for (uint32_t j = lane; j < qn; j += 64) {
                     const uint32_t idx = qw[j];
                     const int hh = idx % H;
@@ -630,7 +644,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         for (; j < n; ++j) run += seg[j];
                     }
                 }
-            } else if (r > 0 && chain_lane) {
+            } else if (r > 0 && chain_lane && !(gen.probe & 1u)) {
                 const uint32_t qr = r - 1;
                 const bool cls0 = qr < r0;
                 if (KIND == 2 && qr == r0 && role == 0) {   // first orientation round
@@ -653,6 +667,8 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                 };
                 // batches of kB 16-byte reads all in flight, then 2 kB adds:
                 // the fold is bound by LDS latency under the compute waves' load
+                // (a software-pipelined variant, batch b+1 in flight while
+                // batch b is added, measured slower: 0.149 vs 0.135 ms)
                 constexpr int kB = KIND == 2 ? 10 : 12;
                 for (; j + kB <= np; j += kB) {
                     double2 v[kB];
@@ -696,6 +712,425 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                     }
                 }
                 // candidates of the update rule: score > 0 and a valid model
+                const bool cand = valid_h && sum > 0.0 && (KIND != 2 || valid_model_sift22(gen_m[h]));
+                fin_sh[h] = cand ? sum : -1.0;
+            }
+        }
+        if constexpr (kGen) {
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) {
+                // the workgroup's first strict best, slots in order
+                WgBest b{0.0, -1, 0, 0, 0, 0};
+                for (int q = 0; q < H; ++q) {
+                    const uint32_t gq = blockIdx.x * H + q;
+                    if (gq >= nh) break;
+                    const int a = gen_a[q];
+                    b.iterations += (uint64_t)(a == 127 ? 102 : a + 1);
+                    if (a != 127) ++b.models;
+                    const double s = fin_sh[q];
+                    if (s > 0.0 && b.score < s) {
+                        b.score = s;
+                        b.slot = (int32_t)gq;
+                        b.n0 = cnt_sh[0][q];
+                        b.n1 = KIND == 2 ? cnt_sh[1][q] : 0;
+                    }
+                }
+                gen.wg[blockIdx.x] = b;
+            }
+        }
+    }
+}
+
+
+// ------------------------------------------------ diagnostic stamps ----
+// Built only into libgcr_stamps.so (make stamps, -DGCR_STAMPS): s_memtime at
+// the segment boundaries of k_score_fm for the first kStWG workgroups, read
+// back by tools/stamp_probe.py.  The product build executes no stamp.
+#ifdef GCR_STAMPS
+constexpr int kStWG = 4, kStRounds = 16, kStSlots = 8;
+__device__ uint64_t g_stamps[kStWG][16][kStRounds][kStSlots];
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define GCR_STAMP(slot, rr)                                                                   \
+    do {                                                                                      \
+        const uint64_t _t = stamp_now();                                                      \
+        if (blockIdx.x < kStWG && (rr) < (uint32_t)kStRounds && lane == 0)                    \
+            g_stamps[blockIdx.x][wave][rr][slot] = _t;                                        \
+    } while (0)
+#define GCR_STAMP_VAL(slot, rr, v)                                                            \
+    do {                                                                                      \
+        if (blockIdx.x < kStWG && (rr) < (uint32_t)kStRounds && lane == 0)                    \
+            g_stamps[blockIdx.x][wave][rr][slot] = (v);                                       \
+    } while (0)
+#else
+#define GCR_STAMP(slot, rr) do {} while (0)
+#define GCR_STAMP_VAL(slot, rr, v) do {} while (0)
+#endif
+
+// ------------------------------------------- feature-major split scoring ----
+// Exact MSAC with one feature per compute lane and a sparse, in-order fold.
+//
+// A workgroup owns H <= 16 hypotheses.  Compute wave w (0..14) owns features
+// [64 w, 64 w + 64) of each round of 960 (rounds never straddle the class
+// boundary): every lane holds its own feature in registers and tests it
+// against the H hypotheses in turn with the conservative band, so the
+// survivors of a wave-round are appended hypothesis by hypothesis, each
+// hypothesis's entries in feature order.  The exact residuals of the
+// survivors are then evaluated with all 64 lanes busy, and the inlier values
+// -r^2 are packed by a running ballot prefix: hypothesis q's inlier values of
+// the wave-round are a contiguous run of outv[w], in feature order, delimited
+// by lohi[.][w][q], lohi[.][w][q + 1].
+//
+// Wave 15 (the chain wave) folds the runs wave by wave and round by round:
+// exactly the inliers in feature order, which is the reference's sequential
+// sum (MSAC_scoring_function.hpp:73-85, score.hpp:45-50) because an outlier's
+// +0.0 never changes it.  Outliers cost the chain nothing.  Waves hand over
+// through LDS flags instead of barriers (ready[w]: rounds published by wave
+// w; done[w]: rounds of wave w the chain has folded), so a compute wave only
+// waits when the chain still reads its previous run.
+constexpr int kFmWaves = 15;
+constexpr uint32_t kFmRound = kFmWaves * 64;
+constexpr int kFmCB = 8;            // chain batch: 16-byte LDS reads (2 values each) per run step
+
+__device__ __forceinline__ void fm_wait_ge(const uint32_t* f, uint32_t v) {
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void fm_publish(uint32_t* f, uint32_t v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int KIND>
+__device__ __forceinline__ HypConst make_hyp(const typename ModelOf<KIND>::type& m, double band0) {
+    HypConst q;
+    if constexpr (KIND >= 3) {
+        for (int j = 0; j < 9; ++j) q.g[j] = m.h[j];
+    } else {
+        q.h7 = m.h7;
+        q.h8 = m.h8;
+        q.ac = alpha_cube(m);
+        // s / t^3 must lie in [exp(-tau), exp(tau)] / ac (new) or * ac (original)
+        q.lo = (KIND == 1 ? q.ac : 1.0 / q.ac) * (1.0 / band0) * (1.0 - 1e-9);
+        q.hi = (KIND == 1 ? q.ac : 1.0 / q.ac) * band0 * (1.0 + 1e-9);
+        q.cphi = 0.0; q.cphi2 = 0.0; q.cf = 1.0; q.sf = 0.0;
+        if constexpr (KIND == 2) {
+            const OrientConst oc = orient_const(m);
+            q.cphi = oc.cphi;
+            q.cphi2 = oc.cphi2;
+            sincos(m.phi, &q.sf, &q.cf);
+        }
+    }
+    return q;
+}
+
+template <int KIND, int H, bool kGen>
+__global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double T0, double T1, double band0,
+                                                            double tan_tau1,
+                                                            const typename ModelOf<KIND>::type* __restrict__ models,
+                                                            const uint8_t* __restrict__ inc, uint32_t nh,
+                                                            ScoreOut out, GenArgs gen) {
+    static_assert(H >= 1 && H <= 16 && KIND <= 3, "feature-major scorer: H <= 16, band estimators");
+    static_assert(!kGen || KIND < 3, "in-kernel generation: rectification solvers");
+    constexpr int kCap = 64 * H;                        // pairs of one wave-round
+    // packed inlier values (-r^2) of hypothesis q in wave w's features, in
+    // feature order, zero-padded to whole chain batches
+    // region stride 66 doubles: the 16 chain lanes' 16-byte reads (and the
+    // exact pass's scattered writes) fall in distinct banks
+    constexpr int kReg = 66;
+    __shared__ double2 outv[kFmWaves][H][kReg / 2];
+    __shared__ uint16_t queue[kFmWaves][kCap];          // survivors: q | lane << 4 | k << 10
+    __shared__ uint32_t wcnt[2][kFmWaves][H];           // survivors of (wave, q) in the round
+    __shared__ uint32_t ready[kFmWaves], done[kFmWaves];
+    __shared__ HypConst hyp[H];
+    __shared__ uint32_t hval[H];
+    __shared__ uint32_t cnt_sh[2][H];
+    __shared__ int gen_a[kGen ? H : 1];
+    __shared__ RectModel gen_m[kGen ? H : 1];
+    __shared__ double fin_sh[kGen ? H : 1];
+
+    const int t = threadIdx.x;
+    const int wave = t >> 6;
+    const int lane = t & 63;
+    const bool chain_wave = wave == kFmWaves;
+
+    GCR_STAMP(5, 15u);
+    // ---- prologue: this workgroup's H slots (kGen), k_generate's rule
+    if constexpr (kGen) {
+        const int G = gen.glanes ? (int)gen.glanes : kSplitThreads / H;
+        const bool gact = t < H * G;
+        if (t < H) gen_a[t] = 127;
+        __syncthreads();
+        const int gh = gact ? t / G : 0, g = t % G;
+        const uint32_t gs = blockIdx.x * H + gh;
+        for (uint32_t rr = 0; rr * G < 101; ++rr) {
+            const uint32_t a = rr * G + g;
+            RectModel m = default_model();
+            bool ok = false;
+            if (gact && gs < nh && a < 101 && gen_a[gh] == 127)
+                ok = (gen.probe & 8u) ? a == 0 : attempt<KIND>(p, gen.seed, gen.slot0 + gs, a, m);
+            if (ok) atomicMin(&gen_a[gh], (int)a);
+            __syncthreads();
+            if (ok && gen_a[gh] == (int)a) gen_m[gh] = m;
+            bool all = true;
+            for (int q = 0; q < H; ++q) all = all && (gen_a[q] != 127 || blockIdx.x * H + q >= nh);
+            __syncthreads();
+            if (all) break;
+        }
+        if (t < H && blockIdx.x * H + t < nh) {
+            const int a = gen_a[t];
+            gen.inc[blockIdx.x * H + t] = (uint8_t)(a == 127 ? 102 : a + 1);
+            gen.models[blockIdx.x * H + t] = a == 127 ? default_model() : gen_m[t];
+        }
+    }
+    if (t < H) {
+        const uint32_t hg = blockIdx.x * H + t;
+        const bool v = hg < nh && (kGen ? gen_a[t] != 127 : (inc == nullptr || inc[hg] <= 101));
+        typename ModelOf<KIND>::type m = ModelOf<KIND>::def();
+        if (v) {
+            if constexpr (kGen && KIND < 3) m = gen_m[t];
+            else m = models[hg];
+        }
+        hyp[t] = make_hyp<KIND>(m, band0);
+        hval[t] = v ? 1u : 0u;
+        cnt_sh[0][t] = 0;
+        cnt_sh[1][t] = 0;
+    }
+    GCR_STAMP(6, 15u);
+    if (t < kFmWaves) { ready[t] = 0; done[t] = 0; }
+    __syncthreads();
+    GCR_STAMP(7, 15u);
+
+    const uint32_t n0 = p.cls[0].n;
+    const uint32_t n1 = (KIND == 2) ? p.cls[1].n : 0;
+    const uint32_t r0 = (n0 + kFmRound - 1) / kFmRound;
+    const uint32_t rounds = r0 + (n1 + kFmRound - 1) / kFmRound;
+
+    if (!chain_wave) {
+        // ---------------------------------------------------- compute waves
+        uint64_t vmask = __ballot(lane < H && hval[lane < H ? lane : 0] != 0);
+        if (gen.probe & 4u) vmask = 0;
+        uint16_t* qw = queue[wave];
+        // this lane's feature of round rr (x, y, s | x2 | cos, - | y2 | sin)
+        auto load = [&](uint32_t rr, double* f, bool& ok) {
+            const int cls = rr < r0 ? 0 : 1;
+            const DevClass& c = p.cls[cls];
+            const uint32_t i = (cls == 0 ? rr : rr - r0) * kFmRound + wave * 64 + lane;
+            ok = i < c.n;
+            const uint32_t ic = ok ? i : 0u;
+            f[0] = c.x[ic];
+            f[1] = c.y[ic];
+            if (cls == 0) {
+                f[2] = c.a[ic];
+                f[3] = (KIND == 3) ? c.c0[ic] : 0.0;
+            } else {
+                f[2] = c.c0[ic];
+                f[3] = c.c1[ic];
+            }
+        };
+        double nxt[4];
+        bool nok = false;
+        if (rounds > 0) load(0, nxt, nok);
+        for (uint32_t r = 0; r < rounds; ++r) {
+            GCR_STAMP(0, r);
+            const double f0 = nxt[0], f1 = nxt[1], f2 = nxt[2], f3 = nxt[3];
+            const bool ok = nok;
+            if (r + 1 < rounds) load(r + 1, nxt, nok);
+            const int cls = r < r0 ? 0 : 1;
+            // 1) band test against each hypothesis.  Each lane holds one
+            //    feature, so q's survivors are one ballot: survivor k of q (in
+            //    feature order) owns slot k of the region outv[wave][q], and
+            //    the queue entry q | lane << 4 | k << 10 carries all of it
+            uint32_t qn = 0, my_n = 0;
+            uint32_t* wc = wcnt[r & 1][wave];
+            if (__ballot(ok) != 0) {
+#pragma unroll 4
+                for (int q = 0; q < H; ++q) {
+                    if (!((vmask >> q) & 1ull)) continue;
+                    const HypConst& hq = hyp[q];
+                    bool cand = false;
+                    if (ok) {
+                        if constexpr (KIND == 3) cand = h_band(f0, f1, f2, f3, hq.g, band0);
+                        else if (cls == 0) cand = scale_band<KIND>(f0, f1, f2, hq);
+                        else if constexpr (KIND == 2) cand = orient_band(f0, f1, f2, f3, hq, tan_tau1);
+                    }
+                    const uint64_t m = __ballot(cand);
+                    const uint32_t k =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (cand) qw[qn + k] = (uint16_t)(q | (lane << 4) | (k << 10));
+                    const uint32_t c = (uint32_t)__builtin_popcountll(m);
+                    if (lane == q) my_n = c;
+                    qn += c;
+                }
+            }
+            if (gen.probe & 2u) qn = my_n = 0;
+            if (lane < H) wc[lane] = my_n;                 // survivors (run length) of (wave, q)
+            GCR_STAMP(1, r);
+            // 2) the chain has folded this wave's previous runs (outv reuse)
+            if (r > 0) fm_wait_ge(&done[wave], r);
+            GCR_STAMP(2, r);
+            // 3) exact residuals of the survivors, all 64 lanes busy: -r^2 for
+            //    an inlier, +0.0 (an exact no-op of the sum) otherwise
+            double* ow = reinterpret_cast<double*>(&outv[wave][0][0]);
+            for (uint32_t j0 = 0; j0 < qn; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                const bool v = j < qn;
+                const uint32_t e = v ? qw[j] : 0u;
+                const int q = (int)(e & 15u);
+                const int src = (int)((e >> 4) & 63u);
+                const uint32_t k = e >> 10;
+                double x, y, a2, a3 = 0.0;
+                if (gen.probe & 32u) {
+                    // the survivor's feature from its owner lane (LDS permute)
+                    x = __shfl(f0, src);
+                    y = __shfl(f1, src);
+                    a2 = __shfl(f2, src);
+                    if (KIND == 3 || cls == 1) a3 = __shfl(f3, src);
+                } else {
+                    // ... or re-read from L2 (keeps the LDS pipe to the chain)
+                    const DevClass& c = p.cls[cls];
+                    const uint32_t fi = (cls == 0 ? r : r - r0) * kFmRound + wave * 64 + src;
+                    x = c.x[fi];
+                    y = c.y[fi];
+                    a2 = cls == 0 ? c.a[fi] : c.c0[fi];
+                    if (KIND == 3) a3 = c.c0[fi];
+                    else if (cls == 1) a3 = c.c1[fi];
+                }
+                if (v) {
+                    const HypConst& hq = hyp[q];
+                    double r2;
+                    bool inl;
+                    if constexpr (KIND == 3) {
+                        r2 = h_sq_residual(x, y, a2, a3, hq.g);
+                        inl = r2 <= T0;
+                    } else {
+                        RectModel m = default_model();
+                        m.h7 = hq.h7;
+                        m.h8 = hq.h8;
+                        if (cls == 0) {
+                            r2 = scale_sq_residual<KIND == 1, true>(x, y, a2, m, hq.ac);
+                            inl = r2 <= T0;
+                        } else {
+                            const OrientConst oc{hq.cphi, hq.cphi2};
+                            r2 = orient_sq_residual<true>(x, y, a2, a3, m, oc);
+                            inl = r2 <= T1;
+                        }
+                    }
+                    ow[q * kReg + k] = inl ? -r2 : 0.0;
+                    if (inl) atomicAdd(&cnt_sh[cls][q], 1u);
+                }
+            }
+            GCR_STAMP(3, r);
+            GCR_STAMP_VAL(6, r, (uint64_t)qn);
+            // 4) zero-pad each run to a whole chain batch
+            {
+                const int q = lane % H, part = lane / H;
+                const uint32_t n = wc[q];
+                const uint32_t end = (n + 2 * kFmCB - 1) & ~(uint32_t)(2 * kFmCB - 1);
+#pragma unroll
+                for (int i = 0; i < 2 * kFmCB * H / 64; ++i) {
+                    const uint32_t s = n + part + i * (64 / H);
+                    if (s < end) ow[q * kReg + s] = 0.0;
+                }
+            }
+            fm_publish(&ready[wave], r + 1);
+            GCR_STAMP(4, r);
+        }
+    } else {
+        // ------------------------------------------------------- chain wave
+        __builtin_amdgcn_s_setprio(3);
+        // lanes [0, H): class sums; lanes [H, 2H) (KIND 2): the running total
+        constexpr bool kTot = KIND == 2;
+        const int h = lane % H;
+        const int role = kTot ? lane / H : 0;
+        const bool chain_lane = lane < (kTot ? 2 * H : H);
+        double run = 0.0, hold = 0.0;
+        uint32_t c0 = 0, c1 = 0;
+        const bool fold_on = !(gen.probe & 1u) && chain_lane;
+        for (uint32_t r = 0; r < rounds; ++r) {
+            if (KIND == 2 && r == r0 && role == 0) {      // first orientation round
+                hold = run;
+                run = 0.0;
+            }
+            GCR_STAMP(0, r);
+            // waves that have published round r (bit w), polled all at once
+            auto poll = [&]() -> uint64_t {
+                const uint32_t f = lane < kFmWaves
+                                       ? __hip_atomic_load(&ready[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
+                                       : 0u;
+                return __ballot(lane < kFmWaves && f >= r + 1);
+            };
+            uint64_t rmask = poll();
+            uint32_t n = 0;
+            bool have = false;
+#pragma unroll 1
+            for (int w = 0; w < kFmWaves; ++w) {
+                while (!((rmask >> w) & 1ull)) {
+                    __builtin_amdgcn_s_sleep(1);
+                    rmask = poll();
+                }
+                if (!have) n = wcnt[r & 1][w][h];
+                // the next run's length, read ahead if that wave has published
+                const bool nhave = w + 1 < kFmWaves && ((rmask >> (w + 1)) & 1ull);
+                const uint32_t nn = nhave ? wcnt[r & 1][w + 1][h] : 0u;
+                if (fold_on) {
+                    // whole batches of kFmCB 16-byte reads (zero-padded runs),
+                    // all in flight before their adds (a software-pipelined
+                    // variant, the next batch in flight during the adds,
+                    // measured slower: 175 vs 128 us)
+                    const double2* reg = outv[w][h];
+                    for (uint32_t j = 0; j < n; j += 2 * kFmCB) {
+                        double2 v[kFmCB];
+#pragma unroll
+                        for (int u = 0; u < kFmCB; ++u) v[u] = reg[j / 2 + u];
+#pragma unroll
+                        for (int u = 0; u < kFmCB; ++u) {
+                            run += v[u].x;
+                            run += v[u].y;
+                        }
+                    }
+                }
+                // this wave's region is consumed (the adds used every read)
+                __hip_atomic_store(&done[w], r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                n = nn;
+                have = nhave;
+            }
+            GCR_STAMP(4, r);
+        }
+        const uint32_t hg = blockIdx.x * H + h;
+        const bool valid_h = hval[h] != 0;
+        // inlier counts: every compute wave's last atomics precede its final
+        // publication, which the loop above has acquired
+        c0 = cnt_sh[0][h];
+        c1 = cnt_sh[1][h];
+        double tot = run;
+        if constexpr (kTot) tot = __shfl(run, (lane + H) & 63);
+        if (lane < H && hg < nh) {
+            const double acc0 = KIND == 2 ? hold : run;
+            const double acc1 = KIND == 2 ? run : 0.0;
+            const uint32_t k0 = valid_h ? c0 : 0, k1 = valid_h ? c1 : 0;
+            out.n0[hg] = k0;
+            out.n1[hg] = k1;
+            out.v0[hg] = valid_h ? acc0 : 0.0;
+            out.v1[hg] = valid_h ? acc1 : 0.0;
+            out.tot[hg] = valid_h ? tot : 0.0;
+            if constexpr (kGen) {
+                // MSACScoringFunction::getScore finish (MSAC_scoring_function.hpp:108-127)
+                double sum = 0.0;
+                if (valid_h && k0 >= gen.m0 && (KIND != 2 || k1 >= gen.m1)) {
+                    sum = tot;
+                    const double ms0 = acc0 / T0 + static_cast<double>(k0);
+                    sum -= acc0;
+                    sum += ms0;
+                    if (KIND == 2) {
+                        const double ms1 = acc1 / T1 + static_cast<double>(k1);
+                        sum -= acc1;
+                        sum += ms1;
+                    }
+                }
                 const bool cand = valid_h && sum > 0.0 && (KIND != 2 || valid_model_sift22(gen_m[h]));
                 fin_sh[h] = cand ? sum : -1.0;
             }
@@ -1113,6 +1548,29 @@ void launch_split_t(const DevProblem& p, const double T[2], const RectModel* mod
     }
 }
 
+// GCR_SCORER=split selects the round-synchronous split scorer (k_score_split)
+// instead of the feature-major one (k_score_fm) for the band estimators
+bool use_fm() {
+    static const bool fm = [] {
+        const char* e = getenv("GCR_SCORER");
+        return !(e && e[0] == 's');
+    }();
+    return fm;
+}
+
+template <int H, bool kGen>
+void launch_fm_t(const DevProblem& p, const double T[2], uint32_t nh, const ScoreOut& out, const GenArgs& g,
+                 hipStream_t stream, const RectModel* models = nullptr, const uint8_t* inc = nullptr) {
+    const dim3 grid((nh + H - 1) / H), block(kSplitThreads);
+    double band0, tan_tau1;
+    band_consts(T, band0, tan_tau1);
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL((k_score_fm<0, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, g); break;
+        case 1: hipLaunchKernelGGL((k_score_fm<1, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, g); break;
+        default: hipLaunchKernelGGL((k_score_fm<2, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, g); break;
+    }
+}
+
 int score_mode() {
     static const int mode = [] {          // thread-safe one-time init (gcr_solve_batch threads)
         const char* e = getenv("GCR_SCORE_KERNEL");
@@ -1149,6 +1607,7 @@ hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel*
     else {
         const int h = split_h(nh);
         if (h == 64) launch_split_t<64, 120>(p, T, models, inc, nh, out, stream);
+        else if (h == 16 && use_fm()) launch_fm_t<16, false>(p, T, nh, out, GenArgs{}, stream, models, inc);
         else if (h == 16) launch_split_t<16, 420>(p, T, models, inc, nh, out, stream);
         else launch_split_t<4, 960>(p, T, models, inc, nh, out, stream);
     }
@@ -1218,9 +1677,27 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
     const int h = split_h(nslots);
     const uint32_t nwg = (nslots + h - 1) / h;
     if (nwg > wg_cap) return hipErrorInvalidValue;
-    const GenArgs g{seed, slot0, inc, models, wg, m[0], m[1]};
+    GenArgs g{seed, slot0, inc, models, wg, m[0], m[1]};
+    // GCR_GEN_LANES pins the prologue's lanes per slot (sweeps); must be a
+    // power of two dividing 1024 / H
+    static const uint32_t glanes = [] {
+        const char* e = getenv("GCR_GEN_LANES");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    static const uint32_t probe = [] {
+        const char* e = getenv("GCR_PROBE");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    g.probe = probe;
+    // default 16 lanes per slot (one wave per SIMD at H = 16): 16 parallel
+    // attempts resolve nearly every slot in one round, and fewer contending
+    // waves finish it sooner (sweep at 4096 slots: 64 -> 16 lanes, 142 ->
+    // 134.5 us per fused launch)
+    const uint32_t gl = glanes ? glanes : 16u;
+    g.glanes = ((1024u / h) % gl == 0 && (gl & (gl - 1)) == 0) ? gl : 0u;
     if (ev0) (void)hipEventRecord(ev0, stream);
-    if (h == 64) launch_fused_t<64, 120>(p, T, nslots, out, g, stream);
+    if (h == 16 && use_fm()) launch_fm_t<16, true>(p, T, nslots, out, g, stream);
+    else if (h == 64) launch_fused_t<64, 120>(p, T, nslots, out, g, stream);
     else if (h == 16) launch_fused_t<16, 420>(p, T, nslots, out, g, stream);
     else launch_fused_t<4, 960>(p, T, nslots, out, g, stream);
     if (ev1) (void)hipEventRecord(ev1, stream);
@@ -1332,3 +1809,10 @@ hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_
 }
 
 }  // namespace gcr
+
+#ifdef GCR_STAMPS
+extern "C" int gcr_debug_stamps(uint64_t* host, size_t bytes) {
+    const size_t n = bytes < sizeof(gcr::g_stamps) ? bytes : sizeof(gcr::g_stamps);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gcr::g_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
+#endif

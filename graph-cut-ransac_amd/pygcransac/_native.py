@@ -11,7 +11,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgcr.so")
+# GCR_LIB selects an alternative in-tree build of the same engine (the
+# diagnostic libgcr_stamps.so of tools/stamp_probe.py)
+LIB_PATH = os.path.join(_HERE, os.environ.get("GCR_LIB", "libgcr.so"))
 
 GCR_OK = 0
 GCR_EINVAL = -22

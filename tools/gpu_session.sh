@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python __graft_entry__.py ;;
-    tests) run tests 1200 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} ;;
+    tests) run tests ${TESTS_TO:-1200} python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     sweep) i=0; while IFS= read -r line; do [ -z "$line" ] && continue; i=$((i+1));
              run "sweep$i" 300 env $line ; done < "${SWEEP_FILE:-tools/sweep.txt}" ;;
