@@ -46,6 +46,10 @@ def score_kernel_name(kind, slots):
         h = 64 if slots >= 16384 else 16 if slots >= 2048 else 4
     # the homography path generates in k_generate<3, G> and scores unfused
     fused = "false" if kind >= 3 else "true"
+    # H = 16 rectification launches use the feature-major scorer unless
+    # GCR_SCORER=split (kernels.hip use_fm)
+    if h == 16 and kind < 3 and not os.environ.get("GCR_SCORER", "").startswith("s"):
+        return f"k_score_fm<{kind}, 16, {fused}>"
     return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, {fused}>"
 
 
