@@ -48,7 +48,7 @@ def score_kernel_name(kind, slots):
     fused = "false" if kind >= 3 else "true"
     # H = 16 rectification launches use the feature-major scorer unless
     # GCR_SCORER=split (kernels.hip use_fm)
-    if h == 16 and kind < 3 and not os.environ.get("GCR_SCORER", "").startswith("s"):
+    if h == 16 and kind <= 3 and not os.environ.get("GCR_SCORER", "").startswith("s"):
         return f"k_score_fm<{kind}, 16, {fused}>"
     return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, {fused}>"
 

@@ -1777,8 +1777,16 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
         else if (h == 16) go(ktag, std::integral_constant<int, 16>{}, std::integral_constant<int, 420>{});
         else go(ktag, std::integral_constant<int, 4>{}, std::integral_constant<int, 960>{});
     };
-    if (p.solver == 4) by_h(std::integral_constant<int, 4>{});
-    else by_h(std::integral_constant<int, 3>{});
+    if (p.solver == 4) {
+        by_h(std::integral_constant<int, 4>{});
+    } else if (split_h(nh) == 16 && use_fm() && hmap == nullptr) {
+        // homography: the feature-major scorer with the h_band prefilter
+        const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;
+        hipLaunchKernelGGL((k_score_fm<3, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), 0, stream, p, T,
+                           0.0, sb * sb, 0.0, models, inc, nh, out, ga);
+    } else {
+        by_h(std::integral_constant<int, 3>{});
+    }
     return hipGetLastError();
 }
 
