@@ -109,18 +109,44 @@ struct PinBuf {
     ~PinBuf() { if (p) (void)hipHostFree(p); }
 };
 
-// Score arrays for `cap` hypotheses, device and pinned host mirrors.
+template <class T>
+struct Ptr {
+    T* p = nullptr;
+};
+
+// Score arrays for `cap` hypotheses, device and pinned host mirrors, each set
+// in one allocation laid out n0 | n1 | v0 | v1 | tot (capacity-sized fields),
+// so that a small batch comes back in one copy instead of five (every copy
+// is a ~5 us blit on the stream).
 struct ScoreBufs {
-    DevBuf<uint32_t> n0, n1;
-    DevBuf<double> v0, v1, tot;
-    PinBuf<uint32_t> hn0, hn1;
-    PinBuf<double> hv0, hv1, htot;
+    DevBuf<double> dblk;
+    PinBuf<double> hblk;
+    size_t cap = 0;
+    Ptr<uint32_t> n0, n1, hn0, hn1;
+    Ptr<double> v0, v1, tot, hv0, hv1, htot;
     void ensure(size_t n) {
-        n0.ensure(n); n1.ensure(n); v0.ensure(n); v1.ensure(n); tot.ensure(n);
-        hn0.ensure(n); hn1.ensure(n); hv0.ensure(n); hv1.ensure(n); htot.ensure(n);
+        if (n <= cap) return;
+        dblk.ensure(4 * n);
+        hblk.ensure(4 * n);
+        cap = n;
+        auto carve = [n](double* b, Ptr<uint32_t>& a0, Ptr<uint32_t>& a1, Ptr<double>& b0, Ptr<double>& b1,
+                         Ptr<double>& b2) {
+            a0.p = reinterpret_cast<uint32_t*>(b);
+            a1.p = a0.p + n;
+            b0.p = b + n;
+            b1.p = b + 2 * n;
+            b2.p = b + 3 * n;
+        };
+        carve(dblk.p, n0, n1, v0, v1, tot);
+        carve(hblk.p, hn0, hn1, hv0, hv1, htot);
     }
     ScoreOut dev() const { return ScoreOut{n0.p, n1.p, v0.p, v1.p, tot.p}; }
     void d2h(size_t n, hipStream_t s) {
+        const size_t span = (3 * cap + n) * sizeof(double);    // n0 .. tot[n)
+        if (span <= (size_t)256 * 1024 || 2 * n >= cap) {
+            HIPC(hipMemcpyAsync(hblk.p, dblk.p, span, hipMemcpyDeviceToHost, s));
+            return;
+        }
         HIPC(hipMemcpyAsync(hn0.p, n0.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         HIPC(hipMemcpyAsync(hn1.p, n1.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         HIPC(hipMemcpyAsync(hv0.p, v0.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -164,13 +190,15 @@ struct Workspace {
     ScoreBufs lo_sb;
     DevBuf<uint8_t> mask[2];
     PinBuf<uint8_t> h_mask[2];
+    DevBuf<uint8_t> mask_all;           // inlier_lists: both classes, one copy back
+    PinBuf<uint8_t> h_mask_all;
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
     DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
     DevBuf<double> rf_part;             // GPU refit: reduction block partials
     PinBuf<double> rf_hpart;
-    PinBuf<double> rf_htop;             // GPU refit: top-row mirror + async upload ring
+    PinBuf<double> rf_htop;             // GPU refit: async upload ring
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
@@ -216,25 +244,27 @@ struct DevQRStore {
     bool valid[4][kTop] = {};
     int ring_used = 0;
 
-    double* top() { return P->w->rf_htop.p; }             // 4 x kTop staging
-    double* ring() { return P->w->rf_htop.p + 4 * kTop; }
-    void prepare() { P->w->rf_htop.ensure(4 * kTop + kRing); }
+    double* ring() { return P->w->rf_htop.p; }            // async upload ring
+    void prepare() { P->w->rf_htop.ensure(kRing); }
 
-    // queue the copies of rows 0..kTop-1 of every column (complete after the
-    // caller's next stream synchronisation)
-    void enqueue_top() {
-        const size_t n = std::min<size_t>(kTop, m);
-        for (int c = 0; c < 4; ++c)
-            HIPC(hipMemcpyAsync(top() + c * kTop, col[c], n * sizeof(double), hipMemcpyDeviceToHost, s));
+    // gather rows 0..kTop-1 of every column to rf_part[off .. off + 4 kTop) on
+    // the device and queue ONE copy of rf_part[0 .. off + 4 kTop) back
+    // (complete after the caller's next stream synchronisation)
+    void enqueue_with_top(size_t off) {
+        P->w->rf_part.ensure(off + 4 * kTop);
+        P->w->rf_hpart.ensure(off + 4 * kTop);
+        HIPC(launch_qr_top(col[0], col[1], col[2], col[3], m, P->w->rf_part.p + off, s));
+        HIPC(hipMemcpyAsync(P->w->rf_hpart.p, P->w->rf_part.p, (off + 4 * kTop) * sizeof(double),
+                            hipMemcpyDeviceToHost, s));
     }
-    void sync_and_take_top() {
+    void sync_and_take_top(size_t off) {
         HIPC(hipStreamSynchronize(s));
         ring_used = 0;                                    // every queued upload has completed
         const size_t n = std::min<size_t>(kTop, m);
         for (int c = 0; c < 4; ++c)
             for (size_t i = 0; i < (size_t)kTop; ++i) {
                 valid[c][i] = i < n;
-                if (i < n) cache[c][i] = top()[c * kTop + i];
+                if (i < n) cache[c][i] = P->w->rf_hpart.p[off + c * kTop + i];
             }
     }
     void invalidate(int c, size_t lo, size_t hi) {
@@ -244,12 +274,11 @@ struct DevQRStore {
     double dot(int a, int c, size_t lo, size_t hi) {
         if (hi <= lo) return 0.0;
         size_t nb = (hi - 1) / kSumBlock - lo / kSumBlock + 1;
-        P->w->rf_part.ensure(nb);
-        P->w->rf_hpart.ensure(nb);
+        P->w->rf_part.ensure(nb + 4 * kTop);
+        P->w->rf_hpart.ensure(nb + 4 * kTop);
         HIPC(launch_qr_partials(col[a], col[c], lo, hi, P->w->rf_part.p, &nb, s));
-        HIPC(hipMemcpyAsync(P->w->rf_hpart.p, P->w->rf_part.p, nb * sizeof(double), hipMemcpyDeviceToHost, s));
-        enqueue_top();
-        sync_and_take_top();
+        enqueue_with_top(nb);
+        sync_and_take_top(nb);
         double total = 0.0;
         for (size_t b = 0; b < nb; ++b) total += P->w->rf_hpart.p[b];
         return total;
@@ -258,8 +287,8 @@ struct DevQRStore {
     double get(int c, size_t i) {
         if (i < (size_t)kTop && valid[c][i]) return cache[c][i];
         if (i < (size_t)kTop) {
-            enqueue_top();
-            sync_and_take_top();
+            enqueue_with_top(0);
+            sync_and_take_top(0);
             return cache[c][i];
         }
         HIPC(hipMemcpyAsync(P->w->rf_hpart.p, col[c] + i, sizeof(double), hipMemcpyDeviceToHost, s));
@@ -1021,18 +1050,19 @@ private:
     // Inlier index lists of one model: rule 0 with thresholds T, or (1-class
     // LO) the graph-cut labeling (rule 2).
     void inlier_lists(const Model& model, const double T[2], int rule, std::vector<uint32_t> lists[2]) {
-        for (int c = 0; c < K_; ++c) {
-            P_->w->mask[c].ensure(N_[c]);
-            P_->w->h_mask[c].ensure(N_[c]);
-            HIPC(Tr::mask(P_, c, model, rule, T[c], prm_.spatial_coherence_weight, P_->w->mask[c].p, s_));
-            HIPC(hipMemcpyAsync(P_->w->h_mask[c].p, P_->w->mask[c].p, N_[c], hipMemcpyDeviceToHost, s_));
-        }
+        const size_t tot = N_[0] + (K_ == 2 ? N_[1] : 0);
+        P_->w->mask_all.ensure(tot);
+        P_->w->h_mask_all.ensure(tot);
+        for (int c = 0; c < K_; ++c)
+            HIPC(Tr::mask(P_, c, model, rule, T[c], prm_.spatial_coherence_weight,
+                          P_->w->mask_all.p + (c ? N_[0] : 0), s_));
+        HIPC(hipMemcpyAsync(P_->w->h_mask_all.p, P_->w->mask_all.p, tot, hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
         st_.launches += K_;
         for (int c = 0; c < 2; ++c) {
             lists[c].clear();
             if (c >= K_) continue;
-            const uint8_t* mk = P_->w->h_mask[c].p;
+            const uint8_t* mk = P_->w->h_mask_all.p + (c ? N_[0] : 0);
             for (uint64_t i = 0; i < N_[c]; ++i)
                 if (mk[i]) lists[c].push_back((uint32_t)i);
         }

@@ -102,6 +102,9 @@ hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32
 // partials[0 .. nblocks) in block order.  Returns the block count via nblocks.
 hipError_t launch_qr_partials(const double* a, const double* c, size_t lo, size_t hi, double* partials,
                               size_t* nblocks, hipStream_t stream);
+// rows 0..2 of the four columns into out[c * 3 + i] (0 past m)
+hipError_t launch_qr_top(const double* c0, const double* c1, const double* c2, const double* c3, size_t m,
+                         double* out, hipStream_t stream);
 // element-wise updates on [lo, hi): c = c / den; c = 0; c -= (tau * e) * t
 hipError_t launch_qr_scale(double* c, size_t lo, size_t hi, double den, hipStream_t stream);
 hipError_t launch_qr_zero(double* c, size_t lo, size_t hi, hipStream_t stream);

@@ -1379,6 +1379,17 @@ __global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* _
     }
 }
 
+// rows 0..2 of the four columns (the only rows the QR driver reads on the
+// host) into out[c * 3 + i]
+__global__ void k_qr_top(const double* c0, const double* c1, const double* c2, const double* c3, uint64_t m,
+                         double* out) {
+    const int t = threadIdx.x;
+    if (t >= 12) return;
+    const int c = t / 3, i = t % 3;
+    const double* col = c == 0 ? c0 : c == 1 ? c1 : c == 2 ? c2 : c3;
+    out[t] = (uint64_t)i < m ? col[i] : 0.0;
+}
+
 __global__ void k_qr_scale(double* c, uint64_t lo, uint64_t hi, double den) {
     const uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < hi) c[i] = c[i] / den;
@@ -1631,6 +1642,12 @@ hipError_t launch_qr_partials(const double* a, const double* c, size_t lo, size_
     *nblocks = nblk;
     hipLaunchKernelGGL(k_qr_partials, dim3((unsigned)((nblk + kPartWaves - 1) / kPartWaves)), dim3(64 * kPartWaves),
                        0, stream, a, c, (uint64_t)lo, (uint64_t)hi, blk0, nblk, partials);
+    return hipGetLastError();
+}
+
+hipError_t launch_qr_top(const double* c0, const double* c1, const double* c2, const double* c3, size_t m,
+                         double* out, hipStream_t stream) {
+    hipLaunchKernelGGL(k_qr_top, dim3(1), dim3(64), 0, stream, c0, c1, c2, c3, (uint64_t)m, out);
     return hipGetLastError();
 }
 
