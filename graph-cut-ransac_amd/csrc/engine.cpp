@@ -191,6 +191,8 @@ struct Workspace {
     DevBuf<uint8_t> mask[2];
     PinBuf<uint8_t> h_mask[2];
     DevBuf<uint8_t> mask_all;           // inlier_lists: both classes, one copy back
+    DevBuf<double> sm_vals;             // launch_score_small: pair values
+    DevBuf<uint64_t> sm_bits;           // launch_score_small: inlier bitmasks
     PinBuf<uint8_t> h_mask_all;
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
@@ -436,6 +438,17 @@ HostPool& host_pool() {
         return (unsigned)std::max(1L, std::min(64L, n));
     }());
     return pool;
+}
+
+// LO trials, refits and reconciliations of at most kSmallScore models use
+// launch_score_small; GCR_SMALL_SCORE=0 routes them through the batch scorers
+constexpr uint32_t kSmallScore = 256;
+bool small_score_on() {
+    static const bool on = [] {
+        const char* e = getenv("GCR_SMALL_SCORE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // verify_batches records kernel-timing events on every n-th batch
@@ -1035,7 +1048,17 @@ private:
         bool identity = true;
         for (uint32_t i = 0; i < n; ++i) identity = identity && Tr::identity(models[i]);
         HIPC(hipMemcpyAsync(lm.p, models, n * sizeof(Model), hipMemcpyHostToDevice, s_));
-        HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
+        if (identity && n <= kSmallScore && small_score_on()) {
+            // a few models: all pairs in parallel, then one wave per model
+            // adds its inliers in order (no ~90 us batch-scorer chain)
+            const size_t pairs = small_score_pairs(P_->dp);
+            P_->w->sm_vals.ensure(pairs * n);
+            P_->w->sm_bits.ensure(pairs * n / 64);
+            HIPC(launch_score_small(P_->dp, Tm_, lm.p, n, P_->w->lo_sb.dev(), P_->w->sm_vals.p, P_->w->sm_bits.p,
+                                    s_));
+        } else {
+            HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
+        }
         P_->w->lo_sb.d2h(n, s_);
         HIPC(hipStreamSynchronize(s_));
         st_.launches += 1;

@@ -1160,6 +1160,121 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
     }
 }
 
+
+// ------------------------------------------------- small-batch scoring ----
+// LO trials, refits and reconciliations score a handful of models, so the
+// per-workgroup sequential chain of the batch scorers (~90 us at N = 10 000)
+// is the whole cost.  Here every (model, feature) pair is evaluated in
+// parallel (k_lo_values: -r^2 or +0.0 per pair plus an inlier bitmask, in
+// HBM), and one wave per model then adds the inlier values in feature order
+// from LDS (k_lo_chain), so the dependent chain holds only the inliers and no
+// compute traffic competes with it.  The sums are the reference's sequential
+// sums (MSAC_scoring_function.hpp:73-85): inliers in index order, class 0
+// then class 1, the running total continuing across classes.
+//
+// Layout per model: class 0 at [0, pad0), class 1 at [pad0, pad0 + pad1),
+// pad_c = n_c rounded up to 64 (unused pairs: value 0, bit 0).
+template <int KIND>
+__global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
+                                                  double T0, double T1, uint32_t pad0, uint32_t ntot,
+                                                  double* __restrict__ vals, uint64_t* __restrict__ bits) {
+    const uint32_t mi = blockIdx.y;
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x * 256 >= ntot) return;                // whole block (ntot is a multiple of 64)
+    const int cls = j < pad0 ? 0 : 1;
+    const uint32_t i = cls == 0 ? j : j - pad0;
+    const DevClass& c = p.cls[cls];
+    const auto m = models[mi];
+    double r2 = 0.0;
+    bool inl = false;
+    if (j < ntot && i < c.n) {
+        if constexpr (KIND >= 3) {
+            r2 = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
+        } else if (cls == 0) {
+            r2 = scale_sq_residual<KIND == 1, true>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
+        } else {
+            r2 = orient_sq_residual<true>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
+        }
+        inl = r2 <= (cls == 0 ? T0 : T1);
+    }
+    const uint64_t b = __ballot(inl);
+    if (j < ntot) {
+        vals[(size_t)mi * ntot + j] = inl ? -r2 : 0.0;
+        if ((threadIdx.x & 63) == 0) bits[((size_t)mi * ntot + j) / 64] = b;
+    }
+}
+
+constexpr uint32_t kLoSpan = 1024;      // features compacted into LDS per step
+
+template <int KIND>
+__global__ __launch_bounds__(64) void k_lo_chain(uint32_t n0, uint32_t n1, uint32_t pad0, uint32_t ntot,
+                                                const double* __restrict__ vals, const uint64_t* __restrict__ bits,
+                                                ScoreOut out) {
+    __shared__ double cbuf[kLoSpan];
+    const uint32_t mi = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint64_t below = (1ull << lane) - 1ull;
+    constexpr int K = KIND == 2 ? 2 : 1;
+    // lane 0: the class sum; lane 1 (KIND 2): the running total
+    constexpr int kChains = KIND == 2 ? 2 : 1;
+    double run = 0.0, hold = 0.0;
+    uint32_t cnt[2] = {0, 0};
+    const double* mv = vals + (size_t)mi * ntot;
+    const uint64_t* mb = bits + (size_t)mi * ntot / 64;
+    for (int c = 0; c < K; ++c) {
+        if (c == 1 && lane == 0) {
+            hold = run;
+            run = 0.0;
+        }
+        const uint32_t base = c ? pad0 : 0;
+        const uint32_t len = c ? (ntot - pad0) : pad0;
+        for (uint32_t s0 = 0; s0 < len; s0 += kLoSpan) {
+            const uint32_t nch = min(kLoSpan, len - s0) / 64;
+            // the span's values and bit words, all in flight, then an in-order
+            // compaction of its inlier values into LDS
+            double v[kLoSpan / 64];
+            uint64_t w[kLoSpan / 64];
+#pragma unroll
+            for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
+                const uint32_t q = ch < nch ? ch : 0;
+                v[ch] = mv[base + s0 + q * 64 + lane];
+                w[ch] = mb[(base + s0) / 64 + q];
+            }
+            uint32_t off = 0;
+#pragma unroll
+            for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
+                if (ch < nch) {
+                    if ((w[ch] >> lane) & 1ull) cbuf[off + (uint32_t)__builtin_popcountll(w[ch] & below)] = v[ch];
+                    off += (uint32_t)__builtin_popcountll(w[ch]);
+                }
+            }
+            cnt[c] += off;
+            __builtin_amdgcn_wave_barrier();
+            if (lane < kChains) {
+                // batches of 16 reads in flight, then 16 dependent adds
+                uint32_t k = 0;
+                for (; k + 16 <= off; k += 16) {
+                    double t[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) t[u] = cbuf[k + u];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) run += t[u];
+                }
+                for (; k < off; ++k) run += cbuf[k];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    const double tot = KIND == 2 ? __shfl(run, 1) : run;
+    if (lane == 0) {
+        out.n0[mi] = cnt[0];
+        out.n1[mi] = cnt[1];
+        out.v0[mi] = KIND == 2 ? hold : run;
+        out.v1[mi] = KIND == 2 ? run : 0.0;
+        out.tot[mi] = tot;
+    }
+}
+
 // -------------------------------------------------------------- compact ----
 // Order-preserving list of the live hypotheses (inc <= 101) of a launch: one
 // workgroup, contiguous chunks per thread, exclusive scan in LDS.  Used by the
@@ -1719,6 +1834,39 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
     else launch_fused_t<4, 960>(p, T, nslots, out, g, stream);
     if (ev1) (void)hipEventRecord(ev1, stream);
     hipLaunchKernelGGL(k_select_wg, dim3(1), dim3(kSelectThreads), 0, stream, wg, nwg, models, slot0, rec);
+    return hipGetLastError();
+}
+
+
+size_t small_score_pairs(const DevProblem& p) {
+    const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
+    const uint32_t pad1 = (p.solver == 2) ? ((p.cls[1].n + 63u) & ~63u) : 0u;
+    return (size_t)pad0 + pad1;
+}
+
+hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, uint32_t nm,
+                              const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream) {
+    if (nm == 0) return hipSuccess;
+    const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
+    const uint32_t ntot = (uint32_t)small_score_pairs(p);
+    if (ntot == 0) return hipErrorInvalidValue;
+    const dim3 ga((ntot + 255) / 256, nm), ba(256);
+    const uint32_t n1 = p.solver == 2 ? p.cls[1].n : 0u;
+    auto go = [&](auto ktag) {
+        constexpr int KIND = decltype(ktag)::value;
+        using M = typename ModelOf<KIND>::type;
+        hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), T[0], T[1], pad0,
+                           ntot, vals, bits);
+        hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(64), 0, stream, p.cls[0].n, n1, pad0, ntot, vals, bits,
+                           out);
+    };
+    switch (p.solver) {
+        case 0: go(std::integral_constant<int, 0>{}); break;
+        case 1: go(std::integral_constant<int, 1>{}); break;
+        case 2: go(std::integral_constant<int, 2>{}); break;
+        case 3: go(std::integral_constant<int, 3>{}); break;
+        default: go(std::integral_constant<int, 4>{}); break;
+    }
     return hipGetLastError();
 }
 
