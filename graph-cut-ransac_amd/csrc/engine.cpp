@@ -178,6 +178,7 @@ struct BufferT {             // one of temp_inner_inliers[2]
 // allocating and freeing pinned memory per call costs milliseconds.
 struct Workspace {
     DevBuf<double> feat;                // feature SoA (make_problem)
+    PinBuf<double> feat_stage;          // its pinned host image (one upload)
     DevBuf<uint8_t> inc;
     DevBuf<RectModel> models;
     PinBuf<uint8_t> h_inc;
@@ -549,8 +550,11 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
         P->w = P->own.get();
     }
     P->w->feat.ensure(total);
-    HIPC(hipMemsetAsync(P->w->feat.p, 0, total * sizeof(double), ctx->stream));
-    double* cur = P->w->feat.p;
+    // the whole SoA image (pads zeroed) is staged in pinned memory and goes
+    // up in ONE copy (ten pageable copies cost ~150 us of a one-shot call)
+    P->w->feat_stage.ensure(total);
+    double* hst = P->w->feat_stage.p;
+    size_t off = 0;
     P->dp.solver = solver;
     for (int c = 0; c < 2; ++c) {
         DevClass& d = P->dp.cls[c];
@@ -559,11 +563,13 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
         const std::vector<double>* arrs[5] = {&P->hc[c].x, &P->hc[c].y, &P->hc[c].a, &P->hc[c].c0, &P->hc[c].c1};
         const double** dst[5] = {&d.x, &d.y, &d.a, &d.c0, &d.c1};
         for (int q = 0; q < 5; ++q) {
-            HIPC(hipMemcpyAsync(cur, arrs[q]->data(), ns[c] * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-            *dst[q] = cur;
-            cur += np[c];
+            std::memcpy(hst + off, arrs[q]->data(), ns[c] * sizeof(double));
+            for (size_t i = ns[c]; i < np[c]; ++i) hst[off + i] = 0.0;
+            *dst[q] = P->w->feat.p + off;
+            off += np[c];
         }
     }
+    HIPC(hipMemcpyAsync(P->w->feat.p, hst, total * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
     *out = P.release();
     return GCR_OK;
@@ -1024,7 +1030,17 @@ private:
         const size_t nh = cnt * kP;
         t0 = Clock::now();
         HIPC(hipEventRecord(P_->ctx->ev0, s_));
-        HIPC(Tr::score_live(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(), s_));
+        if (kP == 1 && nh <= kSmallScore && small_score_on()) {
+            // the few slots a short run needs: all pairs in parallel, one
+            // wave per model (the batch scorers' chain would dominate)
+            const size_t pairs = small_score_pairs(P_->dp);
+            P_->w->sm_vals.ensure(pairs * nh);
+            P_->w->sm_bits.ensure(pairs * nh / 64);
+            HIPC(launch_score_small(P_->dp, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(),
+                                    P_->w->sm_vals.p, P_->w->sm_bits.p, s_));
+        } else {
+            HIPC(Tr::score_live(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(), s_));
+        }
         cursor_ = 0;
         HIPC(hipEventRecord(P_->ctx->ev1, s_));
         P_->w->sb.d2h(nh, s_);
@@ -1054,8 +1070,8 @@ private:
             const size_t pairs = small_score_pairs(P_->dp);
             P_->w->sm_vals.ensure(pairs * n);
             P_->w->sm_bits.ensure(pairs * n / 64);
-            HIPC(launch_score_small(P_->dp, Tm_, lm.p, n, P_->w->lo_sb.dev(), P_->w->sm_vals.p, P_->w->sm_bits.p,
-                                    s_));
+            HIPC(launch_score_small(P_->dp, Tm_, lm.p, nullptr, n, P_->w->lo_sb.dev(), P_->w->sm_vals.p,
+                                    P_->w->sm_bits.p, s_));
         } else {
             HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
         }

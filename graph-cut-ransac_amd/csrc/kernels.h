@@ -150,10 +150,11 @@ hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_
 // parallel into vals / bits (small_score_pairs(p) doubles and /64 words per
 // model), then one wave per model adds the inlier values in feature order.
 // Same raw accumulators as launch_score / launch_score_geo.  `models` points
-// to RectModel (solvers 0-2) or GeoModel (3, 4), identity normalisation only.
+// to RectModel (solvers 0-2) or GeoModel (3, 4), identity normalisation only;
+// models with inc > 101 (inc may be null) score zeros.
 size_t small_score_pairs(const DevProblem& p);
-hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, uint32_t nm,
-                              const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream);
+hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
+                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream);
 
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)

@@ -1176,8 +1176,9 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
 // pad_c = n_c rounded up to 64 (unused pairs: value 0, bit 0).
 template <int KIND>
 __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
-                                                  double T0, double T1, uint32_t pad0, uint32_t ntot,
-                                                  double* __restrict__ vals, uint64_t* __restrict__ bits) {
+                                                  const uint8_t* __restrict__ inc, double T0, double T1,
+                                                  uint32_t pad0, uint32_t ntot, double* __restrict__ vals,
+                                                  uint64_t* __restrict__ bits) {
     const uint32_t mi = blockIdx.y;
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (blockIdx.x * 256 >= ntot) return;                // whole block (ntot is a multiple of 64)
@@ -1185,9 +1186,10 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
     const uint32_t i = cls == 0 ? j : j - pad0;
     const DevClass& c = p.cls[cls];
     const auto m = models[mi];
+    const bool live = inc == nullptr || inc[mi] <= 101;   // a slot without a model scores zeros
     double r2 = 0.0;
     bool inl = false;
-    if (j < ntot && i < c.n) {
+    if (live && j < ntot && i < c.n) {
         if constexpr (KIND >= 3) {
             r2 = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
         } else if (cls == 0) {
@@ -1844,8 +1846,8 @@ size_t small_score_pairs(const DevProblem& p) {
     return (size_t)pad0 + pad1;
 }
 
-hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, uint32_t nm,
-                              const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream) {
+hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
+                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream) {
     if (nm == 0) return hipSuccess;
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t ntot = (uint32_t)small_score_pairs(p);
@@ -1855,8 +1857,8 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
     auto go = [&](auto ktag) {
         constexpr int KIND = decltype(ktag)::value;
         using M = typename ModelOf<KIND>::type;
-        hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), T[0], T[1], pad0,
-                           ntot, vals, bits);
+        hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), inc, T[0], T[1],
+                           pad0, ntot, vals, bits);
         hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(64), 0, stream, p.cls[0].n, n1, pad0, ntot, vals, bits,
                            out);
     };
