@@ -452,6 +452,13 @@ bool small_score_on() {
     return on;
 }
 
+// gcr_debug_score[_h]: GCR_DEBUG_SCORER=small scores through
+// launch_score_small (read per call, so tests can compare both paths)
+bool debug_small_scorer(uint32_t n) {
+    const char* e = getenv("GCR_DEBUG_SCORER");
+    return e && e[0] == 's' && n > 0 && n <= kSmallScore;
+}
+
 // verify_batches records kernel-timing events on every n-th batch
 // (GCR_TIMING_STRIDE, default 1 = every batch)
 uint32_t timing_stride() {
@@ -1500,7 +1507,16 @@ int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double*
         prob->w->lo_gmodels.ensure(nmodels);
         prob->w->lo_sb.ensure(nmodels);
         HIPC(hipMemcpyAsync(prob->w->lo_gmodels.p, H, nmodels * sizeof(GeoModel), hipMemcpyHostToDevice, s));
-        HIPC(launch_score_geo(prob->dp, T, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(), s));
+        if (debug_small_scorer(nmodels)) {
+            const double Tt[2] = {T, 0.0};
+            const size_t pairs = small_score_pairs(prob->dp);
+            prob->w->sm_vals.ensure(pairs * nmodels);
+            prob->w->sm_bits.ensure(pairs * nmodels / 64);
+            HIPC(launch_score_small(prob->dp, Tt, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(),
+                                    prob->w->sm_vals.p, prob->w->sm_bits.p, s));
+        } else {
+            HIPC(launch_score_geo(prob->dp, T, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(), s));
+        }
         prob->w->lo_sb.d2h(nmodels, s);
         HIPC(hipStreamSynchronize(s));
         std::memcpy(n0, prob->w->lo_sb.hn0.p, nmodels * sizeof(uint32_t));
@@ -1584,7 +1600,15 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
         prob->w->lo_models.ensure(nmodels);
         prob->w->lo_sb.ensure(nmodels);
         HIPC(hipMemcpyAsync(prob->w->lo_models.p, hm.data(), nmodels * sizeof(RectModel), hipMemcpyHostToDevice, s));
-        HIPC(launch_score(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, identity, prob->w->lo_sb.dev(), s));
+        if (identity && debug_small_scorer(nmodels)) {
+            const size_t pairs = small_score_pairs(prob->dp);
+            prob->w->sm_vals.ensure(pairs * nmodels);
+            prob->w->sm_bits.ensure(pairs * nmodels / 64);
+            HIPC(launch_score_small(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, prob->w->lo_sb.dev(),
+                                    prob->w->sm_vals.p, prob->w->sm_bits.p, s));
+        } else {
+            HIPC(launch_score(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, identity, prob->w->lo_sb.dev(), s));
+        }
         prob->w->lo_sb.d2h(nmodels, s);
         HIPC(hipStreamSynchronize(s));
         std::memcpy(n0, prob->w->lo_sb.hn0.p, nmodels * sizeof(uint32_t));

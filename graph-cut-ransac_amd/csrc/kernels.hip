@@ -796,6 +796,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
 constexpr int kFmWaves = 15;
 constexpr uint32_t kFmRound = kFmWaves * 64;
 constexpr int kFmCB = 8;            // chain batch: 16-byte LDS reads (2 values each) per run step
+                                    // (16, i.e. 32-value batches: 130.8 vs 127.8 us)
 
 __device__ __forceinline__ void fm_wait_ge(const uint32_t* f, uint32_t v) {
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);

@@ -140,8 +140,11 @@ def test_generate_matches_oracle_slots(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nh", [100, 2048, 16384])
-def test_score_matches_oracle_bitwise(gpu, nh):
+@pytest.mark.parametrize("nh", [100, 2048, 16384, "small"])
+def test_score_matches_oracle_bitwise(gpu, nh, monkeypatch):
+    if nh == "small":              # launch_score_small (LO trials, refits)
+        monkeypatch.setenv("GCR_DEBUG_SCORER", "small")
+        nh = 200
     corr, _, _, thr = S.problem_f(1337, 0.5, seed=22)
     prob = CorrProblem(N.SOLVER_FUNDAMENTAL7, corr)
     inc, F = prob.generate(5, 0, 128)

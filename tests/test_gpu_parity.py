@@ -117,6 +117,28 @@ def test_score_kernel_matches_oracle_bitwise(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("nh", [1, 37, 256])
+def test_small_batch_scorer_matches_oracle_bitwise(kind, nh, monkeypatch):
+    # launch_score_small (LO trials, refits, short replay chunks): every pair in
+    # parallel, then one wave per model adds its inliers in order; ragged class
+    # tails (n not a multiple of 64) exercise the padded layout
+    monkeypatch.setenv("GCR_DEBUG_SCORER", "small")
+    f0, f1, thr0, thr1 = _problem_data(kind, 1337, seed=61 + kind)
+    prob = Problem(kind, f0, f1)
+    inc, models = prob.generate(19, 0, 256)
+    uniq = models[inc <= 101][:96]
+    tiled = np.resize(uniq, (nh, 7))
+    n0, n1, v0, v1, tot = prob.score_raw(tiled, thr0, thr1)
+    refs = [O.score(kind, f0, f1, m, thr0, thr1) for m in uniq[:nh]]
+    for i in range(nh):
+        ref = refs[i % len(refs)]
+        got = finish_score(kind, n0[i], n1[i], v0[i], v1[i], tot[i], thr0, thr1)
+        assert got["counts"] == [int(c) for c in ref["counts"]], i
+        assert np.array_equal(bits(got["values"]), bits(ref["values"])), i
+        assert bits(got["value"]) == bits(ref["value"]), i
+
+
+@pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("nh", [300, 2048, 16384])
 def test_every_split_variant_matches_oracle_bitwise(kind, nh):
     # launch_score picks H = 4 / 16 / 64 hypotheses per workgroup by batch size

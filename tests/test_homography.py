@@ -142,8 +142,11 @@ def test_generate_matches_oracle_slots(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nh", [100, 2048, 16384])
-def test_score_matches_oracle_bitwise(gpu, nh):
+@pytest.mark.parametrize("nh", [100, 2048, 16384, "small"])
+def test_score_matches_oracle_bitwise(gpu, nh, monkeypatch):
+    if nh == "small":              # launch_score_small (LO trials, refits)
+        monkeypatch.setenv("GCR_DEBUG_SCORER", "small")
+        nh = 200
     # covers the H = 4 / 16 / 64 hypotheses-per-workgroup variants
     corr, _, _, thr = S.problem_h(1337, 0.5, seed=22)
     prob = CorrProblem(N.SOLVER_HOMOGRAPHY4, corr)
