@@ -36,6 +36,8 @@ sys.path.insert(0, os.path.join(REPO, "graph-cut-ransac_amd"))
 METRIC = "model hypotheses/sec + wall-time to 0.99 confidence, N=10k corrs 50% outliers"
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector fp64 spec
+N_SIMD = 256 * 4               # CUs x SIMDs
+CLOCK_GHZ = 2.4                # MI355X peak engine clock (spec)
 
 
 def score_kernel_name(kind, slots):
@@ -59,14 +61,19 @@ def traffic_per_launch(kernel, slots):
     tools/pmc_summary.py from separate --pmc passes: 2 x FETCH_SIZE + WRITE_SIZE
     per dispatch, the gfx950 correction of MI355X_MICROARCH.md); None if that
     kernel/batch was not profiled."""
+    ent = pmc_entry(kernel, slots)
+    return None if ent is None else ent.get("hbm_bytes_per_launch")
+
+
+def pmc_entry(kernel, slots):
+    """The committed PMC summary of `kernel` at this batch size, or None."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             table = json.load(f)
     except (OSError, ValueError):
         return None
-    ent = table.get(f"{kernel}@{slots}")
-    return None if ent is None else ent.get("hbm_bytes_per_launch")
+    return table.get(f"{kernel}@{slots}")
 
 
 def parse():
@@ -224,6 +231,21 @@ def main():
         tf = models_per_launch * n_total * flops_pair / avg_kernel_s / 1e12
         valu = {"achieved_tflops": tf, "peak_tflops": FP64_VALU_PEAK_TFLOPS, "frac": tf / FP64_VALU_PEAK_TFLOPS,
                 "flops_per_pair": flops_pair}
+    # measured VALU occupancy of the dominant kernel from the committed PMC pass
+    # (SQ_ACTIVE_INST_VALU counts quad-cycles): the fraction of the 1024 SIMDs'
+    # cycles spent issuing VALU during one launch -- the bound the algorithmic
+    # HBM figure above does not see (the features are L2-resident)
+    pmc = pmc_entry(kernel_name, args.slots)
+    if pmc and "SQ_ACTIVE_INST_VALU" in pmc and avg_kernel_s > 0:
+        simd_cycles = N_SIMD * avg_kernel_s * CLOCK_GHZ * 1e9
+        valu = dict(valu or {})
+        valu.update({"active_frac": 4.0 * pmc["SQ_ACTIVE_INST_VALU"] / simd_cycles,
+                     "insts_per_launch": pmc.get("SQ_INSTS_VALU"),
+                     "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"),
+                     "wait_frac": (pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
+                                   if pmc.get("SQ_WAVE_CYCLES") else None),
+                     "clock_ghz": CLOCK_GHZ,
+                     "source": "profiles/pmc_traffic.json (rocprofv3 --pmc, separate passes)"})
 
     # wall time to 0.99 confidence: full estimator call (incl. upload, LO, refit)
     latency = None

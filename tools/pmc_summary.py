@@ -48,8 +48,14 @@ def main(root, slots=None, traffic_json=None):
             rd = 2048 * sum(vals[k]["FETCH_SIZE"]) / len(vals[k]["FETCH_SIZE"])
             wr = vals[k].get("WRITE_SIZE")
             wrb = 1024 * sum(wr) / len(wr) if wr else 0.0
-            table[f"{k}@{slots}"] = {"hbm_bytes_per_launch": rd + wrb, "read_bytes": rd, "write_bytes": wrb,
-                                     "source": os.path.normpath(root)}
+            ent = {"hbm_bytes_per_launch": rd + wrb, "read_bytes": rd, "write_bytes": wrb,
+                   "source": os.path.normpath(root)}
+            # VALU view (bench.py "valu"): instructions issued and active VALU
+            # quad-cycles per launch, when that pass was collected
+            for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
+                if c in vals[k]:
+                    ent[c] = sum(vals[k][c]) / len(vals[k][c])
+            table[f"{k}@{slots}"] = ent
         with open(traffic_json, "w") as f:
             json.dump(table, f, indent=1, sort_keys=True)
 
