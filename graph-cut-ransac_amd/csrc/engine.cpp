@@ -200,6 +200,7 @@ struct Workspace {
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
     DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
     DevBuf<double> rf_part;             // GPU refit: reduction block partials
+    DevBuf<QRDevState> rf_qrst;         // GPU refit: device-resident QR driver state
     PinBuf<double> rf_hpart;
     PinBuf<double> rf_htop;             // GPU refit: async upload ring
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
@@ -226,6 +227,14 @@ struct gcr_problem {
 };
 
 namespace {
+
+// The GPU refit runs qr3.h's driver on the device (launch_qr_device) unless
+// GCR_QR_DEVICE=0 (host-driven reductions, one synchronisation each)
+constexpr size_t kQrDeviceMaxRows = (size_t)256 * kSumSuper;
+bool qr_device_on() {
+    const char* e = getenv("GCR_QR_DEVICE");           // read per refit (tests switch it)
+    return !(e && e[0] == '0');
+}
 
 // --------------------------------------------------------- GPU refit ----
 // qr3.h storage backend in HBM: element-wise steps are kernels, reductions are
@@ -282,8 +291,18 @@ struct DevQRStore {
         HIPC(launch_qr_partials(col[a], col[c], lo, hi, P->w->rf_part.p, &nb, s));
         enqueue_with_top(nb);
         sync_and_take_top(nb);
-        double total = 0.0;
-        for (size_t b = 0; b < nb; ++b) total += P->w->rf_hpart.p[b];
+        // block partials: sequentially inside each aligned super-block, then
+        // the super-block partials sequentially (blocked_sum's order)
+        const size_t blk0 = lo / kSumBlock, per = kSumSuper / kSumBlock;
+        double total = 0.0, sup = 0.0;
+        for (size_t b = 0; b < nb; ++b) {
+            if (b > 0 && (blk0 + b) % per == 0) {
+                total += sup;
+                sup = 0.0;
+            }
+            sup += P->w->rf_hpart.p[b];
+        }
+        total += sup;
         return total;
     }
     double sumsq(int c, size_t lo, size_t hi) { return dot(c, c, lo, hi); }
@@ -343,6 +362,16 @@ struct GpuSiftSolver final : SiftSystemSolver {
         HIPC(launch_sift_rows(P->dp.cls[0], P->dp.cls[1], P->w->rf_idx.p, (uint32_t)ns, P->w->rf_idx.p + ns, (uint32_t)no,
                               rows, A, A + rows, A + 2 * rows, A + 3 * rows, s));
         HIPC(hipStreamSynchronize(s));          // index lists are pageable host vectors
+        if (qr_device_on() && rows >= 4 && rows <= kQrDeviceMaxRows) {
+            // the QR driver's decisions on the device: one synchronisation
+            P->w->rf_qrst.ensure(1);
+            P->w->rf_part.ensure((rows - 1) / kSumBlock + 1);
+            P->w->rf_hpart.ensure(3);
+            double* const cols[4] = {A, A + rows, A + 2 * rows, A + 3 * rows};
+            HIPC(launch_qr_device(cols, rows, P->w->rf_qrst.p, P->w->rf_part.p, P->w->rf_hpart.p, s));
+            for (int q = 0; q < 3; ++q) x[q] = P->w->rf_hpart.p[q];
+            return;
+        }
         DevQRStore st{{A, A + rows, A + 2 * rows, A + 3 * rows}, s, P};
         st.m = rows;
         st.prepare();

@@ -102,6 +102,28 @@ hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32
 // partials[0 .. nblocks) in block order.  Returns the block count via nblocks.
 hipError_t launch_qr_partials(const double* a, const double* c, size_t lo, size_t hi, double* partials,
                               size_t* nblocks, hipStream_t stream);
+// Device-resident qr_solve<3> (qr3.h) on the columns cols[0..2] | b = cols[3]
+// of length m (4 <= m <= 256 * kSumSuper): the driver's decisions run in
+// one-thread control kernels between the reductions, with the same fp64
+// operations and blocked summation order as the host driver; one host
+// synchronisation for x.  st: device scratch; partials: (m-1)/kSumBlock+1.
+struct QRDevState {
+    int red_a, red_c, red_on, pad0;                      // next reduction
+    uint64_t red_lo, red_hi;
+    int ew_op, ew_c, ew_e, pad1;                         // next element-wise step
+    uint64_t ew_lo, ew_hi;
+    double ew_p0, ew_p1;
+    uint64_t m;
+    int pc[3], transp[3], nonzero, ck, done, ddflag[3];
+    double nu[3], nd[3], tau_k[3], thr_helper;
+    double x[3];
+};
+struct QRCols {
+    double* col[4];
+};
+enum { kQsInit = 0, kQsNorm, kQsTail, kQsRefl, kQsDd, kQsDd2, kQsBStart, kQsBRefl, kQsFinal };
+hipError_t launch_qr_device(double* const cols[4], size_t m, QRDevState* st, double* partials, double x_out[3],
+                            hipStream_t stream);
 // rows 0..2 of the four columns into out[c * 3 + i] (0 past m)
 hipError_t launch_qr_top(const double* c0, const double* c1, const double* c2, const double* c3, size_t m,
                          double* out, hipStream_t stream);

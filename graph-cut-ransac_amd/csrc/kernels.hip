@@ -1438,10 +1438,9 @@ __global__ __launch_bounds__(kRowBlock) void k_sift_rows(DevClass sc, DevClass o
 // one wave per aligned block of kSumBlock rows: coalesced products into LDS,
 // then lane 0 folds them in row order (16-byte reads, 8 in flight)
 constexpr int kPartWaves = 4;
-__global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* __restrict__ a,
-                                                                 const double* __restrict__ c, uint64_t lo,
-                                                                 uint64_t hi, uint64_t blk0, uint64_t nblk,
-                                                                 double* __restrict__ partials) {
+__device__ __forceinline__ void qr_partials_body(const double* __restrict__ a, const double* __restrict__ c,
+                                                 uint64_t lo, uint64_t hi, uint64_t blk0, uint64_t nblk,
+                                                 double* __restrict__ partials) {
     __shared__ double prod[kPartWaves][kSumBlock];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t blk = (uint64_t)blockIdx.x * kPartWaves + wave;
@@ -1494,6 +1493,230 @@ __global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* _
             if (s1 > e0 && s0 < e1) part += subp[wave][l];
         }
         partials[blk] = part;
+    }
+}
+
+__global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* __restrict__ a,
+                                                                 const double* __restrict__ c, uint64_t lo,
+                                                                 uint64_t hi, uint64_t blk0, uint64_t nblk,
+                                                                 double* __restrict__ partials) {
+    qr_partials_body(a, c, lo, hi, blk0, nblk, partials);
+}
+
+// ---- device-resident QR driver (qr3.h qr_solve<3> with its decisions on
+// the GPU): a fixed launch sequence of reductions (k_qrd_partials),
+// control steps (k_qrd_ctl, one thread: the driver's scalar logic, the
+// same fp64 operations in the same order as qr3.h) and element-wise steps
+// (k_qrd_ew), whose parameters live in a QRDevState in device memory.  The
+// host enqueues the whole sequence and synchronises once for x.
+__global__ __launch_bounds__(64 * kPartWaves) void k_qrd_partials(QRCols cols, const QRDevState* __restrict__ st,
+                                                                  double* __restrict__ partials) {
+    if (!st->red_on) return;
+    const uint64_t lo = st->red_lo, hi = st->red_hi;
+    const uint64_t blk0 = lo / kSumBlock, nblk = (hi - 1) / kSumBlock - blk0 + 1;
+    qr_partials_body(cols.col[st->red_a], cols.col[st->red_c], lo, hi, blk0, nblk, partials);
+}
+
+__global__ __launch_bounds__(256) void k_qrd_ew(QRCols cols, const QRDevState* __restrict__ st) {
+    const int op = st->ew_op;
+    if (op == 0) return;
+    const uint64_t i = st->ew_lo + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= st->ew_hi) return;
+    double* c = cols.col[st->ew_c];
+    if (op == 1) c[i] = c[i] / st->ew_p0;                                   // scale
+    else if (op == 2) c[i] = 0.0;                                          // zero
+    else c[i] -= (st->ew_p0 * cols.col[st->ew_e][i]) * st->ew_p1;          // update
+}
+
+constexpr int kQrdSup = 256;            // super-blocks a control step can sum (16.7 M rows)
+
+__global__ __launch_bounds__(64) void k_qrd_ctl(QRCols cols, QRDevState* st, const double* __restrict__ partials,
+                                                uint64_t m_rows, int step, int k, int j) {
+    __shared__ double sup[kQrdSup];
+    __shared__ double total_sh;
+    const int t = threadIdx.x;
+    const bool had = st->red_on != 0;
+    if (had) {
+        // the previous reduction's block partials in blocked_sum's order:
+        // sequentially inside each aligned super-block, then the super-block
+        // partials sequentially
+        const uint64_t lo = st->red_lo, hi = st->red_hi;
+        const uint64_t blk0 = lo / kSumBlock, nblk = (hi - 1) / kSumBlock - blk0 + 1;
+        constexpr uint64_t per = kSumSuper / kSumBlock;
+        const uint64_t s0 = blk0 / per, nsup = (blk0 + nblk - 1) / per - s0 + 1;
+        for (uint64_t u = t; u < nsup; u += 64) {
+            const uint64_t b_lo = max(blk0, (s0 + u) * per), b_hi = min(blk0 + nblk, (s0 + u + 1) * per);
+            double sp = 0.0;
+            for (uint64_t b = b_lo; b < b_hi; ++b) sp += partials[b - blk0];
+            sup[u] = sp;
+        }
+        __syncthreads();
+        if (t == 0) {
+            double tot = 0.0;
+            for (uint64_t u = 0; u < nsup; ++u) tot += sup[u];
+            total_sh = tot;
+        }
+    }
+    __syncthreads();
+    if (t != 0) return;
+    const double total = had ? total_sh : 0.0;
+    st->red_on = 0;
+    st->ew_op = 0;
+    if (st->done) return;
+    const uint64_t m = m_rows;
+    const double eps = 2.220446049250313e-16;           // numeric_limits<double>::epsilon()
+    double* const* col = cols.col;
+    auto set_red = [&](int a, int c, uint64_t lo, uint64_t hi) {
+        st->red_a = a;
+        st->red_c = c;
+        st->red_lo = lo;
+        st->red_hi = hi;
+        st->red_on = hi > lo ? 1 : 0;
+    };
+    auto set_ew = [&](int op, int c, int e, uint64_t lo, uint64_t hi, double p0, double p1) {
+        st->ew_op = hi > lo ? op : 0;
+        st->ew_c = c;
+        st->ew_e = e;
+        st->ew_lo = lo;
+        st->ew_hi = hi;
+        st->ew_p0 = p0;
+        st->ew_p1 = p1;
+    };
+    auto pivot = [&](int kk) {                           // qr3.h: pivot choice of step kk
+        int big = kk;
+        double bign = st->nu[kk];
+        for (int jj = kk + 1; jj < 3; ++jj)
+            if (bign < st->nu[jj]) { bign = st->nu[jj]; big = jj; }
+        if (st->nonzero == 3 && bign * bign < st->thr_helper * (double)(m - kk)) st->nonzero = kk;
+        st->transp[kk] = big;
+        if (kk != big) {
+            int tp = st->pc[kk]; st->pc[kk] = st->pc[big]; st->pc[big] = tp;
+            double tv = st->nu[kk]; st->nu[kk] = st->nu[big]; st->nu[big] = tv;
+            tv = st->nd[kk]; st->nd[kk] = st->nd[big]; st->nd[big] = tv;
+        }
+        st->ck = st->pc[kk];
+    };
+    switch (step) {
+        case kQsInit:
+            for (int q = 0; q < 3; ++q) { st->pc[q] = q; st->tau_k[q] = 0.0; st->transp[q] = q; }
+            st->m = m_rows;
+            st->nonzero = 3;
+            set_red(0, 0, 0, m);
+            break;
+        case kQsNorm:
+            st->nd[k] = sqrt(total);
+            st->nu[k] = st->nd[k];
+            if (k < 2) {
+                set_red(k + 1, k + 1, 0, m);
+            } else {
+                double maxn = st->nu[0];
+                for (int q = 1; q < 3; ++q)
+                    if (maxn < st->nu[q]) maxn = st->nu[q];
+                const double me = maxn * eps;
+                st->thr_helper = (me * me) / (double)m;
+                pivot(0);
+                set_red(st->ck, st->ck, 1, m);
+            }
+            break;
+        case kQsTail: {
+            const int ck = st->ck;
+            const double tail = total;
+            const double c0 = col[ck][k];
+            double tau, beta;
+            if (tail <= 2.2250738585072014e-308) {       // numeric_limits<double>::min()
+                tau = 0.0;
+                beta = c0;
+                set_ew(2, ck, 0, k + 1, m, 0.0, 0.0);
+            } else {
+                beta = sqrt(c0 * c0 + tail);
+                if (c0 >= 0.0) beta = -beta;
+                set_ew(1, ck, 0, k + 1, m, c0 - beta, 0.0);
+                tau = (beta - c0) / beta;
+            }
+            st->tau_k[k] = tau;
+            col[ck][k] = beta;
+            if (k + 1 < 3 && tau != 0.0) set_red(ck, st->pc[k + 1], k + 1, m);
+            break;
+        }
+        case kQsRefl: {                                  // apply_reflector(ck, k, tau, pc[j])
+            const int ck = st->ck, c = st->pc[j];
+            const double tau = st->tau_k[k];
+            if (tau != 0.0) {
+                double tt = total;
+                const double ckv = col[c][k];
+                tt += ckv;
+                col[c][k] = ckv - tau * tt;
+                set_ew(3, c, ck, k + 1, m, tau, tt);
+                if (j + 1 < 3) set_red(ck, st->pc[j + 1], k + 1, m);
+            }
+            break;
+        }
+        case kQsDd: {                                    // norm downdates of step k
+            const double downdate_thr = sqrt(eps);
+            for (int jj = k + 1; jj < 3; ++jj) {
+                st->ddflag[jj] = 0;
+                if (st->nu[jj] != 0.0) {
+                    double temp = fabs(col[st->pc[jj]][k]) / st->nu[jj];
+                    temp = (1.0 + temp) * (1.0 - temp);
+                    temp = temp < 0.0 ? 0.0 : temp;
+                    const double r = st->nu[jj] / st->nd[jj];
+                    const double temp2 = temp * (r * r);
+                    if (temp2 <= downdate_thr) st->ddflag[jj] = 1;
+                    else st->nu[jj] *= sqrt(temp);
+                }
+            }
+            if (st->ddflag[k + 1]) set_red(st->pc[k + 1], st->pc[k + 1], k + 1, m);
+            break;
+        }
+        case kQsDd2:
+            if (st->ddflag[j]) {
+                st->nd[j] = sqrt(total);
+                st->nu[j] = st->nd[j];
+            }
+            if (j + 1 < 3) {
+                if (st->ddflag[j + 1]) set_red(st->pc[j + 1], st->pc[j + 1], k + 1, m);
+            } else {
+                pivot(k + 1);
+                set_red(st->ck, st->ck, k + 2, m);
+            }
+            break;
+        case kQsBStart:
+            if (st->nonzero == 0) {
+                st->x[0] = st->x[1] = st->x[2] = 0.0;
+                st->done = 1;
+                break;
+            }
+            if (st->tau_k[0] != 0.0) set_red(st->pc[0], 3, 1, m);
+            break;
+        case kQsBRefl: {                                 // apply_reflector(pc[k], k, tau_k[k], b)
+            if (k < st->nonzero && st->tau_k[k] != 0.0) {
+                double tt = total;
+                const double bk = col[3][k];
+                tt += bk;
+                col[3][k] = bk - st->tau_k[k] * tt;
+                set_ew(3, 3, st->pc[k], k + 1, m, st->tau_k[k], tt);
+            }
+            if (k + 1 < 3 && k + 1 < st->nonzero && st->tau_k[k + 1] != 0.0) set_red(st->pc[k + 1], 3, k + 2, m);
+            break;
+        }
+        default: {                                       // kQsFinal: back substitution
+            int perm[3] = {0, 1, 2};
+            for (int q = 0; q < 3; ++q) {
+                const int tq = st->transp[q];
+                const int tv = perm[q]; perm[q] = perm[tq]; perm[tq] = tv;
+            }
+            const int nz = st->nonzero;
+            double c[3];
+            for (int q = 0; q < 3; ++q) c[q] = col[3][q];
+            for (int jj = nz; jj-- > 0;) {
+                c[jj] = c[jj] / col[st->pc[jj]][jj];
+                for (int i = 0; i < jj; ++i) c[i] -= c[jj] * col[st->pc[jj]][i];
+            }
+            for (int i = 0; i < nz; ++i) st->x[perm[i]] = c[i];
+            for (int i = nz; i < 3; ++i) st->x[perm[i]] = 0.0;
+            st->done = 1;
+            break;
+        }
     }
 }
 
@@ -1761,6 +1984,42 @@ hipError_t launch_qr_partials(const double* a, const double* c, size_t lo, size_
     hipLaunchKernelGGL(k_qr_partials, dim3((unsigned)((nblk + kPartWaves - 1) / kPartWaves)), dim3(64 * kPartWaves),
                        0, stream, a, c, (uint64_t)lo, (uint64_t)hi, blk0, nblk, partials);
     return hipGetLastError();
+}
+
+hipError_t launch_qr_device(double* const cols[4], size_t m, QRDevState* st, double* partials, double x_out[3],
+                            hipStream_t stream) {
+    if (m < 4 || m > (size_t)kQrdSup * kSumSuper) return hipErrorInvalidValue;
+    QRCols qc{{cols[0], cols[1], cols[2], cols[3]}};
+    const uint64_t nblk = (m - 1) / kSumBlock + 1;
+    const dim3 gr((unsigned)((nblk + kPartWaves - 1) / kPartWaves)), br(64 * kPartWaves);
+    const dim3 ge((unsigned)((m + 255) / 256)), be(256);
+    hipError_t e = hipMemsetAsync(st, 0, sizeof(QRDevState), stream);   // no reduction pending, not done
+    if (e != hipSuccess) return e;
+    auto C = [&](int step, int k, int j) {
+        hipLaunchKernelGGL(k_qrd_ctl, dim3(1), dim3(64), 0, stream, qc, st, partials, (uint64_t)m, step, k, j);
+    };
+    auto R = [&]() { hipLaunchKernelGGL(k_qrd_partials, gr, br, 0, stream, qc, st, partials); };
+    auto E = [&]() { hipLaunchKernelGGL(k_qrd_ew, ge, be, 0, stream, qc, st); };
+    // qr3.h qr_solve<3>, step for step
+    C(kQsInit, 0, 0);
+    for (int k = 0; k < 3; ++k) { R(); C(kQsNorm, k, 0); }
+    for (int k = 0; k < 3; ++k) {
+        R(); C(kQsTail, k, 0); E();
+        for (int j = k + 1; j < 3; ++j) { R(); C(kQsRefl, k, j); E(); }
+        if (k < 2) {
+            C(kQsDd, k, 0);
+            for (int j = k + 1; j < 3; ++j) { R(); C(kQsDd2, k, j); }
+        }
+    }
+    C(kQsBStart, 0, 0);
+    for (int k = 0; k < 3; ++k) { R(); C(kQsBRefl, k, 0); E(); }
+    C(kQsFinal, 0, 0);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const double* dx = reinterpret_cast<const double*>(reinterpret_cast<const char*>(st) + offsetof(QRDevState, x));
+    e = hipMemcpyAsync(x_out, dx, 3 * sizeof(double), hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(stream);
 }
 
 hipError_t launch_qr_top(const double* c0, const double* c1, const double* c2, const double* c3, size_t m,

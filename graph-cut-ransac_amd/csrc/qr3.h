@@ -7,10 +7,12 @@
 //
 // Reductions use ONE fixed order, blocked_sum: sequential inside aligned
 // sub-blocks of kSumSub rows, sub-block partials sequentially inside aligned
-// blocks of kSumBlock rows, then the block partials sequentially.  Eigen's own
-// order is packet-vectorised and unpinned (no Eigen here); for m <= kSumSub
-// the blocked order is plain sequential summation.  The oracle restates the same
-// order (oracle/gcr_oracle.cpp), so host, GPU and oracle agree bitwise.
+// blocks of kSumBlock rows, block partials sequentially inside aligned
+// super-blocks of kSumSuper rows, then the super-block partials sequentially.
+// Eigen's own order is packet-vectorised and unpinned (no Eigen here); for
+// m <= kSumSub the blocked order is plain sequential summation.  The oracle
+// restates the same order (oracle/gcr_oracle.cpp), so host, GPU and oracle
+// agree bitwise.
 #pragma once
 
 #include <algorithm>
@@ -23,26 +25,34 @@ namespace gcr {
 
 constexpr size_t kSumBlock = 1024;
 constexpr size_t kSumSub = 64;         // sub-blocks: 16 per block
+constexpr size_t kSumSuper = 64 * kSumBlock;   // super-blocks: 64 blocks
 
 // sum_{i in [lo, hi)} f(i) in blocked order: sequential inside each aligned
 // sub-block of kSumSub rows, the sub-block partials of an aligned block of
-// kSumBlock rows sequentially, then the block partials sequentially.  (The
-// two-level block keeps the GPU's sequential chains at 64 + 16 adds instead
-// of 1024; for m <= 64 it is plain sequential summation.)
+// kSumBlock rows sequentially, the block partials of an aligned super-block
+// of kSumSuper rows sequentially, then the super-block partials sequentially.
+// (The levels keep the GPU's sequential chains at 64 + 16 + 64 + m / 65536
+// adds; inside one super-block the order is the two-level one, and for
+// m <= 64 it is plain sequential summation.)
 template <class F>
 inline double blocked_sum(size_t lo, size_t hi, F f) {
     double total = 0.0;
     size_t i = lo;
     while (i < hi) {
-        const size_t end = std::min(hi, (i / kSumBlock + 1) * kSumBlock);
-        double part = 0.0;
-        while (i < end) {
-            const size_t send = std::min(end, (i / kSumSub + 1) * kSumSub);
-            double sp = 0.0;
-            for (; i < send; ++i) sp += f(i);
-            part += sp;
+        const size_t send = std::min(hi, (i / kSumSuper + 1) * kSumSuper);
+        double sup = 0.0;
+        while (i < send) {
+            const size_t end = std::min(send, (i / kSumBlock + 1) * kSumBlock);
+            double part = 0.0;
+            while (i < end) {
+                const size_t sbe = std::min(end, (i / kSumSub + 1) * kSumSub);
+                double sp = 0.0;
+                for (; i < sbe; ++i) sp += f(i);
+                part += sp;
+            }
+            sup += part;
         }
-        total += part;
+        total += sup;
     }
     return total;
 }

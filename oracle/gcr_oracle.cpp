@@ -297,25 +297,33 @@ static bool faithful_subset(const std::vector<size_t>& indices, size_t N, std::v
 // (an order that cannot be pinned without Eigen); every reduction here uses the
 // engine's fixed blocked order instead: sequential within aligned sub-blocks
 // of 64 rows, the sub-block partials sequentially within aligned blocks of
-// 1024 rows, then the block partials sequentially -- what the GPU refit
-// reproduces bitwise.
+// 1024 rows, the block partials sequentially within aligned super-blocks of
+// 65536 rows, then the super-block partials sequentially -- what the GPU
+// refit reproduces bitwise.
 static constexpr size_t kSumBlockRows = 1024;
 static constexpr size_t kSumSubRows = 64;
+static constexpr size_t kSumSuperRows = 64 * kSumBlockRows;
 template <class F>
 static double bsum(size_t lo, size_t hi, F f) {
     double total = 0.0;
-    for (size_t b0 = lo; b0 < hi;) {
-        const size_t b1 = std::min(hi, (b0 / kSumBlockRows + 1) * kSumBlockRows);
-        double part = 0.0;
-        for (size_t s0 = b0; s0 < b1;) {
-            const size_t s1 = std::min(b1, (s0 / kSumSubRows + 1) * kSumSubRows);
-            double sp = 0.0;
-            for (size_t i = s0; i < s1; ++i) sp += f(i);
-            part += sp;
-            s0 = s1;
+    for (size_t u0 = lo; u0 < hi;) {
+        const size_t u1 = std::min(hi, (u0 / kSumSuperRows + 1) * kSumSuperRows);
+        double sup = 0.0;
+        for (size_t b0 = u0; b0 < u1;) {
+            const size_t b1 = std::min(u1, (b0 / kSumBlockRows + 1) * kSumBlockRows);
+            double part = 0.0;
+            for (size_t s0 = b0; s0 < b1;) {
+                const size_t s1 = std::min(b1, (s0 / kSumSubRows + 1) * kSumSubRows);
+                double sp = 0.0;
+                for (size_t i = s0; i < s1; ++i) sp += f(i);
+                part += sp;
+                s0 = s1;
+            }
+            sup += part;
+            b0 = b1;
         }
-        total += part;
-        b0 = b1;
+        total += sup;
+        u0 = u1;
     }
     return total;
 }

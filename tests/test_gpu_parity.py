@@ -381,9 +381,12 @@ def test_gpu_solver_records_match_direct_calls():
 
 # ------------------------------------------------------------ GPU refit ----
 @pytest.mark.parametrize("ks,ko", [(40, 46), (800, 120), (2000, 260), (2500, 2500)])
-def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko):
+@pytest.mark.parametrize("qr_device", ["1", "0"])
+def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko, qr_device, monkeypatch):
     # the hybrid least-squares system (ns + C(no,2) rows, up to 3.1 M) built and
-    # solved on the GPU equals the host path and the oracle bit for bit
+    # solved on the GPU equals the host path and the oracle bit for bit, with
+    # the QR driver on the device (launch_qr_device) or on the host
+    monkeypatch.setenv("GCR_QR_DEVICE", qr_device)
     fs, fo, ts, to, _, _ = S.problem_m2(5000, 5000, seed=ks + 3 * ko)
     rng = np.random.default_rng(ks + ko)
     i0 = np.sort(rng.choice(np.flatnonzero(ts), size=ks, replace=False)).astype(np.uint32)
