@@ -378,6 +378,7 @@ struct GpuSiftSolver final : SiftSystemSolver {
         qr3_solve(st, rows, x);
         HIPC(hipStreamSynchronize(s));          // the pinned ring must outlive its uploads
     }
+    void for_ranges(size_t n, const std::function<void(size_t, size_t)>& fn) override;
 };
 
 // A small persistent pool of host threads for the LO trial fits (independent
@@ -486,6 +487,17 @@ bool small_score_on() {
 bool debug_small_scorer(uint32_t n) {
     const char* e = getenv("GCR_DEBUG_SCORER");
     return e && e[0] == 's' && n > 0 && n <= kSmallScore;
+}
+
+// the final refit's per-inlier host work on the host pool (the refit runs on
+// the solving thread, never inside a pool job)
+void GpuSiftSolver::for_ranges(size_t n, const std::function<void(size_t, size_t)>& fn) {
+    const size_t parts = n < 1024 ? 1 : 8;
+    const size_t step = (n + parts - 1) / parts;
+    host_pool().parallel_for(parts, [&](size_t p) {
+        const size_t lo = p * step, hi = std::min(n, lo + step);
+        if (lo < hi) fn(lo, hi);
+    });
 }
 
 // verify_batches records kernel-timing events on every n-th batch

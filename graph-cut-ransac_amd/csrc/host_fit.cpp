@@ -171,9 +171,17 @@ bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectMode
     if (!finish_model(sol, out)) return false;
     std::vector<double> ang(no), wts(no);
     double wsum = 0;
+    // the rectified angles are independent (a big refit spreads them over
+    // the solver's threads); the weights and the mode stay in order
+    auto angles = [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            const uint32_t j = oi[i];
+            ang[i] = rectified_angle(oc.x[j], oc.y[j], oc.c0[j], oc.c1[j], out.h7, out.h8);
+        }
+    };
+    if (big && rows >= big_rows) big->for_ranges(no, angles);
+    else angles(0, no);
     for (size_t i = 0; i < no; ++i) {
-        const uint32_t j = oi[i];
-        ang[i] = rectified_angle(oc.x[j], oc.y[j], oc.c0[j], oc.c1[j], out.h7, out.h8);
         wts[i] = 1.0;
         wsum += 1.0;
     }

@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "fund.h"
@@ -35,6 +36,9 @@ struct SiftSystemSolver {
     virtual ~SiftSystemSolver() = default;
     virtual void solve(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows,
                        double x[3]) = 0;
+    // fn(lo, hi) over [0, n) in disjoint ranges, possibly in parallel (the
+    // per-inlier work around a big solve); the default runs it in one piece
+    virtual void for_ranges(size_t n, const std::function<void(size_t, size_t)>& fn) { fn(0, n); }
 };
 
 // RectifyingHomographyEstimator::estimateModelNonminimal for the three solvers

@@ -1546,8 +1546,14 @@ __global__ __launch_bounds__(64) void k_qrd_ctl(QRCols cols, QRDevState* st, con
         const uint64_t s0 = blk0 / per, nsup = (blk0 + nblk - 1) / per - s0 + 1;
         for (uint64_t u = t; u < nsup; u += 64) {
             const uint64_t b_lo = max(blk0, (s0 + u) * per), b_hi = min(blk0 + nblk, (s0 + u + 1) * per);
+            // the super-block's (<= 64) partials all in flight, then summed in order
+            double v[per];
+#pragma unroll
+            for (uint64_t q = 0; q < per; ++q) v[q] = b_lo + q < b_hi ? partials[b_lo + q - blk0] : 0.0;
             double sp = 0.0;
-            for (uint64_t b = b_lo; b < b_hi; ++b) sp += partials[b - blk0];
+#pragma unroll
+            for (uint64_t q = 0; q < per; ++q)
+                if (b_lo + q < b_hi) sp += v[q];
             sup[u] = sp;
         }
         __syncthreads();
