@@ -1213,7 +1213,7 @@ template <int KIND>
 __global__ __launch_bounds__(64) void k_lo_chain(uint32_t n0, uint32_t n1, uint32_t pad0, uint32_t ntot,
                                                 const double* __restrict__ vals, const uint64_t* __restrict__ bits,
                                                 ScoreOut out) {
-    __shared__ double cbuf[kLoSpan];
+    __shared__ double cbuf[2][kLoSpan];
     const uint32_t mi = blockIdx.x;
     const int lane = threadIdx.x;
     const uint64_t below = (1ull << lane) - 1ull;
@@ -1221,53 +1221,69 @@ __global__ __launch_bounds__(64) void k_lo_chain(uint32_t n0, uint32_t n1, uint3
     // lane 0: the class sum; lane 1 (KIND 2): the running total
     constexpr int kChains = KIND == 2 ? 2 : 1;
     double run = 0.0, hold = 0.0;
-    uint32_t cnt[2] = {0, 0};
+    uint32_t cnt0 = 0, cnt1 = 0;
     const double* mv = vals + (size_t)mi * ntot;
     const uint64_t* mb = bits + (size_t)mi * ntot / 64;
-    for (int c = 0; c < K; ++c) {
-        if (c == 1 && lane == 0) {
+    // spans of kLoSpan features, class 0's then class 1's; the next span's
+    // values and ballot words are in flight while the current one is folded
+    const uint32_t ns0 = (pad0 + kLoSpan - 1) / kLoSpan;
+    const uint32_t nsp = ns0 + (K == 2 ? (ntot - pad0 + kLoSpan - 1) / kLoSpan : 0u);
+    auto span = [&](uint32_t sidx, uint32_t& base, uint32_t& nch) {
+        const bool c1 = sidx >= ns0;
+        const uint32_t s0 = (c1 ? sidx - ns0 : sidx) * kLoSpan;
+        const uint32_t len = c1 ? ntot - pad0 : pad0;
+        base = (c1 ? pad0 : 0u) + s0;
+        nch = min(kLoSpan, len - s0) / 64;
+    };
+    double v[kLoSpan / 64];
+    uint64_t w[kLoSpan / 64];
+    auto load = [&](uint32_t sidx) {
+        uint32_t base, nch;
+        span(sidx, base, nch);
+#pragma unroll
+        for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
+            const uint32_t q = ch < nch ? ch : 0;
+            v[ch] = mv[base + q * 64 + lane];
+            w[ch] = mb[base / 64 + q];
+        }
+    };
+    if (nsp > 0) load(0);
+    for (uint32_t sidx = 0; sidx < nsp; ++sidx) {
+        uint32_t base, nch;
+        span(sidx, base, nch);
+        if (K == 2 && sidx == ns0 && lane == 0) {        // first class-1 span
             hold = run;
             run = 0.0;
         }
-        const uint32_t base = c ? pad0 : 0;
-        const uint32_t len = c ? (ntot - pad0) : pad0;
-        for (uint32_t s0 = 0; s0 < len; s0 += kLoSpan) {
-            const uint32_t nch = min(kLoSpan, len - s0) / 64;
-            // the span's values and bit words, all in flight, then an in-order
-            // compaction of its inlier values into LDS
-            double v[kLoSpan / 64];
-            uint64_t w[kLoSpan / 64];
+        // in-order compaction of the span's inlier values into LDS
+        double* cb = cbuf[sidx & 1];
+        uint32_t off = 0;
 #pragma unroll
-            for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
-                const uint32_t q = ch < nch ? ch : 0;
-                v[ch] = mv[base + s0 + q * 64 + lane];
-                w[ch] = mb[(base + s0) / 64 + q];
+        for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
+            if (ch < nch) {
+                if ((w[ch] >> lane) & 1ull) cb[off + (uint32_t)__builtin_popcountll(w[ch] & below)] = v[ch];
+                off += (uint32_t)__builtin_popcountll(w[ch]);
             }
-            uint32_t off = 0;
-#pragma unroll
-            for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
-                if (ch < nch) {
-                    if ((w[ch] >> lane) & 1ull) cbuf[off + (uint32_t)__builtin_popcountll(w[ch] & below)] = v[ch];
-                    off += (uint32_t)__builtin_popcountll(w[ch]);
-                }
-            }
-            cnt[c] += off;
-            __builtin_amdgcn_wave_barrier();
-            if (lane < kChains) {
-                // batches of 16 reads in flight, then 16 dependent adds
-                uint32_t k = 0;
-                for (; k + 16 <= off; k += 16) {
-                    double t[16];
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) t[u] = cbuf[k + u];
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) run += t[u];
-                }
-                for (; k < off; ++k) run += cbuf[k];
-            }
-            __builtin_amdgcn_wave_barrier();
         }
+        if (sidx < ns0) cnt0 += off;
+        else cnt1 += off;
+        if (sidx + 1 < nsp) load(sidx + 1);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < kChains) {
+            // batches of 16 reads in flight, then 16 dependent adds
+            uint32_t k = 0;
+            for (; k + 16 <= off; k += 16) {
+                double t[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) t[u] = cb[k + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) run += t[u];
+            }
+            for (; k < off; ++k) run += cb[k];
+        }
+        __builtin_amdgcn_wave_barrier();
     }
+    const uint32_t cnt[2] = {cnt0, cnt1};
     const double tot = KIND == 2 ? __shfl(run, 1) : run;
     if (lane == 0) {
         out.n0[mi] = cnt[0];
