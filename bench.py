@@ -76,6 +76,14 @@ def pmc_entry(kernel, slots):
     return table.get(f"{kernel}@{slots}")
 
 
+# The fundamental matrix yields 1-3 models per 7-point sample (≈1.07 live per
+# slot at the F config), and the batch scorer runs one workgroup of 16 live
+# hypotheses per CU: 4096 slots give ≈4380 live models, 274 workgroups on 256
+# CUs, so the launch takes two waves of workgroups (182 us) for 7 % more work.
+# 3712 slots keep the live count (≈3970, +3 sigma 4040) within one wave.
+F_SLOTS = 3712
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -88,7 +96,8 @@ def parse():
                          "batch: configs[4] mixed H / F / rectification problems, full estimator calls")
     ap.add_argument("--problems", type=int, default=1024, help="batch workload: problems in the whole job")
     ap.add_argument("--concurrency", type=int, default=8, help="batch workload: host threads per GPU")
-    ap.add_argument("--slots", type=int, default=4096, help="outer-iteration slots (hypotheses) per launch")
+    ap.add_argument("--slots", type=int, default=None,
+                    help="outer-iteration slots per launch (default 4096; f: 3712, see F_SLOTS)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-latency", action="store_true")
     return ap.parse_args()
@@ -96,6 +105,8 @@ def parse():
 
 def main():
     args = parse()
+    if args.slots is None:
+        args.slots = F_SLOTS if args.workload == "f" else 4096
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -213,6 +213,7 @@ struct gcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int n_cu = 256;                     // compute units (one batch-scorer workgroup each)
     Workspace shared;                   // reused by the gcr_rect_* calls
 };
 
@@ -648,7 +649,7 @@ struct RectTraits {
         return launch_mask(P->dp, cls, m, rule, T, lambda, mk, s);
     }
     static hipError_t score_live(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t nh,
-                                 const ScoreOut& out, hipStream_t s) {
+                                 uint32_t, const ScoreOut& out, hipStream_t s) {
         return launch_score(P->dp, T, m, inc, nh, true, out, s);
     }
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
@@ -712,15 +713,17 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
         return launch_select_geo(P->solver, P->w->sb.dev(), P->w->inc.p, nh, s0, m[0], Tm[0], rec, s, map, cnt);
     }
     // replay-path scoring of a fetched chunk: fundamental-matrix launches are
-    // compacted to the live hypotheses (results in hypothesis order)
+    // compacted to the live hypotheses (results in hypothesis order); the
+    // host counted them (`live`), so the scorer's shape follows the live count
     static hipError_t score_live(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t nh,
-                                 const ScoreOut& out, hipStream_t s) {
+                                 uint32_t live, const ScoreOut& out, hipStream_t s) {
         if (per(P) == 1) return launch_score_geo(P->dp, T[0], m, inc, nh, out, s);
         P->w->hmap.ensure(nh);
         P->w->hcount.ensure(1);
         hipError_t e = launch_compact(inc, nh, P->w->hmap.p, P->w->hcount.p, s);
         if (e != hipSuccess) return e;
-        return launch_score_geo(P->dp, T[0], m, inc, nh, out, s, P->w->hmap.p, P->w->hcount.p);
+        return launch_score_geo(P->dp, T[0], m, inc, std::max<uint32_t>(live, 1u), out, s, P->w->hmap.p,
+                                P->w->hcount.p);
     }
     static size_t per(gcr_problem* P) { return P->solver == 4 ? kFModels : 1; }
     static bool fit(gcr_problem* P, const std::vector<uint32_t>* lists, Model& out, bool) {
@@ -1062,6 +1065,39 @@ private:
         return cnt;
     }
 
+    // Fundamental matrix (kP models per slot, compacted to the live ones): the
+    // batch scorer runs one workgroup of split_h(live) hypotheses per CU, so a
+    // chunk whose live count spills a little past whole waves of workgroups
+    // pays a whole extra wave (4382 live at 4096 slots: 274 workgroups on 256
+    // CUs, 182 us instead of ~90).  Score only the slots that fill whole waves
+    // when the last wave would be less than half full; the next chunk
+    // regenerates the rest (a slot is a pure function of (seed, slot), so
+    // results do not depend on the cut).  `live` returns the scored count.
+    uint64_t whole_waves(uint64_t cnt, uint64_t& live) {
+        const uint8_t* inc = P_->w->h_inc.p;
+        auto live_of = [&](uint64_t c) {
+            uint64_t l = 0;
+            for (uint64_t j = 0; j < c * kP; ++j) l += inc[j] <= 101;
+            return l;
+        };
+        live = live_of(cnt);
+        const uint64_t cap = (uint64_t)split_h((uint32_t)std::min<uint64_t>(live, UINT32_MAX)) * P_->ctx->n_cu;
+        const uint64_t waves = (live + cap - 1) / cap;
+        if (waves < 2 || live - (waves - 1) * cap > cap / 2) return cnt;
+        const uint64_t target = (waves - 1) * cap;
+        uint64_t c = 0, l = 0;
+        while (c < cnt) {
+            uint64_t add = 0;
+            for (size_t k = 0; k < kP; ++k) add += inc[c * kP + k] <= 101;
+            if (l + add > target) break;
+            l += add;
+            ++c;
+        }
+        if (c == 0) return cnt;
+        live = l;
+        return c;
+    }
+
     uint64_t fetch_chunk(uint64_t s0, uint32_t B, uint64_t L) {
         if (world_ > 1) return fetch_chunk_sharded(s0, B, L);
         const size_t BP = (size_t)B * kP;
@@ -1075,6 +1111,8 @@ private:
         uint64_t itp = it_, cnt = 0;
         while (cnt < B && itp < L) itp += P_->w->h_inc.p[kP * cnt++];
         if (cnt == 0) cnt = 1;
+        uint64_t live = cnt * kP;
+        if (kP > 1) cnt = whole_waves(cnt, live);
         const size_t nh = cnt * kP;
         t0 = Clock::now();
         HIPC(hipEventRecord(P_->ctx->ev0, s_));
@@ -1087,7 +1125,8 @@ private:
             HIPC(launch_score_small(P_->dp, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(),
                                     P_->w->sm_vals.p, P_->w->sm_bits.p, s_));
         } else {
-            HIPC(Tr::score_live(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(), s_));
+            HIPC(Tr::score_live(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, (uint32_t)live,
+                                P_->w->sb.dev(), s_));
         }
         cursor_ = 0;
         HIPC(hipEventRecord(P_->ctx->ev1, s_));
@@ -1323,6 +1362,9 @@ int gcr_create(int device, gcr_ctx** out) {
         HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIPC(hipEventCreate(&c->ev0));
         HIPC(hipEventCreate(&c->ev1));
+        int cu = 0;
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
+            c->n_cu = cu;
         *out = c.release();
         return GCR_OK;
     });

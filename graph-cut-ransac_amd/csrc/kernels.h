@@ -157,6 +157,9 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
 // see k_generate_f).  Score / mask / select dispatch on the same solver.
 hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
                                GeoModel* models, hipStream_t stream);
+// Hypotheses per workgroup of the batch scorers at a launch of nh (64, 16 or
+// 4; GCR_SPLIT_H pins one for sweeps).
+int split_h(uint32_t nh);
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
                             const ScoreOut& out, hipStream_t stream, const uint32_t* hmap = nullptr,
                             const uint32_t* hcount = nullptr);
