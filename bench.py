@@ -284,7 +284,8 @@ def main():
         latency = dict(ms_median=statistics.median(lat), ms_all=lat,
                        iterations=last_stats["iteration_number"], hypotheses=last_stats["hypotheses"],
                        ms_breakdown={k: last_stats[k] for k in ("ms_setup", "ms_generate", "ms_score", "ms_replay",
-                                                                "ms_lo", "ms_refit", "ms_total")})
+                                                                "ms_lo", "ms_lo_lists", "ms_lo_fit", "ms_lo_score",
+                                                                "ms_refit", "ms_total", "graph_cut_number")})
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -354,11 +354,17 @@ struct GpuSiftSolver final : SiftSystemSolver {
     void solve(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows, double x[3]) override {
         hipStream_t s = P->ctx->stream;
         const size_t ns = si.size(), no = oi.size();
-        P->w->rf_idx.ensure(ns + no);
+        // reserve for the largest system this problem can produce (every
+        // feature an inlier, up to 2^24 rows = 512 MB): a workspace that
+        // grows with each bigger refit pays hipFree + hipMalloc (device
+        // synchronisations, ~1-2 ms) inside the timed call
+        const size_t all_s = P->dp.cls[0].n, all_o = P->dp.cls[1].n;
+        const size_t rows_max = std::max(rows, std::min<size_t>(all_s + all_o * (all_o - (all_o > 0)) / 2, 1u << 24));
+        P->w->rf_idx.ensure(all_s + all_o);
         P->w->rf_hpart.ensure(1);
         HIPC(hipMemcpyAsync(P->w->rf_idx.p, si.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
         HIPC(hipMemcpyAsync(P->w->rf_idx.p + ns, oi.data(), no * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        P->w->rf_A.ensure(4 * rows);
+        P->w->rf_A.ensure(4 * rows_max);
         double* A = P->w->rf_A.p;
         HIPC(launch_sift_rows(P->dp.cls[0], P->dp.cls[1], P->w->rf_idx.p, (uint32_t)ns, P->w->rf_idx.p + ns, (uint32_t)no,
                               rows, A, A + rows, A + 2 * rows, A + 3 * rows, s));
@@ -366,7 +372,7 @@ struct GpuSiftSolver final : SiftSystemSolver {
         if (qr_device_on() && rows >= 4 && rows <= kQrDeviceMaxRows) {
             // the QR driver's decisions on the device: one synchronisation
             P->w->rf_qrst.ensure(1);
-            P->w->rf_part.ensure((rows - 1) / kSumBlock + 1);
+            P->w->rf_part.ensure((rows_max - 1) / kSumBlock + 1);
             P->w->rf_hpart.ensure(3);
             double* const cols[4] = {A, A + rows, A + 2 * rows, A + 3 * rows};
             HIPC(launch_qr_device(cols, rows, P->w->rf_qrst.p, P->w->rf_part.p, P->w->rf_hpart.p, s));
@@ -1214,7 +1220,10 @@ private:
         const uint64_t T = prm_.max_local_optimization_number;
         while (++gc_number_ < 10) {
             bool updated = false;
+            auto tp = Clock::now();
             inlier_lists(lo_model, Tlo_, K_ == 2 ? 0 : 2, inl);
+            st_.ms_lo_lists += ms_since(tp);
+            tp = Clock::now();
             uint64_t ssz[2] = {0, 0};
             bool all_deterministic = true;
             for (int c = 0; c < K_; ++c) {
@@ -1261,12 +1270,15 @@ private:
             });
             for (uint64_t i = 0; i < ndrawn; ++i)
                 if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
+            st_.ms_lo_fit += ms_since(tp);
+            tp = Clock::now();
             if (!trial_models.empty()) {
                 trial_scores.resize(trial_models.size());
                 trial_raw.resize(2 * trial_models.size());
                 score_models(trial_models.data(), (uint32_t)trial_models.size(), trial_scores.data(),
                              trial_raw.data());
                 st_.lo_models += trial_models.size();
+                st_.ms_lo_score += ms_since(tp);
                 for (size_t q = 0; q < trial_models.size(); ++q) {
                     if (max_score.sum < trial_scores[q].sum) {
                         updated = true;

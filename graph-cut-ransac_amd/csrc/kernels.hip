@@ -1167,9 +1167,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
 // per-workgroup sequential chain of the batch scorers (~90 us at N = 10 000)
 // is the whole cost.  Here every (model, feature) pair is evaluated in
 // parallel (k_lo_values: -r^2 or +0.0 per pair plus an inlier bitmask, in
-// HBM), and one wave per model then adds the inlier values in feature order
-// from LDS (k_lo_chain), so the dependent chain holds only the inliers and no
-// compute traffic competes with it.  The sums are the reference's sequential
+// HBM), and one workgroup per model then compacts the inlier values in
+// feature order into LDS and one lane adds them (k_lo_chain), so the
+// dependent chain holds only the inliers and no compute traffic competes
+// with it.  The sums are the reference's sequential
 // sums (MSAC_scoring_function.hpp:73-85): inliers in index order, class 0
 // then class 1, the running total continuing across classes.
 //
@@ -1207,90 +1208,119 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
     }
 }
 
-constexpr uint32_t kLoSpan = 1024;      // features compacted into LDS per step
+// k_lo_chain: one 1024-thread workgroup per model, blocks of kLoBlock
+// features.  All 16 waves load the block's values and ballot words at once
+// (one memory round trip; a single wave walking 1024-feature spans spent
+// 42 us per launch at N = 10 000, mostly waiting on its span loads), compact
+// the inlier values in feature order into LDS (chunk popcounts, one wave's
+// scan), and wave 0 folds them: lane 0 the class sum, lane 1 (KIND 2) the
+// running total.  Blocks alternate between two sets of LDS buffers, so the
+// next block's loads are issued while wave 0 still folds.
+constexpr uint32_t kLoBlock = 8192;                    // features per block (128 chunks of 64)
+constexpr uint32_t kLoChunks = kLoBlock / 64;
+constexpr int kLoThreads = 1024;
+constexpr int kLoPer = kLoChunks / (kLoThreads / 64); // chunks per wave per block
 
 template <int KIND>
-__global__ __launch_bounds__(64) void k_lo_chain(uint32_t n0, uint32_t n1, uint32_t pad0, uint32_t ntot,
-                                                const double* __restrict__ vals, const uint64_t* __restrict__ bits,
-                                                ScoreOut out) {
-    __shared__ double cbuf[2][kLoSpan];
+__global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t ntot,
+                                                        const double* __restrict__ vals,
+                                                        const uint64_t* __restrict__ bits, ScoreOut out) {
+    __shared__ double cbuf[2][kLoBlock];
+    __shared__ uint32_t ccnt[2][kLoChunks];                // inliers per chunk
+    __shared__ uint32_t coff[2][kLoChunks + 1];            // exclusive prefix; [kLoChunks] = block total
     const uint32_t mi = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint64_t below = (1ull << lane) - 1ull;
-    constexpr int K = KIND == 2 ? 2 : 1;
-    // lane 0: the class sum; lane 1 (KIND 2): the running total
     constexpr int kChains = KIND == 2 ? 2 : 1;
-    double run = 0.0, hold = 0.0;
-    uint32_t cnt0 = 0, cnt1 = 0;
     const double* mv = vals + (size_t)mi * ntot;
     const uint64_t* mb = bits + (size_t)mi * ntot / 64;
-    // spans of kLoSpan features, class 0's then class 1's; the next span's
-    // values and ballot words are in flight while the current one is folded
-    const uint32_t ns0 = (pad0 + kLoSpan - 1) / kLoSpan;
-    const uint32_t nsp = ns0 + (K == 2 ? (ntot - pad0 + kLoSpan - 1) / kLoSpan : 0u);
-    auto span = [&](uint32_t sidx, uint32_t& base, uint32_t& nch) {
-        const bool c1 = sidx >= ns0;
-        const uint32_t s0 = (c1 ? sidx - ns0 : sidx) * kLoSpan;
-        const uint32_t len = c1 ? ntot - pad0 : pad0;
-        base = (c1 ? pad0 : 0u) + s0;
-        nch = min(kLoSpan, len - s0) / 64;
-    };
-    double v[kLoSpan / 64];
-    uint64_t w[kLoSpan / 64];
-    auto load = [&](uint32_t sidx) {
-        uint32_t base, nch;
-        span(sidx, base, nch);
+    const uint32_t nchunks = ntot / 64;
+    const uint32_t cb0 = pad0 / 64;                        // first class-1 chunk (nchunks: none)
+    const uint32_t nblk = (nchunks + kLoChunks - 1) / kLoChunks;
+    double run = 0.0, hold = 0.0;
+    uint32_t cnt0 = 0, cntall = 0;
+    for (uint32_t b = 0; b < nblk; ++b) {
+        const uint32_t ch0 = b * kLoChunks;
+        const uint32_t nch = min(kLoChunks, nchunks - ch0);
+        double* cb = cbuf[b & 1];
+        uint32_t* cc = ccnt[b & 1];
+        uint32_t* co = coff[b & 1];
+        // 1) this wave's chunks j = wave + 16 i: values and ballot words
+        double v[kLoPer];
+        uint64_t w[kLoPer];
 #pragma unroll
-        for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
-            const uint32_t q = ch < nch ? ch : 0;
-            v[ch] = mv[base + q * 64 + lane];
-            w[ch] = mb[base / 64 + q];
+        for (int i = 0; i < kLoPer; ++i) {
+            const uint32_t j = (uint32_t)wave + 16u * i;
+            const uint32_t q = j < nch ? j : 0u;
+            v[i] = mv[(size_t)(ch0 + q) * 64 + lane];
+            w[i] = mb[ch0 + q];
         }
-    };
-    if (nsp > 0) load(0);
-    for (uint32_t sidx = 0; sidx < nsp; ++sidx) {
-        uint32_t base, nch;
-        span(sidx, base, nch);
-        if (K == 2 && sidx == ns0 && lane == 0) {        // first class-1 span
+#pragma unroll
+        for (int i = 0; i < kLoPer; ++i) {
+            const uint32_t j = (uint32_t)wave + 16u * i;
+            if (lane == 0 && j < nch) cc[j] = (uint32_t)__builtin_popcountll(w[i]);
+        }
+        __syncthreads();
+        // 2) exclusive prefix of the chunk counts (wave 0, two chunks a lane)
+        if (wave == 0) {
+            const uint32_t a = 2u * lane < nch ? cc[2 * lane] : 0u;
+            const uint32_t c = 2u * lane + 1u < nch ? cc[2 * lane + 1] : 0u;
+            uint32_t inc = a + c;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(inc, d);
+                if (lane >= d) inc += o;
+            }
+            const uint32_t ex = inc - (a + c);
+            co[2 * lane] = ex;
+            co[2 * lane + 1] = ex + a;
+            if (lane == 63) co[kLoChunks] = inc;
+        }
+        __syncthreads();
+        // 3) in-order compaction of the inlier values
+#pragma unroll
+        for (int i = 0; i < kLoPer; ++i) {
+            const uint32_t j = (uint32_t)wave + 16u * i;
+            if (j < nch && ((w[i] >> lane) & 1ull)) cb[co[j] + (uint32_t)__builtin_popcountll(w[i] & below)] = v[i];
+        }
+        __syncthreads();
+        // 4) wave 0 folds the block; the other waves go on to the next
+        //    block's loads (the other buffer set: this one is rewritten only
+        //    after the next block's barriers, which wave 0 reaches once this
+        //    fold is done).  KIND 2: lane 0 restarts at the first class-1 value.
+        if (wave != 0) continue;
+        const uint32_t total = co[kLoChunks];
+        const bool has_b = cb0 >= ch0 && cb0 < ch0 + nch;
+        const uint32_t bpos = cb0 < ch0 ? 0u : (has_b ? co[cb0 - ch0] : total);   // values before class 1
+        cnt0 += bpos;
+        cntall += total;
+        auto fold = [&](uint32_t k, uint32_t e) {
+            if (lane >= kChains) return;
+            for (; k + 16 <= e; k += 16) {
+                double tt[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) tt[u] = cb[k + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) run += tt[u];
+            }
+            for (; k < e; ++k) run += cb[k];
+        };
+        fold(0, bpos);
+        if (KIND == 2 && has_b && lane == 0) {
             hold = run;
             run = 0.0;
         }
-        // in-order compaction of the span's inlier values into LDS
-        double* cb = cbuf[sidx & 1];
-        uint32_t off = 0;
-#pragma unroll
-        for (uint32_t ch = 0; ch < kLoSpan / 64; ++ch) {
-            if (ch < nch) {
-                if ((w[ch] >> lane) & 1ull) cb[off + (uint32_t)__builtin_popcountll(w[ch] & below)] = v[ch];
-                off += (uint32_t)__builtin_popcountll(w[ch]);
-            }
-        }
-        if (sidx < ns0) cnt0 += off;
-        else cnt1 += off;
-        if (sidx + 1 < nsp) load(sidx + 1);
-        __builtin_amdgcn_wave_barrier();
-        if (lane < kChains) {
-            // batches of 16 reads in flight, then 16 dependent adds
-            uint32_t k = 0;
-            for (; k + 16 <= off; k += 16) {
-                double t[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) t[u] = cb[k + u];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) run += t[u];
-            }
-            for (; k < off; ++k) run += cb[k];
-        }
-        __builtin_amdgcn_wave_barrier();
+        fold(bpos, total);
     }
-    const uint32_t cnt[2] = {cnt0, cnt1};
-    const double tot = KIND == 2 ? __shfl(run, 1) : run;
-    if (lane == 0) {
-        out.n0[mi] = cnt[0];
-        out.n1[mi] = cnt[1];
-        out.v0[mi] = KIND == 2 ? hold : run;
-        out.v1[mi] = KIND == 2 ? run : 0.0;
-        out.tot[mi] = tot;
+    if (wave == 0) {
+        const double tot = KIND == 2 ? __shfl(run, 1) : run;
+        if (lane == 0) {
+            out.n0[mi] = cnt0;
+            out.n1[mi] = cntall - cnt0;
+            out.v0[mi] = KIND == 2 ? hold : run;
+            out.v1[mi] = KIND == 2 ? run : 0.0;
+            out.tot[mi] = tot;
+        }
     }
 }
 
@@ -2135,14 +2165,12 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
     const uint32_t ntot = (uint32_t)small_score_pairs(p);
     if (ntot == 0) return hipErrorInvalidValue;
     const dim3 ga((ntot + 255) / 256, nm), ba(256);
-    const uint32_t n1 = p.solver == 2 ? p.cls[1].n : 0u;
     auto go = [&](auto ktag) {
         constexpr int KIND = decltype(ktag)::value;
         using M = typename ModelOf<KIND>::type;
         hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), inc, T[0], T[1],
                            pad0, ntot, vals, bits);
-        hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(64), 0, stream, p.cls[0].n, n1, pad0, ntot, vals, bits,
-                           out);
+        hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits, out);
     };
     switch (p.solver) {
         case 0: go(std::integral_constant<int, 0>{}); break;

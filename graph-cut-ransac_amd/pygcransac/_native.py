@@ -60,6 +60,9 @@ class Stats(C.Structure):
         ("ms_refit", C.c_double),
         ("ms_total", C.c_double),
         ("ms_score_kernel", C.c_double),
+        ("ms_lo_lists", C.c_double),
+        ("ms_lo_fit", C.c_double),
+        ("ms_lo_score", C.c_double),
     ]
 
     def as_dict(self):

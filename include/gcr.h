@@ -91,6 +91,9 @@ typedef struct gcr_stats {
     double score;                 /* statistics.score                               */
     double ms_setup, ms_generate, ms_score, ms_replay, ms_lo, ms_refit, ms_total;
     double ms_score_kernel;       /* summed HIP-event time of the scoring kernels   */
+    double ms_lo_lists;           /* LO: inlier lists (GPU labeling + copy back)    */
+    double ms_lo_fit;             /* LO: sample draws + least-squares fits (host)   */
+    double ms_lo_score;           /* LO: scoring the trial models (GPU)             */
 } gcr_stats;
 
 /* ---- context ---------------------------------------------------------- */

@@ -46,7 +46,8 @@ def main():
         t_abi = (time.perf_counter() - t0) * 1e3
         s = out[-1]
         rows.append(dict(py_ms=t_py, abi_ms=t_abi, **{k: s[k] for k in (
-            "ms_setup", "ms_generate", "ms_score", "ms_replay", "ms_lo", "ms_refit", "ms_total",
+            "ms_setup", "ms_generate", "ms_score", "ms_replay", "ms_lo", "ms_lo_lists", "ms_lo_fit", "ms_lo_score",
+            "ms_refit", "ms_total",
             "iteration_number", "graph_cut_number", "lo_models", "launches")}))
     for row in rows:
         print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()}))
