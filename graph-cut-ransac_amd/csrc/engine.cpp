@@ -413,7 +413,14 @@ public:
             for (size_t i = 0; i < n; ++i) fn(i);
             return;
         }
-        std::unique_lock<std::mutex> call(call_mu_);      // one job at a time
+        // one job at a time; a caller that finds the pool busy (concurrent
+        // problems on other host threads) runs its job itself instead of
+        // queueing behind the other job
+        std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
+        if (!call.owns_lock()) {
+            for (size_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
         {
             std::lock_guard<std::mutex> lk(mu_);
             job_ = &fn;
