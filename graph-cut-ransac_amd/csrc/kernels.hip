@@ -1296,12 +1296,37 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
         cntall += total;
         auto fold = [&](uint32_t k, uint32_t e) {
             if (lane >= kChains) return;
-            for (; k + 16 <= e; k += 16) {
-                double tt[16];
+            if (k + 32 <= e) {
+                // ping-pong batches of 16: the next batch's reads are in
+                // flight during the current batch's dependent adds
+                // (sched_barrier keeps the scheduler from sinking the reads
+                // back next to their adds)
+                double ta[16], tb[16];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) tt[u] = cb[k + u];
+                for (int u = 0; u < 16; ++u) ta[u] = cb[k + u];
+#pragma unroll 1
+                for (; k + 32 <= e; k += 32) {
 #pragma unroll
-                for (int u = 0; u < 16; ++u) run += tt[u];
+                    for (int u = 0; u < 16; ++u) tb[u] = cb[k + 16 + u];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) run += ta[u];
+                    __builtin_amdgcn_sched_barrier(0);
+                    // the batch after next (clamped inside the buffer: a
+                    // clamped batch lies past e and is never added)
+                    const uint32_t nx = min(k + 32, kLoBlock - 16);
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) ta[u] = cb[nx + u];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) run += tb[u];
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (k + 16 <= e) {                         // ta = cb[k, k + 16)
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) run += ta[u];
+                    k += 16;
+                }
             }
             for (; k < e; ++k) run += cb[k];
         };
