@@ -1822,4 +1822,65 @@ int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_
     });
 }
 
+int gcr_measure_hbm(gcr_ctx* ctx, size_t bytes, int iters, double* gbps_out) {
+    if (!ctx || !gbps_out || iters < 1 || bytes < 16) return set_err(GCR_EINVAL, "invalid argument");
+    bytes &= ~(size_t)15;
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(ctx->device));
+        void *src = nullptr, *dst = nullptr;
+        HIPC(hipMalloc(&src, bytes));
+        if (hipMalloc(&dst, bytes) != hipSuccess) {
+            (void)hipFree(src);
+            return set_err(GCR_ENOMEM, "hipMalloc of %zu bytes failed", bytes);
+        }
+        hipError_t e = hipMemsetAsync(src, 0x3f, bytes, ctx->stream);
+        double best = 0.0;
+        for (int it = -2; it < 2 * iters && e == hipSuccess; ++it) {      // two untimed copies first
+            e = hipEventRecord(ctx->ev0, ctx->stream);
+            if (e == hipSuccess) e = launch_hbm_copy(src, dst, bytes, it & 1, ctx->stream);
+            if (e == hipSuccess) e = hipEventRecord(ctx->ev1, ctx->stream);
+            if (e == hipSuccess) e = hipEventSynchronize(ctx->ev1);
+            float ms = 0.f;
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+            if (e == hipSuccess && it >= 0 && ms > 0.f) best = std::max(best, 2.0 * (double)bytes / (ms * 1e6));
+        }
+        (void)hipFree(src);
+        (void)hipFree(dst);
+        HIPC(e);
+        *gbps_out = best;
+        return GCR_OK;
+    });
+}
+
+int gcr_warp_perspective(gcr_ctx* ctx, const void* src, int src_h, int src_w, int channels, int dtype,
+                         const double M[9], int border_mode, const double border_value[4], void* dst, int dst_h,
+                         int dst_w) {
+    if (!ctx || !src || !M || !dst) return set_err(GCR_EINVAL, "null argument");
+    if (src_h <= 0 || src_w <= 0 || dst_h < 0 || dst_w < 0) return set_err(GCR_EINVAL, "invalid image size");
+    if (channels < 1 || channels > 4) return set_err(GCR_EINVAL, "channels must be 1..4, got %d", channels);
+    if (dtype != 0 && dtype != 1) return set_err(GCR_EINVAL, "dtype must be 0 (uint8) or 1 (float32)");
+    if (border_mode != 0 && border_mode != 1) return set_err(GCR_EINVAL, "border_mode must be 0 or 1");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(ctx->device));
+        const size_t esz = dtype == 0 ? 1 : 4;
+        const size_t sbytes = (size_t)src_h * src_w * channels * esz;
+        const size_t dbytes = (size_t)dst_h * dst_w * channels * esz;
+        WarpMap wm{};
+        for (int i = 0; i < 9; ++i) wm.m[i] = M[i];
+        for (int c = 0; c < 4; ++c) wm.border[c] = border_value ? (float)border_value[c] : 0.f;
+        void *ds = nullptr, *dd = nullptr;
+        HIPC(hipMalloc(&ds, sbytes));
+        hipError_t e = hipMalloc(&dd, dbytes ? dbytes : 1);
+        if (e == hipSuccess) e = hipMemcpyAsync(ds, src, sbytes, hipMemcpyHostToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = launch_warp(ds, src_h, src_w, channels, dtype, wm, dd, dst_h, dst_w, border_mode, ctx->stream);
+        if (e == hipSuccess && dbytes) e = hipMemcpyAsync(dst, dd, dbytes, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ds);
+        if (dd) (void)hipFree(dd);
+        HIPC(e);
+        return GCR_OK;
+    });
+}
+
 }  // extern "C"

@@ -189,5 +189,16 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
 
 // element-wise evaluation of the device math primitives (parity tests)
 hipError_t launch_math(int op, const double* a, const double* b, size_t n, double* out, hipStream_t stream);
+// perspective warp (examples/utils.py:92-123): M maps dst pixels to source
+// coordinates (row-major 3 x 3), border: constant per-channel values (mode 0)
+// or replicate (mode 1); dtype 0 = uint8, 1 = float32, channels interleaved
+struct WarpMap {
+    double m[9];
+    float border[4];
+};
+hipError_t launch_warp(const void* src, int sh, int sw, int ch, int dtype, const WarpMap& M, void* dst, int dh,
+                       int dw, int border_mode, hipStream_t stream);
+// streaming copy of `bytes` (a multiple of 16) for the HBM peak probe
+hipError_t launch_hbm_copy(const void* src, void* dst, size_t bytes, int nontemporal, hipStream_t stream);
 
 }  // namespace gcr

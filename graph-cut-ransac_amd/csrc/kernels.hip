@@ -2326,3 +2326,117 @@ extern "C" int gcr_debug_stamps(uint64_t* host, size_t bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(gcr::g_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }
 #endif
+
+namespace gcr {
+
+// --------------------------------------------------------- HBM peak probe ----
+// Streaming copy used by bench.py to measure the box's achievable HBM
+// bandwidth (the roofline's measured peak beside the 8 TB/s spec).  16-byte
+// loads and stores, a grid-stride loop with 8 independent strips per thread in
+// flight; NT = nontemporal hints (the probe reports the better of the two).
+typedef double hbm_v2d __attribute__((ext_vector_type(2)));
+template <bool NT>
+__global__ __launch_bounds__(256) void k_hbm_copy(const hbm_v2d* __restrict__ src, hbm_v2d* __restrict__ dst,
+                                                  size_t n) {
+    constexpr int U = 8;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        hbm_v2d v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + u * stride) : src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (NT) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+            else dst[i + u * stride] = v[u];
+        }
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_hbm_copy(const void* src, void* dst, size_t bytes, int nontemporal, hipStream_t stream) {
+    const size_t n = bytes / sizeof(hbm_v2d);
+    if (n == 0) return hipSuccess;
+    const dim3 grid(256 * 8), block(256);
+    if (nontemporal)
+        hipLaunchKernelGGL(k_hbm_copy<true>, grid, block, 0, stream, static_cast<const hbm_v2d*>(src),
+                           static_cast<hbm_v2d*>(dst), n);
+    else
+        hipLaunchKernelGGL(k_hbm_copy<false>, grid, block, 0, stream, static_cast<const hbm_v2d*>(src),
+                           static_cast<hbm_v2d*>(dst), n);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------ perspective warp ----
+// examples/utils.py:92-123 (perspective_warp -> cv2.warpPerspective, INTER_LINEAR):
+// every output pixel (x, y) samples the source at M (x, y, 1)^T / w, M the
+// dst -> src map, with bilinear weights over the 4 neighbours; neighbours
+// outside the source take the border (constant value, or the nearest edge
+// pixel for `replicate`).  One lane per output pixel and channel loop inside:
+// consecutive lanes read neighbouring source pixels, so the gathers coalesce
+// along rows; the output row is written contiguously.
+template <typename T>
+__device__ __forceinline__ float warp_texel(const T* __restrict__ src, int h, int w, int ch, int x, int y, int c,
+                                            int border_mode, float bval) {
+    if (x < 0 || y < 0 || x >= w || y >= h) {
+        if (border_mode == 0) return bval;
+        x = x < 0 ? 0 : (x >= w ? w - 1 : x);
+        y = y < 0 ? 0 : (y >= h ? h - 1 : y);
+    }
+    return (float)src[((size_t)y * w + x) * ch + c];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_warp(const T* __restrict__ src, int sh, int sw, int ch,
+                                              WarpMap M, T* __restrict__ dst, int dh, int dw, int border_mode) {
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= dw || y >= dh) return;
+    const double X = (double)x, Y = (double)y;
+    const double wz = M.m[6] * X + M.m[7] * Y + M.m[8];
+    const double iw = wz != 0.0 ? 1.0 / wz : 0.0;
+    const double sx = (M.m[0] * X + M.m[1] * Y + M.m[2]) * iw;
+    const double sy = (M.m[3] * X + M.m[4] * Y + M.m[5]) * iw;
+    T* out = dst + ((size_t)y * dw + x) * ch;
+    // far outside (or a point at infinity): the border alone
+    if (!(fabs(sx) < 1e9 && fabs(sy) < 1e9)) {
+        for (int c = 0; c < ch; ++c) {
+            const float v = border_mode == 0 ? M.border[c] : 0.f;
+            out[c] = (T)v;
+        }
+        return;
+    }
+    const double fx0 = floor(sx), fy0 = floor(sy);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float ax = (float)(sx - fx0), ay = (float)(sy - fy0);
+    for (int c = 0; c < ch; ++c) {
+        const float b = M.border[c];
+        const float p00 = warp_texel(src, sh, sw, ch, x0, y0, c, border_mode, b);
+        const float p01 = warp_texel(src, sh, sw, ch, x0 + 1, y0, c, border_mode, b);
+        const float p10 = warp_texel(src, sh, sw, ch, x0, y0 + 1, c, border_mode, b);
+        const float p11 = warp_texel(src, sh, sw, ch, x0 + 1, y0 + 1, c, border_mode, b);
+        const float top = p00 + ax * (p01 - p00);
+        const float bot = p10 + ax * (p11 - p10);
+        float v = top + ay * (bot - top);
+        if constexpr (sizeof(T) == 1) {
+            v = rintf(v);
+            v = v < 0.f ? 0.f : (v > 255.f ? 255.f : v);
+        }
+        out[c] = (T)v;
+    }
+}
+
+hipError_t launch_warp(const void* src, int sh, int sw, int ch, int dtype, const WarpMap& M, void* dst, int dh,
+                       int dw, int border_mode, hipStream_t stream) {
+    if (dh <= 0 || dw <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((dw + 255) / 256), (unsigned)dh), block(256);
+    if (dtype == 0)
+        hipLaunchKernelGGL(k_warp<uint8_t>, grid, block, 0, stream, static_cast<const uint8_t*>(src), sh, sw, ch, M,
+                           static_cast<uint8_t*>(dst), dh, dw, border_mode);
+    else
+        hipLaunchKernelGGL(k_warp<float>, grid, block, 0, stream, static_cast<const float*>(src), sh, sw, ch, M,
+                           static_cast<float*>(dst), dh, dw, border_mode);
+    return hipGetLastError();
+}
+
+}  // namespace gcr

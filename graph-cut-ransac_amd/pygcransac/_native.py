@@ -145,6 +145,9 @@ def _load():
     L.gcr_host_sample.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
                                   C.c_uint32, u32p]
     L.gcr_debug_math.argtypes = [vp, C.c_int, dp, dp, C.c_size_t, dp]
+    L.gcr_measure_hbm.argtypes = [vp, C.c_size_t, C.c_int, dp]
+    L.gcr_warp_perspective.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, dp, C.c_int, dp, vp, C.c_int,
+                                       C.c_int]
     L.gcr_host_fit_nonminimal.argtypes = [C.c_int, dp, C.c_size_t, dp, C.c_size_t, u32p, C.c_size_t, u32p,
                                           C.c_size_t, C.POINTER(RectModel)]
     L.gcr_debug_fit_nonminimal.argtypes = [vp, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.POINTER(RectModel)]

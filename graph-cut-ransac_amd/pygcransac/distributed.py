@@ -21,12 +21,31 @@ import numpy as np
 RECORD = 20
 
 
+# Defaults of a problem dict's optional keys, per kind: exactly the defaults of
+# the direct entry point the kind maps to (bindings.cpp:366-396 for the
+# rectification functions -- the reference fixes confidence at 0.95,
+# settings.h:60; pygcransac.findHomography / findFundamentalMatrix for the
+# correspondence kinds), so gpu_solver and batch_solver agree with each other
+# and with the direct calls when a key is omitted.
+_RECT_DEFAULTS = dict(spatial_coherence_weight=0.0, min_iteration_number=10000, max_iteration_number=10000,
+                      max_local_optimization_number=50, confidence=0.95, seed=0)
+_CORR_DEFAULTS = dict(spatial_coherence_weight=0.975, min_iteration_number=50, max_iteration_number=10000,
+                      max_local_optimization_number=50, confidence=0.99, seed=0)
+
+
+def problem_settings(problem: dict) -> dict:
+    """The run settings of a problem dict: its own keys over the defaults of
+    its kind (see _RECT_DEFAULTS / _CORR_DEFAULTS)."""
+    base = _CORR_DEFAULTS if problem["kind"] in ("homography", "fundamental") else _RECT_DEFAULTS
+    return {k: problem.get(k, v) for k, v in base.items()}
+
+
 def problem_cost(problem: dict) -> float:
     """Estimated cost of a problem: feature count x hypotheses budget."""
     n = sum(np.asarray(problem[k]).shape[0]
             for k in ("features", "scale_features", "orientation_features", "correspondences")
             if k in problem and problem[k] is not None)
-    return float(n) * float(problem.get("max_iteration_number", 10000))
+    return float(n) * float(problem_settings(problem)["max_iteration_number"])
 
 
 def assign_lpt(costs: Sequence[float], world: int) -> list[list[int]]:
@@ -121,18 +140,19 @@ def gpu_solver(device: int) -> Callable[[dict], dict]:
     from . import pygcransac as P
 
     def solve(pr: dict) -> dict:
+        st = problem_settings(pr)
         if pr["kind"] in ("homography", "fundamental"):
             fn = P.findHomography if pr["kind"] == "homography" else P.findFundamentalMatrix
-            out = fn(pr["correspondences"], 0, 0, 0, 0, threshold=pr["threshold"],
-                     conf=pr.get("confidence", 0.99), spatial_coherence_weight=pr.get("spatial_coherence_weight", 0.0),
-                     max_iters=pr.get("max_iteration_number", 10000), min_iters=pr.get("min_iteration_number", 50),
-                     lo_number=pr.get("max_local_optimization_number", 50), seed=pr.get("seed", 0), device=device,
+            out = fn(pr["correspondences"], *pr.get("image_sizes", (0, 0, 0, 0)), threshold=pr["threshold"],
+                     conf=st["confidence"], spatial_coherence_weight=st["spatial_coherence_weight"],
+                     max_iters=st["max_iteration_number"], min_iters=st["min_iteration_number"],
+                     lo_number=st["max_local_optimization_number"], seed=st["seed"], device=device,
                      return_stats=True)
             M, mask, stats = out
             return dict(H=M, model=None, num_inliers=int(mask.sum()), stats=stats, masks=(mask,))
-        common = [pr.get("spatial_coherence_weight", 0.0), pr.get("min_iteration_number", 10000),
-                  pr.get("max_iteration_number", 10000), pr.get("max_local_optimization_number", 50)]
-        kw = dict(seed=pr.get("seed", 0), confidence=pr.get("confidence", 0.95), device=device, return_stats=True)
+        common = [st["spatial_coherence_weight"], st["min_iteration_number"], st["max_iteration_number"],
+                  st["max_local_optimization_number"]]
+        kw = dict(seed=st["seed"], confidence=st["confidence"], device=device, return_stats=True)
         if pr["kind"] == "sift":
             out = P.findRectifyingHomographySIFT(pr["scale_features"], pr["orientation_features"],
                                                  pr["scale_residual_thresh"], pr["orientation_residual_thresh"],
@@ -258,14 +278,15 @@ def batch_solver(device: int = 0, concurrency: int = 4) -> Callable[[list], list
             it.f1, it.n1 = (dp(f1), f1.shape[0]) if f1 is not None else (None, 0)
             it.mask0_out = u8(m0)
             it.mask1_out = u8(m1) if m1 is not None else None
+            st = problem_settings(pr)
             p = N.default_params()
             p.scale_residual_thresh, p.orientation_residual_thresh = float(t0), float(t1)
-            p.spatial_coherence_weight = float(pr.get("spatial_coherence_weight", 0.0))
-            p.min_iteration_number = int(pr.get("min_iteration_number", 10000))
-            p.max_iteration_number = int(pr.get("max_iteration_number", 10000))
-            p.max_local_optimization_number = int(pr.get("max_local_optimization_number", 50))
-            p.seed = int(pr.get("seed", 0))
-            p.confidence = float(pr.get("confidence", 0.95))
+            p.spatial_coherence_weight = float(st["spatial_coherence_weight"])
+            p.min_iteration_number = int(st["min_iteration_number"])
+            p.max_iteration_number = int(st["max_iteration_number"])
+            p.max_local_optimization_number = int(st["max_local_optimization_number"])
+            p.seed = int(st["seed"])
+            p.confidence = float(st["confidence"])
             it.params = p
         N.check(N.lib.gcr_solve_batch(device, items, len(problems), concurrency))
         out = []

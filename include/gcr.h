@@ -249,6 +249,20 @@ int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream
 /* device evaluation of the same primitives over arrays (GPU parity tests):
  * op 0 log(a), 1 pow_m3(a), 2 atan2(a, b), 3 a / b, 4 sqrt(a) */
 int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out);
+/* perspective_warp's resampling (examples/utils.py:92-123, cv2.warpPerspective
+ * with INTER_LINEAR): dst pixel (x, y) <- bilinear sample of src at
+ * M (x, y, 1)^T / w, M = the dst -> src map (the inverse of the translated
+ * homography), row-major.  Host buffers, channels interleaved, 1 <= channels
+ * <= 4; dtype 0 = uint8 (rounded, saturated), 1 = float32.  border_mode 0 =
+ * constant border_value[c], 1 = replicate the nearest edge pixel. */
+int gcr_warp_perspective(gcr_ctx* ctx, const void* src, int src_h, int src_w, int channels, int dtype,
+                         const double M[9], int border_mode, const double border_value[4], void* dst, int dst_h,
+                         int dst_w);
+/* measurement (bench.py): achievable HBM bandwidth of the device, GB/s of
+ * read + write traffic of a streaming device-to-device copy of `bytes` bytes,
+ * best of `iters` timed copies of each of two variants, plain and nontemporal
+ * (no reference counterpart) */
+int gcr_measure_hbm(gcr_ctx* ctx, size_t bytes, int iters, double* gbps_out);
 
 #ifdef __cplusplus
 }

@@ -128,3 +128,29 @@ def test_allgather_callback_gloo_world2(tmp_path):
         out = json.load(open(tmp_path / f"ag{r}.json"))
         assert out["rcs"] == [0, 0, 0]
         assert out["recv"] == exp
+
+
+def test_problem_defaults_are_the_direct_entry_points_defaults():
+    # gpu_solver and batch_solver fill omitted keys from one per-kind table,
+    # which must equal the defaults of the direct call each kind maps to
+    import inspect
+
+    import pygcransac as P
+    from pygcransac import distributed as D
+
+    sig = inspect.signature(P.findHomography).parameters
+    corr = D.problem_settings({"kind": "homography"})
+    assert corr == D.problem_settings({"kind": "fundamental"})
+    assert corr["confidence"] == sig["conf"].default
+    assert corr["spatial_coherence_weight"] == sig["spatial_coherence_weight"].default
+    assert corr["max_iteration_number"] == sig["max_iters"].default
+    assert corr["min_iteration_number"] == sig["min_iters"].default
+    assert corr["max_local_optimization_number"] == sig["lo_number"].default
+    sig = inspect.signature(P.findRectifyingHomographySIFT).parameters
+    for kind in ("sift", "scale_only", "scale_only_original"):
+        rect = D.problem_settings({"kind": kind})
+        for k in ("spatial_coherence_weight", "min_iteration_number", "max_iteration_number",
+                  "max_local_optimization_number"):
+            assert rect[k] == sig[k].default, (kind, k)
+        assert rect["confidence"] == 0.95          # settings.h:60, fixed by the reference
+    assert D.problem_settings({"kind": "sift", "seed": 5, "confidence": 0.99})["seed"] == 5

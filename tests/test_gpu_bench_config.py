@@ -1,0 +1,147 @@
+"""Parity of the EXACT kernels behind bench.py's numbers, at the bench's own
+configurations (run on an MI355X: pytest -m gpu).
+
+bench.py's step is gcr_problem_verify_batches: at 4096 slots per launch the
+fused generate + score + per-workgroup-best kernel k_score_fm<K, 16, true>
+plus k_select_wg; at 16384 slots k_score_split<K, 64, 120, true>; the
+homography generates in k_generate<3, 16> and scores in k_score_fm<3, 16,
+false>; the fundamental matrix at 3712 slots (bench F_SLOTS) in
+k_generate_f + k_compact + k_score_split<4, 16, 420, false>.  Each batch's
+record is checked against a pure ORACLE replay of the same slots: the
+oracle's Philox sampler and minimal solvers (O.slot / h_slot / f_slot), its
+twin-math MSAC score of every model, and the reference's update rule
+`best < score && isValidModel` in slot order (GCRANSAC.h:440-446,
+MSAC_scoring_function.hpp:108-127).  Full-size problems (M2 5000 + 5000, M1
+10 000, H 5000, F 10 000 at 80 % outliers), the bench's seed, three
+consecutive batches from an unaligned slot.
+"""
+import ctypes as C
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from gcr_testutil import CorrProblem, Problem, bits
+from pygcransac import _native as N
+from pygcransac import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20251121          # bench.py's problem and sampler seed (rank 0)
+NB = 3
+SLOT0 = 7
+THREADS = 16             # the box's CPU share; ctypes releases the GIL in the oracle
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if N.lib.gcr_device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    N.context(0)
+    O.lib()
+
+
+def _pmap(fn, items):
+    with ThreadPoolExecutor(THREADS) as ex:
+        return list(ex.map(fn, items, chunksize=64))
+
+
+def _verify(h, thr0, thr1, nslots):
+    p = N.default_params()
+    p.scale_residual_thresh, p.orientation_residual_thresh, p.seed = thr0, thr1, SEED
+    res = (N.BatchResult * NB)()
+    st = N.Stats()
+    N.check(N.lib.gcr_problem_verify_batches(h, C.byref(p), SLOT0, nslots, NB, res, C.byref(st)))
+    return res
+
+
+def _rect_oracle_slot(args):
+    kind, f0, f1, thr0, thr1, s = args
+    inc, m = O.slot(kind, f0, f1, SEED, s)
+    if inc > 101:
+        return inc, None, None
+    sc = O.score(kind, f0, f1, m, thr0, thr1)
+    return inc, m, sc
+
+
+def _rect_problem(kind):
+    if kind == N.SOLVER_SIFT22:
+        fs, fo, _, _, ts, to = S.problem_m2(5000, 5000, seed=SEED)
+        return fs, fo, ts, to
+    f, _, thr = S.problem_m1(10_000, seed=SEED)
+    return f, None, thr, 0.0
+
+
+@pytest.mark.parametrize("nslots", [4096, 16384])
+@pytest.mark.parametrize("kind", [N.SOLVER_SIFT22, N.SOLVER_SCALE3])
+def test_fused_verify_kernel_matches_oracle_replay_at_bench_config(kind, nslots):
+    f0, f1, thr0, thr1 = _rect_problem(kind)
+    prob = Problem(kind, f0, f1)
+    res = _verify(prob.h, thr0, thr1, nslots)
+    for b in range(NB):
+        s0 = SLOT0 + b * nslots
+        outs = _pmap(_rect_oracle_slot, [(kind, prob.f0, prob.f1, thr0, thr1, s) for s in range(s0, s0 + nslots)])
+        models = iters = 0
+        best, bslot, bcnt, bmodel = 0.0, -1, None, None
+        for j, (inc, m, sc) in enumerate(outs):
+            iters += inc
+            if m is None:
+                continue
+            models += 1
+            valid = kind != N.SOLVER_SIFT22 or max(abs(m[3]), abs(m[4])) < 1e-3     # two_sift.hpp:45-61
+            if best < sc["value"] and valid:
+                best, bslot, bcnt, bmodel = sc["value"], s0 + j, [int(c) for c in sc["counts"]], m
+        r = res[b]
+        assert r.models == models, (b, r.models, models)
+        assert r.iterations == iters, b
+        assert r.best_slot == bslot, (b, r.best_slot, bslot)
+        assert bslot >= 0                        # 50 % outliers: every batch finds a model
+        assert bits(r.best_score) == bits(best), b
+        cnt = [r.best_inliers[0], r.best_inliers[1]]
+        assert cnt == bcnt, (b, cnt, bcnt)
+        got = [r.best_model.x0, r.best_model.y0, r.best_model.s, r.best_model.h7, r.best_model.h8,
+               r.best_model.alpha, r.best_model.phi]
+        assert np.array_equal(bits(got), bits(bmodel)), b
+
+
+def _h_oracle_slot(args):
+    corr, thr, s = args
+    inc, h = O.h_slot(corr, SEED, s)
+    if inc > 101:
+        return inc, []
+    return inc, [O.h_score(corr, h, thr)]
+
+
+def _f_oracle_slot(args):
+    corr, thr, s = args
+    inc, ms = O.f_slot(corr, SEED, s)
+    return inc, [O.f_score(corr, m, thr) for m in ms]
+
+
+@pytest.mark.parametrize("solver,nslots", [(N.SOLVER_HOMOGRAPHY4, 4096), (N.SOLVER_FUNDAMENTAL7, 3712)])
+def test_correspondence_verify_matches_oracle_replay_at_bench_config(solver, nslots):
+    if solver == N.SOLVER_HOMOGRAPHY4:
+        corr, _, _, thr = S.problem_h(5000, 0.5, seed=SEED)
+        fn = _h_oracle_slot
+    else:
+        corr, _, _, thr = S.problem_f(10_000, 0.8, seed=SEED)
+        fn = _f_oracle_slot
+    prob = CorrProblem(solver, corr)
+    res = _verify(prob.h, thr, 0.0, nslots)
+    for b in range(NB):
+        s0 = SLOT0 + b * nslots
+        outs = _pmap(fn, [(prob.c, thr, s) for s in range(s0, s0 + nslots)])
+        models = iters = 0
+        best, bslot, bcnt = 0.0, -1, None
+        for j, (inc, scores) in enumerate(outs):
+            iters += inc
+            for sc in scores:
+                models += 1
+                if best < sc["value"]:
+                    best, bslot, bcnt = sc["value"], s0 + j, sc["count"]
+        r = res[b]
+        assert r.models == models and r.iterations == iters, b
+        assert r.best_slot == bslot and bslot >= 0, (b, r.best_slot, bslot)
+        assert bits(r.best_score) == bits(best), b
+        assert r.best_inliers[0] == bcnt, b
