@@ -47,6 +47,7 @@
 #include "kernels.h"
 #include "philox.h"
 #include "qr3.h"
+#include "graphcut.h"
 
 using namespace gcr;
 
@@ -192,6 +193,8 @@ struct Workspace {
     DevBuf<uint8_t> mask[2];
     PinBuf<uint8_t> h_mask[2];
     DevBuf<uint8_t> mask_all;           // inlier_lists: both classes, one copy back
+    DevBuf<double> r2;                  // graph-cut labeling: squared residuals of the LO model
+    PinBuf<double> h_r2;
     DevBuf<double> sm_vals;             // launch_score_small: pair values
     DevBuf<uint64_t> sm_bits;           // launch_score_small: inlier bitmasks
     PinBuf<uint8_t> h_mask_all;
@@ -662,6 +665,8 @@ struct RectTraits {
                            hipStream_t s) {
         return launch_mask(P->dp, cls, m, rule, T, lambda, mk, s);
     }
+    // the rectification entry points never have pairwise terms (empty grid)
+    static hipError_t sqres(gcr_problem*, const Model&, double*, hipStream_t) { return hipErrorNotSupported; }
     static hipError_t score_live(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t nh,
                                  uint32_t, const ScoreOut& out, hipStream_t s) {
         return launch_score(P->dp, T, m, inc, nh, true, out, s);
@@ -704,6 +709,9 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     static hipError_t mask(gcr_problem* P, int, const Model& m, int rule, double T, double lambda, uint8_t* mk,
                            hipStream_t s) {
         return launch_mask_geo(P->dp, m, rule, T, lambda, mk, s);
+    }
+    static hipError_t sqres(gcr_problem* P, const Model& m, double* r2, hipStream_t s) {
+        return launch_sqres_geo(P->dp, m, r2, s);
     }
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
@@ -989,6 +997,25 @@ private:
 
     bool valid_model(const Model& m) const { return Tr::valid(P_->solver, m); }
 
+    // neighbourhood graph (homography / fundamental matrix with a grid and
+    // lambda > 0): the grid's edges are built once per run, on first use
+    NeighbourEdges edges_;
+    MaxFlow maxflow_;
+    std::vector<double> gc_q_;
+    int graph_state_ = -1;        // -1 unknown, 0 no pairwise terms, 1 edges_ built
+    bool use_graph() {
+        if (graph_state_ < 0) {
+            graph_state_ = 0;
+            if (P_->solver >= 3 && prm_.cell_number > 0 && prm_.spatial_coherence_weight > 0) {
+                const HostClass& c = P_->hc[0];
+                const double* cols[4] = {c.x.data(), c.y.data(), c.a.data(), c.c0.data()};
+                grid_edges(cols, 4, c.n, prm_.cell_size, prm_.cell_number, edges_);
+                graph_state_ = edges_.size() > 0 ? 1 : 0;
+            }
+        }
+        return graph_state_ == 1;
+    }
+
     HScore finish(const uint32_t rn[2], double v0, double v1, double tot) const {
         HScore s;
         s.n[0] = rn[0];
@@ -1192,6 +1219,22 @@ private:
     // Inlier index lists of one model: rule 0 with thresholds T, or (1-class
     // LO) the graph-cut labeling (rule 2).
     void inlier_lists(const Model& model, const double T[2], int rule, std::vector<uint32_t> lists[2]) {
+        if (rule == 2 && use_graph()) {
+            // labeling() with pairwise terms (GCRANSAC.h:759-870): the LO
+            // model's squared residuals from the GPU, the st-mincut on the host
+            const size_t n = N_[0];
+            P_->w->r2.ensure(n);
+            P_->w->h_r2.ensure(n);
+            HIPC(Tr::sqres(P_, model, P_->w->r2.p, s_));
+            HIPC(hipMemcpyAsync(P_->w->h_r2.p, P_->w->r2.p, n * sizeof(double), hipMemcpyDeviceToHost, s_));
+            HIPC(hipStreamSynchronize(s_));
+            st_.launches += 1;
+            lists[0].clear();
+            lists[1].clear();
+            graphcut_labeling(P_->w->h_r2.p, n, T[0], prm_.spatial_coherence_weight, edges_, maxflow_, gc_q_,
+                              lists[0]);
+            return;
+        }
         const size_t tot = N_[0] + (K_ == 2 ? N_[1] : 0);
         P_->w->mask_all.ensure(tot);
         P_->w->h_mask_all.ensure(tot);
@@ -1337,7 +1380,14 @@ int check_params(const gcr_params* p, int solver) {
     if (!p) return set_err(GCR_EINVAL, "null params");
     if (!(p->confidence > 0.0 && p->confidence < 1.0))
         return set_err(GCR_EINVAL, "confidence must be in (0, 1)");
-    (void)solver;
+    if (p->cell_number > 0) {
+        if (solver < 3)
+            return set_err(GCR_EINVAL, "a neighbourhood grid is only supported for the homography and fundamental "
+                                       "matrix estimators (the rectification entry points use an empty grid)");
+        for (int d = 0; d < 4; ++d)
+            if (!(p->cell_size[d] > 0.0) || !std::isfinite(p->cell_size[d]))
+                return set_err(GCR_EINVAL, "neighbourhood cell sizes must be positive and finite");
+    }
     return GCR_OK;
 }
 
@@ -1879,6 +1929,70 @@ int gcr_warp_perspective(gcr_ctx* ctx, const void* src, int src_h, int src_w, in
         (void)hipFree(ds);
         if (dd) (void)hipFree(dd);
         HIPC(e);
+        return GCR_OK;
+    });
+}
+
+int gcr_host_grid_edges(const double* points, size_t n, int dims, const double* cell_size, uint64_t cell_number,
+                        uint32_t* edges_out, size_t cap, size_t* m_out) {
+    if ((!points && n) || !cell_size || !m_out || dims < 1 || dims > 4 || (cap && !edges_out))
+        return set_err(GCR_EINVAL, "invalid argument");
+    return guard([&]() -> int {
+        std::vector<double> cols[4];
+        const double* cp[4] = {};
+        for (int d = 0; d < dims; ++d) {
+            cols[d].resize(n);
+            for (size_t i = 0; i < n; ++i) cols[d][i] = points[i * dims + d];
+            cp[d] = cols[d].data();
+        }
+        NeighbourEdges e;
+        grid_edges(cp, dims, n, cell_size, cell_number, e);
+        *m_out = e.size();
+        for (size_t k = 0; k < e.size() && k < cap; ++k) {
+            edges_out[2 * k] = e.u[k];
+            edges_out[2 * k + 1] = e.v[k];
+        }
+        return GCR_OK;
+    });
+}
+
+int gcr_host_bk_energy(size_t n, const double* unary, const uint32_t* edges, const double* pair, size_t m,
+                       uint8_t* seg) {
+    if ((!unary && n) || (m && (!edges || !pair)) || (!seg && n)) return set_err(GCR_EINVAL, "null argument");
+    return guard([&]() -> int {
+        MaxFlow g;
+        g.reset(n, m);
+        for (size_t i = 0; i < n; ++i) g.add_term1((int32_t)i, unary[2 * i], unary[2 * i + 1]);
+        for (size_t k = 0; k < m; ++k) {
+            if (edges[2 * k] >= n || edges[2 * k + 1] >= n || edges[2 * k] == edges[2 * k + 1])
+                return set_err(GCR_EINVAL, "invalid edge %zu", k);
+            g.add_term2((int32_t)edges[2 * k], (int32_t)edges[2 * k + 1], pair[4 * k], pair[4 * k + 1],
+                        pair[4 * k + 2], pair[4 * k + 3]);
+        }
+        g.maxflow();
+        for (size_t i = 0; i < n; ++i) seg[i] = g.is_sink((int32_t)i) ? 1 : 0;
+        return GCR_OK;
+    });
+}
+
+int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, const uint32_t* edges, size_t m,
+                      uint8_t* seg) {
+    if ((!r2 && n) || (m && !edges) || (!seg && n)) return set_err(GCR_EINVAL, "null argument");
+    return guard([&]() -> int {
+        NeighbourEdges e;
+        e.u.resize(m);
+        e.v.resize(m);
+        for (size_t k = 0; k < m; ++k) {
+            e.u[k] = edges[2 * k];
+            e.v[k] = edges[2 * k + 1];
+            if (e.u[k] >= n || e.v[k] >= n || e.u[k] == e.v[k]) return set_err(GCR_EINVAL, "invalid edge %zu", k);
+        }
+        MaxFlow g;
+        std::vector<double> q;
+        std::vector<uint32_t> inl;
+        graphcut_labeling(r2, n, sqt, lambda, e, g, q, inl);
+        std::memset(seg, 0, n);
+        for (uint32_t i : inl) seg[i] = 1;
         return GCR_OK;
     });
 }

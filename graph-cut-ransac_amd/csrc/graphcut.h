@@ -1,0 +1,414 @@
+// graphcut.h -- host graph-cut labeling for the 1-class local optimisation:
+// the neighbourhood grid's edge list and a Boykov-Kolmogorov st-mincut.
+//
+// GCRANSAC::labeling (HDR/GCRANSAC.h:759-870) builds, per graph-cut round, an
+// Energy<double,double,double> (HDR/energy.h:204-245) over the points: unary
+// terms from the truncated quadratic cost of the LO model, and for
+// lambda > 0 a pairwise term for every pair of points that share a cell of the
+// neighbourhood grid (neighborhood/grid_neighborhood_graph.h:229-301), then
+// runs BK max-flow (HDR/graph.h, graph.ti, maxflow.ti) and returns the SINK
+// nodes as inliers.  The reference's own entry points build the grid over an
+// empty point set (gcransac_python.cpp:60-67), so only the correspondence
+// estimators (findHomography / findFundamentalMatrix, an extension here) ever
+// have pairwise terms.
+//
+// The cut found is the minimal sink side (the nodes that can still reach the
+// sink), which is unique for exact arithmetic; to stay bit-identical with the
+// reference under floating-point rounding the max-flow below performs the
+// reference's operations in the reference's order: arcs in sister pairs
+// prepended to their tail's list, the two-queue active list, orphans at the
+// front after an augmentation and at the rear during adoption, the TS/DIST
+// origin heuristics.  The data layout is flat arrays with 32-bit indices (no
+// pointers, no block allocator) sized once and reused across rounds.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <numeric>
+#include <vector>
+
+namespace gcr {
+
+// Edges of the neighbourhood grid in labeling()'s order (GCRANSAC.h:821-857):
+// for every point i in row order, every later point of its cell, ascending.
+// The cell of a point is sum_d idx_d * cell_number^d (size_t arithmetic) with
+// idx_d = floor(coord_d / cell_size_d) converted to size_t as on x86-64 (the
+// 64-bit two's-complement value; 2^63 when out of range), grid_neighborhood_
+// graph.h:246-267 / GridCell :70-82; cells are keyed by that index alone.
+struct NeighbourEdges {
+    std::vector<uint32_t> u, v;
+    size_t size() const { return u.size(); }
+};
+
+inline uint64_t grid_axis_index(double v) {
+    const double f = std::floor(v);
+    if (!(f >= -9.2233720368547758e18 && f < 9.2233720368547758e18)) return (uint64_t)1 << 63;
+    return (uint64_t)(int64_t)f;
+}
+
+// coords: `dims` column pointers of n values each
+inline void grid_edges(const double* const* coords, int dims, size_t n, const double* cell_size,
+                       uint64_t cell_number, NeighbourEdges& out) {
+    out.u.clear();
+    out.v.clear();
+    std::vector<uint64_t> key(n);
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t k = 0, off = 1;
+        for (int d = 0; d < dims; ++d) {
+            k += off * grid_axis_index(coords[d][i] / cell_size[d]);
+            off *= cell_number;
+        }
+        key[i] = k;
+    }
+    std::vector<uint32_t> order(n);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    // position of every point inside its cell's (ascending) member list
+    std::vector<uint32_t> cell_end(n), pos(n);
+    for (size_t s = 0; s < n;) {
+        size_t e = s;
+        while (e < n && key[order[e]] == key[order[s]]) ++e;
+        for (size_t q = s; q < e; ++q) {
+            pos[order[q]] = (uint32_t)q;
+            cell_end[order[q]] = (uint32_t)e;
+        }
+        s = e;
+    }
+    size_t m = 0;
+    for (size_t i = 0; i < n; ++i) m += cell_end[i] - pos[i] - 1;
+    out.u.reserve(m);
+    out.v.reserve(m);
+    for (size_t i = 0; i < n; ++i)
+        for (uint32_t q = pos[i] + 1; q < cell_end[i]; ++q) {
+            out.u.push_back((uint32_t)i);
+            out.v.push_back(order[q]);
+        }
+}
+
+// Boykov-Kolmogorov max-flow, Graph<double,double,double> semantics.
+class MaxFlow {
+public:
+    void reset(size_t n_nodes, size_t n_edges) {
+        n_ = n_nodes;
+        first_.assign(n_, kNone);
+        parent_.assign(n_, kNone);
+        next_.assign(n_, kNone);
+        ts_.assign(n_, 0);
+        dist_.assign(n_, 0);
+        sink_.assign(n_, 0);
+        tr_.assign(n_, 0.0);
+        head_.clear();
+        anext_.clear();
+        rcap_.clear();
+        head_.reserve(2 * n_edges);
+        anext_.reserve(2 * n_edges);
+        rcap_.reserve(2 * n_edges);
+    }
+    // Graph::add_tweights (graph.h:405-418)
+    void add_tweights(int32_t i, double cap_source, double cap_sink) {
+        const double delta = tr_[i];
+        if (delta > 0) cap_source += delta;
+        else cap_sink -= delta;
+        tr_[i] = cap_source - cap_sink;
+    }
+    // Graph::add_edge (graph.h:420-452): arc 2k = i -> j, arc 2k+1 = j -> i
+    void add_edge(int32_t i, int32_t j, double cap, double rev_cap) {
+        const int32_t a = (int32_t)head_.size();
+        head_.push_back(j);
+        anext_.push_back(first_[i]);
+        rcap_.push_back(cap);
+        first_[i] = a;
+        head_.push_back(i);
+        anext_.push_back(first_[j]);
+        rcap_.push_back(rev_cap);
+        first_[j] = a + 1;
+    }
+    // Energy::add_term1 / add_term2 (energy.h:204-245)
+    void add_term1(int32_t x, double A, double B) { add_tweights(x, B, A); }
+    void add_term2(int32_t x, int32_t y, double A, double B, double C, double D) {
+        add_tweights(x, D, A);
+        B -= A;
+        C -= D;
+        if (B < 0) {
+            add_tweights(x, 0, B);
+            add_tweights(y, 0, -B);
+            add_edge(x, y, 0, B + C);
+        } else if (C < 0) {
+            add_tweights(x, 0, -C);
+            add_tweights(y, 0, C);
+            add_edge(x, y, B + C, 0);
+        } else {
+            add_edge(x, y, B, C);
+        }
+    }
+    // what_segment (graph.h:476-487) with the default SOURCE: 1 = SINK
+    bool is_sink(int32_t i) const { return parent_[i] != kNone && sink_[i]; }
+
+    // Graph::maxflow (maxflow.ti:463-597), first call (no tree reuse)
+    void maxflow() {
+        init();
+        int32_t cur = kNone;
+        while (true) {
+            int32_t i = cur;
+            if (i != kNone) {
+                next_[i] = kNone;
+                if (parent_[i] == kNone) i = kNone;
+            }
+            if (i == kNone) {
+                i = next_active();
+                if (i == kNone) break;
+            }
+            int32_t a;
+            if (!sink_[i]) {                              // grow the source tree
+                for (a = first_[i]; a != kNone; a = anext_[a])
+                    if (rcap_[a] != 0.0) {
+                        const int32_t j = head_[a];
+                        if (parent_[j] == kNone) {
+                            sink_[j] = 0;
+                            parent_[j] = a ^ 1;
+                            ts_[j] = ts_[i];
+                            dist_[j] = dist_[i] + 1;
+                            set_active(j);
+                        } else if (sink_[j]) {
+                            break;
+                        } else if (ts_[j] <= ts_[i] && dist_[j] > dist_[i]) {
+                            parent_[j] = a ^ 1;
+                            ts_[j] = ts_[i];
+                            dist_[j] = dist_[i] + 1;
+                        }
+                    }
+            } else {                                      // grow the sink tree
+                for (a = first_[i]; a != kNone; a = anext_[a])
+                    if (rcap_[a ^ 1] != 0.0) {
+                        const int32_t j = head_[a];
+                        if (parent_[j] == kNone) {
+                            sink_[j] = 1;
+                            parent_[j] = a ^ 1;
+                            ts_[j] = ts_[i];
+                            dist_[j] = dist_[i] + 1;
+                            set_active(j);
+                        } else if (!sink_[j]) {
+                            a = a ^ 1;
+                            break;
+                        } else if (ts_[j] <= ts_[i] && dist_[j] > dist_[i]) {
+                            parent_[j] = a ^ 1;
+                            ts_[j] = ts_[i];
+                            dist_[j] = dist_[i] + 1;
+                        }
+                    }
+            }
+            ++time_;
+            if (a != kNone) {
+                next_[i] = i;                             // keep i active
+                cur = i;
+                augment(a);
+                // adoption (maxflow.ti:560-583): the orphan list is the
+                // augmentation's front insertions, i.e. their reverse order;
+                // each orphan is processed with everything its processing
+                // appends before the next one
+                for (size_t k = aug_.size(); k-- > 0;) {
+                    adopt_.clear();
+                    adopt_.push_back(aug_[k]);
+                    for (size_t h = 0; h < adopt_.size(); ++h) {
+                        const int32_t o = adopt_[h];
+                        if (sink_[o]) process_orphan<true>(o);
+                        else process_orphan<false>(o);
+                    }
+                }
+                aug_.clear();
+            } else {
+                cur = kNone;
+            }
+        }
+    }
+
+private:
+    static constexpr int32_t kNone = -1, kTerminal = -2, kOrphan = -3;
+    static constexpr int kInfD = 0x7fffffff;
+    size_t n_ = 0;
+    std::vector<int32_t> first_, parent_, next_;
+    std::vector<int> ts_, dist_;
+    std::vector<uint8_t> sink_;
+    std::vector<double> tr_;
+    std::vector<int32_t> head_, anext_;
+    std::vector<double> rcap_;
+    int32_t qf_[2] = {kNone, kNone}, ql_[2] = {kNone, kNone};
+    std::vector<int32_t> aug_, adopt_;
+    int time_ = 0;
+
+    void set_active(int32_t i) {
+        if (next_[i] == kNone) {
+            if (ql_[1] != kNone) next_[ql_[1]] = i;
+            else qf_[1] = i;
+            ql_[1] = i;
+            next_[i] = i;
+        }
+    }
+    int32_t next_active() {
+        while (true) {
+            int32_t i = qf_[0];
+            if (i == kNone) {
+                qf_[0] = i = qf_[1];
+                ql_[0] = ql_[1];
+                qf_[1] = ql_[1] = kNone;
+                if (i == kNone) return kNone;
+            }
+            if (next_[i] == i) qf_[0] = ql_[0] = kNone;
+            else qf_[0] = next_[i];
+            next_[i] = kNone;
+            if (parent_[i] != kNone) return i;
+        }
+    }
+    void init() {
+        qf_[0] = ql_[0] = qf_[1] = ql_[1] = kNone;
+        aug_.clear();
+        time_ = 0;
+        for (size_t k = 0; k < n_; ++k) {
+            const int32_t i = (int32_t)k;
+            next_[i] = kNone;
+            ts_[i] = 0;
+            if (tr_[i] > 0) {
+                sink_[i] = 0;
+                parent_[i] = kTerminal;
+                set_active(i);
+                dist_[i] = 1;
+            } else if (tr_[i] < 0) {
+                sink_[i] = 1;
+                parent_[i] = kTerminal;
+                set_active(i);
+                dist_[i] = 1;
+            } else {
+                parent_[i] = kNone;
+            }
+        }
+    }
+    void orphan_front(int32_t i) {
+        parent_[i] = kOrphan;
+        aug_.push_back(i);
+    }
+    // maxflow.ti augment: the middle arc runs from the source tree to the sink tree
+    void augment(int32_t mid) {
+        double bottleneck = rcap_[mid];
+        int32_t i, a;
+        for (i = head_[mid ^ 1];; i = head_[a]) {
+            a = parent_[i];
+            if (a == kTerminal) break;
+            if (bottleneck > rcap_[a ^ 1]) bottleneck = rcap_[a ^ 1];
+        }
+        if (bottleneck > tr_[i]) bottleneck = tr_[i];
+        for (i = head_[mid];; i = head_[a]) {
+            a = parent_[i];
+            if (a == kTerminal) break;
+            if (bottleneck > rcap_[a]) bottleneck = rcap_[a];
+        }
+        if (bottleneck > -tr_[i]) bottleneck = -tr_[i];
+        rcap_[mid ^ 1] += bottleneck;
+        rcap_[mid] -= bottleneck;
+        for (i = head_[mid ^ 1];; i = head_[a]) {
+            a = parent_[i];
+            if (a == kTerminal) break;
+            rcap_[a] += bottleneck;
+            rcap_[a ^ 1] -= bottleneck;
+            if (rcap_[a ^ 1] == 0.0) orphan_front(i);
+        }
+        tr_[i] -= bottleneck;
+        if (tr_[i] == 0.0) orphan_front(i);
+        for (i = head_[mid];; i = head_[a]) {
+            a = parent_[i];
+            if (a == kTerminal) break;
+            rcap_[a ^ 1] += bottleneck;
+            rcap_[a] -= bottleneck;
+            if (rcap_[a] == 0.0) orphan_front(i);
+        }
+        tr_[i] += bottleneck;
+        if (tr_[i] == 0.0) orphan_front(i);
+    }
+    // process_source_orphan / process_sink_orphan (maxflow.ti:326-459)
+    template <bool kSink>
+    void process_orphan(int32_t i) {
+        int32_t a0_min = kNone;
+        int d_min = kInfD;
+        for (int32_t a0 = first_[i]; a0 != kNone; a0 = anext_[a0]) {
+            if ((kSink ? rcap_[a0] : rcap_[a0 ^ 1]) == 0.0) continue;
+            int32_t j = head_[a0];
+            if ((bool)sink_[j] != kSink || parent_[j] == kNone) continue;
+            int d = 0;
+            while (true) {                                // origin of j
+                if (ts_[j] == time_) {
+                    d += dist_[j];
+                    break;
+                }
+                const int32_t a = parent_[j];
+                d++;
+                if (a == kTerminal) {
+                    ts_[j] = time_;
+                    dist_[j] = 1;
+                    break;
+                }
+                if (a == kOrphan) {
+                    d = kInfD;
+                    break;
+                }
+                j = head_[a];
+            }
+            if (d < kInfD) {
+                if (d < d_min) {
+                    a0_min = a0;
+                    d_min = d;
+                }
+                for (j = head_[a0]; ts_[j] != time_; j = head_[parent_[j]]) {
+                    ts_[j] = time_;
+                    dist_[j] = d--;
+                }
+            }
+        }
+        parent_[i] = a0_min;
+        if (a0_min != kNone) {
+            ts_[i] = time_;
+            dist_[i] = d_min + 1;
+            return;
+        }
+        for (int32_t a0 = first_[i]; a0 != kNone; a0 = anext_[a0]) {
+            const int32_t j = head_[a0];
+            const int32_t a = parent_[j];
+            if ((bool)sink_[j] != kSink || a == kNone) continue;
+            if ((kSink ? rcap_[a0] : rcap_[a0 ^ 1]) != 0.0) set_active(j);
+            if (a != kTerminal && a != kOrphan && head_[a] == i) {
+                parent_[j] = kOrphan;                     // set_orphan_rear
+                adopt_.push_back(j);
+            }
+        }
+    }
+};
+
+// labeling() of GCRANSAC.h:759-870 for one class: r2 = squared residuals of
+// the LO model, sqt = squared truncated threshold, pairwise terms over
+// `edges` when lambda > 0.  Appends the SINK points (inliers) in order.
+inline void graphcut_labeling(const double* r2, size_t n, double sqt, double lambda, const NeighbourEdges& edges,
+                              MaxFlow& g, std::vector<double>& q, std::vector<uint32_t>& inliers) {
+    const double oml = 1.0 - lambda;
+    const bool pairwise = lambda > 0 && edges.size() > 0;
+    g.reset(n, pairwise ? edges.size() : 0);
+    q.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+        const double qq = std::clamp(r2[i] / sqt, 0.0, 1.0);
+        q[i] = qq;
+        const double energy = 1.0 - qq;
+        if (r2[i] <= sqt) g.add_term1((int32_t)i, oml * energy, 0.0);
+        else g.add_term1((int32_t)i, 0.0, oml * (1.0 - energy));
+    }
+    if (pairwise) {
+        const double e11 = 0;
+        for (size_t k = 0; k < edges.size(); ++k) {
+            const uint32_t i = edges.u[k], j = edges.v[k];
+            const double e00 = 0.5 * (q[i] + q[j]);
+            g.add_term2((int32_t)i, (int32_t)j, e00 * lambda, lambda, lambda, e11 * lambda);
+        }
+    }
+    g.maxflow();
+    for (size_t i = 0; i < n; ++i)
+        if (g.is_sink((int32_t)i)) inliers.push_back((uint32_t)i);
+}
+
+}  // namespace gcr

@@ -169,6 +169,7 @@ hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc,
                              uint32_t m, double Tm, BatchRecord* out, hipStream_t stream,
                              const uint32_t* hmap = nullptr, const uint32_t* hcount = nullptr);
 // order-preserving list of live hypotheses (inc <= 101): map[0 .. *count)
+hipError_t launch_sqres_geo(const DevProblem& p, const GeoModel& model, double* r2, hipStream_t stream);
 hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_t* count, hipStream_t stream);
 
 // Low-latency scoring of a few models (LO trials, refits): every pair in

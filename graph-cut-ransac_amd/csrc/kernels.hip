@@ -2304,6 +2304,24 @@ hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule,
     return hipGetLastError();
 }
 
+// squared residuals of one model against every correspondence (graph-cut
+// labeling with pairwise terms, GCRANSAC.h:789-811)
+template <int KIND>
+__global__ __launch_bounds__(kMaskBlock) void k_sqres(DevClass c, GeoModel m, double* __restrict__ r2) {
+    const uint32_t i = blockIdx.x * kMaskBlock + threadIdx.x;
+    if (i >= c.n) return;
+    r2[i] = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
+}
+
+hipError_t launch_sqres_geo(const DevProblem& p, const GeoModel& model, double* r2, hipStream_t stream) {
+    const DevClass& c = p.cls[0];
+    if (c.n == 0) return hipSuccess;
+    const dim3 grid(blocks_for(c.n, kMaskBlock)), block(kMaskBlock);
+    if (p.solver == 4) hipLaunchKernelGGL(k_sqres<4>, grid, block, 0, stream, c, model, r2);
+    else hipLaunchKernelGGL(k_sqres<3>, grid, block, 0, stream, c, model, r2);
+    return hipGetLastError();
+}
+
 hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint64_t slot0,
                              uint32_t m, double Tm, BatchRecord* out, hipStream_t stream, const uint32_t* hmap,
                              const uint32_t* hcount) {

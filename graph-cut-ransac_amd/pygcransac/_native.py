@@ -34,6 +34,9 @@ class Params(C.Structure):
         ("seed", C.c_uint64),
         ("batch_slots", C.c_uint32),
         ("flags", C.c_uint32),
+        ("cell_size", C.c_double * 4),      # H / F neighbourhood grid (x1, y1, x2, y2)
+        ("cell_number", C.c_uint32),        # cells along every axis, 0 = empty grid
+        ("reserved", C.c_uint32),
     ]
 
 
@@ -158,6 +161,10 @@ def _load():
     L.gcr_host_fit_h.argtypes = [dp, C.c_size_t, u32p, C.c_size_t, dp]
     L.gcr_find_fundamental_matrix.argtypes = L.gcr_find_homography.argtypes
     L.gcr_host_fit_f.argtypes = L.gcr_host_fit_h.argtypes
+    L.gcr_host_grid_edges.argtypes = [dp, C.c_size_t, C.c_int, dp, C.c_uint64, u32p, C.c_size_t,
+                                      C.POINTER(C.c_size_t)]
+    L.gcr_host_bk_energy.argtypes = [C.c_size_t, dp, u32p, dp, C.c_size_t, u8p]
+    L.gcr_host_labeling.argtypes = [dp, C.c_size_t, C.c_double, C.c_double, u32p, C.c_size_t, u8p]
     L.gcr_host_homography.argtypes = [C.POINTER(RectModel), dp]
     L.gcr_host_homography.restype = None
     return L

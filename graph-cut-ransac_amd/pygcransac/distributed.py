@@ -30,7 +30,8 @@ RECORD = 20
 _RECT_DEFAULTS = dict(spatial_coherence_weight=0.0, min_iteration_number=10000, max_iteration_number=10000,
                       max_local_optimization_number=50, confidence=0.95, seed=0)
 _CORR_DEFAULTS = dict(spatial_coherence_weight=0.975, min_iteration_number=50, max_iteration_number=10000,
-                      max_local_optimization_number=50, confidence=0.99, seed=0)
+                      max_local_optimization_number=50, confidence=0.99, seed=0, image_sizes=(0, 0, 0, 0),
+                      neighborhood_size=8)
 
 
 def problem_settings(problem: dict) -> dict:
@@ -143,11 +144,11 @@ def gpu_solver(device: int) -> Callable[[dict], dict]:
         st = problem_settings(pr)
         if pr["kind"] in ("homography", "fundamental"):
             fn = P.findHomography if pr["kind"] == "homography" else P.findFundamentalMatrix
-            out = fn(pr["correspondences"], *pr.get("image_sizes", (0, 0, 0, 0)), threshold=pr["threshold"],
+            out = fn(pr["correspondences"], *st["image_sizes"], threshold=pr["threshold"],
                      conf=st["confidence"], spatial_coherence_weight=st["spatial_coherence_weight"],
                      max_iters=st["max_iteration_number"], min_iters=st["min_iteration_number"],
-                     lo_number=st["max_local_optimization_number"], seed=st["seed"], device=device,
-                     return_stats=True)
+                     lo_number=st["max_local_optimization_number"], neighborhood_size=st["neighborhood_size"],
+                     seed=st["seed"], device=device, return_stats=True)
             M, mask, stats = out
             return dict(H=M, model=None, num_inliers=int(mask.sum()), stats=stats, masks=(mask,))
         common = [st["spatial_coherence_weight"], st["min_iteration_number"], st["max_iteration_number"],
@@ -252,6 +253,7 @@ def batch_solver(device: int = 0, concurrency: int = 4) -> Callable[[list], list
     import ctypes as C
 
     from . import _native as N
+    from . import pygcransac as P
 
     dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
     u8 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))  # noqa: E731
@@ -287,6 +289,8 @@ def batch_solver(device: int = 0, concurrency: int = 4) -> Callable[[list], list
             p.max_local_optimization_number = int(st["max_local_optimization_number"])
             p.seed = int(st["seed"])
             p.confidence = float(st["confidence"])
+            if kind in ("homography", "fundamental"):
+                P._set_grid(p, f0, *st["image_sizes"], st["neighborhood_size"])
             it.params = p
         N.check(N.lib.gcr_solve_batch(device, items, len(problems), concurrency))
         out = []

@@ -367,9 +367,36 @@ def findRectifyingHomographySIFT(scale_features, orientation_features, scale_res
     return (H.reshape(3, 3), s_in, o_in, model) + extra
 
 
+def grid_cell_sizes(correspondences, h1, w1, h2, w2, neighborhood_size):
+    """Cell sizes of the neighbourhood grid over (x1, y1, x2, y2): each image
+    extent divided by `neighborhood_size` cells (upstream GC-RANSAC's
+    GridNeighborhoodGraph<4> over {w1, h1, w2, h2} / cells).  An image size
+    <= 0 (unknown) is replaced by the correspondences' extent along that axis
+    (max coordinate + 1, at least 1 px)."""
+    f = np.asarray(correspondences, dtype=np.float64)
+    k = float(neighborhood_size)
+    out = []
+    for col, size in zip(range(4), (w1, h1, w2, h2)):
+        size = float(size)
+        if not size > 0.0 or not math.isfinite(size):
+            finite = f[:, col][np.isfinite(f[:, col])] if f.size else np.zeros(0)
+            size = max(1.0, float(finite.max()) + 1.0) if finite.size else 1.0
+        out.append(size / k)
+    return out
+
+
+def _set_grid(p, correspondences, h1, w1, h2, w2, neighborhood_size):
+    cells = _as_size_t(neighborhood_size, "neighborhood_size")
+    if cells > 0xFFFFFFFF:
+        raise ValueError("neighborhood_size does not fit 32 bits")
+    p.cell_number = cells
+    if cells:
+        p.cell_size[:] = grid_cell_sizes(correspondences, h1, w1, h2, w2, cells)
+
+
 def _correspondence_call(entry, correspondences, h1, w1, h2, w2, probabilities, threshold, conf,
                          spatial_coherence_weight, max_iters, min_iters, sampler, lo_number, seed, device,
-                         batch_slots, return_stats, min_rows):
+                         batch_slots, return_stats, min_rows, neighborhood_size):
     for name, v in (("h1", h1), ("w1", w1), ("h2", h2), ("w2", w2)):
         _as_double(v, name)
     if probabilities is not None and len(probabilities) != 0:
@@ -385,6 +412,7 @@ def _correspondence_call(entry, correspondences, h1, w1, h2, w2, probabilities, 
                          f"It has {cols} columns and {n} rows.")
     f = np.ascontiguousarray(f)
     p = _params(threshold, 2.0, spatial_coherence_weight, min_iters, max_iters, lo_number, seed, conf, batch_slots)
+    _set_grid(p, f, h1, w1, h2, w2, neighborhood_size)
     mask = np.zeros(n, dtype=np.uint8)
     M = np.zeros(9, dtype=np.float64)
     st = N.Stats()
@@ -400,31 +428,35 @@ def _correspondence_call(entry, correspondences, h1, w1, h2, w2, probabilities, 
 
 def findHomography(correspondences, h1, w1, h2, w2, probabilities=None, threshold=1.0, conf=0.99,
                    spatial_coherence_weight=0.975, max_iters=10000, min_iters=50, sampler=0, lo_number=50, *,
-                   seed=0, device=None, batch_slots=0, return_stats=False):
+                   neighborhood_size=8, seed=0, device=None, batch_slots=0, return_stats=False):
     """4-point homography with graph-cut LO -- an EXTENSION (SURVEY.md §8(f)
     row 3): this fork has no homography estimator (finding 0.1); the argument
     names and order follow upstream pygcransac's findHomography.
 
     ``correspondences`` is (N, 4) float64: x1, y1, x2, y2.  ``h1, w1, h2, w2``
-    (image sizes) are accepted for signature compatibility; they only feed
-    upstream's neighbourhood grid and non-uniform samplers, which are not part
-    of this path: ``sampler`` must be 0 (uniform) and ``probabilities`` empty.
-    ``threshold`` is the inlier threshold in pixels of the second image
-    (MSAC threshold 2.25 * threshold, as the rectification solvers).
+    are the image sizes: the graph-cut's neighbourhood grid over (x1, y1, x2,
+    y2) has ``neighborhood_size`` cells along each axis (cell sizes w1/k, h1/k,
+    w2/k, h2/k; a size <= 0 is taken from the data's extent), and
+    ``spatial_coherence_weight`` (lambda) weighs its pairwise terms in every
+    graph-cut labeling (GCRANSAC.h:759-870); ``neighborhood_size=0`` or
+    lambda = 0 gives the empty grid.  ``sampler`` must be 0 (uniform) and
+    ``probabilities`` empty.  ``threshold`` is the inlier threshold in pixels
+    of the second image (MSAC threshold 2.25 * threshold, as the rectification
+    solvers).
 
     Returns ``(H, inliers)`` with H (3, 3) and H[2, 2] = 1, or ``(None, inliers)``.
     """
     return _correspondence_call(N.lib.gcr_find_homography, correspondences, h1, w1, h2, w2, probabilities,
                                 threshold, conf, spatial_coherence_weight, max_iters, min_iters, sampler, lo_number,
-                                seed, device, batch_slots, return_stats, 4)
+                                seed, device, batch_slots, return_stats, 4, neighborhood_size)
 
 
 def findFundamentalMatrix(correspondences, h1, w1, h2, w2, probabilities=None, threshold=1.0, conf=0.99,
                           spatial_coherence_weight=0.975, max_iters=10000, min_iters=50, sampler=0, lo_number=50,
-                          *, seed=0, device=None, batch_slots=0, return_stats=False):
+                          *, neighborhood_size=8, seed=0, device=None, batch_slots=0, return_stats=False):
     """7-point fundamental matrix with graph-cut LO -- an EXTENSION like
-    findHomography (same arguments; upstream pygcransac's findFundamentalMatrix
-    order).  The residual is the Sampson distance in pixels; a sample yields up
+    findHomography (same arguments, the same neighbourhood grid; upstream
+    pygcransac's findFundamentalMatrix order).  The residual is the Sampson distance in pixels; a sample yields up
     to three models, each scored.
 
     Returns ``(F, inliers)`` with F (3, 3), unit Frobenius norm and
@@ -432,4 +464,4 @@ def findFundamentalMatrix(correspondences, h1, w1, h2, w2, probabilities=None, t
     """
     return _correspondence_call(N.lib.gcr_find_fundamental_matrix, correspondences, h1, w1, h2, w2, probabilities,
                                 threshold, conf, spatial_coherence_weight, max_iters, min_iters, sampler, lo_number,
-                                seed, device, batch_slots, return_stats, 7)
+                                seed, device, batch_slots, return_stats, 7, neighborhood_size)

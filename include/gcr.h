@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GCR_ABI_VERSION 1
+#define GCR_ABI_VERSION 2
 
 /* error codes */
 #define GCR_OK 0
@@ -68,6 +68,14 @@ typedef struct gcr_params {
     uint64_t seed;                       /* extension: Philox key (reference is unseeded) */
     uint32_t batch_slots;                /* extension: outer-iteration slots per launch, 0 = auto */
     uint32_t flags;                      /* bit 0: disable local optimisation (bench only) */
+    /* extension (homography / fundamental matrix only): the neighbourhood grid
+     * over (x1, y1, x2, y2) whose cells give labeling()'s pairwise terms
+     * (GridNeighborhoodGraph<4>, grid_neighborhood_graph.h:229-301); cell
+     * sizes in pixels, cell_number cells along every axis; 0 = the empty grid
+     * of the reference's entry points (no pairwise terms) */
+    double cell_size[4];
+    uint32_t cell_number;
+    uint32_t reserved;
 } gcr_params;
 
 #define GCR_FLAG_NO_LO 1u
@@ -240,6 +248,21 @@ int gcr_host_fit_h(const double* correspondences, size_t n, const uint32_t* idx,
 int gcr_host_fit_f(const double* correspondences, size_t n, const uint32_t* idx, size_t k, double* F_out);
 /* host-only: RectifyingHomography::getHomography (model.h:211-226), row-major */
 void gcr_host_homography(const gcr_rect_model* model, double* H_out);
+/* host-only (no GPU): the graph-cut labeling's pieces (graphcut.h).
+ * grid_edges: the neighbourhood grid's edges over n points of `dims` (<= 4)
+ * row-major coordinates in labeling()'s order (GCRANSAC.h:821-857,
+ * grid_neighborhood_graph.h:229-301); writes min(m, cap) pairs, *m_out = m.
+ * bk_energy: BK st-mincut of sum_i E_i(x_i) + sum_k E_k(x_u, x_v), unary
+ * (n x 2: E(0), E(1)), pair (m x 4: E(00), E(01), E(10), E(11)), Energy::
+ * add_term1 / add_term2 (energy.h:204-245); seg[i] = 1 iff SINK.
+ * labeling: labeling() itself from squared residuals r2, squared truncated
+ * threshold sqt, lambda and an edge list; seg[i] = 1 iff inlier (SINK). */
+int gcr_host_grid_edges(const double* points, size_t n, int dims, const double* cell_size, uint64_t cell_number,
+                        uint32_t* edges_out, size_t cap, size_t* m_out);
+int gcr_host_bk_energy(size_t n, const double* unary, const uint32_t* edges, const double* pair, size_t m,
+                       uint8_t* seg);
+int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, const uint32_t* edges, size_t m,
+                      uint8_t* seg);
 /* host-only (no GPU): deterministic math and sampler used on both sides */
 double gcr_host_log(double x);
 double gcr_host_pow_m3(double t);

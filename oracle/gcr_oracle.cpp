@@ -36,6 +36,7 @@
 #include <random>
 #include <stdexcept>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../graph-cut-ransac_amd/csrc/detmath.h"   // TWIN mode primitives only
@@ -1244,6 +1245,374 @@ static Score<S::K> getScore(const S& solver, const Data<S::K>& data, const typen
     return score;
 }
 
+// ------------------------------------------------- neighbourhood graph ----
+// GridNeighborhoodGraph<D>::initialize (neighborhood/grid_neighborhood_graph.h:
+// 229-292) and getNeighbors (:294-301).  A point's cell index along axis d is
+// floor(coord_d / cell_size_d) stored as size_t (:251-252; the double ->
+// size_t conversion of a negative / non-finite floor is undefined in C++, x86-64
+// gives the 64-bit two's-complement value, 0x8000000000000000 out of range),
+// the cell key sum_d idx_d * cell_number^d in size_t arithmetic (GridCell,
+// :70-82), points appended to their cell in row order.  The cell map is keyed
+// by that index alone, so keys that collide share a cell, as in the reference.
+// The Python entry points of the reference build it over an EMPTY point set
+// (gcransac_python.cpp:60-67): no cells, no pairwise terms.
+struct GridGraph {
+    std::unordered_map<size_t, std::vector<size_t>> grid;
+    std::vector<size_t> cells_of_points;
+    size_t neighbor_number = 0;
+
+    static size_t axis_index(double v) {
+        const double f = std::floor(v);
+        if (!(f >= -9.2233720368547758e18 && f < 9.2233720368547758e18)) return (size_t)1 << 63;
+        return (size_t)(int64_t)f;
+    }
+    void build(const Features& f, const double* cell_sizes, size_t dims, size_t cell_number) {
+        grid.clear();
+        cells_of_points.assign(f.n, 0);
+        neighbor_number = 0;
+        for (size_t row = 0; row < f.n; ++row) {
+            size_t index = 0, offset = 1;
+            for (size_t d = 0; d < dims; ++d) {
+                index += offset * axis_index(f.at(row, d) / cell_sizes[d]);
+                offset *= cell_number;
+            }
+            grid[index].push_back(row);
+            cells_of_points[row] = index;
+        }
+        for (const auto& kv : grid) {
+            const size_t n = kv.second.size();
+            neighbor_number += n * (n - 1) / 2;
+        }
+    }
+    bool empty() const { return grid.empty(); }
+    const std::vector<size_t>& neighbors(size_t i) const { return grid.at(cells_of_points[i]); }
+};
+
+// ---------------------------------------------------- BK max-flow (st-mincut)
+// Graph<double,double,double> of graph.h / graph.ti / maxflow.ti (Boykov-
+// Kolmogorov, reuse_trees = false) and the Energy wrapper of energy.h:204-245,
+// restated with the same data structures and operation order: arcs allocated
+// in sister pairs and prepended to their tail's list (graph.h add_edge), the
+// two-queue active list (maxflow.ti set_active / next_active), orphans at the
+// front after an augmentation and at the rear during adoption, growth with the
+// TS/DIST shortest-origin heuristics, adoption processed per orphan with its
+// own descendants first (maxflow.ti:560-583).
+class BKGraph {
+public:
+    enum Term { SOURCE = 0, SINK = 1 };
+    struct Arc;
+    struct Node {
+        Arc* first = nullptr;
+        Arc* parent = nullptr;
+        Node* next = nullptr;
+        int TS = 0, DIST = 0;
+        bool is_sink = false;
+        double tr_cap = 0.0;
+    };
+    struct Arc {
+        Node* head;
+        Arc* next;
+        Arc* sister;
+        double r_cap;
+    };
+
+    explicit BKGraph(size_t n_nodes, size_t n_edges) : nodes_(n_nodes) { arcs_.reserve(2 * n_edges + 2); }
+
+    // Graph::add_tweights (graph.h:405-418)
+    void add_tweights(size_t i, double cap_source, double cap_sink) {
+        const double delta = nodes_[i].tr_cap;
+        if (delta > 0) cap_source += delta;
+        else cap_sink -= delta;
+        flow_ += (cap_source < cap_sink) ? cap_source : cap_sink;
+        nodes_[i].tr_cap = cap_source - cap_sink;
+    }
+    // Graph::add_edge (graph.h:420-452)
+    void add_edge(size_t i, size_t j, double cap, double rev_cap) {
+        if (arcs_.size() + 2 > arcs_.capacity()) throw std::runtime_error("BKGraph: arc capacity");
+        arcs_.push_back(Arc{});
+        arcs_.push_back(Arc{});
+        Arc* a = &arcs_[arcs_.size() - 2];
+        Arc* ar = &arcs_[arcs_.size() - 1];
+        Node* ni = &nodes_[i];
+        Node* nj = &nodes_[j];
+        a->sister = ar;
+        ar->sister = a;
+        a->next = ni->first;
+        ni->first = a;
+        ar->next = nj->first;
+        nj->first = ar;
+        a->head = nj;
+        ar->head = ni;
+        a->r_cap = cap;
+        ar->r_cap = rev_cap;
+    }
+    // Energy::add_term1 (energy.h:204-208): E(0) = A, E(1) = B
+    void add_term1(size_t x, double A, double B) { add_tweights(x, B, A); }
+    // Energy::add_term2 (energy.h:210-245)
+    void add_term2(size_t x, size_t y, double A, double B, double C, double D) {
+        add_tweights(x, D, A);
+        B -= A;
+        C -= D;
+        if (B < 0) {
+            add_tweights(x, 0, B);
+            add_tweights(y, 0, -B);
+            add_edge(x, y, 0, B + C);
+        } else if (C < 0) {
+            add_tweights(x, 0, -C);
+            add_tweights(y, 0, C);
+            add_edge(x, y, B + C, 0);
+        } else {
+            add_edge(x, y, B, C);
+        }
+    }
+    // Graph::what_segment (graph.h:476-487), default SOURCE
+    Term what_segment(size_t i) const {
+        if (nodes_[i].parent) return nodes_[i].is_sink ? SINK : SOURCE;
+        return SOURCE;
+    }
+
+    // Graph::maxflow (maxflow.ti:463-597), first call, no reuse
+    double maxflow() {
+        Node *i, *j, *current_node = nullptr;
+        Arc* a;
+        maxflow_init();
+        while (true) {
+            if ((i = current_node)) {
+                i->next = nullptr;
+                if (!i->parent) i = nullptr;
+            }
+            if (!i) {
+                if (!(i = next_active())) break;
+            }
+            if (!i->is_sink) {
+                for (a = i->first; a; a = a->next)
+                    if (a->r_cap) {
+                        j = a->head;
+                        if (!j->parent) {
+                            j->is_sink = false;
+                            j->parent = a->sister;
+                            j->TS = i->TS;
+                            j->DIST = i->DIST + 1;
+                            set_active(j);
+                        } else if (j->is_sink) {
+                            break;
+                        } else if (j->TS <= i->TS && j->DIST > i->DIST) {
+                            j->parent = a->sister;
+                            j->TS = i->TS;
+                            j->DIST = i->DIST + 1;
+                        }
+                    }
+            } else {
+                for (a = i->first; a; a = a->next)
+                    if (a->sister->r_cap) {
+                        j = a->head;
+                        if (!j->parent) {
+                            j->is_sink = true;
+                            j->parent = a->sister;
+                            j->TS = i->TS;
+                            j->DIST = i->DIST + 1;
+                            set_active(j);
+                        } else if (!j->is_sink) {
+                            a = a->sister;
+                            break;
+                        } else if (j->TS <= i->TS && j->DIST > i->DIST) {
+                            j->parent = a->sister;
+                            j->TS = i->TS;
+                            j->DIST = i->DIST + 1;
+                        }
+                    }
+            }
+            ++TIME_;
+            if (a) {
+                i->next = i;
+                current_node = i;
+                augment(a);
+                // adoption (maxflow.ti:560-583)
+                while (!orphans_.empty()) {
+                    // the first orphan and everything its processing appends,
+                    // then the rest of the augmentation's orphans
+                    std::vector<Node*> rest(orphans_.begin() + 1, orphans_.end());
+                    std::vector<Node*> cur{orphans_.front()};
+                    orphans_.swap(cur);
+                    size_t k = 0;
+                    while (k < orphans_.size()) {
+                        Node* o = orphans_[k++];
+                        if (o->is_sink) process_sink_orphan(o);
+                        else process_source_orphan(o);
+                    }
+                    orphans_.swap(rest);
+                }
+            } else {
+                current_node = nullptr;
+            }
+        }
+        return flow_;
+    }
+
+private:
+    std::vector<Node> nodes_;
+    std::vector<Arc> arcs_;
+    Arc* const TERMINAL = reinterpret_cast<Arc*>(1);
+    Arc* const ORPHAN = reinterpret_cast<Arc*>(2);
+    static constexpr int INFINITE_D = (int)(((unsigned)-1) / 2);
+    Node* queue_first_[2] = {nullptr, nullptr};
+    Node* queue_last_[2] = {nullptr, nullptr};
+    std::vector<Node*> orphans_;        // the current adoption list, in order
+    int TIME_ = 0;
+    double flow_ = 0.0;
+
+    void set_active(Node* i) {
+        if (!i->next) {
+            if (queue_last_[1]) queue_last_[1]->next = i;
+            else queue_first_[1] = i;
+            queue_last_[1] = i;
+            i->next = i;
+        }
+    }
+    Node* next_active() {
+        Node* i;
+        while (true) {
+            if (!(i = queue_first_[0])) {
+                queue_first_[0] = i = queue_first_[1];
+                queue_last_[0] = queue_last_[1];
+                queue_first_[1] = nullptr;
+                queue_last_[1] = nullptr;
+                if (!i) return nullptr;
+            }
+            if (i->next == i) queue_first_[0] = queue_last_[0] = nullptr;
+            else queue_first_[0] = i->next;
+            i->next = nullptr;
+            if (i->parent) return i;
+        }
+    }
+    void set_orphan_front(Node* i) {
+        i->parent = ORPHAN;
+        orphans_.insert(orphans_.begin(), i);
+    }
+    void set_orphan_rear(Node* i) {
+        i->parent = ORPHAN;
+        orphans_.push_back(i);
+    }
+    void maxflow_init() {
+        queue_first_[0] = queue_last_[0] = nullptr;
+        queue_first_[1] = queue_last_[1] = nullptr;
+        orphans_.clear();
+        TIME_ = 0;
+        for (Node& n : nodes_) {
+            Node* i = &n;
+            i->next = nullptr;
+            i->TS = TIME_;
+            if (i->tr_cap > 0) {
+                i->is_sink = false;
+                i->parent = TERMINAL;
+                set_active(i);
+                i->DIST = 1;
+            } else if (i->tr_cap < 0) {
+                i->is_sink = true;
+                i->parent = TERMINAL;
+                set_active(i);
+                i->DIST = 1;
+            } else {
+                i->parent = nullptr;
+            }
+        }
+    }
+    void augment(Arc* middle_arc) {
+        Node* i;
+        Arc* a;
+        double bottleneck = middle_arc->r_cap;
+        for (i = middle_arc->sister->head;; i = a->head) {
+            a = i->parent;
+            if (a == TERMINAL) break;
+            if (bottleneck > a->sister->r_cap) bottleneck = a->sister->r_cap;
+        }
+        if (bottleneck > i->tr_cap) bottleneck = i->tr_cap;
+        for (i = middle_arc->head;; i = a->head) {
+            a = i->parent;
+            if (a == TERMINAL) break;
+            if (bottleneck > a->r_cap) bottleneck = a->r_cap;
+        }
+        if (bottleneck > -i->tr_cap) bottleneck = -i->tr_cap;
+        middle_arc->sister->r_cap += bottleneck;
+        middle_arc->r_cap -= bottleneck;
+        for (i = middle_arc->sister->head;; i = a->head) {
+            a = i->parent;
+            if (a == TERMINAL) break;
+            a->r_cap += bottleneck;
+            a->sister->r_cap -= bottleneck;
+            if (!a->sister->r_cap) set_orphan_front(i);
+        }
+        i->tr_cap -= bottleneck;
+        if (!i->tr_cap) set_orphan_front(i);
+        for (i = middle_arc->head;; i = a->head) {
+            a = i->parent;
+            if (a == TERMINAL) break;
+            a->sister->r_cap += bottleneck;
+            a->r_cap -= bottleneck;
+            if (!a->r_cap) set_orphan_front(i);
+        }
+        i->tr_cap += bottleneck;
+        if (!i->tr_cap) set_orphan_front(i);
+        flow_ += bottleneck;
+    }
+    // process_source_orphan / process_sink_orphan (maxflow.ti:326-459)
+    template <bool kSink>
+    void process_orphan(Node* i) {
+        Node* j;
+        Arc *a0, *a0_min = nullptr, *a;
+        int d, d_min = INFINITE_D;
+        for (a0 = i->first; a0; a0 = a0->next)
+            if (kSink ? a0->r_cap : a0->sister->r_cap) {
+                j = a0->head;
+                if (j->is_sink == kSink && (a = j->parent)) {
+                    d = 0;
+                    while (true) {
+                        if (j->TS == TIME_) {
+                            d += j->DIST;
+                            break;
+                        }
+                        a = j->parent;
+                        d++;
+                        if (a == TERMINAL) {
+                            j->TS = TIME_;
+                            j->DIST = 1;
+                            break;
+                        }
+                        if (a == ORPHAN) {
+                            d = INFINITE_D;
+                            break;
+                        }
+                        j = a->head;
+                    }
+                    if (d < INFINITE_D) {
+                        if (d < d_min) {
+                            a0_min = a0;
+                            d_min = d;
+                        }
+                        for (j = a0->head; j->TS != TIME_; j = j->parent->head) {
+                            j->TS = TIME_;
+                            j->DIST = d--;
+                        }
+                    }
+                }
+            }
+        if ((i->parent = a0_min)) {
+            i->TS = TIME_;
+            i->DIST = d_min + 1;
+        } else {
+            for (a0 = i->first; a0; a0 = a0->next) {
+                j = a0->head;
+                if (j->is_sink == kSink && (a = j->parent)) {
+                    if (kSink ? a0->r_cap : a0->sister->r_cap) set_active(j);
+                    if (a != TERMINAL && a != ORPHAN && a->head == i) set_orphan_rear(j);
+                }
+            }
+        }
+    }
+    void process_source_orphan(Node* i) { process_orphan<false>(i); }
+    void process_sink_orphan(Node* i) { process_orphan<true>(i); }
+};
+
 // -------------------------------------------------------------- GCRANSAC ----
 struct Settings {
     double threshold[2] = {2.0, 2.0};
@@ -1273,6 +1642,7 @@ public:
     Settings settings;
     Statistics stats;
     Inliers<K> final_inliers{};
+    const GridGraph* neighborhood = nullptr;      // null / empty: the reference's empty grid
 
     void run(const Data<K>& data, const S& solver, Model& out_model) {
         auto t0 = std::chrono::steady_clock::now();
@@ -1396,21 +1766,56 @@ private:
         return static_cast<size_t>(std::ceil(log_probability / lg));
     }
 
-    // labeling(): BK max-flow on the empty neighbourhood graph (no pairwise
-    // terms): node i ends in SINK iff its terminal residual capacity is < 0.
+    // labeling() (GCRANSAC.h:759-870): unary terms from the truncated
+    // quadratic cost, pairwise terms over the neighbourhood graph's cells when
+    // lambda > 0, BK st-mincut, SINK = inlier.  On the empty graph of the
+    // reference's entry points the cut needs no search: node i ends in SINK
+    // iff its terminal residual capacity is < 0 (the reference's
+    // getNeighbors on an empty grid is out of range, i.e. undefined; no
+    // edges is the only defined reading).
     void labeling1(const Data<K>& data, const S& solver, const Model& model, double lambda, double sqt,
                    std::vector<size_t>& inliers) const {
         const Features& f = *data[0];
         const double oml = 1.0 - lambda;
-        for (size_t i = 0; i < f.n; ++i) {
-            const double r2 = solver.squaredResidual(0, f, i, model);
-            const double q = std::clamp(r2 / sqt, 0.0, 1.0);
-            const double energy = 1.0 - q;
-            double tr;
-            if (r2 <= sqt) tr = 0.0 - oml * energy;          // add_term1(i, A, 0) -> tweights(0, A)
-            else tr = oml * (1.0 - energy) - 0.0;             // add_term1(i, 0, B) -> tweights(B, 0)
-            if (tr < 0) inliers.push_back(i);
+        if (!(lambda > 0) || !neighborhood || neighborhood->empty()) {
+            for (size_t i = 0; i < f.n; ++i) {
+                const double r2 = solver.squaredResidual(0, f, i, model);
+                const double q = std::clamp(r2 / sqt, 0.0, 1.0);
+                const double energy = 1.0 - q;
+                double tr;
+                if (r2 <= sqt) tr = 0.0 - oml * energy;          // add_term1(i, A, 0) -> tweights(0, A)
+                else tr = oml * (1.0 - energy) - 0.0;             // add_term1(i, 0, B) -> tweights(B, 0)
+                if (tr < 0) inliers.push_back(i);
+            }
+            return;
         }
+        BKGraph g(f.n, neighborhood->neighbor_number);
+        std::vector<double> dpt;
+        dpt.reserve(f.n);
+        for (size_t i = 0; i < f.n; ++i) {                                  // :789-811
+            const double r2 = solver.squaredResidual(0, f, i, model);
+            const double q = dpt.emplace_back(std::clamp(r2 / sqt, 0.0, 1.0));
+            const double energy = 1.0 - q;
+            if (r2 <= sqt) g.add_term1(i, oml * energy, 0.0);
+            else g.add_term1(i, 0.0, oml * (1.0 - energy));
+        }
+        std::unordered_set<uint64_t> used;                                   // :813, the N x N marks
+        const double e11 = 0;
+        for (size_t pi = 0; pi < f.n; ++pi) {                                // :821-857
+            const double energy1 = dpt[pi];
+            for (const size_t nb : neighborhood->neighbors(pi)) {
+                if (nb == pi) continue;
+                const uint64_t key = (uint64_t)std::min(pi, nb) * f.n + std::max(pi, nb);
+                if (!used.insert(key).second) continue;
+                const double energy2 = dpt[nb];
+                const double energy_sum = energy1 + energy2;
+                const double e00 = 0.5 * energy_sum;
+                g.add_term2(pi, nb, e00 * lambda, lambda, lambda, e11 * lambda);
+            }
+        }
+        g.maxflow();                                                         // :861
+        for (size_t i = 0; i < f.n; ++i)
+            if (g.what_segment(i) == BKGraph::SINK) inliers.push_back(i);
     }
 
     bool localOptimization(const Data<K>& data, const S& solver, Inliers<K>& sfb_inliers, Model& sfb_model,
@@ -1501,6 +1906,8 @@ struct oracle_params {
     uint64_t seed;
     int32_t math_mode;   // 0 glibc, 1 twin
     int32_t sampler;     // 0 philox, 1 faithful
+    double cell_size[4]; // H / F neighbourhood grid over (x1, y1, x2, y2)
+    uint64_t cell_number;// cells along every axis; 0 = empty grid
 };
 
 struct oracle_stats {
@@ -1601,6 +2008,11 @@ int oracle_find_homography(const double* corr, size_t n, const oracle_params* p,
     g.settings.seed = p->seed;
     g.settings.sampler = p->sampler;
     HModel model;
+    GridGraph grid;
+    if (p->cell_number > 0) {
+        grid.build(f, p->cell_size, 4, p->cell_number);
+        g.neighborhood = &grid;
+    }
     try {
         g.run({&f}, HSolver{}, model);
     } catch (const std::exception& e) {
@@ -1637,6 +2049,11 @@ int oracle_find_fundamental(const double* corr, size_t n, const oracle_params* p
     g.settings.seed = p->seed;
     g.settings.sampler = p->sampler;
     HModel model;
+    GridGraph grid;
+    if (p->cell_number > 0) {
+        grid.build(f, p->cell_size, 4, p->cell_number);
+        g.neighborhood = &grid;
+    }
     try {
         g.run({&f}, FSolver{}, model);
     } catch (const std::exception& e) {
@@ -1976,3 +2393,41 @@ double oracle_weighted_mode(const double* angles, const double* weights, size_t 
 }
 
 }  // extern "C"
+
+// ---- graph-cut hooks (tests): an energy of unary terms E_i(0), E_i(1) and
+// pairwise terms (A, B, C, D) = E(00), E(01), E(10), E(11) over edge list
+// (u_k, v_k) in order, minimised by the BK restatement; seg[i] = 1 for SINK.
+extern "C" int oracle_bk_energy(size_t n, const double* unary, const uint32_t* edges, const double* pair, size_t m,
+                                uint8_t* seg, double* flow) {
+    BKGraph g(n, m);
+    for (size_t i = 0; i < n; ++i) g.add_term1(i, unary[2 * i], unary[2 * i + 1]);
+    for (size_t k = 0; k < m; ++k)
+        g.add_term2(edges[2 * k], edges[2 * k + 1], pair[4 * k], pair[4 * k + 1], pair[4 * k + 2], pair[4 * k + 3]);
+    const double f = g.maxflow();
+    if (flow) *flow = f;
+    for (size_t i = 0; i < n; ++i) seg[i] = g.what_segment(i) == BKGraph::SINK ? 1 : 0;
+    return 0;
+}
+
+// the neighbourhood graph's edges in labeling()'s order (GCRANSAC.h:821-857):
+// pairs (i, j) of points sharing a cell, each once, first seen from i
+extern "C" size_t oracle_grid_edges(const double* corr, size_t n, size_t dims, const double* cell_size,
+                                    uint64_t cell_number, uint32_t* out, size_t cap) {
+    Features f = make_features(corr, n, dims);
+    GridGraph grid;
+    grid.build(f, cell_size, dims, cell_number);
+    std::unordered_set<uint64_t> used;
+    size_t m = 0;
+    for (size_t pi = 0; pi < n; ++pi)
+        for (const size_t nb : grid.neighbors(pi)) {
+            if (nb == pi) continue;
+            const uint64_t key = (uint64_t)std::min(pi, nb) * n + std::max(pi, nb);
+            if (!used.insert(key).second) continue;
+            if (m < cap) {
+                out[2 * m] = (uint32_t)pi;
+                out[2 * m + 1] = (uint32_t)nb;
+            }
+            ++m;
+        }
+    return m;
+}

@@ -26,6 +26,7 @@ class OracleParams(C.Structure):
         ("min_iteration_number", C.c_uint64), ("max_iteration_number", C.c_uint64),
         ("max_local_optimization_number", C.c_uint64), ("confidence", C.c_double),
         ("seed", C.c_uint64), ("math_mode", C.c_int32), ("sampler", C.c_int32),
+        ("cell_size", C.c_double * 4), ("cell_number", C.c_uint64),
     ]
 
 
@@ -74,6 +75,10 @@ def lib():
         L.oracle_h_score.argtypes = [dp, C.c_size_t, dp, C.c_double, u64p, dp, u8p]
         L.oracle_h_residuals.argtypes = [dp, C.c_size_t, dp, dp]
         L.oracle_find_fundamental.argtypes = L.oracle_find_homography.argtypes
+        u32p = C.POINTER(C.c_uint32)
+        L.oracle_bk_energy.argtypes = [C.c_size_t, dp, u32p, dp, C.c_size_t, u8p, dp]
+        L.oracle_grid_edges.argtypes = [dp, C.c_size_t, C.c_size_t, dp, C.c_uint64, u32p, C.c_size_t]
+        L.oracle_grid_edges.restype = C.c_size_t
         L.oracle_f_slot.argtypes = [dp, C.c_size_t, C.c_uint64, C.c_uint64, dp, C.POINTER(C.c_int)]
         L.oracle_f_score.argtypes = L.oracle_h_score.argtypes
         L.oracle_f_residuals.argtypes = L.oracle_h_residuals.argtypes
@@ -115,8 +120,11 @@ def _f64(a):
 
 
 def params(thr0, thr1=0.0, lam=0.0, min_it=10000, max_it=10000, lo=50, confidence=0.95, seed=0,
-           math_mode=MATH_TWIN, sampler=SAMPLER_PHILOX):
-    return OracleParams(thr0, thr1, lam, min_it, max_it, lo, confidence, seed, math_mode, sampler)
+           math_mode=MATH_TWIN, sampler=SAMPLER_PHILOX, cell_size=(0.0, 0.0, 0.0, 0.0), cell_number=0):
+    """cell_size / cell_number: the H / F neighbourhood grid over (x1, y1, x2,
+    y2) (0 cells = the empty grid of the reference's entry points)."""
+    return OracleParams(thr0, thr1, lam, min_it, max_it, lo, confidence, seed, math_mode, sampler,
+                        (C.c_double * 4)(*map(float, cell_size)), int(cell_number))
 
 
 def model7(m):
@@ -339,3 +347,28 @@ def hot_batch(kind, f0, f1, thr0, thr1, seed, slot0, nslots, sampler=SAMPLER_FAI
                                0 if f1 is None else f1.shape[0], thr0, thr1, seed, slot0, nslots, sampler,
                                math_mode, _dp(sec), _dp(best))
     return int(n), float(sec[0]), float(best[0])
+
+
+def bk_energy(unary, edges, pair):
+    """BK restatement over an energy: unary (n, 2) = E_i(0), E_i(1); edges
+    (m, 2); pair (m, 4) = E(00), E(01), E(10), E(11).  Returns (seg (n,) bool,
+    True = SINK, flow)."""
+    u = _f64(np.asarray(unary).reshape(-1, 2))
+    e = np.ascontiguousarray(np.asarray(edges, dtype=np.uint32).reshape(-1, 2))
+    pr = _f64(np.asarray(pair).reshape(-1, 4))
+    seg = np.zeros(u.shape[0], dtype=np.uint8)
+    flow = C.c_double()
+    lib().oracle_bk_energy(u.shape[0], _dp(u), e.ctypes.data_as(C.POINTER(C.c_uint32)), _dp(pr), e.shape[0],
+                           seg.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(flow))
+    return seg.astype(bool), flow.value
+
+
+def grid_edges(points, cell_size, cell_number):
+    """The neighbourhood grid's edge list in labeling()'s order, (m, 2)."""
+    pts = _f64(points)
+    cs = _f64(np.asarray(cell_size, dtype=np.float64))
+    n, d = pts.shape
+    m = lib().oracle_grid_edges(_dp(pts), n, d, _dp(cs), int(cell_number), None, 0)
+    out = np.zeros((max(m, 1), 2), dtype=np.uint32)
+    lib().oracle_grid_edges(_dp(pts), n, d, _dp(cs), int(cell_number), out.ctypes.data_as(C.POINTER(C.c_uint32)), m)
+    return out[:m]

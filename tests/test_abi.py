@@ -32,10 +32,17 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_defaults():
-    assert N.lib.gcr_abi_version() == 1
+    assert N.lib.gcr_abi_version() == 2          # 2: gcr_params carries the neighbourhood grid
     p = N.default_params()
     assert (p.min_iteration_number, p.max_iteration_number, p.max_local_optimization_number) == (10000, 10000, 50)
     assert p.spatial_coherence_weight == 0.0 and p.confidence == 0.95
+    assert p.cell_number == 0 and list(p.cell_size) == [0.0] * 4      # the reference's empty grid
+    # the ctypes mirror has the C struct's size (no silently misaligned fields)
+    import re
+    hdr = open(os.path.join(os.path.dirname(N.LIB_PATH), "..", "..", "include", "gcr.h")).read()
+    body = hdr[hdr.index("typedef struct gcr_params {"):hdr.index("} gcr_params;")]
+    fields = re.findall(r"^\s+(double|uint64_t|uint32_t) ([a-z_]+)(\[4\])?;", body, re.M)
+    assert [f[1] for f in fields] == [f[0] for f in N.Params._fields_]
 
 
 def test_errors_cross_the_abi_as_codes_not_exceptions():

@@ -14,6 +14,7 @@ import pytest
 
 import oracle_ffi as O
 import pygcransac
+from pygcransac import pygcransac as P
 from gcr_testutil import CorrProblem, bits, dp
 from pygcransac import _native as N
 from pygcransac import synthetic as S
@@ -177,7 +178,8 @@ def _run_both(corr, thr, seed, **kw):
     r = pygcransac.findFundamentalMatrix(corr, 960, 1280, 960, 1280, threshold=thr, seed=seed, return_stats=True,
                                          batch_slots=kw.get("batch_slots", 0), **pk)
     ref = O.find_fundamental(corr, thr, min_it=pk["min_iters"], max_it=pk["max_iters"], confidence=pk["conf"],
-                             lam=pk["spatial_coherence_weight"], lo=pk["lo_number"], seed=seed)
+                             lam=pk["spatial_coherence_weight"], lo=pk["lo_number"], seed=seed,
+                             cell_size=P.grid_cell_sizes(corr, 960, 1280, 960, 1280, 8), cell_number=8)
     return r, ref
 
 
@@ -278,7 +280,7 @@ def test_mixed_batch_records_match_direct_calls(gpu):
             continue
         fn = pygcransac.findHomography if pr["kind"] == "homography" else pygcransac.findFundamentalMatrix
         M, mask = fn(pr["correspondences"], 0, 0, 0, 0, threshold=pr["threshold"], conf=0.99,
-                     spatial_coherence_weight=0.0, max_iters=pr["max_iteration_number"], min_iters=50, seed=pr["seed"])
+                     max_iters=pr["max_iteration_number"], min_iters=50, seed=pr["seed"])
         assert recs[i]["num_inliers"] == int(mask.sum())
         assert np.array_equal(bits(recs[i]["H"]), bits(M))
 

@@ -15,6 +15,7 @@ import pytest
 
 import oracle_ffi as O
 import pygcransac
+from pygcransac import pygcransac as P
 from gcr_testutil import CorrProblem, bits, dp
 from pygcransac import _native as N
 from pygcransac import synthetic as S
@@ -182,7 +183,9 @@ def _run_both(corr, thr, seed, **kw):
                                   batch_slots=kw.get("batch_slots", 0), **pk)
     ok = dict(min_it=pk["min_iters"], max_it=pk["max_iters"], confidence=pk["conf"], lam=pk["spatial_coherence_weight"],
               lo=pk["lo_number"], seed=seed)
-    ref = O.find_homography(corr, thr, **ok)
+    # the default neighbourhood grid (8 cells per axis over the image sizes)
+    ref = O.find_homography(corr, thr, cell_size=P.grid_cell_sizes(corr, 960, 1280, 960, 1280, 8), cell_number=8,
+                            **ok)
     return r, ref
 
 
