@@ -471,7 +471,7 @@ def main():
         latency = dict(ms_median=statistics.median(lat), ms_all=lat,
                        iterations=last_stats["iteration_number"], hypotheses=last_stats["hypotheses"],
                        ms_breakdown={k: last_stats[k] for k in ("ms_setup", "ms_generate", "ms_score", "ms_replay",
-                                                                "ms_lo", "ms_lo_lists", "ms_lo_fit", "ms_lo_score",
+                                                                "ms_lo", "ms_lo_lists", "ms_lo_fit", "ms_lo_score", "ms_refit_fit",
                                                                 "ms_refit", "ms_total", "graph_cut_number")})
 
     if cpu is not None and latency is not None and "oracle_call_ms" in cpu:

@@ -201,9 +201,11 @@ struct Workspace {
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
+    PinBuf<uint32_t> rf_hidx;           // GPU refit: their pinned staging
     DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
     DevBuf<double> rf_part;             // GPU refit: reduction block partials
     DevBuf<QRDevState> rf_qrst;         // GPU refit: device-resident QR driver state
+    DevBuf<QRFState> rf_qrf;            // GPU refit: fused-pass QR driver state
     PinBuf<double> rf_hpart;
     PinBuf<double> rf_htop;             // GPU refit: async upload ring
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
@@ -237,6 +239,12 @@ namespace {
 constexpr size_t kQrDeviceMaxRows = (size_t)256 * kSumSuper;
 bool qr_device_on() {
     const char* e = getenv("GCR_QR_DEVICE");           // read per refit (tests switch it)
+    return !(e && e[0] == '0');
+}
+// the device driver in fused passes (launch_sift_refit_fused) unless GCR_QR_FUSED=0
+// (one pass per reduction / element-wise step, launch_qr_device)
+bool qr_fused_on() {
+    const char* e = getenv("GCR_QR_FUSED");
     return !(e && e[0] == '0');
 }
 
@@ -365,19 +373,38 @@ struct GpuSiftSolver final : SiftSystemSolver {
         const size_t rows_max = std::max(rows, std::min<size_t>(all_s + all_o * (all_o - (all_o > 0)) / 2, 1u << 24));
         P->w->rf_idx.ensure(all_s + all_o);
         P->w->rf_hpart.ensure(1);
-        HIPC(hipMemcpyAsync(P->w->rf_idx.p, si.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        HIPC(hipMemcpyAsync(P->w->rf_idx.p + ns, oi.data(), no * sizeof(uint32_t), hipMemcpyHostToDevice, s));
         P->w->rf_A.ensure(4 * rows_max);
         double* A = P->w->rf_A.p;
+        if (qr_device_on() && qr_fused_on() && rows >= 4 && rows <= kQrDeviceMaxRows) {
+            // index lists through pinned memory (no synchronisation before the
+            // solve), rows built inside the first fused pass, one synchronisation
+            P->w->rf_hidx.ensure(all_s + all_o);
+            std::memcpy(P->w->rf_hidx.p, si.data(), ns * sizeof(uint32_t));
+            std::memcpy(P->w->rf_hidx.p + ns, oi.data(), no * sizeof(uint32_t));
+            HIPC(hipMemcpyAsync(P->w->rf_idx.p, P->w->rf_hidx.p, (ns + no) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                s));
+            P->w->rf_part.ensure(kQrfMaxRed * ((rows_max - 1) / kSumBlock + 1));
+            P->w->rf_hpart.ensure(3);
+            P->w->rf_qrf.ensure(1);
+            double* const cols[4] = {A, A + rows, A + 2 * rows, A + 3 * rows};
+            HIPC(launch_sift_refit_fused(P->dp.cls[0], P->dp.cls[1], P->w->rf_idx.p, (uint32_t)ns, P->w->rf_idx.p + ns,
+                                         (uint32_t)no, rows, cols, P->w->rf_qrf.p, P->w->rf_part.p, P->w->rf_hpart.p,
+                                         s));
+            for (int q = 0; q < 3; ++q) x[q] = P->w->rf_hpart.p[q];
+            return;
+        }
+        HIPC(hipMemcpyAsync(P->w->rf_idx.p, si.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIPC(hipMemcpyAsync(P->w->rf_idx.p + ns, oi.data(), no * sizeof(uint32_t), hipMemcpyHostToDevice, s));
         HIPC(launch_sift_rows(P->dp.cls[0], P->dp.cls[1], P->w->rf_idx.p, (uint32_t)ns, P->w->rf_idx.p + ns, (uint32_t)no,
                               rows, A, A + rows, A + 2 * rows, A + 3 * rows, s));
         HIPC(hipStreamSynchronize(s));          // index lists are pageable host vectors
         if (qr_device_on() && rows >= 4 && rows <= kQrDeviceMaxRows) {
-            // the QR driver's decisions on the device: one synchronisation
-            P->w->rf_qrst.ensure(1);
+            // the QR driver's decisions on the device, one pass per step
+            // (GCR_QR_FUSED=0): one synchronisation
             P->w->rf_part.ensure((rows_max - 1) / kSumBlock + 1);
             P->w->rf_hpart.ensure(3);
             double* const cols[4] = {A, A + rows, A + 2 * rows, A + 3 * rows};
+            P->w->rf_qrst.ensure(1);
             HIPC(launch_qr_device(cols, rows, P->w->rf_qrst.p, P->w->rf_part.p, P->w->rf_hpart.p, s));
             for (int q = 0; q < 3; ++q) x[q] = P->w->rf_hpart.p[q];
             return;
@@ -405,6 +432,7 @@ public:
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto& w : workers_) w.join();
@@ -424,18 +452,21 @@ public:
             for (size_t i = 0; i < n; ++i) fn(i);
             return;
         }
+        job_ = &fn;
+        n_ = n;
+        next_.store(0, std::memory_order_relaxed);
+        pending_.store(workers_.size(), std::memory_order_relaxed);
         {
+            // publish under the lock so a worker about to block cannot miss it
             std::lock_guard<std::mutex> lk(mu_);
-            job_ = &fn;
-            n_ = n;
-            next_.store(0);
-            pending_ = workers_.size();
-            ++gen_;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         run();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return pending_ == 0; });
+        // the workers are awake (spinning or just woken) and the jobs are
+        // short: wait for the stragglers by polling
+        for (unsigned spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin)
+            if (spin > 4096) std::this_thread::yield();
         job_ = nullptr;
         if (err_) {
             std::exception_ptr e = err_;
@@ -454,29 +485,46 @@ private:
             next_.store(n_);                      // stop handing out work
         }
     }
+    // A worker polls for the next job for ~kSpinUs after finishing one (the
+    // LO rounds call the pool every ~100 us: a condition-variable wake-up of
+    // 15 threads costs tens of us per call), then blocks.
+    static constexpr int64_t kSpinUs = 300;
     void loop() {
         uint64_t seen = 0;
         for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
+            uint64_t g = gen_.load(std::memory_order_acquire);
+            if (g == seen) {
+                const auto t0 = Clock::now();
+                unsigned k = 0;
+                while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+                    if ((++k & 255) == 0 &&
+                        std::chrono::duration_cast<std::chrono::microseconds>(Clock::now() - t0).count() > kSpinUs)
+                        break;
+#if defined(__x86_64__)
+                    __builtin_ia32_pause();
+#endif
+                }
+                if (g == seen) {
+                    std::unique_lock<std::mutex> lk(mu_);
+                    cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
+                    g = gen_.load(std::memory_order_acquire);
+                }
             }
+            if (stop_) return;
+            seen = g;
             run();
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_one();
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
         }
     }
     std::vector<std::thread> workers_;
     std::mutex mu_, call_mu_, err_mu_;
     std::exception_ptr err_;
-    std::condition_variable cv_, done_;
+    std::condition_variable cv_;
     const std::function<void(size_t)>* job_ = nullptr;
     size_t n_ = 0;
     std::atomic<size_t> next_{0};
-    size_t pending_ = 0;
-    uint64_t gen_ = 0;
+    std::atomic<size_t> pending_{0};
+    std::atomic<uint64_t> gen_{0};
     bool stop_ = false;
 };
 
@@ -570,20 +618,27 @@ void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1
         const size_t n = ns[c];
         h.n = n;
         h.x.resize(n); h.y.resize(n); h.a.resize(n); h.c0.resize(n); h.c1.resize(n);
-        for (size_t i = 0; i < n; ++i) {
-            h.x[i] = src[c][3 * i];
-            h.y[i] = src[c][3 * i + 1];
-            h.a[i] = src[c][3 * i + 2];
-            if (c == 0) {
-                h.c0[i] = std::pow(h.a[i], kScalePower);
-                h.c1[i] = 0.0;
-            } else {
-                double sn, cs;
-                ::sincos(h.a[i], &sn, &cs);
-                h.c0[i] = cs;
-                h.c1[i] = sn;
+        auto fill = [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; ++i) {
+                h.x[i] = src[c][3 * i];
+                h.y[i] = src[c][3 * i + 1];
+                h.a[i] = src[c][3 * i + 2];
+                if (c == 0) {
+                    h.c0[i] = std::pow(h.a[i], kScalePower);
+                    h.c1[i] = 0.0;
+                } else {
+                    double sn, cs;
+                    ::sincos(h.a[i], &sn, &cs);
+                    h.c0[i] = cs;
+                    h.c1[i] = sn;
+                }
             }
-        }
+        };
+        // the glibc pow / sincos of a large class on the host pool (element-
+        // wise, so the split does not change any value)
+        const size_t parts = n >= 4096 ? 16 : 1;
+        const size_t step = (n + parts - 1) / parts;
+        host_pool().parallel_for(parts, [&](size_t p) { fill(std::min(n, p * step), std::min(n, (p + 1) * step)); });
     }
 }
 
@@ -892,7 +947,10 @@ public:
             std::vector<uint32_t> lists[2];
             inlier_lists(bufs_[off_].model, Tm_, 0, lists);
             Model refit;
-            if (Tr::fit(P_, lists, refit, true)) {
+            const auto t_fit = Clock::now();
+            const bool fitted = Tr::fit(P_, lists, refit, true);
+            st_.ms_refit_fit = ms_since(t_fit);
+            if (fitted) {
                 HScore s;
                 uint32_t rn[2];
                 score_models(&refit, 1, &s, rn);
@@ -1995,6 +2053,12 @@ int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, con
         for (uint32_t i : inl) seg[i] = 1;
         return GCR_OK;
     });
+}
+
+double gcr_host_weighted_mode(const double* angles, const double* weights, size_t n, double bin_width) {
+    if (n && (!angles || !weights)) return 0.0 / 0.0;
+    std::vector<double> a(angles, angles + n), w(weights, weights + n);
+    return weighted_mode(a, w, bin_width);
 }
 
 }  // extern "C"

@@ -22,18 +22,56 @@ void colpiv_qr_solve3(std::vector<double>& A, size_t m, std::vector<double>& b, 
 }
 
 double weighted_mode(const std::vector<double>& angles, const std::vector<double>& weights, double bin_width) {
-    std::unordered_map<int, double> wmap;
-    std::unordered_map<int, double> vmap;
-    for (size_t i = 0; i < angles.size(); i++) {
-        const int bin = static_cast<int>(std::round(angles[i] / bin_width));
-        wmap[bin] += weights[i];
-        vmap[bin] += angles[i] * weights[i];
+    // findWeightedMode (two_sift.hpp:354-394): per-bin weight and weighted
+    // angle sums in input order, the mode = the first maximum in
+    // std::unordered_map<int, double> iteration order.  That order depends
+    // only on the sequence in which NEW keys were inserted (lookups of
+    // existing keys do not touch the table), so the sums are accumulated in
+    // flat arrays and only each bin's first occurrence goes into the map.
+    const size_t n = angles.size();
+    std::vector<int> bins(n);
+    int lo = 0, hi = -1;
+    for (size_t i = 0; i < n; i++) {
+        bins[i] = static_cast<int>(std::round(angles[i] / bin_width));
+        if (i == 0 || bins[i] < lo) lo = bins[i];
+        if (i == 0 || bins[i] > hi) hi = bins[i];
+    }
+    const bool dense = n > 0 && (int64_t)hi - (int64_t)lo < (int64_t)(4 * n + 1024);
+    if (!dense) {                                        // sparse / pathological bins: the maps themselves
+        std::unordered_map<int, double> wmap, vmap;
+        for (size_t i = 0; i < n; i++) {
+            wmap[bins[i]] += weights[i];
+            vmap[bins[i]] += angles[i] * weights[i];
+        }
+        int mode_bin = 0;
+        double max_w = -1;
+        for (const auto& kv : wmap)
+            if (kv.second > max_w) { max_w = kv.second; mode_bin = kv.first; }
+        return vmap[mode_bin] / wmap[mode_bin];
+    }
+    const size_t span = (size_t)((int64_t)hi - (int64_t)lo + 1);
+    std::vector<double> w(span, 0.0), v(span, 0.0);
+    std::vector<char> seen(span, 0);
+    std::unordered_map<int, double> order;               // the reference's wmap keys, in its insertion order
+    for (size_t i = 0; i < n; i++) {
+        const size_t k = (size_t)(bins[i] - lo);
+        if (!seen[k]) {
+            seen[k] = 1;
+            order.emplace(bins[i], 0.0);
+        }
+        w[k] += weights[i];
+        v[k] += angles[i] * weights[i];
     }
     int mode_bin = 0;
     double max_w = -1;
-    for (const auto& kv : wmap)
-        if (kv.second > max_w) { max_w = kv.second; mode_bin = kv.first; }
-    return vmap[mode_bin] / wmap[mode_bin];
+    for (const auto& kv : order) {
+        const double wk = w[(size_t)(kv.first - lo)];
+        if (wk > max_w) { max_w = wk; mode_bin = kv.first; }
+    }
+    if (max_w < 0) {                                     // no weight > -1 (NaN weights): vmap[0] / wmap[0]
+        if (0 < lo || 0 > hi || !seen[(size_t)(0 - lo)]) return 0.0 / 0.0;
+    }
+    return v[(size_t)(mode_bin - lo)] / w[(size_t)(mode_bin - lo)];
 }
 
 void homography_of(const RectModel& md, double H[9]) {

@@ -122,6 +122,42 @@ struct QRCols {
     double* col[4];
 };
 enum { kQsInit = 0, kQsNorm, kQsTail, kQsRefl, kQsDd, kQsDd2, kQsBStart, kQsBRefl, kQsFinal };
+
+// Fused device QR (launch_sift_refit_fused): qr3.h qr_solve<3> in 6 passes over the
+// rows instead of ~25.  Every reduction of the sequential driver is still one
+// blocked_sum over the same values in the same order, and every element-wise
+// step the same per-element operation; a pass applies one step's element-wise
+// operation and, from the values it just produced, every reduction the driver
+// needs next (they do not depend on each other).  Passes: P0 column norms
+// and step-0 tails; per step k: A(k) scales the Householder column and takes
+// its dots with the remaining columns and b; U(k) applies the reflector to
+// them and takes the norm-downdate and next-tail sums (no U(2): rows past the
+// top of b are never read again).  A one-thread control kernel between passes
+// runs the driver's scalar logic.
+constexpr int kQrfMaxRed = 6;
+struct QRFState {
+    // the next pass (written by the control kernel)
+    int mode;               // 0 none, 1 reductions only, 2 apply (scale / zero + dots), 3 update (+ sums)
+    int ck, zero, write_ck; // Householder column; zero instead of scale; store the scaled column (slot 0)
+    int nslot, nt;          // columns the pass reads (slots), of which slots 1 .. nt are updated (mode 3)
+    int scol[4];            // stored column of each slot (slot 0 = the Householder column in modes 2 / 3)
+    int nred, pad0;
+    double den, tau;
+    double tt[3];           // reflector multiplier of slots 1 .. nt
+    uint64_t lo;            // element-wise range start (rows [lo, m))
+    int ra[kQrfMaxRed], rc[kQrfMaxRed];
+    uint64_t rlo[kQrfMaxRed];   // reduction r: blocked sum of slot ra * slot rc over [rlo, m)
+    // driver state
+    int pc[3], transp[3], nonzero, done, dob, pad1;
+    double nu[3], nd[3], tau_k[3], thr_helper;
+    double x[3];
+};
+enum { kQfStep = 1, kQfApply, kQfFinal };
+// the hybrid refit's system (rows as launch_sift_rows) built inside P0 and
+// solved by the same fused passes; x_out pinned, one synchronisation
+hipError_t launch_sift_refit_fused(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns,
+                                   const uint32_t* oi, uint32_t no, size_t m, double* const cols[4], QRFState* st,
+                                   double* partials, double x_out[3], hipStream_t stream);
 hipError_t launch_qr_device(double* const cols[4], size_t m, QRDevState* st, double* partials, double x_out[3],
                             hipStream_t stream);
 // rows 0..2 of the four columns into out[c * 3 + i] (0 past m)

@@ -1472,19 +1472,16 @@ constexpr int kRowBlock = 256;
 
 // thread per row; pair p = r - ns maps to (i, j), i < j, row-major over i:
 // off(i) = i * (2 no - i - 1) / 2 pairs precede row i
-__global__ __launch_bounds__(kRowBlock) void k_sift_rows(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
-                                                         uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no,
-                                                         uint64_t rows, double* A0, double* A1, double* A2,
-                                                         double* b) {
-    const uint64_t r = (uint64_t)blockIdx.x * kRowBlock + threadIdx.x;
-    if (r >= rows) return;
+__device__ __forceinline__ void sift_row_at(const DevClass& sc, const DevClass& oc, const uint32_t* __restrict__ si,
+                                            uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no, uint64_t r,
+                                            double out[4]) {
     if (r < ns) {
         const uint32_t j = si[r];
         const double w = 1.0;
-        A0[r] = w * sc.x[j];
-        A1[r] = w * sc.y[j];
-        A2[r] = w * sc.c0[j];
-        b[r] = w;
+        out[0] = w * sc.x[j];
+        out[1] = w * sc.y[j];
+        out[2] = w * sc.c0[j];
+        out[3] = w;
         return;
     }
     const uint64_t p = r - ns;
@@ -1498,73 +1495,82 @@ __global__ __launch_bounds__(kRowBlock) void k_sift_rows(DevClass sc, DevClass o
     while ((uint64_t)i + 2 < n && off((uint64_t)i + 1) <= p) ++i;
     const uint64_t j = p - off((uint64_t)i) + (uint64_t)i + 1;
     const uint32_t a = oi[i], c = oi[j];
+    sift_pair_row(oc.x[a], oc.y[a], oc.c0[a], oc.c1[a], oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], out);
+}
+
+__global__ __launch_bounds__(kRowBlock) void k_sift_rows(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
+                                                         uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no,
+                                                         uint64_t rows, double* A0, double* A1, double* A2,
+                                                         double* b) {
+    const uint64_t r = (uint64_t)blockIdx.x * kRowBlock + threadIdx.x;
+    if (r >= rows) return;
     double row[4];
-    sift_pair_row(oc.x[a], oc.y[a], oc.c0[a], oc.c1[a], oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], row);
+    sift_row_at(sc, oc, si, ns, oi, no, r, row);
     A0[r] = row[0];
     A1[r] = row[1];
     A2[r] = row[2];
     b[r] = row[3];
 }
 
-// one wave per aligned block of kSumBlock rows: coalesced products into LDS,
-// then lane 0 folds them in row order (16-byte reads, 8 in flight)
+// blocked_sum's block partial (qr3.h) of one 256-thread workgroup: thread t
+// holds the sequential sum of its rows base + t + 256 q; the halving tree's
+// levels 128 and 64 go through LDS, the rest is a butterfly in wave 0, whose
+// lane 0 then holds x[0] of the halving tree.  `acc` / `lds` hold nred
+// reductions (lds: nred x 256 doubles); the results are valid in thread 0.
+__device__ __forceinline__ double qr_butterfly(double a) {
+#pragma unroll
+    for (int sft = 32; sft >= 1; sft >>= 1) a += __shfl_xor(a, sft, 64);
+    return a;
+}
+template <int NR>
+__device__ __forceinline__ void qr_block_tree(double (&acc)[NR], int nred, double* lds) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+        if (r < nred) lds[r * 256 + t] = acc[r];
+    __syncthreads();
+    if (t < 128) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+            if (r < nred) lds[r * 256 + t] = lds[r * 256 + t] + lds[r * 256 + t + 128];
+    }
+    __syncthreads();
+    if (t < 64) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+            if (r < nred) acc[r] = qr_butterfly(lds[r * 256 + t] + lds[r * 256 + t + 64]);
+    }
+}
+
+// one 256-thread workgroup per aligned block of kSumBlock rows: thread t sums
+// rows base + t + 256 q of [lo, hi) sequentially (coalesced loads, all in
+// flight), then the block tree -- blocked_sum's block partial
 constexpr int kPartWaves = 4;
 __device__ __forceinline__ void qr_partials_body(const double* __restrict__ a, const double* __restrict__ c,
                                                  uint64_t lo, uint64_t hi, uint64_t blk0, uint64_t nblk,
                                                  double* __restrict__ partials) {
-    __shared__ double prod[kPartWaves][kSumBlock];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t blk = (uint64_t)blockIdx.x * kPartWaves + wave;
+    __shared__ double lds[256];
+    const int t = threadIdx.x;
+    const uint64_t blk = blockIdx.x;
     if (blk >= nblk) return;
     const uint64_t base = (blk0 + blk) * kSumBlock;
-    const uint64_t b0 = base < lo ? lo : base;
-    const uint64_t b1 = base + kSumBlock < hi ? base + kSumBlock : hi;
-    double* pw = prod[wave];
-    // all 2 x 16 loads of the lane in flight before any product is stored
-    constexpr int kPerLane = kSumBlock / 64;
-    double av[kPerLane], cv[kPerLane];
+    constexpr int kPer = (int)(kSumBlock / 256);
+    double av[kPer], cv[kPer];
 #pragma unroll
-    for (int q = 0; q < kPerLane; ++q) {
-        const uint64_t i = base + lane + 64 * q;
-        const uint64_t ii = (i >= b0 && i < b1) ? i : b0;
-        av[q] = a[ii];
-        cv[q] = c[ii];
+    for (int q = 0; q < kPer; ++q) {
+        const uint64_t i = base + t + 256 * q;
+        const bool in = i >= lo && i < hi;
+        av[q] = in ? a[i] : 0.0;
+        cv[q] = in ? c[i] : 0.0;
     }
+    double acc[1] = {0.0};
 #pragma unroll
-    for (int q = 0; q < kPerLane; ++q) pw[lane + 64 * q] = av[q] * cv[q];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // blocked_sum's order (qr3.h): lane l < 16 folds sub-block l (64 rows,
-    // clipped to [b0, b1)) sequentially, then lane 0 folds the sub-block
-    // partials of the sub-blocks that meet the range, in order
-    constexpr int kSubs = (int)(kSumBlock / kSumSub);
-    __shared__ double subp[kPartWaves][kSubs];
-    const uint64_t e0 = b0 - base, e1 = b1 - base;
-    if (lane < kSubs) {
-        const uint64_t s0 = (uint64_t)lane * kSumSub, s1 = s0 + kSumSub;
-        const uint64_t lo_e = s0 > e0 ? s0 : e0, hi_e = s1 < e1 ? s1 : e1;
-        double sp = 0.0;
-        uint64_t e = lo_e;
-        for (; e + 8 <= hi_e; e += 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = pw[e + u];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) sp += v[u];
-        }
-        for (; e < hi_e; ++e) sp += pw[e];
-        subp[wave][lane] = sp;
+    for (int q = 0; q < kPer; ++q) {
+        const uint64_t i = base + t + 256 * q;
+        if (i >= lo && i < hi) acc[0] += av[q] * cv[q];
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (lane == 0) {
-        double part = 0.0;
-        for (int l = 0; l < kSubs; ++l) {
-            const uint64_t s0 = (uint64_t)l * kSumSub, s1 = s0 + kSumSub;
-            if (s1 > e0 && s0 < e1) part += subp[wave][l];
-        }
-        partials[blk] = part;
-    }
+    qr_block_tree<1>(acc, 1, lds);
+    if (t == 0) partials[blk] = acc[0];
 }
 
 __global__ __launch_bounds__(64 * kPartWaves) void k_qr_partials(const double* __restrict__ a,
@@ -1794,6 +1800,362 @@ __global__ __launch_bounds__(64) void k_qrd_ctl(QRCols cols, QRDevState* st, con
             st->done = 1;
             break;
         }
+    }
+}
+
+// ---- fused device QR (QRFState, kernels.h) ------------------------------
+// One pass: a 256-thread workgroup per aligned block of kSumBlock rows; thread
+// t walks rows base + t + 256 q (q = 0..3, coalesced, all loads in flight),
+// applies the pass's element-wise step to rows >= lo, stores the changed
+// columns, and accumulates every reduction's products of its range
+// sequentially; the block tree then gives blocked_sum's block partial, stored
+// at partials[r * nblk + blk].  Columns are addressed through slots (slot 0 =
+// the Householder column in modes 2 / 3).
+constexpr int kQrfWaves = 4;
+__global__ __launch_bounds__(256) void k_qrf_pass(QRCols cols, const QRFState* __restrict__ st, uint64_t m,
+                                                  uint64_t nblk, double* __restrict__ partials) {
+    __shared__ double lds[kQrfMaxRed * 256];
+    const int mode = st->mode;
+    if (mode == 0) return;
+    const int t = threadIdx.x;
+    const uint64_t blk = blockIdx.x;
+    if (blk >= nblk) return;
+    const uint64_t base = blk * kSumBlock;
+    const uint64_t lo = st->lo;
+    const int nslot = st->nslot, nred = st->nred, nt = st->nt;
+    const double* src[4];
+    double* dst[4];
+    for (int k = 0; k < 4; ++k) {
+        src[k] = k < nslot ? cols.col[st->scol[k]] : nullptr;
+        dst[k] = k < nslot ? cols.col[st->scol[k]] : nullptr;
+    }
+    const bool zero = st->zero != 0, wr0 = st->write_ck != 0;
+    const double den = st->den, tau = st->tau;
+    const double tt[4] = {0.0, st->tt[0], st->tt[1], st->tt[2]};
+    int ra[kQrfMaxRed], rb[kQrfMaxRed];
+    uint64_t rlo[kQrfMaxRed];
+    double acc[kQrfMaxRed];
+#pragma unroll
+    for (int r = 0; r < kQrfMaxRed; ++r) {
+        ra[r] = r < nred ? st->ra[r] : 0;
+        rb[r] = r < nred ? st->rc[r] : 0;
+        rlo[r] = r < nred ? st->rlo[r] : m;
+        acc[r] = 0.0;
+    }
+    constexpr int kU = (int)(kSumBlock / 256);
+    double v[kU][4];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint64_t i = base + t + 256 * u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[u][k] = (k < nslot && i < m) ? src[k][i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint64_t i = base + t + 256 * u;
+        if (i >= m) continue;
+        if (i >= lo) {
+            if (mode == 2) {                    // Householder column: scale (or zero)
+                v[u][0] = zero ? 0.0 : v[u][0] / den;
+                if (wr0) dst[0][i] = v[u][0];
+            } else if (mode == 3) {             // reflector on the targets (slots 1 .. nt)
+#pragma unroll
+                for (int k = 1; k < 4; ++k)
+                    if (k <= nt) {
+                        v[u][k] -= (tau * v[u][0]) * tt[k];
+                        dst[k][i] = v[u][k];
+                    }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kQrfMaxRed; ++r) {
+            if (r >= nred || i < rlo[r]) continue;
+            double pa = 0.0, pb = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (ra[r] == k) pa = v[u][k];
+                if (rb[r] == k) pb = v[u][k];
+            }
+            acc[r] += pa * pb;
+        }
+    }
+    qr_block_tree<kQrfMaxRed>(acc, nred, lds);
+    if (t == 0)
+        for (int r = 0; r < nred; ++r) partials[(uint64_t)r * nblk + blk] = acc[r];
+}
+
+// P0 of the hybrid refit: builds the rows (sift_row_at, as k_sift_rows) of a
+// block and takes the six reductions the first step needs from them:
+// r = c: sumsq(col c, 0, m), r = 3 + c: sumsq(col c, 1, m), c = 0..2
+__global__ __launch_bounds__(256) void k_qrf_p0(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
+                                                uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no,
+                                                QRCols cols, uint64_t m, uint64_t nblk,
+                                                double* __restrict__ partials) {
+    __shared__ double lds[6 * 256];
+    const int t = threadIdx.x;
+    const uint64_t blk = blockIdx.x;
+    if (blk >= nblk) return;
+    const uint64_t base = blk * kSumBlock;
+    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < (int)(kSumBlock / 256); ++q) {
+        const uint64_t i = base + t + 256 * q;
+        if (i >= m) break;
+        double row[4];
+        sift_row_at(sc, oc, si, ns, oi, no, i, row);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cols.col[c][i] = row[c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double pr = row[c] * row[c];
+            acc[c] += pr;
+            if (i >= 1) acc[3 + c] += pr;
+        }
+    }
+    qr_block_tree<6>(acc, 6, lds);
+    if (t == 0)
+        for (int r = 0; r < 6; ++r) partials[(uint64_t)r * nblk + blk] = acc[r];
+}
+
+constexpr int kQrfCtlThreads = 512;     // >= kQrfMaxRed x 64 super-blocks (4 M rows) in one sweep
+__global__ __launch_bounds__(kQrfCtlThreads) void k_qrf_ctl(QRCols cols, QRFState* st,
+                                                            const double* __restrict__ partials, uint64_t m,
+                                                            uint64_t nblk, int step, int k) {
+    constexpr uint64_t per = kSumSuper / kSumBlock;
+    __shared__ double sup[kQrfMaxRed * kQrdSup];
+    // totals of the previous pass's reductions (all ranges start in block 0):
+    // the block partials sequentially inside each aligned super-block (one
+    // lane per (reduction, super-block), its <= 64 loads in flight), then the
+    // super-block partials sequentially -- blocked_sum's order
+    // STEP(0) follows P0 (six reductions, state not yet initialised)
+    const bool first = step == kQfStep && k == 0;
+    const int nred = first ? 6 : (st->mode == 0 ? 0 : st->nred);
+    const uint64_t nsup = (nblk - 1) / per + 1;
+    for (uint64_t idx = threadIdx.x; idx < (uint64_t)nred * nsup; idx += kQrfCtlThreads) {
+        const uint64_t r = idx / nsup, u = idx % nsup;
+        const double* part = partials + r * nblk;
+        const uint64_t b_lo = u * per, b_hi = min(nblk, (u + 1) * per);
+        double w[per];
+#pragma unroll
+        for (uint64_t q = 0; q < per; ++q) w[q] = b_lo + q < b_hi ? part[b_lo + q] : 0.0;
+        double sp = 0.0;
+#pragma unroll
+        for (uint64_t q = 0; q < per; ++q)
+            if (b_lo + q < b_hi) sp += w[q];
+        sup[idx] = sp;
+    }
+    __syncthreads();
+    // lane r: the super-block partials of reduction r, sequentially
+    __shared__ double tot_sh[kQrfMaxRed];
+    if (threadIdx.x < (unsigned)nred) {
+        const double* sr = sup + (uint64_t)threadIdx.x * nsup;
+        double tv = 0.0;
+        uint64_t u = 0;
+        for (; u + 8 <= nsup; u += 8) {
+            double w[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = sr[u + q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) tv += w[q];
+        }
+        for (; u < nsup; ++u) tv += sr[u];
+        tot_sh[threadIdx.x] = tv;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double tot[kQrfMaxRed];
+    for (int r = 0; r < kQrfMaxRed; ++r) tot[r] = r < nred ? tot_sh[r] : 0.0;
+    if (first) {
+        for (int q = 0; q < 3; ++q) { st->pc[q] = q; st->tau_k[q] = 0.0; st->transp[q] = q; }
+        st->nonzero = 3;
+        st->done = 0;
+    }
+    double* const* col = cols.col;
+    const double eps = 2.220446049250313e-16;           // numeric_limits<double>::epsilon()
+    st->mode = 0;
+    st->nred = 0;
+    st->nt = 0;
+    if (st->done) return;
+    if (step == kQfStep) {
+        double tail_of[3] = {0.0, 0.0, 0.0};
+        if (k == 0) {
+            for (int c = 0; c < 3; ++c) {
+                st->nd[c] = sqrt(tot[c]);               // pc[c] == c before the first pivot
+                st->nu[c] = st->nd[c];
+                tail_of[c] = tot[3 + c];
+            }
+            double maxn = st->nu[0];
+            for (int q = 1; q < 3; ++q)
+                if (maxn < st->nu[q]) maxn = st->nu[q];
+            const double me = maxn * eps;
+            st->thr_helper = (me * me) / (double)m;
+        } else {
+            // the norm downdates of step k - 1 (qr3.h): remaining columns
+            // pc[j], j >= k; U(k-1) summed sumsq(pc[j], k, m) at 2 (j - k) and
+            // sumsq(pc[j], k + 1, m) at 2 (j - k) + 1
+            const double downdate_thr = sqrt(eps);
+            for (int j = k; j < 3; ++j) {
+                const int cj = st->pc[j];
+                tail_of[cj] = tot[2 * (j - k) + 1];
+                if (st->nu[j] != 0.0) {
+                    double temp = fabs(col[cj][k - 1]) / st->nu[j];
+                    temp = (1.0 + temp) * (1.0 - temp);
+                    temp = temp < 0.0 ? 0.0 : temp;
+                    const double r = st->nu[j] / st->nd[j];
+                    const double temp2 = temp * (r * r);
+                    if (temp2 <= downdate_thr) {
+                        st->nd[j] = sqrt(tot[2 * (j - k)]);
+                        st->nu[j] = st->nd[j];
+                    } else {
+                        st->nu[j] *= sqrt(temp);
+                    }
+                }
+            }
+        }
+        // pivot of step k
+        int big = k;
+        double bign = st->nu[k];
+        for (int jj = k + 1; jj < 3; ++jj)
+            if (bign < st->nu[jj]) { bign = st->nu[jj]; big = jj; }
+        if (st->nonzero == 3 && bign * bign < st->thr_helper * (double)(m - k)) st->nonzero = k;
+        st->transp[k] = big;
+        if (k != big) {
+            int tp = st->pc[k]; st->pc[k] = st->pc[big]; st->pc[big] = tp;
+            double tv = st->nu[k]; st->nu[k] = st->nu[big]; st->nu[big] = tv;
+            tv = st->nd[k]; st->nd[k] = st->nd[big]; st->nd[big] = tv;
+        }
+        const int ck = st->pc[k];
+        const double tail = tail_of[ck];
+        const double c0 = col[ck][k];
+        double tau, beta;
+        st->ck = ck;
+        st->lo = (uint64_t)k + 1;
+        if (tail <= 2.2250738585072014e-308) {       // numeric_limits<double>::min()
+            tau = 0.0;
+            beta = c0;
+            st->zero = 1;
+            st->den = 0.0;
+        } else {
+            beta = sqrt(c0 * c0 + tail);
+            if (c0 >= 0.0) beta = -beta;
+            st->zero = 0;
+            st->den = c0 - beta;
+            tau = (beta - c0) / beta;
+        }
+        st->tau_k[k] = tau;
+        st->tau = tau;
+        col[ck][k] = beta;
+        // A(k): the reflector's dots with the remaining columns and with b
+        // (b's reflector k runs iff k < nonzero, decided by this pivot)
+        st->dob = (k < st->nonzero && tau != 0.0) ? 1 : 0;
+        st->scol[0] = ck;
+        int n = 0;
+        if (tau != 0.0)
+            for (int j = k + 1; j < 3; ++j) {
+                st->scol[1 + n] = st->pc[j];
+                st->ra[n] = 0;
+                st->rc[n] = 1 + n;
+                st->rlo[n] = (uint64_t)k + 1;
+                ++n;
+            }
+        if (st->dob) {
+            st->scol[1 + n] = 3;
+            st->ra[n] = 0;
+            st->rc[n] = 1 + n;
+            st->rlo[n] = (uint64_t)k + 1;
+            ++n;
+        }
+        st->nslot = 1 + n;
+        st->nred = n;
+        st->nt = 0;
+        st->write_ck = k < 2 ? 1 : 0;     // v_2 is only needed for b's dot, taken in this pass
+        st->mode = 2;
+        return;
+    }
+    if (step == kQfApply) {
+        // reflector k applied to the tops of its targets (apply_reflector)
+        const int ck = st->ck;
+        const double tau = st->tau_k[k];
+        int n = 0, nt = 0;
+        st->scol[0] = ck;
+        if (tau != 0.0)
+            for (int j = k + 1; j < 3; ++j) {
+                const int c = st->pc[j];
+                double tt = tot[n++];
+                const double ckv = col[c][k];
+                tt += ckv;
+                col[c][k] = ckv - tau * tt;
+                st->scol[1 + nt] = c;
+                st->tt[nt] = tt;
+                ++nt;
+            }
+        if (st->dob) {
+            double tt = tot[n++];
+            const double bk = col[3][k];
+            tt += bk;
+            col[3][k] = bk - tau * tt;
+            st->scol[1 + nt] = 3;
+            st->tt[nt] = tt;
+            ++nt;
+        }
+        // U(k): the updates (slots 1 .. nt), then the downdate sums
+        // sumsq(pc[j], k+1, m) and the next tails sumsq(pc[j], k+2, m) of the
+        // remaining columns (read-only slots when tau = 0)
+        int ns = 1 + nt;
+        st->nt = nt;
+        st->ck = ck;
+        st->tau = tau;
+        st->lo = (uint64_t)k + 1;
+        int r = 0;
+        for (int j = k + 1; j < 3; ++j) {
+            int slot = -1;
+            for (int q = 1; q < ns; ++q)
+                if (st->scol[q] == st->pc[j]) slot = q;
+            if (slot < 0) {
+                slot = ns++;
+                st->scol[slot] = st->pc[j];
+            }
+            st->ra[r] = st->rc[r] = slot;
+            st->rlo[r] = (uint64_t)k + 1;
+            ++r;
+            st->ra[r] = st->rc[r] = slot;
+            st->rlo[r] = (uint64_t)k + 2;
+            ++r;
+        }
+        st->nslot = ns;
+        st->nred = r;
+        st->mode = 3;
+        return;
+    }
+    // kQfFinal (after A(2)): b's reflector 2 on the top row, back substitution
+    {
+        const double tau = st->tau_k[2];
+        if (st->dob) {
+            double tt = tot[0];
+            const double bk = col[3][2];
+            tt += bk;
+            col[3][2] = bk - tau * tt;
+        }
+        if (st->nonzero == 0) {
+            st->x[0] = st->x[1] = st->x[2] = 0.0;
+            st->done = 1;
+            return;
+        }
+        int perm[3] = {0, 1, 2};
+        for (int q = 0; q < 3; ++q) {
+            const int tq = st->transp[q];
+            const int tv = perm[q]; perm[q] = perm[tq]; perm[tq] = tv;
+        }
+        const int nz = st->nonzero;
+        double c[3];
+        for (int q = 0; q < 3; ++q) c[q] = col[3][q];
+        for (int jj = nz; jj-- > 0;) {
+            c[jj] = c[jj] / col[st->pc[jj]][jj];
+            for (int i = 0; i < jj; ++i) c[i] -= c[jj] * col[st->pc[jj]][i];
+        }
+        for (int i = 0; i < nz; ++i) st->x[perm[i]] = c[i];
+        for (int i = nz; i < 3; ++i) st->x[perm[i]] = 0.0;
+        st->done = 1;
     }
 }
 
@@ -2058,8 +2420,8 @@ hipError_t launch_qr_partials(const double* a, const double* c, size_t lo, size_
     if (hi <= lo) return hipSuccess;
     const uint64_t blk0 = lo / kSumBlock, nblk = (hi - 1) / kSumBlock - blk0 + 1;
     *nblocks = nblk;
-    hipLaunchKernelGGL(k_qr_partials, dim3((unsigned)((nblk + kPartWaves - 1) / kPartWaves)), dim3(64 * kPartWaves),
-                       0, stream, a, c, (uint64_t)lo, (uint64_t)hi, blk0, nblk, partials);
+    hipLaunchKernelGGL(k_qr_partials, dim3((unsigned)nblk), dim3(256), 0, stream, a, c, (uint64_t)lo, (uint64_t)hi,
+                       blk0, nblk, partials);
     return hipGetLastError();
 }
 
@@ -2068,7 +2430,7 @@ hipError_t launch_qr_device(double* const cols[4], size_t m, QRDevState* st, dou
     if (m < 4 || m > (size_t)kQrdSup * kSumSuper) return hipErrorInvalidValue;
     QRCols qc{{cols[0], cols[1], cols[2], cols[3]}};
     const uint64_t nblk = (m - 1) / kSumBlock + 1;
-    const dim3 gr((unsigned)((nblk + kPartWaves - 1) / kPartWaves)), br(64 * kPartWaves);
+    const dim3 gr((unsigned)nblk), br(256);
     const dim3 ge((unsigned)((m + 255) / 256)), be(256);
     hipError_t e = hipMemsetAsync(st, 0, sizeof(QRDevState), stream);   // no reduction pending, not done
     if (e != hipSuccess) return e;
@@ -2094,6 +2456,36 @@ hipError_t launch_qr_device(double* const cols[4], size_t m, QRDevState* st, dou
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double* dx = reinterpret_cast<const double*>(reinterpret_cast<const char*>(st) + offsetof(QRDevState, x));
+    e = hipMemcpyAsync(x_out, dx, 3 * sizeof(double), hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t launch_sift_refit_fused(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns,
+                                   const uint32_t* oi, uint32_t no, size_t m, double* const cols[4], QRFState* st,
+                                   double* partials, double x_out[3], hipStream_t stream) {
+    if (m < 4 || m > (size_t)kQrdSup * kSumSuper) return hipErrorInvalidValue;
+    QRCols qc{{cols[0], cols[1], cols[2], cols[3]}};
+    const uint64_t nblk = (m - 1) / kSumBlock + 1;
+    const dim3 gp((unsigned)nblk), bp(256);
+    auto C = [&](int step, int k) {
+        hipLaunchKernelGGL(k_qrf_ctl, dim3(1), dim3(kQrfCtlThreads), 0, stream, qc, st, partials, (uint64_t)m, nblk,
+                           step, k);
+    };
+    auto P = [&]() { hipLaunchKernelGGL(k_qrf_pass, gp, bp, 0, stream, qc, st, (uint64_t)m, nblk, partials); };
+    hipLaunchKernelGGL(k_qrf_p0, gp, bp, 0, stream, sc, oc, si, ns, oi, no, qc, (uint64_t)m, nblk, partials);
+    for (int k = 0; k < 3; ++k) {
+        C(kQfStep, k);
+        P();                                // A(k)
+        if (k < 2) {
+            C(kQfApply, k);
+            P();                            // U(k)
+        }
+    }
+    C(kQfFinal, 2);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const double* dx = reinterpret_cast<const double*>(reinterpret_cast<const char*>(st) + offsetof(QRFState, x));
     e = hipMemcpyAsync(x_out, dx, 3 * sizeof(double), hipMemcpyDeviceToHost, stream);
     if (e != hipSuccess) return e;
     return hipStreamSynchronize(stream);

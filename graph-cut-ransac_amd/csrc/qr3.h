@@ -5,14 +5,18 @@
 // systems) and the GPU (the hybrid final refit's ~n_o^2/2 pair rows) run the
 // same control flow and the same per-element arithmetic.
 //
-// Reductions use ONE fixed order, blocked_sum: sequential inside aligned
-// sub-blocks of kSumSub rows, sub-block partials sequentially inside aligned
-// blocks of kSumBlock rows, block partials sequentially inside aligned
-// super-blocks of kSumSuper rows, then the super-block partials sequentially.
-// Eigen's own order is packet-vectorised and unpinned (no Eigen here); for
-// m <= kSumSub the blocked order is plain sequential summation.  The oracle
-// restates the same order (oracle/gcr_oracle.cpp), so host, GPU and oracle
-// agree bitwise.
+// Reductions use ONE fixed order, blocked_sum: rows are grouped into aligned
+// blocks of kSumBlock = 1024 rows; inside a block, "lane" l (0..255) sums the
+// rows base + l + 256 q (q = 0..3) of the range sequentially, and the 256 lane
+// partials are combined by a halving tree (x[l] += x[l + h] for h = 128, 64,
+// .., 1; the value of x[0]); block partials are summed sequentially inside
+// aligned super-blocks of kSumSuper rows, then the super-block partials
+// sequentially.  It is the order a 256-thread GPU workgroup produces with
+// coalesced loads (one block per workgroup, the tree's two top levels through
+// LDS, the rest as a wave butterfly, whose lane 0 equals the halving tree), so
+// the refit's passes are bandwidth-bound.  Eigen's own order is
+// packet-vectorised and unpinned (no Eigen here).  The oracle restates the
+// same order (oracle/gcr_oracle.cpp), so host, GPU and oracle agree bitwise.
 #pragma once
 
 #include <algorithm>
@@ -24,16 +28,22 @@
 namespace gcr {
 
 constexpr size_t kSumBlock = 1024;
-constexpr size_t kSumSub = 64;         // sub-blocks: 16 per block
-constexpr size_t kSumSuper = 64 * kSumBlock;   // super-blocks: 64 blocks
+constexpr size_t kSumLanes = 256;                // lanes of a block (rows l + 256 q)
+constexpr size_t kSumSuper = 64 * kSumBlock;     // super-blocks: 64 blocks
 
-// sum_{i in [lo, hi)} f(i) in blocked order: sequential inside each aligned
-// sub-block of kSumSub rows, the sub-block partials of an aligned block of
-// kSumBlock rows sequentially, the block partials of an aligned super-block
-// of kSumSuper rows sequentially, then the super-block partials sequentially.
-// (The levels keep the GPU's sequential chains at 64 + 16 + 64 + m / 65536
-// adds; inside one super-block the order is the two-level one, and for
-// m <= 64 it is plain sequential summation.)
+// the block partial of block `base` (aligned) over rows [lo, hi) ∩ block
+template <class F>
+inline double block_partial(size_t base, size_t lo, size_t hi, F f) {
+    double acc[kSumLanes];
+    for (size_t l = 0; l < kSumLanes; ++l) acc[l] = 0.0;
+    const size_t b0 = std::max(base, lo), b1 = std::min(base + kSumBlock, hi);
+    for (size_t i = b0; i < b1; ++i) acc[(i - base) & (kSumLanes - 1)] += f(i);   // each lane in q order
+    for (size_t h = kSumLanes / 2; h >= 1; h >>= 1)
+        for (size_t l = 0; l < h; ++l) acc[l] = acc[l] + acc[l + h];
+    return acc[0];
+}
+
+// sum_{i in [lo, hi)} f(i) in blocked order (see the file comment)
 template <class F>
 inline double blocked_sum(size_t lo, size_t hi, F f) {
     double total = 0.0;
@@ -42,15 +52,10 @@ inline double blocked_sum(size_t lo, size_t hi, F f) {
         const size_t send = std::min(hi, (i / kSumSuper + 1) * kSumSuper);
         double sup = 0.0;
         while (i < send) {
-            const size_t end = std::min(send, (i / kSumBlock + 1) * kSumBlock);
-            double part = 0.0;
-            while (i < end) {
-                const size_t sbe = std::min(end, (i / kSumSub + 1) * kSumSub);
-                double sp = 0.0;
-                for (; i < sbe; ++i) sp += f(i);
-                part += sp;
-            }
-            sup += part;
+            const size_t base = i / kSumBlock * kSumBlock;
+            const size_t end = std::min(send, base + kSumBlock);
+            sup += block_partial(base, i, end, f);
+            i = end;
         }
         total += sup;
     }

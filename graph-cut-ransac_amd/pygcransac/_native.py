@@ -66,6 +66,7 @@ class Stats(C.Structure):
         ("ms_lo_lists", C.c_double),
         ("ms_lo_fit", C.c_double),
         ("ms_lo_score", C.c_double),
+        ("ms_refit_fit", C.c_double),
     ]
 
     def as_dict(self):
@@ -165,6 +166,8 @@ def _load():
                                       C.POINTER(C.c_size_t)]
     L.gcr_host_bk_energy.argtypes = [C.c_size_t, dp, u32p, dp, C.c_size_t, u8p]
     L.gcr_host_labeling.argtypes = [dp, C.c_size_t, C.c_double, C.c_double, u32p, C.c_size_t, u8p]
+    L.gcr_host_weighted_mode.argtypes = [dp, dp, C.c_size_t, C.c_double]
+    L.gcr_host_weighted_mode.restype = C.c_double
     L.gcr_host_homography.argtypes = [C.POINTER(RectModel), dp]
     L.gcr_host_homography.restype = None
     return L

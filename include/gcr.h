@@ -102,6 +102,9 @@ typedef struct gcr_stats {
     double ms_lo_lists;           /* LO: inlier lists (GPU labeling + copy back)    */
     double ms_lo_fit;             /* LO: sample draws + least-squares fits (host)   */
     double ms_lo_score;           /* LO: scoring the trial models (GPU)             */
+    double ms_refit_fit;          /* final refit: the non-minimal fit itself (system,
+                                     QR, weighted mode); the rest of ms_refit is the
+                                     buffer reconciliation, rescoring and lists      */
 } gcr_stats;
 
 /* ---- context ---------------------------------------------------------- */
@@ -263,6 +266,8 @@ int gcr_host_bk_energy(size_t n, const double* unary, const uint32_t* edges, con
                        uint8_t* seg);
 int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, const uint32_t* edges, size_t m,
                       uint8_t* seg);
+/* host-only: findWeightedMode (two_sift.hpp:354-394) as the fits use it */
+double gcr_host_weighted_mode(const double* angles, const double* weights, size_t n, double bin_width);
 /* host-only (no GPU): deterministic math and sampler used on both sides */
 double gcr_host_log(double x);
 double gcr_host_pow_m3(double t);

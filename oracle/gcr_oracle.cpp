@@ -296,13 +296,13 @@ static bool faithful_subset(const std::vector<size_t>& indices, size_t N, std::v
 // Restatement of Eigen::ColPivHouseholderQR<MatrixX3d>::compute + solve for an
 // m x 3 column-major matrix.  Eigen reduces with packet-vectorised partial sums
 // (an order that cannot be pinned without Eigen); every reduction here uses the
-// engine's fixed blocked order instead: sequential within aligned sub-blocks
-// of 64 rows, the sub-block partials sequentially within aligned blocks of
-// 1024 rows, the block partials sequentially within aligned super-blocks of
-// 65536 rows, then the super-block partials sequentially -- what the GPU
-// refit reproduces bitwise.
+// engine's fixed blocked order instead: aligned blocks of 1024 rows, inside a
+// block 256 partial sums (rows base + l + 256 q, q = 0..3, sequentially), those
+// combined by a halving tree (l += l + h, h = 128 .. 1, the value at l = 0),
+// block partials sequentially within aligned super-blocks of 65536 rows, then
+// the super-block partials sequentially -- what the GPU refit reproduces
+// bitwise.
 static constexpr size_t kSumBlockRows = 1024;
-static constexpr size_t kSumSubRows = 64;
 static constexpr size_t kSumSuperRows = 64 * kSumBlockRows;
 template <class F>
 static double bsum(size_t lo, size_t hi, F f) {
@@ -311,16 +311,19 @@ static double bsum(size_t lo, size_t hi, F f) {
         const size_t u1 = std::min(hi, (u0 / kSumSuperRows + 1) * kSumSuperRows);
         double sup = 0.0;
         for (size_t b0 = u0; b0 < u1;) {
-            const size_t b1 = std::min(u1, (b0 / kSumBlockRows + 1) * kSumBlockRows);
-            double part = 0.0;
-            for (size_t s0 = b0; s0 < b1;) {
-                const size_t s1 = std::min(b1, (s0 / kSumSubRows + 1) * kSumSubRows);
-                double sp = 0.0;
-                for (size_t i = s0; i < s1; ++i) sp += f(i);
-                part += sp;
-                s0 = s1;
+            const size_t base = b0 - b0 % kSumBlockRows;
+            const size_t b1 = std::min(u1, base + kSumBlockRows);
+            double lane[256];
+            for (int l = 0; l < 256; ++l) {
+                lane[l] = 0.0;
+                for (size_t q = 0; q < 4; ++q) {
+                    const size_t i = base + (size_t)l + 256 * q;
+                    if (i >= b0 && i < b1) lane[l] += f(i);
+                }
             }
-            sup += part;
+            for (int h = 128; h >= 1; h /= 2)
+                for (int l = 0; l < h; ++l) lane[l] += lane[l + h];
+            sup += lane[0];
             b0 = b1;
         }
         total += sup;

@@ -59,3 +59,34 @@ def test_sift_fit_matches_oracle_bitwise(ks, ko):
         assert got is None
     else:
         assert np.array_equal(got.view(np.uint64), exp.view(np.uint64))
+
+
+def test_weighted_mode_matches_oracle_including_ties():
+    # findWeightedMode (two_sift.hpp:354-394): the first maximum in
+    # unordered_map iteration order decides ties; the product accumulates in
+    # arrays and rebuilds only the map's key order (first occurrences)
+    import ctypes as C
+
+    import numpy as np
+
+    import oracle_ffi as O
+    from pygcransac import _native as N
+
+    dp = C.POINTER(C.c_double)
+    bw = 0.5 * np.pi / 180.0
+    rng = np.random.default_rng(17)
+    cases = []
+    for n in (1, 2, 14, 91, 500, 2500, 6000):
+        a = rng.uniform(0, np.pi, n)
+        cases.append((a, np.full(n, 1.0 / n)))                       # equal weights: many ties
+        cases.append((np.round(a / bw) * bw + rng.uniform(-0.2, 0.2, n) * bw, rng.uniform(0, 1, n)))
+    cases.append((np.array([0.1, 0.1 + 1e5, -3.0, 7e3]), np.ones(4) / 4))   # sparse bins
+    cases.append((np.array([0.2, np.nan, 0.3]), np.array([0.5, 0.25, 0.25])))
+    cases.append((np.zeros(0), np.zeros(0)))
+    for a, w in cases:
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        got = N.lib.gcr_host_weighted_mode(a.ctypes.data_as(dp), w.ctypes.data_as(dp), a.size, bw)
+        ref = O.lib().oracle_weighted_mode(a.ctypes.data_as(dp), w.ctypes.data_as(dp), a.size, bw)
+        assert np.array_equal(np.float64(got).view(np.uint64), np.float64(ref).view(np.uint64)) or \
+            (np.isnan(got) and np.isnan(ref)), (a.size, got, ref)
