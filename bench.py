@@ -552,7 +552,8 @@ def bench_strong(args, rank, world, dist, device, coll_dev, backend):
     "nccl") and the replay / LO / refit run identically on every rank
     (gcr_problem_run_sharded), so every rank returns the single-rank result.
     value = the problem's scored hypotheses / the max-over-ranks wall time of
-    the whole call (LO and refit included, they do not shard)."""
+    the whole call (LO and refit included, they do not shard).  `--warmup W`
+    runs the same call W times untimed first."""
     from pygcransac import _native as N
     from pygcransac import distributed as D
 
@@ -572,7 +573,8 @@ def bench_strong(args, rank, world, dist, device, coll_dev, backend):
         if dist is not None:
             dist.barrier()
 
-    run(max(1, args.warmup) * args.slots)                 # untimed warm-up (same code path)
+    for _ in range(max(1, args.warmup)):                  # untimed warm-up: whole runs (their workspace
+        run(budget)                                       # -- pinned buffers included -- is reused)
     barrier()
     t0 = time.perf_counter()
     _, masks, st, _ = run(budget)

@@ -115,6 +115,12 @@ struct Ptr {
     T* p = nullptr;
 };
 
+template <class B>
+void swap_buf(B& a, B& b) {
+    std::swap(a.p, b.p);
+    std::swap(a.cap, b.cap);
+}
+
 // Score arrays for `cap` hypotheses, device and pinned host mirrors, each set
 // in one allocation laid out n0 | n1 | v0 | v1 | tot (capacity-sized fields),
 // so that a small batch comes back in one copy instead of five (every copy
@@ -142,6 +148,14 @@ struct ScoreBufs {
         carve(hblk.p, hn0, hn1, hv0, hv1, htot);
     }
     ScoreOut dev() const { return ScoreOut{n0.p, n1.p, v0.p, v1.p, tot.p}; }
+    void swap(ScoreBufs& o) {
+        std::swap(dblk.p, o.dblk.p); std::swap(dblk.cap, o.dblk.cap);
+        std::swap(hblk.p, o.hblk.p); std::swap(hblk.cap, o.hblk.cap);
+        std::swap(cap, o.cap);
+        std::swap(n0, o.n0); std::swap(n1, o.n1); std::swap(hn0, o.hn0); std::swap(hn1, o.hn1);
+        std::swap(v0, o.v0); std::swap(v1, o.v1); std::swap(tot, o.tot);
+        std::swap(hv0, o.hv0); std::swap(hv1, o.hv1); std::swap(htot, o.htot);
+    }
     void d2h(size_t n, hipStream_t s) {
         const size_t span = (3 * cap + n) * sizeof(double);    // n0 .. tot[n)
         if (span <= (size_t)256 * 1024 || 2 * n >= cap) {
@@ -208,6 +222,15 @@ struct Workspace {
     DevBuf<QRFState> rf_qrf;            // GPU refit: fused-pass QR driver state
     PinBuf<double> rf_hpart;
     PinBuf<double> rf_htop;             // GPU refit: async upload ring
+    // the next chunk of slots, generated and scored on the side stream while
+    // the host replays the current one (RunnerT prefetch); swapped in whole
+    DevBuf<uint8_t> pf_inc;
+    DevBuf<RectModel> pf_models;
+    DevBuf<GeoModel> pf_gmodels;
+    PinBuf<uint8_t> pf_h_inc;
+    PinBuf<RectModel> pf_h_models;
+    PinBuf<GeoModel> pf_h_gmodels;
+    ScoreBufs pf_sb;
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
@@ -216,10 +239,17 @@ struct Workspace {
 
 struct gcr_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;       // the replay's stream: LO, refit, fetched chunks (high priority)
+    hipStream_t side = nullptr;         // speculative next chunks (low priority)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t pev0 = nullptr, pev1 = nullptr, pdone = nullptr;
     int n_cu = 256;                     // compute units (one batch-scorer workgroup each)
     Workspace shared;                   // reused by the gcr_rect_* calls
+    // workspaces of destroyed problems, reused by the next gcr_problem_create
+    // (their device and pinned buffers stay allocated: pinned allocations
+    // cost milliseconds)
+    std::mutex ws_mu;
+    std::vector<std::unique_ptr<Workspace>> ws_free;
 };
 
 struct gcr_problem {
@@ -667,7 +697,14 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     if (shared_workspace) {
         P->w = &ctx->shared;
     } else {
-        P->own.reset(new Workspace());
+        {
+            std::lock_guard<std::mutex> lk(ctx->ws_mu);
+            if (!ctx->ws_free.empty()) {
+                P->own = std::move(ctx->ws_free.back());
+                ctx->ws_free.pop_back();
+            }
+        }
+        if (!P->own) P->own.reset(new Workspace());
         P->w = P->own.get();
     }
     P->w->feat.ensure(total);
@@ -705,6 +742,8 @@ struct RectTraits {
     static Model def() { return default_model(); }
     static DevBuf<Model>& dmodels(Workspace* w) { return w->models; }
     static PinBuf<Model>& hmodels(Workspace* w) { return w->h_models; }
+    static DevBuf<Model>& pf_dmodels(Workspace* w) { return w->pf_models; }
+    static PinBuf<Model>& pf_hmodels(Workspace* w) { return w->pf_h_models; }
     static DevBuf<Model>& lomodels(Workspace* w) { return w->lo_models; }
     static bool identity(const Model& m) { return identity_norm(m); }
     static bool valid(int solver, const Model& m) { return solver == 2 ? valid_model_sift22(m) : true; }
@@ -750,6 +789,8 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     static Model def() { return default_geo(); }
     static DevBuf<Model>& dmodels(Workspace* w) { return w->gmodels; }
     static PinBuf<Model>& hmodels(Workspace* w) { return w->h_gmodels; }
+    static DevBuf<Model>& pf_dmodels(Workspace* w) { return w->pf_gmodels; }
+    static PinBuf<Model>& pf_hmodels(Workspace* w) { return w->pf_h_gmodels; }
     static DevBuf<Model>& lomodels(Workspace* w) { return w->lo_gmodels; }
     static bool identity(const Model&) { return true; }
     static bool valid(int, const Model&) { return true; }
@@ -824,6 +865,9 @@ public:
     using Model = typename Tr::Model;
     using Buffer = BufferT<Model>;
     static constexpr size_t kP = Tr::kPer;           // hypotheses per slot
+    ~RunnerT() {
+        if (pf_active_) (void)hipEventSynchronize(P_->ctx->pdone);     // an exception left one in flight
+    }
     RunnerT(gcr_problem* P, const gcr_params& prm) : P_(P), prm_(prm), s_(P->ctx->stream) {
         K_ = P->K;
         m_[0] = P->solver == 2 ? 2 : P->solver == 3 ? 4 : P->solver == 4 ? 7 : 3;
@@ -864,18 +908,21 @@ public:
         while (min_it > it_ || it_ < std::min(max_iteration, max_it)) {
             if (slot == chunk_end) {
                 replay_ms += ms_since(t_rep);
-                uint64_t B;
-                if (prm_.batch_slots) B = prm_.batch_slots;
-                else if (min_it >= max_it) B = 65536;
-                // first chunk: kSmallScore slots (the small-batch scorer; a
-                // 0.99-confidence run at 50 % outliers needs 35-90), then x4
-                else B = chunk_no == 0 ? kSmallScore : std::min<uint64_t>(65536, last_chunk * 4);
-                B = std::min<uint64_t>(B, L - it_);
-                B = std::max<uint64_t>(B, 1);
+                const uint64_t B = plan_chunk(chunk_no, last_chunk, it_, L);
                 last_chunk = B;
                 chunk_begin = slot;
-                chunk_end = slot + fetch_chunk(slot, (uint32_t)B, L);
+                uint64_t cnt;
+                if (pf_active_ && pf_s0_ == slot && pf_B_ == B) {
+                    cnt = take_prefetch(L);
+                } else {
+                    drain_prefetch();
+                    cnt = fetch_chunk(slot, (uint32_t)B, L);
+                }
+                chunk_end = slot + cnt;
                 ++chunk_no;
+                finish_chunk(cnt);
+                plan_prefetch(chunk_no, B, cnt, chunk_end);
+                if (pf_pending_ && pf_trigger_ < 0) maybe_prefetch(0, max_iteration, L);
                 t_rep = Clock::now();
             }
             const size_t j = slot - chunk_begin;
@@ -893,7 +940,8 @@ public:
                 const size_t si = compact_ ? cursor_++ : hj;
                 const Model& model = Tr::hmodels(P_->w).p[hj];
                 const uint32_t rn[2] = {P_->w->sb.hn0.p[si], P_->w->sb.hn1.p[si]};
-                const HScore cur = finish(rn, P_->w->sb.hv0.p[si], P_->w->sb.hv1.p[si], P_->w->sb.htot.p[si]);
+                const HScore cur = kP == 1 ? chunk_sc_[j]
+                                           : finish(rn, P_->w->sb.hv0.p[si], P_->w->sb.hv1.p[si], P_->w->sb.htot.p[si]);
                 bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
                 ++st_.hypotheses;
                 if (best_.sum < cur.sum && valid_model(model)) {
@@ -913,6 +961,9 @@ public:
                 max_iteration = iteration_number(best_.n);
                 t_rep = Clock::now();
             }
+            // past the chunk's last possible new best (and its LO): the rest
+            // of the chunk is bookkeeping, the next chunk can be speculated
+            if (pf_pending_ && (int64_t)j == pf_trigger_) maybe_prefetch(j + 1, max_iteration, L);
         }
         replay_ms += ms_since(t_rep);
         st_.slots = slot;
@@ -969,6 +1020,7 @@ public:
             st_.score = best_.sum;
             st_.ms_refit = ms_since(t_ref);
         }
+        drain_prefetch();                 // the side stream idle before the workspace is reused
         Tr::output(out_model, H, model_out);
         st_.iteration_number = it_;
         st_.local_optimization_number = lo_number_;
@@ -1058,8 +1110,8 @@ private:
     // neighbourhood graph (homography / fundamental matrix with a grid and
     // lambda > 0): the grid's edges are built once per run, on first use
     NeighbourEdges edges_;
-    MaxFlow maxflow_;
     std::vector<double> gc_q_;
+    std::vector<uint8_t> gc_seg_;
     int graph_state_ = -1;        // -1 unknown, 0 no pairwise terms, 1 edges_ built
     bool use_graph() {
         if (graph_state_ < 0) {
@@ -1067,8 +1119,8 @@ private:
             if (P_->solver >= 3 && prm_.cell_number > 0 && prm_.spatial_coherence_weight > 0) {
                 const HostClass& c = P_->hc[0];
                 const double* cols[4] = {c.x.data(), c.y.data(), c.a.data(), c.c0.data()};
-                grid_edges(cols, 4, c.n, prm_.cell_size, prm_.cell_number, edges_);
-                graph_state_ = edges_.size() > 0 ? 1 : 0;
+                grid_edges(cols, 4, c.n, prm_.cell_size, prm_.cell_number, edges_, false);
+                graph_state_ = edges_.cells() > 0 ? 1 : 0;
             }
         }
         return graph_state_ == 1;
@@ -1244,6 +1296,152 @@ private:
         return cnt;
     }
 
+    // Chunk sizes: a fixed budget (min >= max) runs 65536-slot chunks; an
+    // adaptive run starts with kSmallScore slots (the small-batch scorer; a
+    // 0.99-confidence run at 50 % outliers needs 35-90) and grows x4; never
+    // past the budget L from iteration count `it`.
+    uint64_t plan_chunk(uint64_t chunk_no, uint64_t last_chunk, uint64_t it, uint64_t L) const {
+        const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
+        uint64_t B;
+        if (prm_.batch_slots) B = prm_.batch_slots;
+        else if (min_it >= max_it) B = 65536;
+        else B = chunk_no == 0 ? kSmallScore : std::min<uint64_t>(65536, last_chunk * 4);
+        B = std::min<uint64_t>(B, L > it ? L - it : 0);
+        return std::max<uint64_t>(B, 1);
+    }
+
+    // ---- next chunk on the side stream (north_star's side stream) ----------
+    // While the host replays the rest of chunk c, the side stream generates and
+    // scores chunk c + 1 into the second set of chunk buffers.  Slots are pure
+    // functions of (seed, slot), so the prefetched results are exactly what a
+    // fetch would return; the budget cut is applied on the device
+    // (launch_truncate).  Started only past chunk c's last possible new best,
+    // and only when the loop will reach chunk c + 1, so nothing is wasted and
+    // no LO / refit kernel waits behind it.  One-model slots on one rank, from
+    // the second chunk on.  GCR_PREFETCH=0 disables.
+    bool pf_active_ = false;
+    uint64_t pf_s0_ = 0, pf_B_ = 0;
+
+    static bool prefetch_on() {
+        const char* e = getenv("GCR_PREFETCH");              // read per run (tests switch it)
+        return !(e && e[0] == '0');
+    }
+
+    // At a chunk's fetch: where the replay may still find a new best (the last
+    // slot whose score beats the running maximum from best_ with a valid
+    // model -- an LO can only raise the bar, so no later slot can trigger
+    // one).  The speculation starts after that slot, so it never competes
+    // with an LO's or the final refit's kernels.
+    bool pf_pending_ = false;
+    int64_t pf_trigger_ = -1;
+    uint64_t pf_chunk_no_ = 0, pf_chunk_B_ = 0, pf_chunk_cnt_ = 0, pf_next_s_ = 0;
+    // one-model slots: every slot's finished MSAC score, computed once per
+    // chunk on the host pool (the replay reads them; so does plan_prefetch)
+    std::vector<HScore> chunk_sc_;
+    std::vector<uint8_t> chunk_ok_;       // a model that passes isValidModel
+    void finish_chunk(uint64_t cnt) {
+        if (kP != 1) return;
+        chunk_sc_.resize(cnt);
+        chunk_ok_.resize(cnt);
+        auto body = [&](size_t lo, size_t hi) {
+            for (size_t j = lo; j < hi; ++j) {
+                if (P_->w->h_inc.p[j] > 101) {
+                    chunk_sc_[j] = HScore{};
+                    chunk_ok_[j] = 0;
+                    continue;
+                }
+                const uint32_t rn[2] = {P_->w->sb.hn0.p[j], P_->w->sb.hn1.p[j]};
+                chunk_sc_[j] = finish(rn, P_->w->sb.hv0.p[j], P_->w->sb.hv1.p[j], P_->w->sb.htot.p[j]);
+                chunk_ok_[j] = valid_model(Tr::hmodels(P_->w).p[j]) ? 1 : 0;
+            }
+        };
+        const size_t parts = cnt >= 8192 ? 16 : 1;
+        const size_t step = (cnt + parts - 1) / parts;
+        host_pool().parallel_for(parts, [&](size_t p) { body(std::min(cnt, p * step), std::min(cnt, (p + 1) * step)); });
+    }
+    void plan_prefetch(uint64_t chunk_no, uint64_t B, uint64_t cnt, uint64_t s_next) {
+        pf_pending_ = false;
+        if (kP != 1 || world_ > 1 || chunk_no < 2 || cnt != B || !prefetch_on()) return;
+        double run = best_.sum;
+        int64_t trig = -1;
+        for (uint64_t j = 0; j < cnt; ++j)
+            if (run < chunk_sc_[j].sum && chunk_ok_[j]) {
+                run = chunk_sc_[j].sum;
+                trig = (int64_t)j;
+            }
+        pf_pending_ = true;
+        pf_trigger_ = trig;
+        pf_chunk_no_ = chunk_no;
+        pf_chunk_B_ = B;
+        pf_chunk_cnt_ = cnt;
+        pf_next_s_ = s_next;
+    }
+
+    // `from`: the first slot of the current chunk not yet replayed; it_ holds
+    // the iterations up to it.  Speculates only when the loop will certainly
+    // reach the next chunk (max_iteration no longer changes in this chunk).
+    void maybe_prefetch(uint64_t from, uint64_t max_iteration, uint64_t L) {
+        pf_pending_ = false;
+        uint64_t it_end = it_;
+        for (uint64_t j = from; j < pf_chunk_cnt_; ++j) it_end += P_->w->h_inc.p[j];
+        const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
+        if (getenv("GCR_DEBUG_PF"))
+            fprintf(stderr, "pf: chunk %lu from %lu/%lu it_end %lu max_iteration %lu L %lu\n",
+                    (unsigned long)pf_chunk_no_, (unsigned long)from, (unsigned long)pf_chunk_cnt_,
+                    (unsigned long)it_end, (unsigned long)max_iteration, (unsigned long)L);
+        if (!(min_it > it_end || it_end < std::min(max_iteration, max_it)) || it_end >= L) return;
+        const uint64_t Bn = plan_chunk(pf_chunk_no_, pf_chunk_B_, it_end, L);
+        if (Bn <= kSmallScore) return;
+        const uint64_t s_next = pf_next_s_;
+        Workspace* w = P_->w;
+        w->pf_inc.ensure(Bn); Tr::pf_dmodels(w).ensure(Bn); w->pf_sb.ensure(Bn);
+        w->pf_h_inc.ensure(Bn); Tr::pf_hmodels(w).ensure(Bn);
+        hipStream_t s = P_->ctx->side;
+        HIPC(Tr::generate(P_, prm_.seed, s_next, (uint32_t)Bn, w->pf_inc.p, Tr::pf_dmodels(w).p, s));
+        HIPC(launch_truncate(w->pf_inc.p, (uint32_t)Bn, L - it_end, s));
+        HIPC(hipEventRecord(P_->ctx->pev0, s));
+        HIPC(Tr::score_live(P_, Tm_, Tr::pf_dmodels(w).p, w->pf_inc.p, (uint32_t)Bn, (uint32_t)Bn, w->pf_sb.dev(), s));
+        HIPC(hipEventRecord(P_->ctx->pev1, s));
+        HIPC(hipMemcpyAsync(w->pf_h_inc.p, w->pf_inc.p, Bn, hipMemcpyDeviceToHost, s));
+        w->pf_sb.d2h(Bn, s);
+        HIPC(hipMemcpyAsync(Tr::pf_hmodels(w).p, Tr::pf_dmodels(w).p, Bn * sizeof(Model), hipMemcpyDeviceToHost, s));
+        HIPC(hipEventRecord(P_->ctx->pdone, s));
+        pf_active_ = true;
+        pf_s0_ = s_next;
+        pf_B_ = Bn;
+        st_.launches += 3;
+        st_.hypotheses_computed += Bn;
+        ++st_.prefetched_chunks;
+    }
+
+    // the prefetched chunk becomes the current one; returns its slot count
+    // (the budget cut, as fetch_chunk computes it)
+    uint64_t take_prefetch(uint64_t L) {
+        auto t0 = Clock::now();
+        HIPC(hipEventSynchronize(P_->ctx->pdone));
+        pf_active_ = false;
+        Workspace* w = P_->w;
+        swap_buf(w->inc, w->pf_inc);
+        swap_buf(Tr::dmodels(w), Tr::pf_dmodels(w));
+        swap_buf(w->h_inc, w->pf_h_inc);
+        swap_buf(Tr::hmodels(w), Tr::pf_hmodels(w));
+        w->sb.swap(w->pf_sb);
+        float kms = 0;
+        HIPC(hipEventElapsedTime(&kms, P_->ctx->pev0, P_->ctx->pev1));
+        st_.ms_score_kernel += kms;
+        st_.ms_score += ms_since(t0);                    // the wait that remained
+        cursor_ = 0;
+        uint64_t itp = it_, cnt = 0;
+        while (cnt < pf_B_ && itp < L) itp += w->h_inc.p[cnt++];
+        return cnt == 0 ? 1 : cnt;
+    }
+
+    void drain_prefetch() {
+        if (!pf_active_) return;
+        HIPC(hipEventSynchronize(P_->ctx->pdone));
+        pf_active_ = false;
+    }
+
     // Score explicit host models on the GPU (LO trials, refit, reconcile).
     void score_models(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */) {
         auto& lm = Tr::lomodels(P_->w);
@@ -1289,8 +1487,19 @@ private:
             st_.launches += 1;
             lists[0].clear();
             lists[1].clear();
-            graphcut_labeling(P_->w->h_r2.p, n, T[0], prm_.spatial_coherence_weight, edges_, maxflow_, gc_q_,
-                              lists[0]);
+            // the cells are independent components: cut them on the host pool
+            graphcut_labeling(P_->w->h_r2.p, n, T[0], prm_.spatial_coherence_weight, edges_, gc_q_, gc_seg_,
+                              [](size_t ncells, const auto& fn) {
+                                  const size_t parts = ncells < 64 ? 1 : 64;
+                                  const size_t step = (ncells + parts - 1) / parts;
+                                  host_pool().parallel_for(parts, [&](size_t p) {
+                                      thread_local CellScratch cs;
+                                      const size_t c0 = std::min(ncells, p * step);
+                                      fn(c0, std::min(ncells, c0 + step), cs);
+                                  });
+                              });
+            for (size_t i = 0; i < n; ++i)
+                if (gc_seg_[i]) lists[0].push_back((uint32_t)i);
             return;
         }
         const size_t tot = N_[0] + (K_ == 2 ? N_[1] : 0);
@@ -1489,9 +1698,17 @@ int gcr_create(int device, gcr_ctx** out) {
         auto c = std::unique_ptr<gcr_ctx>(new gcr_ctx());
         c->device = device;
         HIPC(hipSetDevice(device));
-        HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        // the replay's dependent steps (LO labeling and trial scores, the
+        // refit) must not queue behind a speculative chunk's workgroups
+        int least = 0, greatest = 0;
+        HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPC(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+        HIPC(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least));
         HIPC(hipEventCreate(&c->ev0));
         HIPC(hipEventCreate(&c->ev1));
+        HIPC(hipEventCreate(&c->pev0));
+        HIPC(hipEventCreate(&c->pev1));
+        HIPC(hipEventCreateWithFlags(&c->pdone, hipEventDisableTiming));
         int cu = 0;
         if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0)
             c->n_cu = cu;
@@ -1514,6 +1731,10 @@ void gcr_destroy(gcr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->pev0) (void)hipEventDestroy(ctx->pev0);
+    if (ctx->pev1) (void)hipEventDestroy(ctx->pev1);
+    if (ctx->pdone) (void)hipEventDestroy(ctx->pdone);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1526,6 +1747,10 @@ int gcr_problem_create(gcr_ctx* ctx, int solver, const double* f0, size_t n0, co
 void gcr_problem_destroy(gcr_problem* prob) {
     if (!prob) return;
     (void)hipSetDevice(prob->ctx->device);
+    if (prob->own) {
+        std::lock_guard<std::mutex> lk(prob->ctx->ws_mu);
+        if (prob->ctx->ws_free.size() < 4) prob->ctx->ws_free.push_back(std::move(prob->own));
+    }
     delete prob;
 }
 
@@ -2005,8 +2230,8 @@ int gcr_host_grid_edges(const double* points, size_t n, int dims, const double* 
         }
         NeighbourEdges e;
         grid_edges(cp, dims, n, cell_size, cell_number, e);
-        *m_out = e.size();
-        for (size_t k = 0; k < e.size() && k < cap; ++k) {
+        *m_out = e.u.size();
+        for (size_t k = 0; k < e.u.size() && k < cap; ++k) {
             edges_out[2 * k] = e.u[k];
             edges_out[2 * k + 1] = e.v[k];
         }
@@ -2033,24 +2258,26 @@ int gcr_host_bk_energy(size_t n, const double* unary, const uint32_t* edges, con
     });
 }
 
-int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, const uint32_t* edges, size_t m,
-                      uint8_t* seg) {
-    if ((!r2 && n) || (m && !edges) || (!seg && n)) return set_err(GCR_EINVAL, "null argument");
+int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, const double* points, int dims,
+                      const double* cell_size, uint64_t cell_number, uint8_t* seg) {
+    if ((!r2 && n) || (!seg && n) || (cell_number && (!points || !cell_size || dims < 1 || dims > 4)))
+        return set_err(GCR_EINVAL, "invalid argument");
     return guard([&]() -> int {
         NeighbourEdges e;
-        e.u.resize(m);
-        e.v.resize(m);
-        for (size_t k = 0; k < m; ++k) {
-            e.u[k] = edges[2 * k];
-            e.v[k] = edges[2 * k + 1];
-            if (e.u[k] >= n || e.v[k] >= n || e.u[k] == e.v[k]) return set_err(GCR_EINVAL, "invalid edge %zu", k);
+        if (cell_number) {
+            std::vector<double> cols[4];
+            const double* cp[4] = {};
+            for (int d = 0; d < dims; ++d) {
+                cols[d].resize(n);
+                for (size_t i = 0; i < n; ++i) cols[d][i] = points[i * dims + d];
+                cp[d] = cols[d].data();
+            }
+            grid_edges(cp, dims, n, cell_size, cell_number, e, false);
         }
-        MaxFlow g;
         std::vector<double> q;
-        std::vector<uint32_t> inl;
-        graphcut_labeling(r2, n, sqt, lambda, e, g, q, inl);
-        std::memset(seg, 0, n);
-        for (uint32_t i : inl) seg[i] = 1;
+        std::vector<uint8_t> sg;
+        graphcut_labeling(r2, n, sqt, lambda, e, q, sg);
+        std::memcpy(seg, sg.data(), n);
         return GCR_OK;
     });
 }

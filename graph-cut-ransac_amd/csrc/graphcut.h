@@ -38,7 +38,11 @@ namespace gcr {
 // graph.h:246-267 / GridCell :70-82; cells are keyed by that index alone.
 struct NeighbourEdges {
     std::vector<uint32_t> u, v;
-    size_t size() const { return u.size(); }
+    // the same graph by cell: cell c's points are nodes[off[c] .. off[c+1])
+    // in ascending order (cells of >= 2 points only); its edges are every
+    // pair of them, in labeling()'s order (a < b, by a then b)
+    std::vector<uint32_t> off, nodes;
+    size_t cells() const { return off.empty() ? 0 : off.size() - 1; }
 };
 
 inline uint64_t grid_axis_index(double v) {
@@ -47,43 +51,63 @@ inline uint64_t grid_axis_index(double v) {
     return (uint64_t)(int64_t)f;
 }
 
-// coords: `dims` column pointers of n values each
+// coords: `dims` column pointers of n values each; the explicit edge list
+// (u, v) only when `with_edges` (the engine needs the cells alone)
 inline void grid_edges(const double* const* coords, int dims, size_t n, const double* cell_size,
-                       uint64_t cell_number, NeighbourEdges& out) {
+                       uint64_t cell_number, NeighbourEdges& out, bool with_edges = true) {
     out.u.clear();
     out.v.clear();
-    std::vector<uint64_t> key(n);
+    out.off.assign(1, 0);
+    out.nodes.clear();
+    // (cell key, point) sorted: cells in key order, points ascending inside
+    std::vector<std::pair<uint64_t, uint32_t>> kp(n);
+    uint64_t kmax = 0;
     for (size_t i = 0; i < n; ++i) {
         uint64_t k = 0, off = 1;
         for (int d = 0; d < dims; ++d) {
             k += off * grid_axis_index(coords[d][i] / cell_size[d]);
             off *= cell_number;
         }
-        key[i] = k;
+        kp[i] = {k, (uint32_t)i};
+        kmax = std::max(kmax, k);
     }
-    std::vector<uint32_t> order(n);
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
-    // position of every point inside its cell's (ascending) member list
-    std::vector<uint32_t> cell_end(n), pos(n);
-    for (size_t s = 0; s < n;) {
-        size_t e = s;
-        while (e < n && key[order[e]] == key[order[s]]) ++e;
-        for (size_t q = s; q < e; ++q) {
-            pos[order[q]] = (uint32_t)q;
-            cell_end[order[q]] = (uint32_t)e;
+    if (kmax < ((uint64_t)1 << 22) && kmax < 64 * (uint64_t)n + 4096) {
+        // the usual case (coordinates inside the image): a counting sort over
+        // the cell keys, stable, so points stay ascending inside a cell
+        std::vector<uint32_t> start(kmax + 2, 0);
+        for (size_t i = 0; i < n; ++i) ++start[kp[i].first + 1];
+        for (uint64_t k = 0; k <= kmax; ++k) start[k + 1] += start[k];
+        std::vector<std::pair<uint64_t, uint32_t>> sorted(n);
+        for (size_t i = 0; i < n; ++i) sorted[start[kp[i].first]++] = kp[i];
+        kp.swap(sorted);
+    } else {
+        std::sort(kp.begin(), kp.end());
+    }
+    for (size_t s0 = 0; s0 < n;) {
+        size_t e = s0;
+        while (e < n && kp[e].first == kp[s0].first) ++e;
+        if (e - s0 >= 2) {
+            for (size_t q = s0; q < e; ++q) out.nodes.push_back(kp[q].second);
+            out.off.push_back((uint32_t)out.nodes.size());
         }
-        s = e;
+        s0 = e;
     }
-    size_t m = 0;
-    for (size_t i = 0; i < n; ++i) m += cell_end[i] - pos[i] - 1;
-    out.u.reserve(m);
-    out.v.reserve(m);
-    for (size_t i = 0; i < n; ++i)
-        for (uint32_t q = pos[i] + 1; q < cell_end[i]; ++q) {
+    if (!with_edges) return;
+    // labeling()'s order: for every point i in row order, every later point
+    // of its cell, ascending
+    std::vector<uint32_t> cell_of(n, UINT32_MAX), pos(n, 0);
+    for (size_t c = 0; c + 1 < out.off.size(); ++c)
+        for (uint32_t q = out.off[c]; q < out.off[c + 1]; ++q) {
+            cell_of[out.nodes[q]] = (uint32_t)c;
+            pos[out.nodes[q]] = q;
+        }
+    for (size_t i = 0; i < n; ++i) {
+        if (cell_of[i] == UINT32_MAX) continue;
+        for (uint32_t q = pos[i] + 1; q < out.off[cell_of[i] + 1]; ++q) {
             out.u.push_back((uint32_t)i);
-            out.v.push_back(order[q]);
+            out.v.push_back(out.nodes[q]);
         }
+    }
 }
 
 // Boykov-Kolmogorov max-flow, Graph<double,double,double> semantics.
@@ -384,31 +408,74 @@ private:
 
 // labeling() of GCRANSAC.h:759-870 for one class: r2 = squared residuals of
 // the LO model, sqt = squared truncated threshold, pairwise terms over
-// `edges` when lambda > 0.  Appends the SINK points (inliers) in order.
-inline void graphcut_labeling(const double* r2, size_t n, double sqt, double lambda, const NeighbourEdges& edges,
-                              MaxFlow& g, std::vector<double>& q, std::vector<uint32_t>& inliers) {
+// `edges` when lambda > 0.  Writes seg[i] = 1 for the SINK points (inliers).
+//
+// The pairwise terms only join points of one grid cell, so every cell is an
+// independent component of the graph, and BK on the whole graph performs,
+// restricted to one component, exactly the operations BK performs on that
+// component alone: the component's nodes keep their relative order in the
+// active queues and the orphan list, its arcs their order in the adjacency
+// lists, and the TS stamps their relative order (the checks compare stamps of
+// the component's own nodes, or test "stamped in this adoption").  So each
+// cell is cut on its own -- in parallel through `for_cells(ncells, fn)` --
+// and a point outside any multi-point cell takes the terminal test.
+// (tests/test_graphcut.py checks this against the oracle's whole-graph BK.)
+struct CellScratch {
+    MaxFlow g;
+    std::vector<int32_t> local;
+};
+
+inline void graphcut_cell(const double* q, const double* r2, double sqt, double lambda, const uint32_t* nodes,
+                          uint32_t k, CellScratch& cs, uint8_t* seg) {
     const double oml = 1.0 - lambda;
-    const bool pairwise = lambda > 0 && edges.size() > 0;
-    g.reset(n, pairwise ? edges.size() : 0);
+    MaxFlow& g = cs.g;
+    g.reset(k, (size_t)k * (k - 1) / 2);
+    for (uint32_t a = 0; a < k; ++a) {
+        const uint32_t i = nodes[a];
+        const double energy = 1.0 - q[i];
+        if (r2[i] <= sqt) g.add_term1((int32_t)a, oml * energy, 0.0);
+        else g.add_term1((int32_t)a, 0.0, oml * (1.0 - energy));
+    }
+    const double e11 = 0;
+    for (uint32_t a = 0; a < k; ++a)
+        for (uint32_t b = a + 1; b < k; ++b) {
+            const double e00 = 0.5 * (q[nodes[a]] + q[nodes[b]]);
+            g.add_term2((int32_t)a, (int32_t)b, e00 * lambda, lambda, lambda, e11 * lambda);
+        }
+    g.maxflow();
+    for (uint32_t a = 0; a < k; ++a) seg[nodes[a]] = g.is_sink((int32_t)a) ? 1 : 0;
+}
+
+template <class ForCells>
+inline void graphcut_labeling(const double* r2, size_t n, double sqt, double lambda, const NeighbourEdges& edges,
+                              std::vector<double>& q, std::vector<uint8_t>& seg, ForCells&& for_cells) {
+    const double oml = 1.0 - lambda;
     q.resize(n);
+    seg.assign(n, 0);
     for (size_t i = 0; i < n; ++i) {
         const double qq = std::clamp(r2[i] / sqt, 0.0, 1.0);
         q[i] = qq;
+        // the terminal test (a node without pairwise terms): SINK iff its
+        // terminal residual capacity is < 0
         const double energy = 1.0 - qq;
-        if (r2[i] <= sqt) g.add_term1((int32_t)i, oml * energy, 0.0);
-        else g.add_term1((int32_t)i, 0.0, oml * (1.0 - energy));
+        const double tr = (r2[i] <= sqt) ? (0.0 - oml * energy) : (oml * (1.0 - energy) - 0.0);
+        seg[i] = tr < 0 ? 1 : 0;
     }
-    if (pairwise) {
-        const double e11 = 0;
-        for (size_t k = 0; k < edges.size(); ++k) {
-            const uint32_t i = edges.u[k], j = edges.v[k];
-            const double e00 = 0.5 * (q[i] + q[j]);
-            g.add_term2((int32_t)i, (int32_t)j, e00 * lambda, lambda, lambda, e11 * lambda);
-        }
-    }
-    g.maxflow();
-    for (size_t i = 0; i < n; ++i)
-        if (g.is_sink((int32_t)i)) inliers.push_back((uint32_t)i);
+    if (!(lambda > 0) || edges.off.size() < 2) return;
+    const size_t ncells = edges.off.size() - 1;
+    for_cells(ncells, [&](size_t c0, size_t c1, CellScratch& cs) {
+        for (size_t c = c0; c < c1; ++c)
+            graphcut_cell(q.data(), r2, sqt, lambda, edges.nodes.data() + edges.off[c], edges.off[c + 1] - edges.off[c],
+                          cs, seg.data());
+    });
+}
+
+// serial driver (tests, small problems)
+inline void graphcut_labeling(const double* r2, size_t n, double sqt, double lambda, const NeighbourEdges& edges,
+                              std::vector<double>& q, std::vector<uint8_t>& seg) {
+    CellScratch cs;
+    graphcut_labeling(r2, n, sqt, lambda, edges, q, seg,
+                      [&](size_t ncells, const auto& fn) { fn(0, ncells, cs); });
 }
 
 }  // namespace gcr

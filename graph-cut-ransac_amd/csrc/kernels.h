@@ -205,6 +205,9 @@ hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc,
                              uint32_t m, double Tm, BatchRecord* out, hipStream_t stream,
                              const uint32_t* hmap = nullptr, const uint32_t* hcount = nullptr);
 // order-preserving list of live hypotheses (inc <= 101): map[0 .. *count)
+// budget cut of a prefetched chunk: slots whose preceding increments reach
+// `budget` get inc = 255 (no model)
+hipError_t launch_truncate(uint8_t* inc, uint32_t n, uint64_t budget, hipStream_t stream);
 hipError_t launch_sqres_geo(const DevProblem& p, const GeoModel& model, double* r2, hipStream_t stream);
 hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_t* count, hipStream_t stream);
 

@@ -2405,6 +2405,40 @@ hipError_t launch_score(const DevProblem& p, const double T[2], const RectModel*
     return hipGetLastError();
 }
 
+// A prefetched chunk's budget cut (the replay's `while (cnt < B && itp < L)`):
+// slot j stays iff budget - sum_{k < j} inc[k] > 0; later slots are marked
+// absent (inc = 255: no model), so the scorer skips them.  One workgroup,
+// each thread a contiguous run of slots.
+constexpr int kTruncThreads = 1024;
+__global__ __launch_bounds__(kTruncThreads) void k_truncate(uint8_t* __restrict__ inc, uint32_t n, uint64_t budget) {
+    __shared__ uint64_t part[kTruncThreads];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (n + kTruncThreads - 1) / kTruncThreads;
+    const uint32_t b = t * per, e = min(n, b + per);
+    uint64_t sum = 0;
+    for (uint32_t j = b; j < e; ++j) sum += inc[j];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < kTruncThreads; off <<= 1) {     // inclusive scan
+        const uint64_t v = t >= off ? part[t - off] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t before = t == 0 ? 0 : part[t - 1];
+    for (uint32_t j = b; j < e; ++j) {
+        const uint64_t cur = inc[j];
+        if (before >= budget) inc[j] = 255;
+        before += cur;
+    }
+}
+
+hipError_t launch_truncate(uint8_t* inc, uint32_t n, uint64_t budget, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_truncate, dim3(1), dim3(kTruncThreads), 0, stream, inc, n, budget);
+    return hipGetLastError();
+}
+
 hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns,
                             const uint32_t* oi, uint32_t no, size_t rows, double* A0, double* A1, double* A2,
                             double* b, hipStream_t stream) {

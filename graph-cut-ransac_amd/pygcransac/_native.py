@@ -67,6 +67,7 @@ class Stats(C.Structure):
         ("ms_lo_fit", C.c_double),
         ("ms_lo_score", C.c_double),
         ("ms_refit_fit", C.c_double),
+        ("prefetched_chunks", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -165,7 +166,7 @@ def _load():
     L.gcr_host_grid_edges.argtypes = [dp, C.c_size_t, C.c_int, dp, C.c_uint64, u32p, C.c_size_t,
                                       C.POINTER(C.c_size_t)]
     L.gcr_host_bk_energy.argtypes = [C.c_size_t, dp, u32p, dp, C.c_size_t, u8p]
-    L.gcr_host_labeling.argtypes = [dp, C.c_size_t, C.c_double, C.c_double, u32p, C.c_size_t, u8p]
+    L.gcr_host_labeling.argtypes = [dp, C.c_size_t, C.c_double, C.c_double, dp, C.c_int, dp, C.c_uint64, u8p]
     L.gcr_host_weighted_mode.argtypes = [dp, dp, C.c_size_t, C.c_double]
     L.gcr_host_weighted_mode.restype = C.c_double
     L.gcr_host_homography.argtypes = [C.POINTER(RectModel), dp]

@@ -105,6 +105,8 @@ typedef struct gcr_stats {
     double ms_refit_fit;          /* final refit: the non-minimal fit itself (system,
                                      QR, weighted mode); the rest of ms_refit is the
                                      buffer reconciliation, rescoring and lists      */
+    uint64_t prefetched_chunks;   /* chunks generated + scored on the side stream
+                                     while the host replayed the previous one        */
 } gcr_stats;
 
 /* ---- context ---------------------------------------------------------- */
@@ -258,14 +260,15 @@ void gcr_host_homography(const gcr_rect_model* model, double* H_out);
  * bk_energy: BK st-mincut of sum_i E_i(x_i) + sum_k E_k(x_u, x_v), unary
  * (n x 2: E(0), E(1)), pair (m x 4: E(00), E(01), E(10), E(11)), Energy::
  * add_term1 / add_term2 (energy.h:204-245); seg[i] = 1 iff SINK.
- * labeling: labeling() itself from squared residuals r2, squared truncated
- * threshold sqt, lambda and an edge list; seg[i] = 1 iff inlier (SINK). */
+ * labeling: labeling() itself as the engine runs it -- squared residuals r2,
+ * squared truncated threshold sqt, lambda, the grid over n points of `dims`
+ * row-major coordinates (cell_number 0: no grid); seg[i] = 1 iff inlier. */
 int gcr_host_grid_edges(const double* points, size_t n, int dims, const double* cell_size, uint64_t cell_number,
                         uint32_t* edges_out, size_t cap, size_t* m_out);
 int gcr_host_bk_energy(size_t n, const double* unary, const uint32_t* edges, const double* pair, size_t m,
                        uint8_t* seg);
-int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, const uint32_t* edges, size_t m,
-                      uint8_t* seg);
+int gcr_host_labeling(const double* r2, size_t n, double sqt, double lambda, const double* points, int dims,
+                      const double* cell_size, uint64_t cell_number, uint8_t* seg);
 /* host-only: findWeightedMode (two_sift.hpp:354-394) as the fits use it */
 double gcr_host_weighted_mode(const double* angles, const double* weights, size_t n, double bin_width);
 /* host-only (no GPU): deterministic math and sampler used on both sides */

@@ -470,3 +470,48 @@ def test_band_prefilter_is_conservative_at_the_threshold(kind):
             got = finish_score(kind, n0[i], n1[i], v0[i], v1[i], tot[i], thr0, thr1)
             assert got["counts"] == [int(c) for c in ref["counts"]], (nh, i)
             assert bits(got["value"]) == bits(ref["value"]), (nh, i)
+
+
+# --------------------------------------------------- speculative prefetch ----
+@pytest.mark.parametrize("kind", list(KINDS) + [N.SOLVER_HOMOGRAPHY4])
+@pytest.mark.parametrize("budget", ["fixed", "adaptive"])
+def test_prefetched_chunks_give_identical_runs(kind, budget, monkeypatch):
+    # the next chunk generated and scored on the side stream while the host
+    # replays the current one (GCR_PREFETCH) must not change anything: the
+    # same slots, the same budget cut, the same replay
+    if kind == N.SOLVER_HOMOGRAPHY4:
+        corr, _, _, thr = S.problem_h(3000, 0.7, seed=81)
+        f0, f1, thr0, thr1 = corr, None, thr, 0.0
+    else:
+        f0, f1, thr0, thr1 = _problem_data(kind, 2500, seed=83 + kind)
+    p = N.default_params()
+    p.scale_residual_thresh, p.orientation_residual_thresh, p.seed = thr0, thr1, 5
+    if budget == "fixed":               # 65536-slot chunks up to a budget that cuts the last one
+        p.min_iteration_number = p.max_iteration_number = 400_000 if kind in (0, 1) else 1_500_000
+    else:                               # 256 -> 1024 -> 4096 ... slots, adaptive termination
+        p.min_iteration_number, p.max_iteration_number, p.confidence = 0, 10**7, 0.9999999
+    outs = []
+    for pf in ("0", "1"):
+        monkeypatch.setenv("GCR_PREFETCH", pf)
+        prob = Problem(kind, f0, f1) if kind != N.SOLVER_HOMOGRAPHY4 else None
+        if prob is None:
+            from gcr_testutil import CorrProblem
+            prob = CorrProblem(kind, f0)
+        m0 = np.zeros(f0.shape[0], np.uint8)
+        m1 = np.zeros(0 if f1 is None else f1.shape[0], np.uint8)
+        H = np.zeros(9)
+        model = N.RectModel()
+        st = N.Stats()
+        u8 = C.POINTER(C.c_uint8)
+        n = N.check(N.lib.gcr_problem_run(prob.h, C.byref(p), m0.ctypes.data_as(u8),
+                                          m1.ctypes.data_as(u8) if f1 is not None else None,
+                                          H.ctypes.data_as(C.POINTER(C.c_double)), C.byref(model), C.byref(st)))
+        outs.append((n, m0.tobytes(), m1.tobytes(), bits(H).tobytes(), st.iteration_number, st.hypotheses,
+                     st.local_optimization_number, st.graph_cut_number, bits(st.score).tobytes(), st.slots))
+        if pf == "0":
+            assert st.prefetched_chunks == 0
+        else:
+            prefetched = st.prefetched_chunks
+    assert outs[0] == outs[1]
+    if budget == "fixed":
+        assert prefetched > 0                                   # the path under test ran

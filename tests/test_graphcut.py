@@ -47,12 +47,15 @@ def product_edges(points, cell_size, cells):
     return out[:m.value]
 
 
-def product_labeling(r2, sqt, lam, edges):
+def product_labeling(r2, sqt, lam, points=None, cell_size=(0.0,) * 4, cells=0):
+    """labeling() as the engine runs it: the grid built from `points`, every
+    multi-point cell cut on its own (its own component of the graph)."""
     r = np.ascontiguousarray(r2, dtype=np.float64)
-    e = np.ascontiguousarray(np.asarray(edges, dtype=np.uint32).reshape(-1, 2))
     seg = np.zeros(r.size, dtype=np.uint8)
-    N.check(N.lib.gcr_host_labeling(r.ctypes.data_as(dp), r.size, sqt, lam, e.ctypes.data_as(u32p), e.shape[0],
-                                    seg.ctypes.data_as(u8p)))
+    pts = np.ascontiguousarray(points if points is not None else np.zeros((r.size, 1)), dtype=np.float64)
+    cs = np.ascontiguousarray(cell_size, dtype=np.float64)
+    N.check(N.lib.gcr_host_labeling(r.ctypes.data_as(dp), r.size, sqt, lam, pts.ctypes.data_as(dp), pts.shape[1],
+                                    cs.ctypes.data_as(dp), cells, seg.ctypes.data_as(u8p)))
     return seg.astype(bool)
 
 
@@ -201,17 +204,24 @@ def test_grid_edges_match_oracle_including_collisions_and_non_finite():
 
 
 @pytest.mark.parametrize("lam", [0.975, 0.5, 0.14])
-def test_labeling_matches_oracle_energy_and_independent_cut(lam):
-    corr, _, _, thr = S.problem_h(2500, 0.5, seed=11)
-    edges = O.grid_edges(corr, (160.0, 120.0, 160.0, 120.0), 8)
-    rng = np.random.default_rng(int(lam * 1000))
+@pytest.mark.parametrize("kind,cells", [("h", 8), ("f", 8), ("h", 3)])
+def test_labeling_matches_oracle_energy_and_independent_cut(lam, kind, cells):
+    # the engine cuts every grid cell on its own; the oracle runs BK once over
+    # the whole graph (GCRANSAC.h:759-870): the labelings must be identical
+    if kind == "h":
+        corr, _, _, thr = S.problem_h(2500, 0.5, seed=11)
+    else:
+        corr, _, _, thr = S.problem_f(6000, 0.8, seed=12)
+    sizes = (1280.0 / cells, 960.0 / cells, 1280.0 / cells, 960.0 / cells)
+    edges = O.grid_edges(corr, sizes, cells)
+    rng = np.random.default_rng(int(lam * 1000) + cells)
     sqt = (1.5 * thr) ** 2
     r2 = np.where(rng.random(corr.shape[0]) < 0.5, rng.uniform(0, 1.2 * sqt, corr.shape[0]),
                   rng.uniform(0, 30 * sqt, corr.shape[0]))
     r2[::17] = sqt                                        # exactly at the truncation
-    got = product_labeling(r2, sqt, lam, edges)
+    got = product_labeling(r2, sqt, lam, corr, sizes, cells)
     unary, pair = labeling_energy(r2, sqt, lam, edges)
-    ref = product_bk(unary, edges, pair)
+    ref = product_bk(unary, edges, pair)                  # whole-graph BK, product code
     assert np.array_equal(got, ref)
     assert np.array_equal(got, O.bk_energy(unary, edges, pair)[0])
     # pairwise terms change the labeling relative to the terminal test
@@ -231,7 +241,7 @@ def test_labeling_without_edges_is_the_terminal_test():
     r2 = rng.uniform(0, 8, 1000)
     r2[:5] = [0.0, sqt, np.nextafter(sqt, 0), np.nextafter(sqt, 9), 8.0]
     for lam in (0.0, 0.5, 0.975):
-        got = product_labeling(r2, sqt, lam, np.zeros((0, 2), np.uint32))
+        got = product_labeling(r2, sqt, lam)
         q = np.clip(r2 / sqt, 0, 1)
         tr = np.where(r2 <= sqt, 0.0 - (1 - lam) * (1 - q), (1 - lam) * (1 - (1 - q)) - 0.0)
         assert np.array_equal(got, tr < 0)
