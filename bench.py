@@ -10,8 +10,10 @@ One step = one pass of the hot path over one batch: `--slots` (default 4096,
 configs[1]) outer-iteration slots are drawn (Philox), validated and solved,
 every resulting model is MSAC-scored against all 10 000 features, and the
 batch's first strict best (the reference's update rule, GCRANSAC.h:440-446) is
-selected -- all on the device: one fused kernel (k_score_split<..., true>:
+selected -- all on the device: one fused kernel (k_score_fm<..., true>:
 in-kernel generation, exact MSAC sums, per-workgroup best) plus k_select_wg.
+The correspondence workloads (h, f) generate in their own kernel and are
+pipelined over two streams (batch b + 1 generated while batch b is scored).
 The K timed steps are queued back to back on one HIP stream (gcr_problem_verify_batches)
 and bracketed by device synchronisation.  Features are uploaded once before
 timing (HBM-resident).  `value` is the whole-job hypotheses/s; the end-to-end
@@ -52,13 +54,16 @@ def score_kernel_name(kind, slots):
     """The fused generate+score instantiation launch_verify_fused picks
     (kernels.hip split_h); the bench's step launches it plus k_select_wg."""
     h = int(os.environ.get("GCR_SPLIT_H", "0") or 0)
+    # the fundamental matrix scores up to 3 models per slot (launch size 3 x slots)
+    nh = slots * 3 if kind == 4 else slots
     if h not in (64, 16, 4):
-        h = 64 if slots >= 16384 else 16 if slots >= 2048 else 4
-    # the homography path generates in k_generate<3, G> and scores unfused
+        h = 64 if nh >= 16384 else 16 if nh >= 2048 else 4
+    # the correspondence paths generate in k_generate<3, G> / k_generate_f<G>
+    # and score unfused
     fused = "false" if kind >= 3 else "true"
-    # H = 16 rectification launches use the feature-major scorer unless
-    # GCR_SCORER=split (kernels.hip use_fm)
-    if h == 16 and kind <= 3 and not os.environ.get("GCR_SCORER", "").startswith("s"):
+    # H = 16 launches use the feature-major scorer unless GCR_SCORER=split
+    # (kernels.hip use_fm)
+    if h == 16 and not os.environ.get("GCR_SCORER", "").startswith("s"):
         return f"k_score_fm<{kind}, 16, {fused}>"
     return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, {fused}>"
 

@@ -231,9 +231,13 @@ struct Workspace {
     PinBuf<RectModel> pf_h_models;
     PinBuf<GeoModel> pf_h_gmodels;
     ScoreBufs pf_sb;
+    DevBuf<uint32_t> pf_hmap, pf_hcount;   // verify_batches: the second batch's compaction
+    hipEvent_t vb_gen[2] = {nullptr, nullptr}, vb_done[2] = {nullptr, nullptr}, vb_start = nullptr;
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start})
+            if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -765,6 +769,16 @@ struct RectTraits {
                                  uint32_t, const ScoreOut& out, hipStream_t s) {
         return launch_score(P->dp, T, m, inc, nh, true, out, s);
     }
+    static constexpr bool kPipe = false;   // generation is fused into the scorer
+    struct VBufs {};
+    static VBufs vbufs(gcr_problem*, int, uint32_t) { return {}; }
+    static hipError_t verify_gen(gcr_problem*, uint64_t, uint64_t, uint32_t, const VBufs&, hipStream_t) {
+        return hipErrorNotSupported;
+    }
+    static hipError_t verify_score(gcr_problem*, const double*, uint64_t, uint32_t, const uint32_t*, BatchRecord*,
+                                   hipEvent_t, hipEvent_t, const VBufs&, hipStream_t) {
+        return hipErrorNotSupported;
+    }
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t wg_cap, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
                              hipStream_t s) {
@@ -809,26 +823,59 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     static hipError_t sqres(gcr_problem* P, const Model& m, double* r2, hipStream_t s) {
         return launch_sqres_geo(P->dp, m, r2, s);
     }
+    // One batch = generate (+ compact the live models of multi-model slots)
+    // -> score -> first strict best, split in two halves so verify_batches
+    // can pipeline them over two streams: batch b + 1 is generated on the side
+    // stream while batch b is scored on the main one (the generator is
+    // latency-bound at 2 waves per SIMD and co-resides with the scorer's
+    // workgroups), each batch in its own buffer set (`set` 0 / 1)
+    static constexpr bool kPipe = true;
+    struct VBufs {
+        uint8_t* inc;
+        Model* models;
+        uint32_t* hmap;
+        uint32_t* hcount;
+        ScoreOut sb;
+    };
+    static VBufs vbufs(gcr_problem* P, int set, uint32_t n) {
+        Workspace* w = P->w;
+        const size_t nh = (size_t)n * per(P);
+        auto& inc = set ? w->pf_inc : w->inc;
+        auto& mod = set ? w->pf_gmodels : w->gmodels;
+        auto& map = set ? w->pf_hmap : w->hmap;
+        auto& cnt = set ? w->pf_hcount : w->hcount;
+        auto& sb = set ? w->pf_sb : w->sb;
+        inc.ensure(nh);
+        mod.ensure(nh);
+        sb.ensure(nh);
+        if (per(P) > 1) {
+            map.ensure(nh);
+            cnt.ensure(1);
+        }
+        return VBufs{inc.p, mod.p, per(P) > 1 ? map.p : nullptr, per(P) > 1 ? cnt.p : nullptr, sb.dev()};
+    }
+    static hipError_t verify_gen(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, const VBufs& b,
+                                 hipStream_t s) {
+        hipError_t e = launch_generate_geo(P->dp, seed, s0, n, b.inc, b.models, s);
+        if (e != hipSuccess || b.hmap == nullptr) return e;
+        return launch_compact(b.inc, n * (uint32_t)per(P), b.hmap, b.hcount, s);
+    }
+    static hipError_t verify_score(gcr_problem* P, const double Tm[2], uint64_t s0, uint32_t n, const uint32_t m[2],
+                                   BatchRecord* rec, hipEvent_t e0, hipEvent_t e1, const VBufs& b, hipStream_t s) {
+        const uint32_t nh = n * (uint32_t)per(P);
+        if (e0) (void)hipEventRecord(e0, s);
+        hipError_t e = launch_score_geo(P->dp, Tm[0], b.models, b.inc, nh, b.sb, s, b.hmap, b.hcount);
+        if (e != hipSuccess) return e;
+        if (e1) (void)hipEventRecord(e1, s);
+        return launch_select_geo(P->solver, b.sb, b.inc, nh, s0, m[0], Tm[0], rec, s, b.hmap, b.hcount);
+    }
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
                              hipStream_t s) {
-        const uint32_t nh = n * (uint32_t)per(P);
-        hipError_t e = launch_generate_geo(P->dp, seed, s0, n, P->w->inc.p, P->w->gmodels.p, s);
+        const VBufs b = vbufs(P, 0, n);
+        const hipError_t e = verify_gen(P, seed, s0, n, b, s);
         if (e != hipSuccess) return e;
-        const uint32_t *map = nullptr, *cnt = nullptr;
-        if (per(P) > 1) {
-            P->w->hmap.ensure(nh);
-            P->w->hcount.ensure(1);
-            map = P->w->hmap.p;
-            cnt = P->w->hcount.p;
-            e = launch_compact(P->w->inc.p, nh, P->w->hmap.p, P->w->hcount.p, s);
-            if (e != hipSuccess) return e;
-        }
-        if (e0) (void)hipEventRecord(e0, s);
-        e = launch_score_geo(P->dp, Tm[0], P->w->gmodels.p, P->w->inc.p, nh, P->w->sb.dev(), s, map, cnt);
-        if (e != hipSuccess) return e;
-        if (e1) (void)hipEventRecord(e1, s);
-        return launch_select_geo(P->solver, P->w->sb.dev(), P->w->inc.p, nh, s0, m[0], Tm[0], rec, s, map, cnt);
+        return verify_score(P, Tm, s0, n, m, rec, e0, e1, b, s);
     }
     // replay-path scoring of a fetched chunk: fundamental-matrix launches are
     // compacted to the live hypotheses (results in hypothesis order); the
@@ -1058,12 +1105,39 @@ public:
             P_->w->evs.push_back(ev);
         }
         uint32_t timed = 0;
-        for (uint32_t b = 0; b < nb; ++b) {
-            const uint64_t s0 = slot0 + (uint64_t)b * nslots;
-            const bool t = b % stride == 0;
-            HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, P_->w->recs.p + b,
-                            t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr, s_));
-            timed += t;
+        if (Tr::kPipe && nb > 1 && pipe_on()) {
+            // two-stream pipeline (Tr::verify_gen / verify_score): generation
+            // of batch b on the side stream once batch b - 2 (same buffer set)
+            // has been scored; scoring of batch b on s_ once it is generated
+            Workspace* w = P_->w;
+            for (hipEvent_t* e : {&w->vb_gen[0], &w->vb_gen[1], &w->vb_done[0], &w->vb_done[1], &w->vb_start})
+                if (*e == nullptr) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            const typename Tr::VBufs bufs[2] = {Tr::vbufs(P_, 0, nslots), Tr::vbufs(P_, 1, nslots)};
+            hipStream_t side = P_->ctx->side;
+            HIPC(hipEventRecord(w->vb_start, s_));
+            HIPC(hipStreamWaitEvent(side, w->vb_start, 0));
+            for (uint32_t b = 0; b < nb; ++b) {
+                const int k = (int)(b & 1u);
+                const uint64_t s0 = slot0 + (uint64_t)b * nslots;
+                const bool t = b % stride == 0;
+                if (b >= 2) HIPC(hipStreamWaitEvent(side, w->vb_done[k], 0));
+                HIPC(Tr::verify_gen(P_, prm_.seed, s0, nslots, bufs[k], side));
+                HIPC(hipEventRecord(w->vb_gen[k], side));
+                HIPC(hipStreamWaitEvent(s_, w->vb_gen[k], 0));
+                HIPC(Tr::verify_score(P_, Tm_, s0, nslots, m32, P_->w->recs.p + b,
+                                      t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr,
+                                      bufs[k], s_));
+                HIPC(hipEventRecord(w->vb_done[k], s_));
+                timed += t;
+            }
+        } else {
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint64_t s0 = slot0 + (uint64_t)b * nslots;
+                const bool t = b % stride == 0;
+                HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, P_->w->recs.p + b,
+                                t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr, s_));
+                timed += t;
+            }
         }
         HIPC(hipMemcpyAsync(out, P_->w->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
@@ -1324,6 +1398,11 @@ private:
 
     static bool prefetch_on() {
         const char* e = getenv("GCR_PREFETCH");              // read per run (tests switch it)
+        return !(e && e[0] == '0');
+    }
+    // GCR_VERIFY_PIPE=0: verify_batches on one stream (A/B of the pipeline)
+    static bool pipe_on() {
+        const char* e = getenv("GCR_VERIFY_PIPE");
         return !(e && e[0] == '0');
     }
 

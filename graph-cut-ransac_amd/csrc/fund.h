@@ -76,8 +76,10 @@ GCR_HD double cubic_root_in(double a, double b, double c, double lo, double hi, 
 // Real roots of c3 l^3 + c2 l^2 + c1 l + c0 in ascending order (basic ops +
 // sqrt only): brackets between the derivative's critical points and the
 // Cauchy bound, one safeguarded-Newton root per sign change.  Returns the
-// count.
-GCR_HD int real_roots_cubic(double c3, double c2, double c1, double c0, double r[3]) {
+// count.  Scalars only (no arrays): on the device a dynamically indexed
+// bracket or root array went to LDS / scratch.
+GCR_HD int real_roots_cubic(double c3, double c2, double c1, double c0, double& r0, double& r1, double& r2) {
+    r0 = r1 = r2 = 0.0;
     const double big = __builtin_fmax(__builtin_fabs(c2), __builtin_fmax(__builtin_fabs(c1), __builtin_fabs(c0)));
     if (!(__builtin_fabs(c3) > 1e-12 * big)) {
         // degenerate leading coefficient: quadratic / linear
@@ -87,59 +89,64 @@ GCR_HD int real_roots_cubic(double c3, double c2, double c1, double c0, double r
             const double sq = sqrt(disc);
             double u = (-c1 - sq) / (2.0 * c2), v = (-c1 + sq) / (2.0 * c2);
             if (v < u) { const double t = u; u = v; v = t; }
-            r[0] = u;
+            r0 = u;
             if (v == u) return 1;
-            r[1] = v;
+            r1 = v;
             return 2;
         }
         if (c1 != 0.0) {
-            r[0] = -c0 / c1;
+            r0 = -c0 / c1;
             return 1;
         }
         return 0;
     }
     const double a = c2 / c3, b = c1 / c3, c = c0 / c3;
     const double R = 1.0 + __builtin_fmax(__builtin_fabs(a), __builtin_fmax(__builtin_fabs(b), __builtin_fabs(c)));
-    double ends[4];
-    int ne;
     const double dd = a * a - 3.0 * b;          // discriminant of the derivative / 4
-    if (dd <= 0.0) {
-        ends[0] = -R; ends[1] = R; ends[2] = R; ends[3] = R; ne = 2;
-    } else {
+    // brackets [-R, e1], [e1, e2], [e2, R] between the critical points (only
+    // [-R, R] when the cubic is monotone)
+    const bool crit = dd > 0.0;
+    double e1 = R, e2 = R;
+    if (crit) {
         const double sq = sqrt(dd);
-        ends[0] = -R;
-        ends[1] = (-a - sq) / 3.0;
-        ends[2] = (-a + sq) / 3.0;
-        ends[3] = R;
-        ne = 4;
+        e1 = (-a - sq) / 3.0;
+        e2 = (-a + sq) / 3.0;
     }
     int n = 0;
-    double r0 = 0.0, r1 = 0.0, r2 = 0.0;       // fixed registers (no dynamic indexing on the device)
+    double o0 = 0.0, o1 = 0.0, o2 = 0.0;
+    // value selects, not an if-chain of stores (which the device compiler
+    // turned into a pointer table in LDS and stores through it)
     auto push = [&](double v) {
-        if (n == 0) r0 = v;
-        else if (n == 1) r1 = v;
-        else r2 = v;
+        o0 = n == 0 ? v : o0;
+        o1 = n == 1 ? v : o1;
+        o2 = n >= 2 ? v : o2;
         ++n;
     };
     double prev = 0.0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        if (k + 1 >= ne) break;
-        const double lo = ends[k], hi = ends[k + 1];
+    auto bracket = [&](double lo, double hi) {
         const double flo = cubic_monic(a, b, c, lo);
         const double fhi = cubic_monic(a, b, c, hi);
         if (flo == 0.0) {
             if (n == 0 || prev != lo) { push(lo); prev = lo; }
-            continue;
+            return;
         }
-        if (!((flo < 0.0) != (fhi < 0.0)) || fhi == 0.0) continue;
+        if (!((flo < 0.0) != (fhi < 0.0)) || fhi == 0.0) return;
         prev = cubic_root_in(a, b, c, lo, hi, flo);
         push(prev);
+    };
+    bracket(-R, e1);
+    if (crit) {
+        bracket(e1, e2);
+        bracket(e2, R);
     }
-    r[0] = r0;
-    r[1] = r1;
-    r[2] = r2;
+    r0 = o0;
+    r1 = o1;
+    r2 = o2;
     return n;
+}
+
+GCR_HD int real_roots_cubic(double c3, double c2, double c1, double c0, double r[3]) {
+    return real_roots_cubic(c3, c2, c1, c0, r[0], r[1], r[2]);
 }
 
 // Hartley normalisation of n points: centroid, mean distance, s = sqrt(2) / d;
@@ -309,11 +316,11 @@ GCR_HD int solve_f7_basis(const double x1[7], const double y1[7], const double x
     const double c0 = det3(out.F1), c3 = det3(out.F2), d1 = det3(P), dm1 = det3(M);
     const double c2 = (d1 + dm1) * 0.5 - c0;
     const double c1 = (d1 - dm1) * 0.5 - c3;
-    double roots[3] = {0.0, 0.0, 0.0};
-    const int nr = real_roots_cubic(c3, c2, c1, c0, roots);
-    out.root0 = roots[0];
-    out.root1 = roots[1];
-    out.root2 = roots[2];
+    double q0, q1, q2;
+    const int nr = real_roots_cubic(c3, c2, c1, c0, q0, q1, q2);
+    out.root0 = q0;
+    out.root1 = q1;
+    out.root2 = q2;
     int n = 0;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {

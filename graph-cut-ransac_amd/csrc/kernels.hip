@@ -307,6 +307,29 @@ __device__ __forceinline__ bool h_band(double x1, double y1, double x2, double y
     return !(e1 * e1 + e2 * e2 > Tb * (w * w));
 }
 
+// Fundamental band: the squared Sampson distance without its division.
+// With num and den computed exactly as f_sq_sampson (fund.h) computes them,
+// r^2 = num^2 / den <= T implies num^2 <= T den up to two roundings, so the
+// test num^2 > Tb den with Tb = T (1 + 1e-9) never rejects an inlier.  den is
+// a sum of squares (>= 0); den = 0 rejects iff num != 0 (r^2 = inf); NaN never
+// rejects (the exact residual decides).
+__device__ __forceinline__ bool f_band(double x1, double y1, double x2, double y2, const double* h, double Tb) {
+    const double fx0 = (h[0] * x1 + h[1] * y1) + h[2];
+    const double fx1 = (h[3] * x1 + h[4] * y1) + h[5];
+    const double fx2 = (h[6] * x1 + h[7] * y1) + h[8];
+    const double ft0 = (h[0] * x2 + h[3] * y2) + h[6];
+    const double ft1 = (h[1] * x2 + h[4] * y2) + h[7];
+    const double num = (x2 * fx0 + y2 * fx1) + fx2;
+    const double den = ((fx0 * fx0 + fx1 * fx1) + ft0 * ft0) + ft1 * ft1;
+    return !(num * num > Tb * den);
+}
+
+template <int KIND>
+__device__ __forceinline__ bool geo_band(double x1, double y1, double x2, double y2, const double* h, double Tb) {
+    if constexpr (KIND == 4) return f_band(x1, y1, x2, y2, h, Tb);
+    else return h_band(x1, y1, x2, y2, h, Tb);
+}
+
 __device__ __forceinline__ bool orient_band(double x, double y, double ct, double st, const HypConst& q,
                                             double tan_tau) {
     const double numer = (-x * st + y * ct) * q.h7 + st;
@@ -834,7 +857,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
                                                             const typename ModelOf<KIND>::type* __restrict__ models,
                                                             const uint8_t* __restrict__ inc, uint32_t nh,
                                                             ScoreOut out, GenArgs gen) {
-    static_assert(H >= 1 && H <= 16 && KIND <= 3, "feature-major scorer: H <= 16, band estimators");
+    static_assert(H >= 1 && H <= 16 && KIND <= 4, "feature-major scorer: H <= 16");
     static_assert(!kGen || KIND < 3, "in-kernel generation: rectification solvers");
     constexpr int kCap = 64 * H;                        // pairs of one wave-round
     // packed inlier values (-r^2) of hypothesis q in wave w's features, in
@@ -858,6 +881,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
     const int lane = t & 63;
     const bool chain_wave = wave == kFmWaves;
 
+    if constexpr (KIND >= 3) {
+        // compacted launches: hypotheses [0, *hcount) are models hmap[j]
+        if (gen.hcount != nullptr) nh = min(nh, *gen.hcount);
+        if (blockIdx.x * H >= nh) return;                // whole workgroup, before any barrier
+    }
     GCR_STAMP(5, 15u);
     // ---- prologue: this workgroup's H slots (kGen), k_generate's rule
     if constexpr (kGen) {
@@ -889,11 +917,12 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
     }
     if (t < H) {
         const uint32_t hg = blockIdx.x * H + t;
-        const bool v = hg < nh && (kGen ? gen_a[t] != 127 : (inc == nullptr || inc[hg] <= 101));
+        const uint32_t mi = (KIND >= 3 && gen.hmap != nullptr && hg < nh) ? gen.hmap[hg] : hg;
+        const bool v = hg < nh && (kGen ? gen_a[t] != 127 : (inc == nullptr || inc[mi] <= 101));
         typename ModelOf<KIND>::type m = ModelOf<KIND>::def();
         if (v) {
             if constexpr (kGen && KIND < 3) m = gen_m[t];
-            else m = models[hg];
+            else m = models[mi];
         }
         hyp[t] = make_hyp<KIND>(m, band0);
         hval[t] = v ? 1u : 0u;
@@ -926,7 +955,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
             f[1] = c.y[ic];
             if (cls == 0) {
                 f[2] = c.a[ic];
-                f[3] = (KIND == 3) ? c.c0[ic] : 0.0;
+                f[3] = (KIND >= 3) ? c.c0[ic] : 0.0;
             } else {
                 f[2] = c.c0[ic];
                 f[3] = c.c1[ic];
@@ -954,7 +983,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
                     const HypConst& hq = hyp[q];
                     bool cand = false;
                     if (ok) {
-                        if constexpr (KIND == 3) cand = h_band(f0, f1, f2, f3, hq.g, band0);
+                        if constexpr (KIND >= 3) cand = geo_band<KIND>(f0, f1, f2, f3, hq.g, band0);
                         else if (cls == 0) cand = scale_band<KIND>(f0, f1, f2, hq);
                         else if constexpr (KIND == 2) cand = orient_band(f0, f1, f2, f3, hq, tan_tau1);
                     }
@@ -989,7 +1018,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
                     x = __shfl(f0, src);
                     y = __shfl(f1, src);
                     a2 = __shfl(f2, src);
-                    if (KIND == 3 || cls == 1) a3 = __shfl(f3, src);
+                    if (KIND >= 3 || cls == 1) a3 = __shfl(f3, src);
                 } else {
                     // ... or re-read from L2 (keeps the LDS pipe to the chain)
                     const DevClass& c = p.cls[cls];
@@ -997,15 +1026,15 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
                     x = c.x[fi];
                     y = c.y[fi];
                     a2 = cls == 0 ? c.a[fi] : c.c0[fi];
-                    if (KIND == 3) a3 = c.c0[fi];
+                    if (KIND >= 3) a3 = c.c0[fi];
                     else if (cls == 1) a3 = c.c1[fi];
                 }
                 if (v) {
                     const HypConst& hq = hyp[q];
                     double r2;
                     bool inl;
-                    if constexpr (KIND == 3) {
-                        r2 = h_sq_residual(x, y, a2, a3, hq.g);
+                    if constexpr (KIND >= 3) {
+                        r2 = geo_sq_residual<KIND>(x, y, a2, a3, hq.g);
                         inl = r2 <= T0;
                     } else {
                         RectModel m = default_model();
@@ -1811,7 +1840,6 @@ __global__ __launch_bounds__(64) void k_qrd_ctl(QRCols cols, QRDevState* st, con
 // sequentially; the block tree then gives blocked_sum's block partial, stored
 // at partials[r * nblk + blk].  Columns are addressed through slots (slot 0 =
 // the Householder column in modes 2 / 3).
-constexpr int kQrfWaves = 4;
 __global__ __launch_bounds__(256) void k_qrf_pass(QRCols cols, const QRFState* __restrict__ st, uint64_t m,
                                                   uint64_t nblk, double* __restrict__ partials) {
     __shared__ double lds[kQrfMaxRed * 256];
@@ -2705,13 +2733,19 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
         else if (h == 16) go(ktag, std::integral_constant<int, 16>{}, std::integral_constant<int, 420>{});
         else go(ktag, std::integral_constant<int, 4>{}, std::integral_constant<int, 960>{});
     };
-    if (p.solver == 4) {
+    if (split_h(nh) == 16 && use_fm()) {
+        // the feature-major scorer with the division-free band prefilter:
+        // h_band (transfer error) or f_band (Sampson distance)
+        if (p.solver == 4) {
+            hipLaunchKernelGGL((k_score_fm<4, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), 0, stream, p,
+                               T, 0.0, T * (1.0 + 1e-9), 0.0, models, inc, nh, out, ga);
+        } else {
+            const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;
+            hipLaunchKernelGGL((k_score_fm<3, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), 0, stream, p,
+                               T, 0.0, sb * sb, 0.0, models, inc, nh, out, ga);
+        }
+    } else if (p.solver == 4) {
         by_h(std::integral_constant<int, 4>{});
-    } else if (split_h(nh) == 16 && use_fm() && hmap == nullptr) {
-        // homography: the feature-major scorer with the h_band prefilter
-        const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;
-        hipLaunchKernelGGL((k_score_fm<3, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), 0, stream, p, T,
-                           0.0, sb * sb, 0.0, models, inc, nh, out, ga);
     } else {
         by_h(std::integral_constant<int, 3>{});
     }

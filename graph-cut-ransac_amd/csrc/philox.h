@@ -90,7 +90,12 @@ GCR_HD bool sample_distinct(WordStream& ws, uint64_t n, int m, uint32_t* out) {
 #pragma unroll
         for (int q = 0; q < MAXM; ++q)
             if (q < j && out[q] == v) dup = true;
-        if (!dup) out[j++] = v;
+        // constant-index stores: on the device out[] stays in registers (a
+        // dynamic out[j] put the caller's index array in LDS / scratch)
+#pragma unroll
+        for (int q = 0; q < MAXM; ++q)
+            if (!dup && q == j) out[q] = v;
+        j += dup ? 0 : 1;
     }
     return true;
 }

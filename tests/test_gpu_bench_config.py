@@ -6,7 +6,10 @@ fused generate + score + per-workgroup-best kernel k_score_fm<K, 16, true>
 plus k_select_wg; at 16384 slots k_score_split<K, 64, 120, true>; the
 homography generates in k_generate<3, 16> and scores in k_score_fm<3, 16,
 false>; the fundamental matrix at 3712 slots (bench F_SLOTS) in
-k_generate_f + k_compact + k_score_split<4, 16, 420, false>.  Each batch's
+k_generate_f + k_compact + k_score_fm<4, 16, false> (f_band prefilter,
+compaction map).  Correspondence batches run as a two-stream pipeline (batch
+b + 1 generated on the side stream while batch b is scored, alternating
+buffer sets), which the NB consecutive batches exercise.  Each batch's
 record is checked against a pure ORACLE replay of the same slots: the
 oracle's Philox sampler and minimal solvers (O.slot / h_slot / f_slot), its
 twin-math MSAC score of every model, and the reference's update rule
@@ -145,3 +148,25 @@ def test_correspondence_verify_matches_oracle_replay_at_bench_config(solver, nsl
         assert r.best_slot == bslot and bslot >= 0, (b, r.best_slot, bslot)
         assert bits(r.best_score) == bits(best), b
         assert r.best_inliers[0] == bcnt, b
+
+
+@pytest.mark.parametrize("solver", [N.SOLVER_HOMOGRAPHY4, N.SOLVER_FUNDAMENTAL7])
+def test_pipelined_batches_equal_single_stream(solver, monkeypatch):
+    # GCR_VERIFY_PIPE=0 runs generate -> score -> select per batch on one
+    # stream; the pipeline must give the same records batch for batch
+    if solver == N.SOLVER_HOMOGRAPHY4:
+        corr, _, _, thr = S.problem_h(5000, 0.5, seed=SEED)
+    else:
+        corr, _, _, thr = S.problem_f(10_000, 0.8, seed=SEED)
+    prob = CorrProblem(solver, corr)
+    p = N.default_params()
+    p.scale_residual_thresh, p.seed = thr, SEED
+    outs = []
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("GCR_VERIFY_PIPE", pipe)
+        res = (N.BatchResult * 7)()
+        N.check(N.lib.gcr_problem_verify_batches(prob.h, C.byref(p), SLOT0, 2048, 7, res, None))
+        outs.append([(r.models, r.iterations, r.best_slot, bits(r.best_score).item(), r.best_inliers[0])
+                     for r in res])
+    assert outs[0] == outs[1]
+    assert all(o[2] >= 0 for o in outs[0])
