@@ -197,7 +197,8 @@ GCR_HD double fmod_2pi(double a) {
     constexpr double c = 2.0 * cf(0x400921fb54442d18ull);   // 2.0 * M_PI
     const double aa = __builtin_fabs(a);
     if (!(aa < 2.0 * c)) return fmod_2pi_slow(a);          // |a| >= 4 pi, inf, NaN
-    return (aa < c) ? a : ((a > 0.0) ? a - c : a + c);
+    // the remainder keeps the dividend's sign (fmod(-c, c) = -0.0)
+    return (aa < c) ? a : ((a < 0.0) ? -(aa - c) : a - c);
 }
 
 GCR_HD double clip_angle(double a) {
@@ -205,6 +206,16 @@ GCR_HD double clip_angle(double a) {
     double r = fmod_2pi(a);
     if (r < 0.0) r += c;
     return r;
+}
+
+// clip_angle for arguments known to satisfy |a| < 4 pi or to be NaN (atan2
+// results and their shifts by pi): the same value as clip_angle, without the
+// out-of-line fmod path, branch-free
+GCR_HD double clip_angle_small(double a) {
+    constexpr double c = 2.0 * cf(0x400921fb54442d18ull);
+    const double aa = __builtin_fabs(a);
+    const double r = (aa < c) ? a : ((a < 0.0) ? -(aa - c) : a - c);   // NaN stays NaN, unnegated
+    return r < 0.0 ? r + c : r;
 }
 
 }  // namespace dm

@@ -285,12 +285,14 @@ struct alignas(16) HypConst {   // per-hypothesis constants of the exact and ban
     };
 };
 
+// branch-free: t is computed exactly as scale_sq_residual computes it, so the
+// band and the exact residual see the same t bit for bit
 template <int KIND>
 __device__ __forceinline__ bool scale_band(double x, double y, double s, const HypConst& q) {
     const double t = (-q.h7 * x - q.h8 * y) + 1.0;
-    if (!(t > 0.0 && s > 0.0)) return true;               // sign / NaN: exact path decides
     const double t3 = (t * t) * t;
-    return !(s < q.lo * t3 || s > q.hi * t3);
+    const bool odd = !(t > 0.0 && s > 0.0);               // sign / NaN: exact path decides
+    return odd | !(s < q.lo * t3 || s > q.hi * t3);
 }
 
 // Homography band: the transfer error without its two divisions.  With
@@ -816,6 +818,22 @@ __device__ __forceinline__ uint64_t stamp_now() {
 // through LDS flags instead of barriers (ready[w]: rounds published by wave
 // w; done[w]: rounds of wave w the chain has folded), so a compute wave only
 // waits when the chain still reads its previous run.
+// compile-time loop: f(std::integral_constant<int, Q>) for Q in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// lane Q of v takes the (wave-uniform) value c: one v_writelane_b32
+template <int Q>
+__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t c) {
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(c), "n"(Q));
+    return v;
+}
+
 constexpr int kFmWaves = 15;
 constexpr uint32_t kFmRound = kFmWaves * 64;
 constexpr int kFmCB = 8;            // chain batch: 16-byte LDS reads (2 values each) per run step
@@ -976,82 +994,128 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
             //    the queue entry q | lane << 4 | k << 10 carries all of it
             uint32_t qn = 0, my_n = 0;
             uint32_t* wc = wcnt[r & 1][wave];
-            if (__ballot(ok) != 0) {
-#pragma unroll 4
-                for (int q = 0; q < H; ++q) {
-                    if (!((vmask >> q) & 1ull)) continue;
-                    const HypConst& hq = hyp[q];
-                    bool cand = false;
-                    if (ok) {
-                        if constexpr (KIND >= 3) cand = geo_band<KIND>(f0, f1, f2, f3, hq.g, band0);
-                        else if (cls == 0) cand = scale_band<KIND>(f0, f1, f2, hq);
-                        else if constexpr (KIND == 2) cand = orient_band(f0, f1, f2, f3, hq, tan_tau1);
+            // one fully unrolled hypothesis loop per band (the class is
+            // uniform over a round): no class branch per q, the band itself
+            // branch-free and evaluated on every lane (out-of-range lanes
+            // read feature 0 and are masked after), the next hypothesis's
+            // constants read from LDS while this one is tested, q's run
+            // length written to lane q with one v_writelane
+            auto run_band = [&](auto load, auto band) {
+                auto cur = load(0);
+                static_for<0, H>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    decltype(cur) nxt = cur;
+                    if constexpr (q + 1 < H) nxt = load(q + 1);
+                    if ((vmask >> q) & 1ull) {
+                        const bool cand = ok & band(cur);
+                        const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
+                        const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        if (cand) qw[qn + k] = (uint16_t)(q | (lane << 4) | (k << 10));
+                        const uint32_t c = (uint32_t)__builtin_popcountll(m);
+                        my_n = write_lane<q>(my_n, c);
+                        qn += c;
                     }
-                    const uint64_t m = __ballot(cand);
-                    const uint32_t k =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (cand) qw[qn + k] = (uint16_t)(q | (lane << 4) | (k << 10));
-                    const uint32_t c = (uint32_t)__builtin_popcountll(m);
-                    if (lane == q) my_n = c;
-                    qn += c;
+                    cur = nxt;
+                });
+            };
+            struct C4 { double a, b, c, d; };
+            if (__ballot(ok) != 0) {
+                if constexpr (KIND >= 3) {
+                    run_band([&](int q) -> const double* { return hyp[q].g; },
+                             [&](const double* g) { return geo_band<KIND>(f0, f1, f2, f3, g, band0); });
+                } else if (cls == 0) {
+                    run_band([&](int q) { return C4{hyp[q].h7, hyp[q].h8, hyp[q].lo, hyp[q].hi}; },
+                             [&](const C4& c) {
+                                 HypConst hq;
+                                 hq.h7 = c.a; hq.h8 = c.b; hq.lo = c.c; hq.hi = c.d;
+                                 return scale_band<KIND>(f0, f1, f2, hq);
+                             });
+                } else if constexpr (KIND == 2) {
+                    run_band([&](int q) { return C4{hyp[q].h7, hyp[q].h8, hyp[q].cf, hyp[q].sf}; },
+                             [&](const C4& c) {
+                                 HypConst hq;
+                                 hq.h7 = c.a; hq.h8 = c.b; hq.cf = c.c; hq.sf = c.d;
+                                 return orient_band(f0, f1, f2, f3, hq, tan_tau1);
+                             });
                 }
             }
             if (gen.probe & 2u) qn = my_n = 0;
             if (lane < H) wc[lane] = my_n;                 // survivors (run length) of (wave, q)
             GCR_STAMP(1, r);
-            // 2) the chain has folded this wave's previous runs (outv reuse)
-            if (r > 0) fm_wait_ge(&done[wave], r);
-            GCR_STAMP(2, r);
-            // 3) exact residuals of the survivors, all 64 lanes busy: -r^2 for
-            //    an inlier, +0.0 (an exact no-op of the sum) otherwise
-            double* ow = reinterpret_cast<double*>(&outv[wave][0][0]);
-            for (uint32_t j0 = 0; j0 < qn; j0 += 64) {
+            // 2) + 3) exact residuals of the survivors, all 64 lanes busy: -r^2
+            //    for an inlier, +0.0 (an exact no-op of the sum) otherwise.
+            //    Each 64-survivor batch's queue entries and features are
+            //    requested one batch ahead: the first batch's before waiting
+            //    for the chain to release outv (the L2 latency hides behind
+            //    the wait), the next batch's before this one is evaluated
+            struct Surv {
+                double x, y, a2, a3;
+                uint32_t e;
+            };
+            auto fetch = [&](uint32_t j0) {
+                Surv sv;
                 const uint32_t j = j0 + lane;
-                const bool v = j < qn;
-                const uint32_t e = v ? qw[j] : 0u;
-                const int q = (int)(e & 15u);
-                const int src = (int)((e >> 4) & 63u);
-                const uint32_t k = e >> 10;
-                double x, y, a2, a3 = 0.0;
+                sv.e = j < qn ? qw[j] : 0u;
+                const int src = (int)((sv.e >> 4) & 63u);
+                sv.a3 = 0.0;
                 if (gen.probe & 32u) {
                     // the survivor's feature from its owner lane (LDS permute)
-                    x = __shfl(f0, src);
-                    y = __shfl(f1, src);
-                    a2 = __shfl(f2, src);
-                    if (KIND >= 3 || cls == 1) a3 = __shfl(f3, src);
+                    sv.x = __shfl(f0, src);
+                    sv.y = __shfl(f1, src);
+                    sv.a2 = __shfl(f2, src);
+                    if (KIND >= 3 || cls == 1) sv.a3 = __shfl(f3, src);
                 } else {
                     // ... or re-read from L2 (keeps the LDS pipe to the chain)
                     const DevClass& c = p.cls[cls];
                     const uint32_t fi = (cls == 0 ? r : r - r0) * kFmRound + wave * 64 + src;
-                    x = c.x[fi];
-                    y = c.y[fi];
-                    a2 = cls == 0 ? c.a[fi] : c.c0[fi];
-                    if (KIND >= 3) a3 = c.c0[fi];
-                    else if (cls == 1) a3 = c.c1[fi];
+                    sv.x = c.x[fi];
+                    sv.y = c.y[fi];
+                    sv.a2 = cls == 0 ? c.a[fi] : c.c0[fi];
+                    if (KIND >= 3) sv.a3 = c.c0[fi];
+                    else if (cls == 1) sv.a3 = c.c1[fi];
                 }
+                return sv;
+            };
+            // GCR_PROBE bit 6: no look-ahead (each batch fetched when used)
+            const bool ahead = !(gen.probe & 64u);
+            Surv cur{0.0, 0.0, 0.0, 0.0, 0u};
+            if (ahead && qn > 0) cur = fetch(0);
+            // the chain has folded this wave's previous runs (outv reuse)
+            if (r > 0) fm_wait_ge(&done[wave], r);
+            GCR_STAMP(2, r);
+            double* ow = reinterpret_cast<double*>(&outv[wave][0][0]);
+            for (uint32_t j0 = 0; j0 < qn; j0 += 64) {
+                if (!ahead) cur = fetch(j0);
+                Surv nxt_s = cur;
+                if (ahead && j0 + 64 < qn) nxt_s = fetch(j0 + 64);
+                const bool v = j0 + lane < qn;
+                const int q = (int)(cur.e & 15u);
+                const uint32_t k = cur.e >> 10;
                 if (v) {
                     const HypConst& hq = hyp[q];
                     double r2;
                     bool inl;
                     if constexpr (KIND >= 3) {
-                        r2 = geo_sq_residual<KIND>(x, y, a2, a3, hq.g);
+                        r2 = geo_sq_residual<KIND>(cur.x, cur.y, cur.a2, cur.a3, hq.g);
                         inl = r2 <= T0;
                     } else {
                         RectModel m = default_model();
                         m.h7 = hq.h7;
                         m.h8 = hq.h8;
                         if (cls == 0) {
-                            r2 = scale_sq_residual<KIND == 1, true>(x, y, a2, m, hq.ac);
+                            r2 = scale_sq_residual<KIND == 1, true>(cur.x, cur.y, cur.a2, m, hq.ac);
                             inl = r2 <= T0;
                         } else {
                             const OrientConst oc{hq.cphi, hq.cphi2};
-                            r2 = orient_sq_residual<true>(x, y, a2, a3, m, oc);
+                            r2 = orient_sq_residual<true>(cur.x, cur.y, cur.a2, cur.a3, m, oc);
                             inl = r2 <= T1;
                         }
                     }
                     ow[q * kReg + k] = inl ? -r2 : 0.0;
                     if (inl) atomicAdd(&cnt_sh[cls][q], 1u);
                 }
+                cur = nxt_s;
             }
             GCR_STAMP(3, r);
             GCR_STAMP_VAL(6, r, (uint64_t)qn);
@@ -2301,6 +2365,8 @@ __global__ void k_math(int op, const double* __restrict__ a, const double* __res
         case 1: r = dm::dm_pow_m3(a[i]); break;
         case 2: r = dm::dm_atan2(a[i], b[i]); break;
         case 3: r = a[i] / b[i]; break;
+        case 5: r = dm::clip_angle_small(a[i]); break;
+        case 6: r = dm::clip_angle(a[i]); break;
         default: r = sqrt(a[i]); break;
     }
     out[i] = r;

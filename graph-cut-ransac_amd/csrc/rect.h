@@ -88,7 +88,7 @@ GCR_HD double min_angle_diff_c(double ca, double cb) {
 GCR_HD double rectified_angle(double px, double py, double ct, double st, double h7, double h8) {
     const double numer = (-px * st + py * ct) * h7 + st;
     const double denom = (px * st - py * ct) * h8 + ct;
-    return dm::clip_angle(dm::dm_atan2(numer, denom));
+    return dm::clip_angle_small(dm::dm_atan2(numer, denom));   // |atan2| <= pi
 }
 
 template <bool kIdentity>
@@ -100,8 +100,8 @@ GCR_HD double orient_sq_residual(double x, double y, double ct, double st, const
         py = m.s * (y - m.y0 * 1.0);
     }
     const double th = rectified_angle(px, py, ct, st, m.h7, m.h8);
-    const double c0 = dm::clip_angle(th);
-    const double c1 = dm::clip_angle(th - kPi);
+    const double c0 = dm::clip_angle_small(th);                // th in [0, 2 pi]
+    const double c1 = dm::clip_angle_small(th - kPi);
     const double l1 = __builtin_fmin(min_angle_diff_c(oc.cphi, c0), min_angle_diff_c(oc.cphi, c1));
     const double l2 = __builtin_fmin(min_angle_diff_c(oc.cphi2, c0), min_angle_diff_c(oc.cphi2, c1));
     const double r = __builtin_fmin(l1, l2);
@@ -297,7 +297,7 @@ GCR_HD bool solve_sift22(const double sx[2], const double sy[2], const double sp
     if (out.alpha < kEps9) return false;
     const double vz = (-out.h7 * vp[0] - out.h8 * vp[1]) + vp[2];   // rectifyPoint(vp)
     if (__builtin_fabs(vz) > kEps9) return false;
-    out.phi = dm::clip_angle(dm::dm_atan2(vp[1], vp[0]));
+    out.phi = dm::clip_angle_small(dm::dm_atan2(vp[1], vp[0]));
     return true;
 }
 

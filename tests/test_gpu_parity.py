@@ -67,6 +67,21 @@ def test_device_math_matches_host_bitwise():
     assert np.array_equal(bits(got), bits(exp))
 
 
+def test_clip_angle_small_equals_clip_angle():
+    # the residuals clip atan2 results (|a| <= pi) and their shifts by -pi
+    # with the branch-free clip_angle_small (detmath.h): same value as
+    # clip_angle and the oracle's clipAngle on |a| < 4 pi and NaN
+    rng = np.random.default_rng(5)
+    tp = 2.0 * math.pi
+    a = np.concatenate([rng.uniform(-2 * tp, 2 * tp, 100000), rng.uniform(-1e-12, 1e-12, 1000),
+                        [0.0, -0.0, math.pi, -math.pi, tp, -tp, np.nextafter(tp, 0), np.nextafter(-tp, 0),
+                         np.nextafter(2 * tp, 0), np.nextafter(-2 * tp, 0), -1e-300, np.nan]])
+    got = _dev_math(5, a)
+    assert np.array_equal(bits(got), bits(_dev_math(6, a)))
+    exp = np.array([O.lib().oracle_clip_angle(v) for v in a])
+    assert np.array_equal(bits(got), bits(exp))
+
+
 def test_device_division_and_sqrt_are_ieee():
     rng = np.random.default_rng(4)
     a = rng.normal(size=50000) * 10.0 ** rng.uniform(-100, 100, 50000)
