@@ -211,8 +211,11 @@ struct Workspace {
     PinBuf<double> h_r2;
     DevBuf<double> sm_vals;             // launch_score_small: pair values
     DevBuf<uint64_t> sm_bits;           // launch_score_small: inlier bitmasks
+    PinBuf<uint64_t> h_lbits;           // launch_score_small: LO list bits (ListBits), written by
+                                        // the kernel straight into this mapped pinned buffer
     PinBuf<uint8_t> h_mask_all;
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
+    PinBuf<BatchRecord> h_recs;         // ... and their pinned host image
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
     PinBuf<uint32_t> rf_hidx;           // GPU refit: their pinned staging
@@ -602,10 +605,13 @@ void GpuSiftSolver::for_ranges(size_t n, const std::function<void(size_t, size_t
 
 // verify_batches records kernel-timing events on every n-th batch
 // (GCR_TIMING_STRIDE, default 1 = every batch)
+// every batch's event pair costs ~6 us of queue time (measured at the
+// driver's 20-step line: stride 1 / 4 / 20 -> 0.136 / 0.130 / 0.129 ms per
+// step), so by default every 4th batch is timed
 uint32_t timing_stride() {
     static uint32_t v = [] {
         const char* e = getenv("GCR_TIMING_STRIDE");
-        const long n = e ? atol(e) : 1;
+        const long n = e ? atol(e) : 4;
         return (uint32_t)(n < 1 ? 1 : n);
     }();
     return v;
@@ -1033,17 +1039,24 @@ public:
             if (diff) off_ = 1 - off_;
             diff = false;
             for (int c = 0; c < K_; ++c) if (bufs_[off_].n[c] != best_.n[c]) diff = true;
+            // the buffer model's MSAC inlier lists come back with its score
+            // when it is (re)scored here (score_models' list bits)
+            const ListReq msac{{Tm_[0], Tm_[1]}, 0};
+            std::vector<uint32_t> lists[2];
+            bool have_lists = false;
             if (diff) {
                 HScore s;
                 uint32_t rn[2];
-                score_models(&best_model_, 1, &s, rn);
+                if (score_models(&best_model_, 1, &s, rn, &msac)) {
+                    list_of(0, lists);
+                    have_lists = true;
+                }
                 best_ = s;
                 bufs_[off_] = Buffer{true, best_model_, {rn[0], rn[1]}};
             }
             // iteratedLeastSquaresFitting never succeeds (GCRANSAC.h:1092-1098):
             // one non-minimal fit on the buffer's inliers, kept if strictly better.
-            std::vector<uint32_t> lists[2];
-            inlier_lists(bufs_[off_].model, Tm_, 0, lists);
+            if (!have_lists) inlier_lists(bufs_[off_].model, Tm_, 0, lists);
             Model refit;
             const auto t_fit = Clock::now();
             const bool fitted = Tr::fit(P_, lists, refit, true);
@@ -1051,13 +1064,14 @@ public:
             if (fitted) {
                 HScore s;
                 uint32_t rn[2];
-                score_models(&refit, 1, &s, rn);
+                const bool rl = score_models(&refit, 1, &s, rn, &msac);
                 const int idx = 1 - off_;
                 bufs_[idx] = Buffer{true, refit, {rn[0], rn[1]}};
                 if (best_.sum < s.sum) {
                     best_model_ = refit;
                     off_ = idx;
-                    inlier_lists(bufs_[off_].model, Tm_, 0, lists);
+                    if (rl) list_of(0, lists);
+                    else inlier_lists(bufs_[off_].model, Tm_, 0, lists);
                 }
             }
             for (uint32_t i : lists[0]) mask0[i] = 1;
@@ -1087,13 +1101,17 @@ public:
         static_assert(offsetof(BatchRecord, best_model) == offsetof(gcr_batch_result, best_model), "record layout");
         const auto t0 = Clock::now();
         P_->w->inc.ensure(nslots * kP); Tr::dmodels(P_->w).ensure(nslots * kP); P_->w->sb.ensure(nslots * kP);
-        P_->w->recs.ensure(nb);
+        // record buffers sized once for up to 4096 batches: a reallocation
+        // (device + pinned) inside a timed call costs milliseconds
+        constexpr uint32_t kRecMin = 4096;
+        P_->w->recs.ensure(std::max(nb, kRecMin));
+        P_->w->h_recs.ensure(std::max(nb, kRecMin));
 
         const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
         const size_t wg_cap = (nslots + 3) / 4;
         P_->w->wg.ensure(wg_cap);
         // score-kernel timing events on every `stride`-th batch
-        // (GCR_TIMING_STRIDE; default every batch), at most kMaxTimed evenly
+        // (GCR_TIMING_STRIDE; default every 4th), at most kMaxTimed evenly
         // spaced batches per call: the event pool is created once and reused
         // (hipEventCreate inside a long queue costs more than the kernels)
         constexpr uint32_t kMaxTimed = 64;
@@ -1139,8 +1157,9 @@ public:
                 timed += t;
             }
         }
-        HIPC(hipMemcpyAsync(out, P_->w->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
+        HIPC(hipMemcpyAsync(P_->w->h_recs.p, P_->w->recs.p, nb * sizeof(BatchRecord), hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
+        std::memcpy(out, P_->w->h_recs.p, nb * sizeof(BatchRecord));
         float kms_sum = 0;
         for (uint32_t q = 0; q < timed; ++q) {
             float kms = 0;
@@ -1522,21 +1541,46 @@ private:
     }
 
     // Score explicit host models on the GPU (LO trials, refit, reconcile).
-    void score_models(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */) {
+    // Scores of n models.  With `req` (thresholds + mask rule of an
+    // inlier_lists call) the small scorer also evaluates that list predicate
+    // on every pair and copies the bits back with the scores: returns true
+    // and list_of(q, ...) then yields model q's inlier lists without another
+    // launch + synchronisation.  False: no bits (batch-scorer path).
+    struct ListReq {
+        double T[2];
+        int rule;
+    };
+    bool score_models(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */,
+                      const ListReq* req = nullptr) {
         auto& lm = Tr::lomodels(P_->w);
         lm.ensure(n);
         P_->w->lo_sb.ensure(n);
         bool identity = true;
         for (uint32_t i = 0; i < n; ++i) identity = identity && Tr::identity(models[i]);
         HIPC(hipMemcpyAsync(lm.p, models, n * sizeof(Model), hipMemcpyHostToDevice, s_));
+        bool lists = false;
         if (identity && n <= kSmallScore && small_score_on()) {
             // a few models: all pairs in parallel, then one wave per model
             // adds its inliers in order (no ~90 us batch-scorer chain)
             const size_t pairs = small_score_pairs(P_->dp);
             P_->w->sm_vals.ensure(pairs * n);
             P_->w->sm_bits.ensure(pairs * n / 64);
+            // the graph-cut labeling with pairwise terms needs the residuals
+            lists = req != nullptr && !(req->rule == 2 && use_graph());
+            ListBits lb{{0.0, 0.0}, 0, prm_.spatial_coherence_weight, nullptr};
+            if (lists) {
+                // sized once for the largest small-scorer launch (a pinned
+                // reallocation costs milliseconds)
+                P_->w->h_lbits.ensure(pairs * kSmallScore / 64);
+                void* dptr = nullptr;
+                HIPC(hipHostGetDevicePointer(&dptr, P_->w->h_lbits.p, 0));
+                lb.T[0] = req->T[0];
+                lb.T[1] = req->T[1];
+                lb.rule = req->rule;
+                lb.bits = static_cast<uint64_t*>(dptr);
+            }
             HIPC(launch_score_small(P_->dp, Tm_, lm.p, nullptr, n, P_->w->lo_sb.dev(), P_->w->sm_vals.p,
-                                    P_->w->sm_bits.p, s_));
+                                    P_->w->sm_bits.p, s_, lists ? &lb : nullptr));
         } else {
             HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
         }
@@ -1548,6 +1592,28 @@ private:
             out[i] = finish(rn, P_->w->lo_sb.hv0.p[i], P_->w->lo_sb.hv1.p[i], P_->w->lo_sb.htot.p[i]);
             raw_n[2 * i] = rn[0];
             raw_n[2 * i + 1] = K_ == 2 ? rn[1] : 0;
+        }
+        return lists;
+    }
+
+    // model q's inlier lists from the bits of the last score_models(req) call
+    // (small scorer pair layout: class 0 at [0, pad0), class 1 after it)
+    void list_of(uint32_t q, std::vector<uint32_t> lists[2]) const {
+        const size_t pairs = small_score_pairs(P_->dp);
+        const size_t pad0 = (N_[0] + 63) & ~(size_t)63;
+        const uint64_t* w = P_->w->h_lbits.p + q * (pairs / 64);
+        for (int c = 0; c < 2; ++c) {
+            lists[c].clear();
+            if (c >= K_) continue;
+            const size_t base = c ? pad0 : 0;
+            for (size_t wi = 0; wi < (N_[c] + 63) / 64; ++wi) {
+                uint64_t b = w[(base >> 6) + wi];
+                while (b) {
+                    const int t = __builtin_ctzll(b);
+                    b &= b - 1;
+                    lists[c].push_back((uint32_t)(wi * 64 + t));
+                }
+            }
         }
     }
 
@@ -1617,10 +1683,16 @@ private:
         std::vector<HScore> trial_scores;
         std::vector<uint32_t> trial_raw;
         const uint64_t T = prm_.max_local_optimization_number;
+        // the LO lists (threshold (1.5 thr)^2, labeling rule) of the round's
+        // winner come back with the trial scores, so the next round starts
+        // without its own mask launch + synchronisation
+        const ListReq lreq{{Tlo_[0], Tlo_[1]}, K_ == 2 ? 0 : 2};
+        bool have_inl = false;
         while (++gc_number_ < 10) {
             bool updated = false;
             auto tp = Clock::now();
-            inlier_lists(lo_model, Tlo_, K_ == 2 ? 0 : 2, inl);
+            if (!have_inl) inlier_lists(lo_model, Tlo_, lreq.rule, inl);
+            have_inl = false;
             st_.ms_lo_lists += ms_since(tp);
             tp = Clock::now();
             uint64_t ssz[2] = {0, 0};
@@ -1674,17 +1746,23 @@ private:
             if (!trial_models.empty()) {
                 trial_scores.resize(trial_models.size());
                 trial_raw.resize(2 * trial_models.size());
-                score_models(trial_models.data(), (uint32_t)trial_models.size(), trial_scores.data(),
-                             trial_raw.data());
+                const bool bits = score_models(trial_models.data(), (uint32_t)trial_models.size(),
+                                               trial_scores.data(), trial_raw.data(), &lreq);
                 st_.lo_models += trial_models.size();
                 st_.ms_lo_score += ms_since(tp);
+                size_t win = 0;
                 for (size_t q = 0; q < trial_models.size(); ++q) {
                     if (max_score.sum < trial_scores[q].sum) {
                         updated = true;
+                        win = q;
                         max_score = trial_scores[q];
                         lo_model = trial_models[q];
                         lo_buf = Buffer{true, trial_models[q], {trial_raw[2 * q], trial_raw[2 * q + 1]}};
                     }
+                }
+                if (updated && bits) {
+                    list_of((uint32_t)win, inl);
+                    have_inl = true;
                 }
             }
             if (!updated) break;

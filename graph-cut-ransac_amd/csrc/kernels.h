@@ -218,8 +218,18 @@ hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_
 // to RectModel (solvers 0-2) or GeoModel (3, 4), identity normalisation only;
 // models with inc > 101 (inc may be null) score zeros.
 size_t small_score_pairs(const DevProblem& p);
+// Optional second per-pair predicate of the same launch (LO inlier lists):
+// rule 0: r^2 <= T[cls]; rule 2: the 1-class labeling of k_mask with T[0] and
+// lambda.  Bits in the layout of `bits`.
+struct ListBits {
+    double T[2];
+    int rule;
+    double lambda;
+    uint64_t* bits;
+};
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
-                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream);
+                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream,
+                              const ListBits* lists = nullptr);
 
 // Per-feature inlier mask of one model for class `cls`.
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)

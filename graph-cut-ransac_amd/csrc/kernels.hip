@@ -1269,11 +1269,25 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
 //
 // Layout per model: class 0 at [0, pad0), class 1 at [pad0, pad0 + pad1),
 // pad_c = n_c rounded up to 64 (unused pairs: value 0, bit 0).
+// mask rule of k_mask / launch_mask on a residual (rule 0: threshold; rule 2:
+// the 1-class labeling without pairwise edges)
+__device__ __forceinline__ bool mask_rule(double r2, int rule, double T, double lambda) {
+    if (rule == 2) {
+        const double oml = 1.0 - lambda;
+        double q = r2 / T;
+        q = (q < 0.0) ? 0.0 : ((1.0 < q) ? 1.0 : q);      // std::clamp
+        const double energy = 1.0 - q;
+        const double tr = (r2 <= T) ? (0.0 - oml * energy) : (oml * (1.0 - energy) - 0.0);
+        return tr < 0.0;
+    }
+    return r2 <= T;
+}
+
 template <int KIND>
 __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
                                                   const uint8_t* __restrict__ inc, double T0, double T1,
                                                   uint32_t pad0, uint32_t ntot, double* __restrict__ vals,
-                                                  uint64_t* __restrict__ bits) {
+                                                  uint64_t* __restrict__ bits, ListBits lb) {
     const uint32_t mi = blockIdx.y;
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (blockIdx.x * 256 >= ntot) return;                // whole block (ntot is a multiple of 64)
@@ -1295,9 +1309,16 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
         inl = r2 <= (cls == 0 ? T0 : T1);
     }
     const uint64_t b = __ballot(inl);
+    // the LO list predicate of the same residual (launch_mask's rule)
+    const bool lin = lb.bits != nullptr && live && j < ntot && i < c.n &&
+                     mask_rule(r2, lb.rule, cls == 0 ? lb.T[0] : lb.T[1], lb.lambda);
+    const uint64_t lbw = __ballot(lin);
     if (j < ntot) {
         vals[(size_t)mi * ntot + j] = inl ? -r2 : 0.0;
-        if ((threadIdx.x & 63) == 0) bits[((size_t)mi * ntot + j) / 64] = b;
+        if ((threadIdx.x & 63) == 0) {
+            bits[((size_t)mi * ntot + j) / 64] = b;
+            if (lb.bits != nullptr) lb.bits[((size_t)mi * ntot + j) / 64] = lbw;
+        }
     }
 }
 
@@ -2338,20 +2359,9 @@ __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, typena
     if constexpr (KIND >= 3) r2 = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
     else if (cls == 0) r2 = scale_sq_residual<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
     else r2 = orient_sq_residual<false>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
-    bool inl;
-    if (rule == 2) {
-        // labeling(): BK max-flow with no pairwise edges (empty grid graph,
-        // gcransac_python.cpp:63-68) -> SINK iff terminal capacity < 0.
-        const double oml = 1.0 - lambda;
-        double q = r2 / T;
-        q = (q < 0.0) ? 0.0 : ((1.0 < q) ? 1.0 : q);      // std::clamp
-        const double energy = 1.0 - q;
-        const double tr = (r2 <= T) ? (0.0 - oml * energy) : (oml * (1.0 - energy) - 0.0);
-        inl = tr < 0.0;
-    } else {
-        inl = r2 <= T;
-    }
-    mask[i] = inl ? 1 : 0;
+    // rule 2: labeling(), BK max-flow with no pairwise edges (empty grid
+    // graph, gcransac_python.cpp:63-68) -> SINK iff terminal capacity < 0
+    mask[i] = mask_rule(r2, rule, T, lambda) ? 1 : 0;
 }
 
 // ----------------------------------------------------------------- math ----
@@ -2704,7 +2714,9 @@ size_t small_score_pairs(const DevProblem& p) {
 }
 
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
-                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream) {
+                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream,
+                              const ListBits* lists) {
+    const ListBits lb = lists ? *lists : ListBits{{0.0, 0.0}, 0, 0.0, nullptr};
     if (nm == 0) return hipSuccess;
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t ntot = (uint32_t)small_score_pairs(p);
@@ -2714,7 +2726,7 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         constexpr int KIND = decltype(ktag)::value;
         using M = typename ModelOf<KIND>::type;
         hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), inc, T[0], T[1],
-                           pad0, ntot, vals, bits);
+                           pad0, ntot, vals, bits, lb);
         hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits, out);
     };
     switch (p.solver) {

@@ -1,0 +1,12 @@
+#!/bin/bash
+# full GPU suite, then the driver-shaped bench line (with the latency leg) and
+# the step-count check of the record buffers
+set -u
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread > gpurun_out/tests_all.log 2>&1
+rc=$?; tail -3 gpurun_out/tests_all.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_drv.log 2>&1 || exit 1
+for k in 200 2000; do
+  timeout -k 10 120 python bench.py --gpus 1 --steps $k --warmup 5 --cpu-seconds 0 --no-latency --no-hbm-probe > gpurun_out/k_$k.log 2>&1 || exit 1
+done
+echo done
