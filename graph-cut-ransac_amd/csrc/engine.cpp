@@ -216,6 +216,8 @@ struct Workspace {
     PinBuf<uint8_t> h_mask_all;
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
     PinBuf<BatchRecord> h_recs;         // ... and their pinned host image
+    DevBuf<uint8_t> pg_inc[2];          // verify_batches: slots generated one launch ahead
+    DevBuf<RectModel> pg_models[2];
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
     PinBuf<uint32_t> rf_hidx;           // GPU refit: their pinned staging
@@ -785,11 +787,35 @@ struct RectTraits {
                                    hipEvent_t, hipEvent_t, const VBufs&, hipStream_t) {
         return hipErrorNotSupported;
     }
+    // batch b of nb: chained launches (the previous launch generated this
+    // batch's slots, this one generates the next batch's) when the kernel
+    // at this batch size supports it (verify_chains)
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t wg_cap, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
-                             hipStream_t s) {
+                             hipStream_t s, uint32_t b = 0, uint32_t nb = 1) {
+        GenChain ch;
+        if (nb > 1 && verify_chains(n) && chain_on()) {
+            Workspace* w = P->w;
+            for (int k = 0; k < 2; ++k) {
+                w->pg_inc[k].ensure(n);
+                w->pg_models[k].ensure(n);
+            }
+            if (b > 0) {
+                ch.pre_inc = w->pg_inc[b & 1].p;
+                ch.pre_models = w->pg_models[b & 1].p;
+            }
+            if (b + 1 < nb) {
+                ch.next_inc = w->pg_inc[(b + 1) & 1].p;
+                ch.next_models = w->pg_models[(b + 1) & 1].p;
+            }
+        }
         return launch_verify_fused(P->dp, Tm, seed, s0, n, m, P->w->inc.p, P->w->models.p, P->w->sb.dev(),
-                                   P->w->wg.p, wg_cap, rec, e0, e1, s);
+                                   P->w->wg.p, wg_cap, rec, e0, e1, s, ch);
+    }
+    // GCR_VERIFY_CHAIN=0: every launch generates its own slots (A/B)
+    static bool chain_on() {
+        const char* e = getenv("GCR_VERIFY_CHAIN");
+        return !(e && e[0] == '0');
     }
     // LO fits on the host; the final hybrid refit solves big systems on the GPU
     static bool fit(gcr_problem* P, const std::vector<uint32_t>* lists, Model& out, bool final_refit) {
@@ -877,7 +903,7 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     }
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
-                             hipStream_t s) {
+                             hipStream_t s, uint32_t = 0, uint32_t = 1) {
         const VBufs b = vbufs(P, 0, n);
         const hipError_t e = verify_gen(P, seed, s0, n, b, s);
         if (e != hipSuccess) return e;
@@ -1153,7 +1179,8 @@ public:
                 const uint64_t s0 = slot0 + (uint64_t)b * nslots;
                 const bool t = b % stride == 0;
                 HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, P_->w->recs.p + b,
-                                t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr, s_));
+                                t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr, s_,
+                                b, nb));
                 timed += t;
             }
         }

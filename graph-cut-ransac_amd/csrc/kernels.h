@@ -181,10 +181,23 @@ struct WgBest {
     uint32_t models;     // slots of the workgroup with a model (inc <= 101)
     uint64_t iterations; // sum of the workgroup's inc
 };
+// Batch chaining of the feature-major fused scorer (H = 16 launches): `pre`
+// holds this batch's slots already generated by the previous launch (null:
+// the launch's prologue generates them), `next` receives the next batch's
+// (slots slot0 + nslots ...), generated by a dedicated wave while this batch
+// is scored (null: none).  Same models and attempt counts as the prologue.
+struct GenChain {
+    const uint8_t* pre_inc = nullptr;
+    const RectModel* pre_models = nullptr;
+    uint8_t* next_inc = nullptr;
+    RectModel* next_models = nullptr;
+};
 hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t seed, uint64_t slot0,
                                uint32_t nslots, const uint32_t m[2], uint8_t* inc, RectModel* models,
                                const ScoreOut& out, WgBest* wg, size_t wg_cap, BatchRecord* rec,
-                               hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream);
+                               hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream, const GenChain& chain = {});
+// true when launch_verify_fused at this batch size uses the chained kernel
+bool verify_chains(uint32_t nslots);
 
 // homography (solver 3) counterparts of launch_generate / launch_score /
 // launch_mask / launch_select

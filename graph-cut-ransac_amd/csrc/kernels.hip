@@ -360,6 +360,7 @@ struct GenArgs {
     // the chain fold, bit 1 the exact pass, bit 2 the band test, bit 3 the
     // prologue's attempts (every slot takes attempt 0's default model)
     uint32_t probe;
+    GenChain chain;                     // k_score_fm<.., true>: batch chaining
 };
 
 template <int KIND, int H, int R, bool kGen>
@@ -835,7 +836,6 @@ __device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t c) {
 }
 
 constexpr int kFmWaves = 15;
-constexpr uint32_t kFmRound = kFmWaves * 64;
 constexpr int kFmCB = 8;            // chain batch: 16-byte LDS reads (2 values each) per run step
                                     // (16, i.e. 32-value batches: 130.8 vs 127.8 us)
 
@@ -877,16 +877,19 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
                                                             ScoreOut out, GenArgs gen) {
     static_assert(H >= 1 && H <= 16 && KIND <= 4, "feature-major scorer: H <= 16");
     static_assert(!kGen || KIND < 3, "in-kernel generation: rectification solvers");
+    // compute waves: 15, or 14 plus the look-ahead generator wave (kGen)
+    constexpr int kW = kGen ? kFmWaves - 1 : kFmWaves;
+    constexpr uint32_t kRound = kW * 64u;
     constexpr int kCap = 64 * H;                        // pairs of one wave-round
     // packed inlier values (-r^2) of hypothesis q in wave w's features, in
     // feature order, zero-padded to whole chain batches
     // region stride 66 doubles: the 16 chain lanes' 16-byte reads (and the
     // exact pass's scattered writes) fall in distinct banks
     constexpr int kReg = 66;
-    __shared__ double2 outv[kFmWaves][H][kReg / 2];
-    __shared__ uint16_t queue[kFmWaves][kCap];          // survivors: q | lane << 4 | k << 10
-    __shared__ uint32_t wcnt[2][kFmWaves][H];           // survivors of (wave, q) in the round
-    __shared__ uint32_t ready[kFmWaves], done[kFmWaves];
+    __shared__ double2 outv[kW][H][kReg / 2];
+    __shared__ uint16_t queue[kW][kCap];                // survivors: q | lane << 4 | k << 10
+    __shared__ uint32_t wcnt[2][kW][H];                 // survivors of (wave, q) in the round
+    __shared__ uint32_t ready[kW], done[kW];
     __shared__ HypConst hyp[H];
     __shared__ uint32_t hval[H];
     __shared__ uint32_t cnt_sh[2][H];
@@ -905,8 +908,22 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
         if (blockIdx.x * H >= nh) return;                // whole workgroup, before any barrier
     }
     GCR_STAMP(5, 15u);
-    // ---- prologue: this workgroup's H slots (kGen), k_generate's rule
+    // ---- prologue: this workgroup's H slots (kGen), k_generate's rule, or
+    // (chained batches) the previous launch's look-ahead wave's results
     if constexpr (kGen) {
+      if (gen.chain.pre_inc != nullptr) {
+        if (t < H) {
+            const uint32_t hs = blockIdx.x * H + t;
+            const uint8_t iv = hs < nh ? gen.chain.pre_inc[hs] : (uint8_t)102;
+            gen_a[t] = iv > 101 ? 127 : (int)iv - 1;
+            gen_m[t] = iv > 101 ? default_model() : gen.chain.pre_models[hs];
+        }
+        __syncthreads();
+        if (t < H && blockIdx.x * H + t < nh) {
+            gen.inc[blockIdx.x * H + t] = gen.chain.pre_inc[blockIdx.x * H + t];
+            gen.models[blockIdx.x * H + t] = gen_m[t];
+        }
+      } else {
         const int G = gen.glanes ? (int)gen.glanes : kSplitThreads / H;
         const bool gact = t < H * G;
         if (t < H) gen_a[t] = 127;
@@ -932,6 +949,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
             gen.inc[blockIdx.x * H + t] = (uint8_t)(a == 127 ? 102 : a + 1);
             gen.models[blockIdx.x * H + t] = a == 127 ? default_model() : gen_m[t];
         }
+      }
     }
     if (t < H) {
         const uint32_t hg = blockIdx.x * H + t;
@@ -948,14 +966,58 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
         cnt_sh[1][t] = 0;
     }
     GCR_STAMP(6, 15u);
-    if (t < kFmWaves) { ready[t] = 0; done[t] = 0; }
+    if (t < kW) { ready[t] = 0; done[t] = 0; }
     __syncthreads();
     GCR_STAMP(7, 15u);
 
     const uint32_t n0 = p.cls[0].n;
     const uint32_t n1 = (KIND == 2) ? p.cls[1].n : 0;
-    const uint32_t r0 = (n0 + kFmRound - 1) / kFmRound;
-    const uint32_t rounds = r0 + (n1 + kFmRound - 1) / kFmRound;
+    const uint32_t r0 = (n0 + kRound - 1) / kRound;
+    const uint32_t rounds = r0 + (n1 + kRound - 1) / kRound;
+
+    if constexpr (kGen) {
+        if (wave == kW) {
+            // ------------------------------------------ look-ahead generator
+            // the next batch's slots of this workgroup (blockIdx.x * H + sl,
+            // slot index slot0 + nh + ...), 64 / H lanes per slot trying
+            // attempts r G + g; the lowest success wins (k_generate's rule).
+            // Overlaps the rounds below; no barrier follows.
+            if (gen.chain.next_inc == nullptr) return;
+            constexpr int G = 64 / H;
+            const int sl = lane / G, g = lane % G;
+            const uint32_t hs = blockIdx.x * H + sl;
+            const bool act = hs < nh;
+            bool open = act;
+            int won = -1;
+            RectModel best = default_model();
+            for (uint32_t rr = 0; rr * G < 101; ++rr) {
+                if (__ballot(open) == 0) break;
+                const uint32_t a = rr * G + g;
+                RectModel m = default_model();
+                bool ok = false;
+                if (open && a < 101)
+                    ok = (gen.probe & 8u) ? a == 0 : attempt<KIND>(p, gen.seed, gen.slot0 + nh + hs, a, m);
+                const uint64_t bm = __ballot(ok);
+                const uint64_t grp = (bm >> (sl * G)) & ((G == 64) ? ~0ull : ((1ull << G) - 1ull));
+                if (open && grp != 0) {
+                    open = false;
+                    if (g == __builtin_ctzll(grp)) {
+                        won = (int)a;
+                        best = m;
+                    }
+                }
+            }
+            if (act && won >= 0) {
+                gen.chain.next_inc[hs] = (uint8_t)(won + 1);
+                gen.chain.next_models[hs] = best;
+            } else if (act && g == 0 && open) {
+                // every attempt failed (inc 102, no model)
+                gen.chain.next_inc[hs] = 102;
+                gen.chain.next_models[hs] = default_model();
+            }
+            return;
+        }
+    }
 
     if (!chain_wave) {
         // ---------------------------------------------------- compute waves
@@ -966,7 +1028,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
         auto load = [&](uint32_t rr, double* f, bool& ok) {
             const int cls = rr < r0 ? 0 : 1;
             const DevClass& c = p.cls[cls];
-            const uint32_t i = (cls == 0 ? rr : rr - r0) * kFmRound + wave * 64 + lane;
+            const uint32_t i = (cls == 0 ? rr : rr - r0) * kRound + wave * 64 + lane;
             ok = i < c.n;
             const uint32_t ic = ok ? i : 0u;
             f[0] = c.x[ic];
@@ -1068,7 +1130,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
                 } else {
                     // ... or re-read from L2 (keeps the LDS pipe to the chain)
                     const DevClass& c = p.cls[cls];
-                    const uint32_t fi = (cls == 0 ? r : r - r0) * kFmRound + wave * 64 + src;
+                    const uint32_t fi = (cls == 0 ? r : r - r0) * kRound + wave * 64 + src;
                     sv.x = c.x[fi];
                     sv.y = c.y[fi];
                     sv.a2 = cls == 0 ? c.a[fi] : c.c0[fi];
@@ -1152,23 +1214,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
             GCR_STAMP(0, r);
             // waves that have published round r (bit w), polled all at once
             auto poll = [&]() -> uint64_t {
-                const uint32_t f = lane < kFmWaves
+                const uint32_t f = lane < kW
                                        ? __hip_atomic_load(&ready[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
                                        : 0u;
-                return __ballot(lane < kFmWaves && f >= r + 1);
+                return __ballot(lane < kW && f >= r + 1);
             };
             uint64_t rmask = poll();
             uint32_t n = 0;
             bool have = false;
 #pragma unroll 1
-            for (int w = 0; w < kFmWaves; ++w) {
+            for (int w = 0; w < kW; ++w) {
                 while (!((rmask >> w) & 1ull)) {
                     __builtin_amdgcn_s_sleep(1);
                     rmask = poll();
                 }
                 if (!have) n = wcnt[r & 1][w][h];
                 // the next run's length, read ahead if that wave has published
-                const bool nhave = w + 1 < kFmWaves && ((rmask >> (w + 1)) & 1ull);
+                const bool nhave = w + 1 < kW && ((rmask >> (w + 1)) & 1ull);
                 const uint32_t nn = nhave ? wcnt[r & 1][w + 1][h] : 0u;
                 if (fold_on) {
                     // whole batches of kFmCB 16-byte reads (zero-padded runs),
@@ -2670,12 +2732,16 @@ void launch_fused_t(const DevProblem& p, const double T[2], uint32_t nh, const S
     }
 }
 
+bool verify_chains(uint32_t nslots) { return split_h(nslots) == 16 && use_fm(); }
+
 hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t seed, uint64_t slot0,
                                uint32_t nslots, const uint32_t m[2], uint8_t* inc, RectModel* models,
                                const ScoreOut& out, WgBest* wg, size_t wg_cap, BatchRecord* rec,
-                               hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream) {
+                               hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream, const GenChain& chain) {
     if (nslots == 0) return hipErrorInvalidValue;
     const int h = split_h(nslots);
+    if ((chain.pre_inc != nullptr || chain.next_inc != nullptr) && !verify_chains(nslots))
+        return hipErrorInvalidValue;
     const uint32_t nwg = (nslots + h - 1) / h;
     if (nwg > wg_cap) return hipErrorInvalidValue;
     GenArgs g{seed, slot0, inc, models, wg, m[0], m[1]};
@@ -2696,6 +2762,7 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
     // 134.5 us per fused launch)
     const uint32_t gl = glanes ? glanes : 16u;
     g.glanes = ((1024u / h) % gl == 0 && (gl & (gl - 1)) == 0) ? gl : 0u;
+    g.chain = chain;
     if (ev0) (void)hipEventRecord(ev0, stream);
     if (h == 16 && use_fm()) launch_fm_t<16, true>(p, T, nslots, out, g, stream);
     else if (h == 64) launch_fused_t<64, 120>(p, T, nslots, out, g, stream);

@@ -3,7 +3,8 @@ configurations (run on an MI355X: pytest -m gpu).
 
 bench.py's step is gcr_problem_verify_batches: at 4096 slots per launch the
 fused generate + score + per-workgroup-best kernel k_score_fm<K, 16, true>
-plus k_select_wg; at 16384 slots k_score_split<K, 64, 120, true>; the
+plus k_select_wg, consecutive launches chained (each launch's look-ahead wave
+generates the next batch's slots, which NB >= 2 exercises); at 16384 slots k_score_split<K, 64, 120, true>; the
 homography generates in k_generate<3, 16> and scores in k_score_fm<3, 16,
 false>; the fundamental matrix at 3712 slots (bench F_SLOTS) in
 k_generate_f + k_compact + k_score_fm<4, 16, false> (f_band prefilter,
@@ -168,5 +169,27 @@ def test_pipelined_batches_equal_single_stream(solver, monkeypatch):
         N.check(N.lib.gcr_problem_verify_batches(prob.h, C.byref(p), SLOT0, 2048, 7, res, None))
         outs.append([(r.models, r.iterations, r.best_slot, bits(r.best_score).item(), r.best_inliers[0])
                      for r in res])
+    assert outs[0] == outs[1]
+    assert all(o[2] >= 0 for o in outs[0])
+
+
+@pytest.mark.parametrize("kind", [N.SOLVER_SIFT22, N.SOLVER_SCALE3, N.SOLVER_SCALE3_ORIGINAL])
+def test_chained_batches_equal_unchained(kind, monkeypatch):
+    # at 4096 slots consecutive fused launches are chained: each one's spare
+    # wave generates the next batch's slots, which the next launch scores
+    # instead of generating them in its prologue.  GCR_VERIFY_CHAIN=0 turns
+    # that off; records must be identical batch for batch
+    f0, f1, thr0, thr1 = _rect_problem(kind)
+    prob = Problem(kind, f0, f1)
+    p = N.default_params()
+    p.scale_residual_thresh, p.orientation_residual_thresh, p.seed = thr0, thr1, SEED
+    outs = []
+    for chain in ("1", "0"):
+        monkeypatch.setenv("GCR_VERIFY_CHAIN", chain)
+        res = (N.BatchResult * 6)()
+        N.check(N.lib.gcr_problem_verify_batches(prob.h, C.byref(p), SLOT0, 4096, 6, res, None))
+        outs.append([(r.models, r.iterations, r.best_slot, bits(r.best_score).item(), r.best_inliers[0],
+                      r.best_inliers[1], bits([r.best_model.h7, r.best_model.h8, r.best_model.alpha,
+                                               r.best_model.phi]).tolist()) for r in res])
     assert outs[0] == outs[1]
     assert all(o[2] >= 0 for o in outs[0])
