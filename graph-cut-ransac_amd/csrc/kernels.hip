@@ -869,8 +869,20 @@ __device__ __forceinline__ HypConst make_hyp(const typename ModelOf<KIND>::type&
     return q;
 }
 
+// Correspondence instantiations (KIND >= 3) keep the survivor regions and
+// queues in dynamic LDS and are held to 64 VGPRs (8 waves per SIMD's worth):
+// with the LDS size unknown at compile time the register cap applies, and a
+// scoring workgroup (16 waves x 64 VGPRs) then leaves room on every SIMD for
+// one wave of the separately launched generator (k_generate_f, ~240 VGPRs,
+// no LDS), which the two-stream batch pipeline of verify_batches overlaps
+template <int H, bool kGen>
+constexpr size_t fm_dyn_lds_bytes() {
+    constexpr int kW = kGen ? kFmWaves - 1 : kFmWaves;
+    return (size_t)kW * H * 66 * sizeof(double) + (size_t)kW * 64 * H * sizeof(uint16_t);
+}
+
 template <int KIND, int H, bool kGen>
-__global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double T0, double T1, double band0,
+__global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(KIND >= 3 ? 8 : 1))) void k_score_fm(DevProblem p, double T0, double T1, double band0,
                                                             double tan_tau1,
                                                             const typename ModelOf<KIND>::type* __restrict__ models,
                                                             const uint8_t* __restrict__ inc, uint32_t nh,
@@ -886,8 +898,16 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
     // region stride 66 doubles: the 16 chain lanes' 16-byte reads (and the
     // exact pass's scattered writes) fall in distinct banks
     constexpr int kReg = 66;
-    __shared__ double2 outv[kW][H][kReg / 2];
-    __shared__ uint16_t queue[kW][kCap];                // survivors: q | lane << 4 | k << 10
+    constexpr bool kDyn = KIND >= 3;                    // regions + queues in dynamic LDS (above)
+    static_assert(!kDyn || fm_dyn_lds_bytes<H, kGen>() == (size_t)kW * H * kReg * 8 + (size_t)kW * kCap * 2,
+                  "dynamic LDS layout");
+    __shared__ double2 outv_st[kDyn ? 1 : kW][H][kReg / 2];
+    __shared__ uint16_t queue_st[kDyn ? 1 : kW][kCap];  // survivors: q | lane << 4 | k << 10
+    extern __shared__ double2 fm_dyn_lds[];
+    double2 (*const outv)[H][kReg / 2] =
+        kDyn ? reinterpret_cast<double2 (*)[H][kReg / 2]>(fm_dyn_lds) : outv_st;
+    uint16_t (*const queue)[kCap] =
+        kDyn ? reinterpret_cast<uint16_t (*)[kCap]>(fm_dyn_lds + (size_t)kW * H * (kReg / 2)) : queue_st;
     __shared__ uint32_t wcnt[2][kW][H];                 // survivors of (wave, q) in the round
     __shared__ uint32_t ready[kW], done[kW];
     __shared__ HypConst hyp[H];
@@ -1084,8 +1104,20 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
             struct C4 { double a, b, c, d; };
             if (__ballot(ok) != 0) {
                 if constexpr (KIND >= 3) {
-                    run_band([&](int q) -> const double* { return hyp[q].g; },
-                             [&](const double* g) { return geo_band<KIND>(f0, f1, f2, f3, g, band0); });
+                    // correspondences: a rolled loop (the unrolled form holds
+                    // ~126 VGPRs; these kernels are held to 64, see above)
+#pragma unroll 1
+                    for (int q = 0; q < H; ++q) {
+                        if (!((vmask >> q) & 1ull)) continue;
+                        const bool cand = ok & geo_band<KIND>(f0, f1, f2, f3, hyp[q].g, band0);
+                        const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
+                        const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        if (cand) qw[qn + k] = (uint16_t)(q | (lane << 4) | (k << 10));
+                        const uint32_t c = (uint32_t)__builtin_popcountll(m);
+                        my_n = lane == q ? c : my_n;
+                        qn += c;
+                    }
                 } else if (cls == 0) {
                     run_band([&](int q) { return C4{hyp[q].h7, hyp[q].h8, hyp[q].lo, hyp[q].hi}; },
                              [&](const C4& c) {
@@ -1140,7 +1172,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_fm(DevProblem p, double
                 return sv;
             };
             // GCR_PROBE bit 6: no look-ahead (each batch fetched when used)
-            const bool ahead = !(gen.probe & 64u);
+            const bool ahead = KIND < 3 && !(gen.probe & 64u);     // (registers, see above)
             Surv cur{0.0, 0.0, 0.0, 0.0, 0u};
             if (ahead && qn > 0) cur = fetch(0);
             // the chain has folded this wave's previous runs (outv reuse)
@@ -2881,12 +2913,21 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
     if (split_h(nh) == 16 && use_fm()) {
         // the feature-major scorer with the division-free band prefilter:
         // h_band (transfer error) or f_band (Sampson distance)
+        constexpr size_t dyn = fm_dyn_lds_bytes<16, false>();
+        static const bool attr = [] {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_score_fm<3, 16, false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_score_fm<4, 16, false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+            return true;
+        }();
+        (void)attr;
         if (p.solver == 4) {
-            hipLaunchKernelGGL((k_score_fm<4, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), 0, stream, p,
+            hipLaunchKernelGGL((k_score_fm<4, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), dyn, stream, p,
                                T, 0.0, T * (1.0 + 1e-9), 0.0, models, inc, nh, out, ga);
         } else {
             const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;
-            hipLaunchKernelGGL((k_score_fm<3, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), 0, stream, p,
+            hipLaunchKernelGGL((k_score_fm<3, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), dyn, stream, p,
                                T, 0.0, sb * sb, 0.0, models, inc, nh, out, ga);
         }
     } else if (p.solver == 4) {
