@@ -888,15 +888,15 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     }
     static hipError_t verify_gen(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, const VBufs& b,
                                  hipStream_t s) {
-        hipError_t e = launch_generate_geo(P->dp, seed, s0, n, b.inc, b.models, s);
-        if (e != hipSuccess || b.hmap == nullptr) return e;
-        return launch_compact(b.inc, n * (uint32_t)per(P), b.hmap, b.hcount, s);
+        // multi-model slots are compacted by the scoring launch (verify_score)
+        return launch_generate_geo(P->dp, seed, s0, n, b.inc, b.models, s);
     }
     static hipError_t verify_score(gcr_problem* P, const double Tm[2], uint64_t s0, uint32_t n, const uint32_t m[2],
                                    BatchRecord* rec, hipEvent_t e0, hipEvent_t e1, const VBufs& b, hipStream_t s) {
         const uint32_t nh = n * (uint32_t)per(P);
         if (e0) (void)hipEventRecord(e0, s);
-        hipError_t e = launch_score_geo(P->dp, Tm[0], b.models, b.inc, nh, b.sb, s, b.hmap, b.hcount);
+        hipError_t e = launch_score_geo(P->dp, Tm[0], b.models, b.inc, nh, b.sb, s, b.hmap, b.hcount,
+                                        b.hmap != nullptr);
         if (e != hipSuccess) return e;
         if (e1) (void)hipEventRecord(e1, s);
         return launch_select_geo(P->solver, b.sb, b.inc, nh, s0, m[0], Tm[0], rec, s, b.hmap, b.hcount);

@@ -209,9 +209,12 @@ hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot
 // Hypotheses per workgroup of the batch scorers at a launch of nh (64, 16 or
 // 4; GCR_SPLIT_H pins one for sweeps).
 int split_h(uint32_t nh);
+// compact: inc covers all nh hypotheses and the launch compacts them itself
+// (hmap / hcount written: in the scorer's prologue, or by k_compact first)
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
                             const ScoreOut& out, hipStream_t stream, const uint32_t* hmap = nullptr,
-                            const uint32_t* hcount = nullptr);
+                            const uint32_t* hcount = nullptr,
+                            bool compact = false);
 hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule, double T, double lambda,
                            uint8_t* mask, hipStream_t stream);
 hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint64_t slot0,

@@ -361,6 +361,10 @@ struct GenArgs {
     // prologue's attempts (every slot takes attempt 0's default model)
     uint32_t probe;
     GenChain chain;                     // k_score_fm<.., true>: batch chaining
+    // k_score_fm, KIND >= 3: compact in the prologue instead of k_compact --
+    // every workgroup scans scan_inc[0 .. nh) (live: <= 101) and scores live
+    // ranks [blockIdx.x H, + H); hmap / hcount are then written, not read
+    bool scan;
 };
 
 template <int KIND, int H, int R, bool kGen>
@@ -922,10 +926,59 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     const int lane = t & 63;
     const bool chain_wave = wave == kFmWaves;
 
+    __shared__ uint32_t smap[KIND >= 3 ? H : 1];
     if constexpr (KIND >= 3) {
-        // compacted launches: hypotheses [0, *hcount) are models hmap[j]
-        if (gen.hcount != nullptr) nh = min(nh, *gen.hcount);
-        if (blockIdx.x * H >= nh) return;                // whole workgroup, before any barrier
+        if (gen.scan) {
+            // in-order compaction of the launch's live hypotheses (k_compact's
+            // result, computed by every workgroup): each thread counts a
+            // contiguous chunk, a block scan gives the chunk's first rank,
+            // and the chunks holding ranks [blockIdx.x H, + H) fill smap
+            __shared__ uint32_t wsum[kSplitThreads / 64];
+            __shared__ uint32_t tot_sh;
+            const int tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
+            const uint32_t per = (nh + kSplitThreads - 1) / kSplitThreads;
+            const uint32_t j0 = min(nh, tid * per), j1 = min(nh, j0 + per);
+            uint32_t c = 0;
+            for (uint32_t j = j0; j < j1; ++j) c += inc[j] <= 101 ? 1u : 0u;
+            uint32_t x = c;                                 // inclusive scan in the wave
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(x, d);
+                if (ln >= d) x += o;
+            }
+            if (ln == 63) wsum[wv] = x;
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t a = 0;
+                for (int w = 0; w < kSplitThreads / 64; ++w) {
+                    const uint32_t v = wsum[w];
+                    wsum[w] = a;
+                    a += v;
+                }
+                tot_sh = a;
+            }
+            __syncthreads();
+            const uint32_t lo = blockIdx.x * H;
+            uint32_t r = wsum[wv] + x - c;                  // rank of this chunk's first live entry
+            if (r < lo + H && r + c > lo)
+                for (uint32_t j = j0; j < j1; ++j)
+                    if (inc[j] <= 101) {
+                        if (r >= lo && r < lo + H) smap[r - lo] = j;
+                        ++r;
+                    }
+            __syncthreads();
+            const uint32_t total = tot_sh;
+            if (blockIdx.x == 0 && tid == 0) *const_cast<uint32_t*>(gen.hcount) = total;
+            if (tid < H && lo + tid < total) const_cast<uint32_t*>(gen.hmap)[lo + tid] = smap[tid];
+            nh = total;
+            if (lo >= nh) return;                           // whole workgroup
+        } else {
+            // compacted launches: hypotheses [0, *hcount) are models hmap[j]
+            if (gen.hcount != nullptr) nh = min(nh, *gen.hcount);
+            if (blockIdx.x * H >= nh) return;            // whole workgroup, before any barrier
+            if (threadIdx.x < H && gen.hmap != nullptr && blockIdx.x * H + threadIdx.x < nh)
+                smap[threadIdx.x] = gen.hmap[blockIdx.x * H + threadIdx.x];
+        }
     }
     GCR_STAMP(5, 15u);
     // ---- prologue: this workgroup's H slots (kGen), k_generate's rule, or
@@ -973,7 +1026,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     }
     if (t < H) {
         const uint32_t hg = blockIdx.x * H + t;
-        const uint32_t mi = (KIND >= 3 && gen.hmap != nullptr && hg < nh) ? gen.hmap[hg] : hg;
+        const uint32_t mi = (KIND >= 3 && gen.hmap != nullptr && hg < nh) ? smap[t] : hg;
         const bool v = hg < nh && (kGen ? gen_a[t] != 127 : (inc == nullptr || inc[mi] <= 101));
         typename ModelOf<KIND>::type m = ModelOf<KIND>::def();
         if (v) {
@@ -2893,11 +2946,22 @@ hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot
 }
 
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,
-                            const ScoreOut& out, hipStream_t stream, const uint32_t* hmap, const uint32_t* hcount) {
+                            const ScoreOut& out, hipStream_t stream, const uint32_t* hmap, const uint32_t* hcount,
+                            bool compact) {
     if (nh == 0) return hipSuccess;
     GenArgs ga{};
     ga.hmap = hmap;
     ga.hcount = hcount;
+    if (compact) {
+        if (hmap == nullptr || hcount == nullptr) return hipErrorInvalidValue;
+        if (split_h(nh) == 16 && use_fm()) {
+            ga.scan = true;                     // the feature-major scorer compacts in its prologue
+        } else {
+            const hipError_t e = launch_compact(inc, nh, const_cast<uint32_t*>(hmap), const_cast<uint32_t*>(hcount),
+                                                stream);
+            if (e != hipSuccess) return e;
+        }
+    }
     auto go = [&](auto ktag, auto htag, auto rtag) {
         constexpr int KIND = decltype(ktag)::value, H = decltype(htag)::value, R = decltype(rtag)::value;
         const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;     // h_band slack
