@@ -2819,6 +2819,15 @@ void launch_fused_t(const DevProblem& p, const double T[2], uint32_t nh, const S
 
 bool verify_chains(uint32_t nslots) { return split_h(nslots) == 16 && use_fm(); }
 
+// GCR_PROBE: timing-probe bits of the batch scorers (GenArgs::probe)
+uint32_t probe_bits() {
+    static const uint32_t v = [] {
+        const char* e = getenv("GCR_PROBE");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    return v;
+}
+
 hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t seed, uint64_t slot0,
                                uint32_t nslots, const uint32_t m[2], uint8_t* inc, RectModel* models,
                                const ScoreOut& out, WgBest* wg, size_t wg_cap, BatchRecord* rec,
@@ -2836,11 +2845,7 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
         const char* e = getenv("GCR_GEN_LANES");
         return e ? (uint32_t)atoi(e) : 0u;
     }();
-    static const uint32_t probe = [] {
-        const char* e = getenv("GCR_PROBE");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    g.probe = probe;
+    g.probe = probe_bits();
     // default 16 lanes per slot (one wave per SIMD at H = 16): 16 parallel
     // attempts resolve nearly every slot in one round, and fewer contending
     // waves finish it sooner (sweep at 4096 slots: 64 -> 16 lanes, 142 ->
@@ -2952,6 +2957,7 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
     GenArgs ga{};
     ga.hmap = hmap;
     ga.hcount = hcount;
+    ga.probe = probe_bits();
     if (compact) {
         if (hmap == nullptr || hcount == nullptr) return hipErrorInvalidValue;
         if (split_h(nh) == 16 && use_fm()) {
