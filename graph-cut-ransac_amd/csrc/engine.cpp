@@ -729,6 +729,19 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     for (int c = 0; c < 2; ++c) {
         DevClass& d = P->dp.cls[c];
         d.n = (uint32_t)ns[c];
+        {
+            const std::vector<double>* ax[4] = {&P->hc[c].x, &P->hc[c].y, &P->hc[c].a, &P->hc[c].c0};
+            for (int q = 0; q < 4; ++q) {
+                double mx = 0.0;
+                bool bad = false;                       // a NaN or infinity anywhere
+                for (size_t i = 0; i < ns[c] && i < ax[q]->size(); ++i) {
+                    const double v = std::fabs((*ax[q])[i]);
+                    if (!(v < HUGE_VAL)) bad = true;
+                    else if (v > mx) mx = v;
+                }
+                d.amax[q] = bad ? HUGE_VAL : mx;
+            }
+        }
         if (ns[c] == 0) { d.x = d.y = d.a = d.c0 = d.c1 = nullptr; continue; }
         const std::vector<double>* arrs[5] = {&P->hc[c].x, &P->hc[c].y, &P->hc[c].a, &P->hc[c].c0, &P->hc[c].c1};
         const double** dst[5] = {&d.x, &d.y, &d.a, &d.c0, &d.c1};

@@ -20,6 +20,9 @@ struct DevClass {
     const double* c0;
     const double* c1;
     uint32_t n;
+    // max |x|, |y|, |a|, |c0| over the class (+inf if any is not finite):
+    // the error bounds of the fundamental matrix's fp32 pre-band
+    double amax[4];
 };
 
 // model type per estimator: rectification solvers 0-2, homography 3

@@ -885,6 +885,79 @@ constexpr size_t fm_dyn_lds_bytes() {
     return (size_t)kW * H * 66 * sizeof(double) + (size_t)kW * 64 * H * sizeof(uint16_t);
 }
 
+// Fundamental matrix: a conservative packed-fp32 pre-band on the Sampson
+// error, two hypotheses per instruction (v_pk_fma_f32).  With inputs rounded
+// to fp32 and every fma rounding counted, each of fx0, fx1, fx2 (F x1) and
+// ft0, ft1 (F^T x2) is within e = 1e-6 (|h| . |coords|max) of its real value
+// (>= 4 u of slack per term, u = 2^-24), num within sn (the same bound carried
+// through num = x2 fx0 + y2 fx1 + fx2), and den <= sum (|f| + e)^2.  A pair is
+// rejected only if (|num| - sn)^2 > T (1 + 4e-6) den_up, i.e. only if even the
+// smallest num and the largest den the bounds allow give r^2 > T; the margin
+// also covers the fp64 rounding of the exact residual.  NaN, overflow or
+// unbounded coordinates (amax = inf) never reject.  Survivors get the exact
+// f_sq_sampson in the exact pass, so the result is unchanged.
+typedef float fpb_f2 __attribute__((ext_vector_type(2)));
+struct FPairBand {                 // hypotheses 2 j (.x) and 2 j + 1 (.y)
+    fpb_f2 g[9];
+    fpb_f2 e[5];                   // error bounds of fx0, fx1, fx2, ft0, ft1
+    fpb_f2 sn;                     // error bound of num
+    fpb_f2 tq;                     // T (1 + 4e-6), rounded up
+};
+
+__device__ __forceinline__ float fpb_up(double v) {
+    // a float >= v (v >= 0); +inf past 1e30 or when not finite
+    return (v < 1e30) ? (float)(v * (1.0 + 1e-6)) + 1e-30f : __builtin_inff();
+}
+
+__device__ __forceinline__ void fpb_setup(FPairBand* fp, int t, const double* h, bool valid, double T,
+                                          const DevClass& c) {
+    const double X1 = c.amax[0], Y1 = c.amax[1], X2 = c.amax[2], Y2 = c.amax[3];
+    double a[9];
+    for (int k = 0; k < 9; ++k) a[k] = __builtin_fabs(h[k]);
+    const double F0 = (a[0] * X1 + a[1] * Y1) + a[2];
+    const double F1 = (a[3] * X1 + a[4] * Y1) + a[5];
+    const double F2 = (a[6] * X1 + a[7] * Y1) + a[8];
+    const double G0 = (a[0] * X2 + a[3] * Y2) + a[6];
+    const double G1 = (a[1] * X2 + a[4] * Y2) + a[7];
+    constexpr double gam = 1e-6;
+    const double e0 = gam * F0, e1 = gam * F1, e2 = gam * F2, e3 = gam * G0, e4 = gam * G1;
+    const double sn = ((X2 * e0 + Y2 * e1) + e2) + gam * ((X2 * (F0 + e0) + Y2 * (F1 + e1)) + (F2 + e2));
+    // each thread writes its own 4-byte half of the pair's vectors (no
+    // read-modify-write of the 8-byte element its neighbour also writes)
+    float* b = reinterpret_cast<float*>(&fp[t >> 1]);
+    const int hf = t & 1;
+    for (int k = 0; k < 9; ++k) b[2 * k + hf] = valid ? (float)h[k] : 0.0f;
+    const double ev[5] = {e0, e1, e2, e3, e4};
+    for (int k = 0; k < 5; ++k) b[2 * (9 + k) + hf] = fpb_up(ev[k]);
+    // an invalid hypothesis is never scored (vmask); keep its constants inert
+    b[2 * 14 + hf] = valid ? fpb_up(sn) : __builtin_inff();
+    b[2 * 15 + hf] = fpb_up(T * (1.0 + 4e-6));
+}
+static_assert(sizeof(FPairBand) == 16 * 8, "FPairBand layout: 16 float pairs");
+
+// reject bits of the pair (.x: hypothesis 2 j, .y: 2 j + 1)
+__device__ __forceinline__ fpb_f2 fpb_fma(fpb_f2 a, fpb_f2 b, fpb_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ void fpb_test(const FPairBand& b, float x1, float y1, float x2, float y2, bool& r0,
+                                         bool& r1) {
+    const fpb_f2 X1 = {x1, x1}, Y1 = {y1, y1}, X2 = {x2, x2}, Y2 = {y2, y2};
+    const fpb_f2 fx0 = fpb_fma(b.g[0], X1, fpb_fma(b.g[1], Y1, b.g[2]));
+    const fpb_f2 fx1 = fpb_fma(b.g[3], X1, fpb_fma(b.g[4], Y1, b.g[5]));
+    const fpb_f2 fx2 = fpb_fma(b.g[6], X1, fpb_fma(b.g[7], Y1, b.g[8]));
+    const fpb_f2 ft0 = fpb_fma(b.g[0], X2, fpb_fma(b.g[3], Y2, b.g[6]));
+    const fpb_f2 ft1 = fpb_fma(b.g[1], X2, fpb_fma(b.g[4], Y2, b.g[7]));
+    const fpb_f2 num = fpb_fma(X2, fx0, fpb_fma(Y2, fx1, fx2));
+    const fpb_f2 d0 = __builtin_elementwise_abs(fx0) + b.e[0];
+    const fpb_f2 d1 = __builtin_elementwise_abs(fx1) + b.e[1];
+    const fpb_f2 d2 = __builtin_elementwise_abs(ft0) + b.e[3];
+    const fpb_f2 d3 = __builtin_elementwise_abs(ft1) + b.e[4];
+    const fpb_f2 den = fpb_fma(d3, d3, fpb_fma(d2, d2, fpb_fma(d1, d1, d0 * d0)));
+    (void)b.e[2];                  // fx2's bound enters through sn only
+    const fpb_f2 a = __builtin_elementwise_abs(num) - b.sn;
+    const fpb_f2 lhs = a * a, rhs = b.tq * den;
+    r0 = a.x > 0.0f && lhs.x > rhs.x;
+    r1 = a.y > 0.0f && lhs.y > rhs.y;
+}
+
 template <int KIND, int H, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(KIND >= 3 ? 8 : 1))) void k_score_fm(DevProblem p, double T0, double T1, double band0,
                                                             double tan_tau1,
@@ -917,6 +990,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     __shared__ HypConst hyp[H];
     __shared__ uint32_t hval[H];
     __shared__ uint32_t cnt_sh[2][H];
+    __shared__ FPairBand fpb[KIND == 4 ? (H + 1) / 2 : 1];
     __shared__ int gen_a[kGen ? H : 1];
     __shared__ RectModel gen_m[kGen ? H : 1];
     __shared__ double fin_sh[kGen ? H : 1];
@@ -1034,9 +1108,13 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             else m = models[mi];
         }
         hyp[t] = make_hyp<KIND>(m, band0);
+        if constexpr (KIND == 4) fpb_setup(fpb, t, m.h, v, T0, p.cls[0]);
         hval[t] = v ? 1u : 0u;
         cnt_sh[0][t] = 0;
         cnt_sh[1][t] = 0;
+    }
+    if constexpr (KIND == 4) {
+        if ((H & 1) && t == H) fpb_setup(fpb, t, hyp[0].g, false, T0, p.cls[0]);   // odd H: inert pad
     }
     GCR_STAMP(6, 15u);
     if (t < kW) { ready[t] = 0; done[t] = 0; }
@@ -1156,7 +1234,30 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             };
             struct C4 { double a, b, c, d; };
             if (__ballot(ok) != 0) {
-                if constexpr (KIND >= 3) {
+                if constexpr (KIND == 4) {
+                    // fundamental matrix: the packed fp32 pre-band (above), two
+                    // hypotheses per pass; survivors go to the exact pass
+                    const float x1 = (float)f0, y1 = (float)f1, x2 = (float)f2, y2 = (float)f3;
+#pragma unroll 1
+                    for (int q = 0; q < H; q += 2) {
+                        if (!((vmask >> q) & 3ull)) continue;
+                        bool rj[2];
+                        fpb_test(fpb[q >> 1], x1, y1, x2, y2, rj[0], rj[1]);
+#pragma unroll
+                        for (int o = 0; o < 2; ++o) {
+                            const int qq = q + o;
+                            if (qq >= H || !((vmask >> qq) & 1ull)) continue;
+                            const bool cand = ok & !rj[o];
+                            const uint64_t m = __builtin_amdgcn_ballot_w64(cand);
+                            const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                            if (cand) qw[qn + k] = (uint16_t)(qq | (lane << 4) | (k << 10));
+                            const uint32_t c = (uint32_t)__builtin_popcountll(m);
+                            my_n = lane == qq ? c : my_n;
+                            qn += c;
+                        }
+                    }
+                } else if constexpr (KIND == 3) {
                     // correspondences: a rolled loop (the unrolled form holds
                     // ~126 VGPRs; these kernels are held to 64, see above)
 #pragma unroll 1

@@ -2,8 +2,10 @@
 
 k_score_fm (graph-cut-ransac_amd/csrc/kernels.hip) rejects a (hypothesis,
 correspondence) pair before its exact residual when h_band (homography,
-|e|^2 > Tb w^2) or f_band (fundamental, num^2 > Tb den) says it cannot be an
-inlier.  A band that drops one pair the exact residual accepts changes the
+|e|^2 > Tb w^2) or the packed fp32 Sampson pre-band (fundamental,
+(|num| - sn)^2 > T' den_up with error bounds from the problem's largest
+coordinates; the split scorers use f_band, num^2 > Tb den) says it cannot be
+an inlier.  A band that drops one pair the exact residual accepts changes the
 count and the MSAC sum.  These tests place correspondences within one ulp of
 the threshold on both sides (bisection on the displacement, evaluated with
 the device's own operation order: Python floats are IEEE doubles without FMA
@@ -42,15 +44,16 @@ def _h_r2(h, x1, y1, x2, y2):
     return du * du + dv * dv
 
 
-def _boundary_corr(solver, models, T, rng, per=80):
+def _boundary_corr(solver, models, T, rng, per=80, span=1200.0):
     """Per model, `per` pairs of correspondences straddling r^2 = T: the last
-    displacement of a bisection with r^2 <= T and the first with r^2 > T."""
+    displacement of a bisection with r^2 <= T and the first with r^2 > T.
+    Points x1 are drawn in [0, span)^2."""
     r2f = _f_r2 if solver == N.SOLVER_FUNDAMENTAL7 else _h_r2
     out = []
     for h in models:
         h = [float(v) for v in h]
         for _ in range(per):
-            x1, y1 = (float(v) for v in rng.uniform(0, 1200, size=2))
+            x1, y1 = (float(v) for v in rng.uniform(0, span, size=2))
             if solver == N.SOLVER_FUNDAMENTAL7:
                 # foot of a random point on the epipolar line, moved along its normal
                 a = (h[0] * x1 + h[1] * y1) + h[2]
@@ -59,7 +62,7 @@ def _boundary_corr(solver, models, T, rng, per=80):
                 nrm = math.hypot(a, b)
                 if nrm == 0.0:
                     continue
-                qx, qy = (float(v) for v in rng.uniform(0, 1200, size=2))
+                qx, qy = (float(v) for v in rng.uniform(0, span, size=2))
                 d = (a * qx + b * qy + c) / nrm
                 px, py = qx - d * a / nrm, qy - d * b / nrm
                 dx, dy = a / nrm, b / nrm
@@ -142,3 +145,30 @@ def test_band_prefilter_is_conservative_at_the_threshold(gpu, solver):
             cnt, val = _finish(n0[i], v0[i], tot[i], thr, mmin)
             assert cnt == ref["count"], (nh, i)
             assert bits(val) == bits(ref["value"]), (nh, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("span", [20_000.0, 200_000.0])
+def test_fundamental_fp32_preband_is_conservative_at_large_coordinates(gpu, span):
+    # the F scorer's packed fp32 pre-band carries error bounds scaled by the
+    # problem's largest coordinates: correspondences one ulp either side of
+    # the Sampson threshold far from the origin still score as the oracle
+    rng = np.random.default_rng(int(span))
+    thr = 0.75
+    T = (2.25 * thr) * thr
+    corr, _, _, _ = S.problem_f(800, 0.3, seed=43)
+    gen = CorrProblem(N.SOLVER_FUNDAMENTAL7, corr)
+    inc, ms = gen.generate(5, 0, 64)
+    models = ms[inc <= 101][:10]
+    bc = _boundary_corr(N.SOLVER_FUNDAMENTAL7, models, T, rng, per=60, span=span)
+    prob = CorrProblem(N.SOLVER_FUNDAMENTAL7, bc)
+    refs = [O.f_score(bc, m, thr) for m in models]
+    assert min(r["count"] for r in refs) >= 60
+    for nh in (2048, 11136):                              # the feature-major scorer
+        tiled = np.resize(models, (nh, 9))
+        n0, v0, tot = prob.score(tiled, thr)
+        for i in range(nh):
+            ref = refs[i % len(models)]
+            cnt, val = _finish(n0[i], v0[i], tot[i], thr, 7)
+            assert cnt == ref["count"], (span, nh, i)
+            assert bits(val) == bits(ref["value"]), (span, nh, i)
