@@ -73,6 +73,55 @@ GCR_HD double cubic_root_in(double a, double b, double c, double lo, double hi, 
     return rts;
 }
 
+// cubic_root_in as a branch-free state machine, so the three brackets of a
+// cubic run their iterations side by side (three independent dependency
+// chains per lane instead of one after another).  Every chain performs
+// exactly cubic_root_in's operations in its order; a step of a finished chain
+// is a no-op, so the roots are bit-identical to three sequential calls.
+struct RtSafe {
+    double xl, xh, rts, dxold, dx, f, df;
+    bool on;
+};
+
+GCR_HD RtSafe rtsafe_init(double a, double b, double c, double lo, double hi, double flo, bool on) {
+    RtSafe s;
+    const bool neg = flo < 0.0;
+    s.xl = neg ? lo : hi;
+    s.xh = neg ? hi : lo;
+    s.rts = 0.5 * (lo + hi);
+    s.dxold = __builtin_fabs(hi - lo);
+    s.dx = s.dxold;
+    s.f = cubic_monic(a, b, c, s.rts);
+    s.df = cubic_monic_d(a, b, s.rts);
+    s.on = on;
+    return s;
+}
+
+GCR_HD void rtsafe_step(RtSafe& s, double a, double b, double c) {
+    const bool run = s.on && !(s.f == 0.0);
+    const bool bis = (((s.rts - s.xh) * s.df - s.f) * ((s.rts - s.xl) * s.df - s.f) > 0.0) ||
+                     (__builtin_fabs(2.0 * s.f) > __builtin_fabs(s.dxold * s.df));
+    const double bdx = 0.5 * (s.xh - s.xl);
+    const double brts = s.xl + bdx;
+    const double ndx = s.f / s.df;
+    const double nrts = s.rts - ndx;
+    const double dx = bis ? bdx : ndx;
+    const double rts = bis ? brts : nrts;
+    const bool same = bis ? (s.xl == rts) : (s.rts == rts);
+    const bool cont = run && !same && !(__builtin_fabs(dx) < 1e-14 * (1.0 + __builtin_fabs(rts)));
+    const double f = cubic_monic(a, b, c, rts);
+    const double df = cubic_monic_d(a, b, rts);
+    s.dxold = run ? s.dx : s.dxold;
+    s.dx = run ? dx : s.dx;
+    s.rts = run ? rts : s.rts;
+    s.f = cont ? f : s.f;
+    s.df = cont ? df : s.df;
+    const bool lo_side = f < 0.0;
+    s.xl = (cont && lo_side) ? rts : s.xl;
+    s.xh = (cont && !lo_side) ? rts : s.xh;
+    s.on = cont;
+}
+
 // Real roots of c3 l^3 + c2 l^2 + c1 l + c0 in ascending order (basic ops +
 // sqrt only): brackets between the derivative's critical points and the
 // Cauchy bound, one safeguarded-Newton root per sign change.  Returns the
@@ -122,22 +171,34 @@ GCR_HD int real_roots_cubic(double c3, double c2, double c1, double c0, double& 
         o2 = n >= 2 ? v : o2;
         ++n;
     };
+    // the three brackets [-R, e1], [e1, e2], [e2, R] (the last two only with
+    // critical points): their safeguarded-Newton roots side by side, then the
+    // sequential bookkeeping (an exact zero at a bracket end is pushed once)
+    const double f0 = cubic_monic(a, b, c, -R), f1 = cubic_monic(a, b, c, e1);
+    const double f2 = cubic_monic(a, b, c, e2), f3 = cubic_monic(a, b, c, R);
+    auto newton = [](double flo, double fhi) { return !(flo == 0.0) && ((flo < 0.0) != (fhi < 0.0)) && !(fhi == 0.0); };
+    RtSafe s0 = rtsafe_init(a, b, c, -R, e1, f0, newton(f0, f1));
+    RtSafe s1 = rtsafe_init(a, b, c, e1, e2, f1, crit && newton(f1, f2));
+    RtSafe s2 = rtsafe_init(a, b, c, e2, R, f2, crit && newton(f2, f3));
+    for (int it = 0; it < 100 && (s0.on || s1.on || s2.on); ++it) {
+        rtsafe_step(s0, a, b, c);
+        rtsafe_step(s1, a, b, c);
+        rtsafe_step(s2, a, b, c);
+    }
     double prev = 0.0;
-    auto bracket = [&](double lo, double hi) {
-        const double flo = cubic_monic(a, b, c, lo);
-        const double fhi = cubic_monic(a, b, c, hi);
+    auto bracket = [&](double lo, double flo, double fhi, double root) {
         if (flo == 0.0) {
             if (n == 0 || prev != lo) { push(lo); prev = lo; }
             return;
         }
         if (!((flo < 0.0) != (fhi < 0.0)) || fhi == 0.0) return;
-        prev = cubic_root_in(a, b, c, lo, hi, flo);
+        prev = root;
         push(prev);
     };
-    bracket(-R, e1);
+    bracket(-R, f0, f1, s0.rts);
     if (crit) {
-        bracket(e1, e2);
-        bracket(e2, R);
+        bracket(e1, f1, f2, s1.rts);
+        bracket(e2, f2, f3, s2.rts);
     }
     r0 = o0;
     r1 = o1;
@@ -187,9 +248,11 @@ GCR_HD bool denormalize_f(const double* fn, double s1, double cx1, double cy1, d
     double nn = 0.0;
     for (int k = 0; k < 9; ++k) nn += f[k] * f[k];
     const double nrm = sqrt(nn);
-    if (!(nrm > 0.0) || !(nrm < 1e300)) return false;
-    for (int k = 0; k < 9; ++k) f[k] = f[k] / nrm;
-    return true;
+    // branch-free: a failed norm divides by 1.0, which leaves f exactly as is
+    const bool ok = (nrm > 0.0) & (nrm < 1e300);
+    const double d = ok ? nrm : 1.0;
+    for (int k = 0; k < 9; ++k) f[k] = f[k] / d;
+    return ok;
 }
 
 // Oriented epipolar constraint (Chum, Werner, Matas 2004): with e2 the
@@ -210,7 +273,7 @@ GCR_HD bool oriented_ok(const double* f, const double* x1, const double* y1, con
         const double nn = (w0 * w0 + w1 * w1) + w2 * w2;
         if (nn > best) { best = nn; e[0] = w0; e[1] = w1; e[2] = w2; }
     }
-    if (!(best > 0.0)) return false;
+    const bool epi = best > 0.0;   // tested last: the sign loop stays branch-free
     int pos = 0, neg = 0;
     for (int i = 0; i < N; ++i) {
         const double fx0 = (f[0] * x1[i] + f[1] * y1[i]) + f[2];
@@ -224,7 +287,7 @@ GCR_HD bool oriented_ok(const double* f, const double* x1, const double* y1, con
         pos += sgn > 0.0;
         neg += sgn < 0.0;
     }
-    return pos == N || neg == N;
+    return epi & ((pos == N) | (neg == N));
 }
 
 // The 7-point solver's intermediate state: normalisation, the null-space
@@ -321,15 +384,17 @@ GCR_HD int solve_f7_basis(const double x1[7], const double y1[7], const double x
     out.root0 = q0;
     out.root1 = q1;
     out.root2 = q2;
+    // all three roots tested without branches (absent roots give inert
+    // models), so their denormalisations and orientation tests overlap
     int n = 0;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-        if (q >= nr) break;
         double fm[9];
-        if (!f7_model(out, f7_root(out, q), fm)) continue;
-        if (!oriented_ok<7>(fm, x1, y1, x2, y2)) continue;
-        out.valid |= 1u << q;
-        ++n;
+        const bool den = f7_model(out, f7_root(out, q), fm);
+        const bool ori = oriented_ok<7>(fm, x1, y1, x2, y2);
+        const bool v = (q < nr) & den & ori;
+        out.valid |= v ? 1u << q : 0u;
+        n += v;
     }
     return n;
 }

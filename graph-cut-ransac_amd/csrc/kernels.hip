@@ -202,6 +202,93 @@ __global__ __launch_bounds__(kGenBlock) void k_generate_f(DevProblem p, uint64_t
     }
 }
 
+// k_generate_f with widening groups.  A wave starts with S = 64 / G slots of
+// G lanes each.  After every round the lanes of finished slots go to the
+// unfinished ones: with k slots left, each gets 64 / pow2ceil(k) lanes.  All
+// unfinished slots of a wave advance by the same width each round, so one
+// wave-uniform counter holds every such slot's lowest untried attempt; each
+// round tries a contiguous range from it and keeps the range's lowest
+// success, so a slot's result is the sequential retry loop's first success,
+// as with fixed groups.  The rare slot that needs many attempts (7.7 on
+// average at 80 % outliers, p99 35) then gets the lanes its finished
+// neighbours no longer use, instead of holding the launch for many rounds of
+// G lanes.
+template <int G>
+__global__ __launch_bounds__(kGenBlock) void k_generate_fw(DevProblem p, uint64_t seed, uint64_t slot0,
+                                                           uint32_t nslots, uint8_t* __restrict__ inc,
+                                                           GeoModel* __restrict__ models) {
+    constexpr int S = 64 / G;
+    static_assert(S >= 1 && S * G == 64, "slots per wave");
+    const int lane = threadIdx.x & 63;
+    const uint32_t s0 = (blockIdx.x * kGenBlock + (threadIdx.x & ~63u)) / G;   // the wave's first slot
+    const uint32_t live = s0 < nslots ? nslots - s0 : 0;
+    uint64_t pend = live >= (uint32_t)S ? (S == 64 ? ~0ull : (1ull << S) - 1ull) : (1ull << live) - 1ull;
+    uint32_t nx = 0;                    // wave-uniform: lowest untried attempt of every unfinished slot
+    while (pend) {
+        const int k = __builtin_popcountll(pend);
+        const int lw = 6 - (k == 1 ? 0 : 32 - __builtin_clz((uint32_t)(k - 1)));   // log2 of lanes per slot
+        const int j = lane >> lw;
+        const uint32_t a = nx + (uint32_t)(lane & ((1 << lw) - 1));
+        int si = -1;                    // this lane's slot: the j-th unfinished one
+        {
+            uint64_t m = pend;
+            for (int c = 0; m; ++c) {
+                const int i = __builtin_ctzll(m);
+                m &= m - 1;
+                si = c == j ? i : si;
+            }
+        }
+        F7Basis b;
+        const int cnt = (si >= 0 && a < 101) ? attempt_f(p, seed, slot0 + s0 + (uint32_t)si, a, b) : 0;
+        const uint64_t mask = __ballot(cnt > 0);
+        nx += 1u << lw;
+        const bool out_of_attempts = nx >= 101;
+        uint64_t np = out_of_attempts ? 0ull : pend;
+        bool win = false;
+        {
+            uint64_t m = pend;
+            for (int c = 0; m; ++c) {
+                const int i = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint64_t grp = lw == 6 ? mask : (mask >> (c << lw)) & ((1ull << (1 << lw)) - 1ull);
+                if (grp) {
+                    np &= ~(1ull << i);
+                    win |= lane == (c << lw) + __builtin_ctzll(grp);
+                }
+            }
+        }
+        // slots with no success and no attempts left report failure (lane 0
+        // of their group)
+        const bool fail = out_of_attempts && si >= 0 && !((mask >> (j << lw)) & ((lw == 6) ? ~0ull : ((1ull << (1 << lw)) - 1ull))) &&
+                          (lane & ((1 << lw) - 1)) == 0;
+        pend = np;
+        const uint32_t s = s0 + (uint32_t)si;   // the winner's / failure writer's own slot
+        if (win) {
+            GeoModel* out = models + (size_t)kFModels * s;
+            uint8_t* oi = inc + (size_t)kFModels * s;
+            int m = 0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (b.valid & (1u << q)) {
+                    double fm[9];
+                    f7_model(b, f7_root(b, q), fm);
+                    for (int t = 0; t < 9; ++t) out[m].h[t] = fm[t];
+                    ++m;
+                }
+            for (int q = m; q < kFModels; ++q) out[q] = default_geo();
+            oi[0] = (uint8_t)(a + 1);
+            oi[1] = cnt > 1 ? 0 : 255;
+            oi[2] = cnt > 2 ? 0 : 255;
+        } else if (fail) {
+#pragma unroll
+            for (int q = 0; q < kFModels; ++q) {
+                models[(size_t)kFModels * s + q] = default_geo();
+                inc[(size_t)kFModels * s + q] = q == 0 ? 102 : 255;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- score ----
 template <int KIND, bool kIdentity>
 __global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, double T1,
@@ -3020,23 +3107,36 @@ hipError_t launch_math(int op, const double* a, const double* b, size_t n, doubl
 hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot0, uint32_t nslots, uint8_t* inc,
                                GeoModel* models, hipStream_t stream) {
     if (nslots == 0) return hipSuccess;
+    // GCR_GEN_WIDEN=0: the fundamental-matrix generator keeps fixed groups of
+    // G lanes per slot (k_generate_f) instead of widening them (k_generate_fw).
+    // Both knobs are read per launch (tests switch them in-process).
+    const char* ew = getenv("GCR_GEN_WIDEN");
+    const bool widen = !(ew && ew[0] == '0');
     auto go = [&](auto gtag) {
         constexpr int G = decltype(gtag)::value;
         const dim3 grid(blocks_for((size_t)nslots * G, kGenBlock)), block(kGenBlock);
-        if (p.solver == 4)
+        if (p.solver == 4) {
+            if constexpr (G >= 1) {
+                if (widen) {
+                    hipLaunchKernelGGL((k_generate_fw<G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+                    return;
+                }
+            }
             hipLaunchKernelGGL((k_generate_f<G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
-        else
+        } else {
             hipLaunchKernelGGL((k_generate<3, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+        }
     };
     // GCR_GEN_G overrides the lanes per slot (1 .. 64)
-    static const int env_g = [] {
-        const char* e = getenv("GCR_GEN_G");
-        return e ? atoi(e) : 0;
-    }();
+    const char* eg = getenv("GCR_GEN_G");
+    const int env_g = eg ? atoi(eg) : 0;
     // 7-point solver: ~7.7 attempts per slot at 80 % outliers (p99 35), latency-
-    // bound per attempt -> a half wave per slot (measured: G = 8 / 16 / 32 / 64
-    // -> 0.46 / 0.37 / 0.34 / 0.36 ms per 4096-slot step)
-    int g = p.solver == 4 ? (nslots <= 8192 ? 32 : nslots <= 32768 ? 8 : 2)
+    // bound per attempt.  Fixed groups (round 1): G = 8 / 16 / 32 / 64 -> 0.46 /
+    // 0.37 / 0.34 / 0.36 ms per 4096-slot step.  Widening groups (F bench line,
+    // 3712 slots, two-stream pipeline, profiles/r2_v8_fwiden.txt): G = 4 / 8 /
+    // 16 / 32 / 64 -> 0.173 / 0.143 / 0.126 / 0.139 / 0.159 ms per step, fixed
+    // G = 32 0.138 ms
+    int g = p.solver == 4 ? (nslots <= 8192 ? 16 : nslots <= 32768 ? 8 : 2)
                           : (nslots <= 8192 ? 16 : nslots <= 32768 ? 4 : 1);
     if (env_g == 1 || env_g == 2 || env_g == 4 || env_g == 8 || env_g == 16 || env_g == 32 || env_g == 64) g = env_g;
     switch (g) {

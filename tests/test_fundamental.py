@@ -141,6 +141,42 @@ def test_generate_matches_oracle_slots(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("g,widen", [(1, "1"), (2, "1"), (4, "1"), (8, "1"), (16, "1"), (32, "1"), (64, "1"), (32, "0"), (2, "0")])
+def test_generate_group_widening_matches_oracle_slots(gpu, g, widen, monkeypatch):
+    """k_generate_fw hands finished slots' lanes to unfinished ones; at 80 %
+    outliers (7.7 attempts per slot on average, some past 64) every slot must
+    still report the sequential loop's first success, for every starting
+    group size, and the fixed-group kernel (GCR_GEN_WIDEN=0) the same.
+    499 slots: a ragged last wave."""
+    monkeypatch.setenv("GCR_GEN_G", str(g))
+    monkeypatch.setenv("GCR_GEN_WIDEN", widen)
+    corr, _, _, _ = S.problem_f(700, 0.8, seed=24)
+    prob = CorrProblem(N.SOLVER_FUNDAMENTAL7, corr)
+    inc, F = prob.generate(77, 9000, 499)
+    late = 0
+    for s in range(499):
+        oinc, oms = O.f_slot(corr, 77, 9000 + s)
+        assert int(inc[s, 0]) == oinc, (s, int(inc[s, 0]), oinc)
+        late += oinc > 33
+        if oinc > 101:
+            assert inc[s, 1] == 255 and inc[s, 2] == 255
+            continue
+        k = len(oms)
+        assert [int(v) for v in inc[s, 1:]] == [0 if q < k else 255 for q in (1, 2)], s
+        assert np.array_equal(bits(F[s, :k]), bits(oms)), s
+    assert late > 0                # some slots needed a widened second round
+    # every attempt fails (all points on one line: rank-deficient 7 x 9
+    # systems): every slot reports 102, written once by its group
+    t = np.linspace(0.0, 500.0, 60)
+    flat = np.column_stack([t, 2.0 * t + 1.0, t + 3.0, 0.5 * t])
+    pf = CorrProblem(N.SOLVER_FUNDAMENTAL7, flat)
+    inc, _ = pf.generate(5, 0, 131)
+    for s in range(131):
+        oinc, _ = O.f_slot(flat, 5, s)
+        assert oinc == 102 and int(inc[s, 0]) == 102 and inc[s, 1] == 255 and inc[s, 2] == 255, s
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nh", [100, 2048, 16384, "small"])
 def test_score_matches_oracle_bitwise(gpu, nh, monkeypatch):
     if nh == "small":              # launch_score_small (LO trials, refits)
