@@ -213,10 +213,10 @@ __global__ __launch_bounds__(kGenBlock) void k_generate_f(DevProblem p, uint64_t
 // average at 80 % outliers, p99 35) then gets the lanes its finished
 // neighbours no longer use, instead of holding the launch for many rounds of
 // G lanes.
-template <int G>
+template <int KIND, int G>
 __global__ __launch_bounds__(kGenBlock) void k_generate_fw(DevProblem p, uint64_t seed, uint64_t slot0,
                                                            uint32_t nslots, uint8_t* __restrict__ inc,
-                                                           GeoModel* __restrict__ models) {
+                                                           typename ModelOf<KIND>::type* __restrict__ models) {
     constexpr int S = 64 / G;
     static_assert(S >= 1 && S * G == 64, "slots per wave");
     const int lane = threadIdx.x & 63;
@@ -238,8 +238,15 @@ __global__ __launch_bounds__(kGenBlock) void k_generate_fw(DevProblem p, uint64_
                 si = c == j ? i : si;
             }
         }
-        F7Basis b;
-        const int cnt = (si >= 0 && a < 101) ? attempt_f(p, seed, slot0 + s0 + (uint32_t)si, a, b) : 0;
+        // KIND 4: the 7-point basis (0..3 models); otherwise one model
+        std::conditional_t<KIND == 4, F7Basis, typename ModelOf<KIND>::type> b;
+        int cnt = 0;
+        if constexpr (KIND == 4) {
+            cnt = (si >= 0 && a < 101) ? attempt_f(p, seed, slot0 + s0 + (uint32_t)si, a, b) : 0;
+        } else {
+            b = ModelOf<KIND>::def();
+            cnt = (si >= 0 && a < 101 && attempt<KIND>(p, seed, slot0 + s0 + (uint32_t)si, a, b)) ? 1 : 0;
+        }
         const uint64_t mask = __ballot(cnt > 0);
         nx += 1u << lw;
         const bool out_of_attempts = nx >= 101;
@@ -264,6 +271,7 @@ __global__ __launch_bounds__(kGenBlock) void k_generate_fw(DevProblem p, uint64_
         pend = np;
         const uint32_t s = s0 + (uint32_t)si;   // the winner's / failure writer's own slot
         if (win) {
+          if constexpr (KIND == 4) {
             GeoModel* out = models + (size_t)kFModels * s;
             uint8_t* oi = inc + (size_t)kFModels * s;
             int m = 0;
@@ -279,11 +287,16 @@ __global__ __launch_bounds__(kGenBlock) void k_generate_fw(DevProblem p, uint64_
             oi[0] = (uint8_t)(a + 1);
             oi[1] = cnt > 1 ? 0 : 255;
             oi[2] = cnt > 2 ? 0 : 255;
+          } else {
+            models[s] = b;
+            inc[s] = (uint8_t)(a + 1);
+          }
         } else if (fail) {
+            constexpr int kM = KIND == 4 ? kFModels : 1;
 #pragma unroll
-            for (int q = 0; q < kFModels; ++q) {
-                models[(size_t)kFModels * s + q] = default_geo();
-                inc[(size_t)kFModels * s + q] = q == 0 ? 102 : 255;
+            for (int q = 0; q < kM; ++q) {
+                models[(size_t)kM * s + q] = ModelOf<KIND>::def();
+                inc[(size_t)kM * s + q] = q == 0 ? 102 : 255;
             }
         }
     }
@@ -1045,6 +1058,72 @@ __device__ __forceinline__ void fpb_test(const FPairBand& b, float x1, float y1,
     r1 = a.y > 0.0f && lhs.y > rhs.y;
 }
 
+// Homography: the same packed-fp32 pre-band on the transfer error.  With
+// w = h6 x1 + h7 y1 + h8, tu = h0 x1 + h1 y1 + h2, tv = h3 x1 + h4 y1 + h5 and
+// e = (tu - x2 w, tv - y2 w), the fp64 band (h_band) keeps a pair iff
+// |e|^2 <= Tb w^2.  In fp32 (inputs rounded, every fma rounding counted) w is
+// within ew = 1e-6 W of its real value (W = |h6| X1 + |h7| Y1 + |h8| with the
+// problem's largest coordinates; >= 4 u of slack per term, u = 2^-24), and e1,
+// e2 within s1 = 1e-6 (U + 3 X2 W), s2 = 1e-6 (V + 3 Y2 W) (U, V the bounds of
+// tu, tv).  A pair is rejected only if even the smallest |e| and the largest
+// |w| the bounds allow fail the fp64 band with Tb (1 + 4e-6):
+// max(|e1| - s1, 0)^2 + max(|e2| - s2, 0)^2 > Tb' (|w| + ew)^2.  The margin
+// covers the fp32 rounding of the test itself; h_band's own slack covers the
+// exact residual's fp64 rounding.  NaN, overflow or unbounded coordinates
+// (amax = inf) never reject.  Survivors get the exact h_sq_residual.
+struct HPairBand {                 // hypotheses 2 j (.x) and 2 j + 1 (.y)
+    fpb_f2 g[9];
+    fpb_f2 ew, s1, s2;             // error bounds of w, e1, e2
+    fpb_f2 tq;                     // Tb (1 + 4e-6), rounded up
+    fpb_f2 pad[3];
+};
+static_assert(sizeof(HPairBand) == sizeof(FPairBand), "pair-band records share the LDS slot");
+
+__device__ __forceinline__ void hpb_setup(HPairBand* hp, int t, const double* h, bool valid, double Tb,
+                                          const DevClass& c) {
+    const double X1 = c.amax[0], Y1 = c.amax[1], X2 = c.amax[2], Y2 = c.amax[3];
+    double a[9];
+    for (int k = 0; k < 9; ++k) a[k] = __builtin_fabs(h[k]);
+    const double W = (a[6] * X1 + a[7] * Y1) + a[8];
+    const double U = (a[0] * X1 + a[1] * Y1) + a[2];
+    const double V = (a[3] * X1 + a[4] * Y1) + a[5];
+    constexpr double gam = 1e-6;
+    float* b = reinterpret_cast<float*>(&hp[t >> 1]);
+    const int hf = t & 1;
+    for (int k = 0; k < 9; ++k) b[2 * k + hf] = valid ? (float)h[k] : 0.0f;
+    b[2 * 9 + hf] = fpb_up(gam * W);
+    // an invalid hypothesis is never scored (vmask); keep its constants inert
+    b[2 * 10 + hf] = valid ? fpb_up(gam * (U + 3.0 * X2 * W)) : __builtin_inff();
+    b[2 * 11 + hf] = valid ? fpb_up(gam * (V + 3.0 * Y2 * W)) : __builtin_inff();
+    b[2 * 12 + hf] = fpb_up(Tb * (1.0 + 4e-6));
+    for (int k = 13; k < 16; ++k) b[2 * k + hf] = 0.0f;
+}
+
+__device__ __forceinline__ void hpb_test(const HPairBand& b, float x1, float y1, float x2, float y2, bool& r0,
+                                         bool& r1) {
+    const fpb_f2 X1 = {x1, x1}, Y1 = {y1, y1}, X2 = {x2, x2}, Y2 = {y2, y2};
+    const fpb_f2 w = fpb_fma(b.g[6], X1, fpb_fma(b.g[7], Y1, b.g[8]));
+    const fpb_f2 tu = fpb_fma(b.g[0], X1, fpb_fma(b.g[1], Y1, b.g[2]));
+    const fpb_f2 tv = fpb_fma(b.g[3], X1, fpb_fma(b.g[4], Y1, b.g[5]));
+    const fpb_f2 e1 = fpb_fma(-X2, w, tu), e2 = fpb_fma(-Y2, w, tv);
+    const fpb_f2 zero = {0.0f, 0.0f};
+    const fpb_f2 a1 = __builtin_elementwise_max(__builtin_elementwise_abs(e1) - b.s1, zero);
+    const fpb_f2 a2 = __builtin_elementwise_max(__builtin_elementwise_abs(e2) - b.s2, zero);
+    const fpb_f2 d = __builtin_elementwise_abs(w) + b.ew;
+    const fpb_f2 lhs = fpb_fma(a2, a2, a1 * a1), rhs = b.tq * (d * d);
+    r0 = lhs.x > rhs.x;
+    r1 = lhs.y > rhs.y;
+}
+
+__device__ __forceinline__ void pb_test(const FPairBand& b, float x1, float y1, float x2, float y2, bool& r0,
+                                        bool& r1) {
+    fpb_test(b, x1, y1, x2, y2, r0, r1);
+}
+__device__ __forceinline__ void pb_test(const HPairBand& b, float x1, float y1, float x2, float y2, bool& r0,
+                                        bool& r1) {
+    hpb_test(b, x1, y1, x2, y2, r0, r1);
+}
+
 template <int KIND, int H, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(KIND >= 3 ? 8 : 1))) void k_score_fm(DevProblem p, double T0, double T1, double band0,
                                                             double tan_tau1,
@@ -1077,7 +1156,8 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     __shared__ HypConst hyp[H];
     __shared__ uint32_t hval[H];
     __shared__ uint32_t cnt_sh[2][H];
-    __shared__ FPairBand fpb[KIND == 4 ? (H + 1) / 2 : 1];
+    using PairBand = std::conditional_t<KIND == 3, HPairBand, FPairBand>;
+    __shared__ PairBand fpb[KIND >= 3 ? (H + 1) / 2 : 1];
     __shared__ int gen_a[kGen ? H : 1];
     __shared__ RectModel gen_m[kGen ? H : 1];
     __shared__ double fin_sh[kGen ? H : 1];
@@ -1196,12 +1276,16 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
         }
         hyp[t] = make_hyp<KIND>(m, band0);
         if constexpr (KIND == 4) fpb_setup(fpb, t, m.h, v, T0, p.cls[0]);
+        if constexpr (KIND == 3) hpb_setup(fpb, t, m.h, v, band0, p.cls[0]);
         hval[t] = v ? 1u : 0u;
         cnt_sh[0][t] = 0;
         cnt_sh[1][t] = 0;
     }
     if constexpr (KIND == 4) {
         if ((H & 1) && t == H) fpb_setup(fpb, t, hyp[0].g, false, T0, p.cls[0]);   // odd H: inert pad
+    }
+    if constexpr (KIND == 3) {
+        if ((H & 1) && t == H) hpb_setup(fpb, t, hyp[0].g, false, band0, p.cls[0]);
     }
     GCR_STAMP(6, 15u);
     if (t < kW) { ready[t] = 0; done[t] = 0; }
@@ -1321,15 +1405,17 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             };
             struct C4 { double a, b, c, d; };
             if (__ballot(ok) != 0) {
-                if constexpr (KIND == 4) {
-                    // fundamental matrix: the packed fp32 pre-band (above), two
+                if constexpr (KIND >= 3) {
+                if (KIND == 4 || !(gen.probe & 128u)) {
+                    // correspondences: the packed fp32 pre-band (above), two
                     // hypotheses per pass; survivors go to the exact pass
+                    // (GCR_PROBE bit 7: the homography's fp64 band instead)
                     const float x1 = (float)f0, y1 = (float)f1, x2 = (float)f2, y2 = (float)f3;
 #pragma unroll 1
                     for (int q = 0; q < H; q += 2) {
                         if (!((vmask >> q) & 3ull)) continue;
                         bool rj[2];
-                        fpb_test(fpb[q >> 1], x1, y1, x2, y2, rj[0], rj[1]);
+                        pb_test(fpb[q >> 1], x1, y1, x2, y2, rj[0], rj[1]);
 #pragma unroll
                         for (int o = 0; o < 2; ++o) {
                             const int qq = q + o;
@@ -1344,8 +1430,8 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                             qn += c;
                         }
                     }
-                } else if constexpr (KIND == 3) {
-                    // correspondences: a rolled loop (the unrolled form holds
+                } else {
+                    // homography, fp64 band: a rolled loop (the unrolled form holds
                     // ~126 VGPRs; these kernels are held to 64, see above)
 #pragma unroll 1
                     for (int q = 0; q < H; ++q) {
@@ -1359,6 +1445,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                         my_n = lane == q ? c : my_n;
                         qn += c;
                     }
+                }
                 } else if (cls == 0) {
                     run_band([&](int q) { return C4{hyp[q].h7, hyp[q].h8, hyp[q].lo, hyp[q].hi}; },
                              [&](const C4& c) {
@@ -3112,17 +3199,19 @@ hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot
     // Both knobs are read per launch (tests switch them in-process).
     const char* ew = getenv("GCR_GEN_WIDEN");
     const bool widen = !(ew && ew[0] == '0');
+    // GCR_GEN_HWIDEN=1: the homography generator widens its groups too (A/B)
+    const char* eh = getenv("GCR_GEN_HWIDEN");
+    const bool hwiden = eh && eh[0] == '1';
     auto go = [&](auto gtag) {
         constexpr int G = decltype(gtag)::value;
         const dim3 grid(blocks_for((size_t)nslots * G, kGenBlock)), block(kGenBlock);
         if (p.solver == 4) {
-            if constexpr (G >= 1) {
-                if (widen) {
-                    hipLaunchKernelGGL((k_generate_fw<G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
-                    return;
-                }
-            }
-            hipLaunchKernelGGL((k_generate_f<G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+            if (widen)
+                hipLaunchKernelGGL((k_generate_fw<4, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+            else
+                hipLaunchKernelGGL((k_generate_f<G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
+        } else if (hwiden) {
+            hipLaunchKernelGGL((k_generate_fw<3, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
         } else {
             hipLaunchKernelGGL((k_generate<3, G>), grid, block, 0, stream, p, seed, slot0, nslots, inc, models);
         }

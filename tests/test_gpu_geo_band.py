@@ -1,11 +1,12 @@
 """Division-free band prefilters of the correspondence scorers at the threshold.
 
 k_score_fm (graph-cut-ransac_amd/csrc/kernels.hip) rejects a (hypothesis,
-correspondence) pair before its exact residual when h_band (homography,
-|e|^2 > Tb w^2) or the packed fp32 Sampson pre-band (fundamental,
-(|num| - sn)^2 > T' den_up with error bounds from the problem's largest
-coordinates; the split scorers use f_band, num^2 > Tb den) says it cannot be
-an inlier.  A band that drops one pair the exact residual accepts changes the
+correspondence) pair before its exact residual when its packed fp32 pre-band
+says it cannot be an inlier: transfer error for the homography
+(max(|e| - s, 0)^2 > Tb' (|w| + ew)^2), Sampson distance for the fundamental
+matrix ((|num| - sn)^2 > T' den_up), both with error bounds from the
+problem's largest coordinates.  The split scorers use the fp64 bands h_band
+(|e|^2 > Tb w^2) and f_band (num^2 > Tb den).  A band that drops one pair the exact residual accepts changes the
 count and the MSAC sum.  These tests place correspondences within one ulp of
 the threshold on both sides (bisection on the displacement, evaluated with
 the device's own operation order: Python floats are IEEE doubles without FMA
@@ -148,27 +149,30 @@ def test_band_prefilter_is_conservative_at_the_threshold(gpu, solver):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("solver", [N.SOLVER_HOMOGRAPHY4, N.SOLVER_FUNDAMENTAL7])
 @pytest.mark.parametrize("span", [20_000.0, 200_000.0])
-def test_fundamental_fp32_preband_is_conservative_at_large_coordinates(gpu, span):
-    # the F scorer's packed fp32 pre-band carries error bounds scaled by the
-    # problem's largest coordinates: correspondences one ulp either side of
-    # the Sampson threshold far from the origin still score as the oracle
-    rng = np.random.default_rng(int(span))
+def test_fp32_preband_is_conservative_at_large_coordinates(gpu, solver, span):
+    # the correspondence scorers' packed fp32 pre-bands (Sampson distance,
+    # transfer error) carry error bounds scaled by the problem's largest
+    # coordinates: correspondences one ulp either side of the threshold far
+    # from the origin still score as the oracle
+    rng = np.random.default_rng(int(span) + solver)
     thr = 0.75
     T = (2.25 * thr) * thr
-    corr, _, _, _ = S.problem_f(800, 0.3, seed=43)
-    gen = CorrProblem(N.SOLVER_FUNDAMENTAL7, corr)
+    fund = solver == N.SOLVER_FUNDAMENTAL7
+    corr, _, _, _ = (S.problem_f if fund else S.problem_h)(800, 0.3, seed=43)
+    gen = CorrProblem(solver, corr)
     inc, ms = gen.generate(5, 0, 64)
     models = ms[inc <= 101][:10]
-    bc = _boundary_corr(N.SOLVER_FUNDAMENTAL7, models, T, rng, per=60, span=span)
-    prob = CorrProblem(N.SOLVER_FUNDAMENTAL7, bc)
-    refs = [O.f_score(bc, m, thr) for m in models]
+    bc = _boundary_corr(solver, models, T, rng, per=60, span=span)
+    prob = CorrProblem(solver, bc)
+    refs = [(O.f_score if fund else O.h_score)(bc, m, thr) for m in models]
     assert min(r["count"] for r in refs) >= 60
     for nh in (2048, 11136):                              # the feature-major scorer
         tiled = np.resize(models, (nh, 9))
         n0, v0, tot = prob.score(tiled, thr)
         for i in range(nh):
             ref = refs[i % len(models)]
-            cnt, val = _finish(n0[i], v0[i], tot[i], thr, 7)
+            cnt, val = _finish(n0[i], v0[i], tot[i], thr, 7 if fund else 4)
             assert cnt == ref["count"], (span, nh, i)
             assert bits(val) == bits(ref["value"]), (span, nh, i)
