@@ -143,6 +143,33 @@ def test_generate_matches_oracle_slots(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("g,widen", [(1, "1"), (4, "1"), (8, "1"), (16, "1"), (64, "1"), (16, "0")])
+def test_generate_group_widening_matches_oracle_slots(gpu, g, widen, monkeypatch):
+    """k_generate_fw<3, G> (GCR_GEN_HWIDEN=1) hands finished slots' lanes to
+    unfinished ones; at 90 % outliers (9.7 attempts per slot, up to 65) every
+    slot reports the sequential loop's first success, for every starting group
+    size; a set where every attempt fails reports 102 everywhere.  499 slots:
+    a ragged last wave."""
+    monkeypatch.setenv("GCR_GEN_G", str(g))
+    monkeypatch.setenv("GCR_GEN_HWIDEN", widen)
+    corr, _, _, _ = S.problem_h(600, 0.9, seed=25)
+    prob = CorrProblem(N.SOLVER_HOMOGRAPHY4, corr)
+    inc, H = prob.generate(78, 9000, 499)
+    late = 0
+    for s in range(499):
+        oinc, om = O.h_slot(corr, 78, 9000 + s)
+        assert int(inc[s]) == oinc, (s, int(inc[s]), oinc)
+        late += oinc > 16
+        if oinc <= 101:
+            assert np.array_equal(bits(H[s]), bits(om)), s
+    assert late > 0
+    t = np.linspace(0.0, 500.0, 60)
+    flat = np.column_stack([t, 2.0 * t + 1.0, t + 3.0, 0.5 * t])
+    inc, _ = CorrProblem(N.SOLVER_HOMOGRAPHY4, flat).generate(5, 0, 131)
+    assert all(O.h_slot(flat, 5, s)[0] == 102 and int(inc[s]) == 102 for s in range(131))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nh", [100, 2048, 16384, "small"])
 def test_score_matches_oracle_bitwise(gpu, nh, monkeypatch):
     if nh == "small":              # launch_score_small (LO trials, refits)
