@@ -219,6 +219,8 @@ struct Workspace {
     DevBuf<uint8_t> pg_inc[2];          // verify_batches: slots generated one launch ahead
     DevBuf<RectModel> pg_models[2];
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
+    DevBuf<WgBest> vb_wg;               // verify_batches: a ring of batches' workgroup bests and
+    DevBuf<RectModel> vb_models;        // models, reduced by one deferred selection launch
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
     PinBuf<uint32_t> rf_hidx;           // GPU refit: their pinned staging
     DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
@@ -822,8 +824,36 @@ struct RectTraits {
                 ch.next_models = w->pg_models[(b + 1) & 1].p;
             }
         }
-        return launch_verify_fused(P->dp, Tm, seed, s0, n, m, P->w->inc.p, P->w->models.p, P->w->sb.dev(),
-                                   P->w->wg.p, wg_cap, rec, e0, e1, s, ch);
+        if (!defer_on()) {
+            return launch_verify_fused(P->dp, Tm, seed, s0, n, m, P->w->inc.p, P->w->models.p, P->w->sb.dev(),
+                                       P->w->wg.p, wg_cap, rec, e0, e1, s, ch);
+        }
+        // deferred selection: batch b leaves its workgroup bests and models in
+        // ring slot b % R; one launch reduces a whole ring (one workgroup per
+        // batch) after its last batch, so the per-batch reduction kernel and
+        // its launch leave the chain of scoring launches
+        const uint32_t R = select_ring(n);
+        Workspace* w = P->w;
+        w->vb_wg.ensure((size_t)R * wg_cap);
+        w->vb_models.ensure((size_t)R * n);
+        const uint32_t k = b % R;
+        hipError_t e = launch_verify_fused(P->dp, Tm, seed, s0, n, m, w->inc.p, w->vb_models.p + (size_t)k * n,
+                                           w->sb.dev(), w->vb_wg.p + (size_t)k * wg_cap, wg_cap, nullptr, e0, e1, s,
+                                           ch);
+        if (e != hipSuccess || !(k == R - 1 || b + 1 == nb)) return e;
+        return launch_select_batches(w->vb_wg.p, wg_cap, w->vb_models.p, s0 - (uint64_t)k * n, n, k + 1, rec - k, s);
+    }
+    // true when batch b's launch directly follows a deferred selection launch
+    // (verify_batches does not time those batches: their start event measured
+    // ~30 us late in 2000-batch runs)
+    static bool select_flush_before(uint32_t b, uint32_t n) { return b > 0 && defer_on() && b % select_ring(n) == 0; }
+    // batches per deferred selection launch: up to 64, the models ring held to
+    // 2^18 models (14.7 MB)
+    static uint32_t select_ring(uint32_t n) { return std::max<uint32_t>(1u, std::min<uint32_t>(64u, (1u << 18) / n)); }
+    // GCR_VERIFY_DEFER=0: every fused launch reduces its own batch (A/B)
+    static bool defer_on() {
+        const char* e = getenv("GCR_VERIFY_DEFER");
+        return !(e && e[0] == '0');
     }
     // GCR_VERIFY_CHAIN=0: every launch generates its own slots (A/B)
     static bool chain_on() {
@@ -922,6 +952,7 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
         if (e != hipSuccess) return e;
         return verify_score(P, Tm, s0, n, m, rec, e0, e1, b, s);
     }
+    static bool select_flush_before(uint32_t, uint32_t) { return false; }   // selection per batch
     // replay-path scoring of a fetched chunk: fundamental-matrix launches are
     // compacted to the live hypotheses (results in hypothesis order); the
     // host counted them (`live`), so the scorer's shape follows the live count
@@ -1190,7 +1221,7 @@ public:
         } else {
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint64_t s0 = slot0 + (uint64_t)b * nslots;
-                const bool t = b % stride == 0;
+                const bool t = b % stride == 0 && !Tr::select_flush_before(b, nslots) && timed < ntimed;
                 HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, P_->w->recs.p + b,
                                 t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr, s_,
                                 b, nb));

@@ -195,10 +195,19 @@ struct GenChain {
     uint8_t* next_inc = nullptr;
     RectModel* next_models = nullptr;
 };
+// rec == nullptr: the launch leaves its workgroup records in `wg` (and its
+// models in `models`) for a later launch_select_batches instead of reducing
+// them right away
 hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t seed, uint64_t slot0,
                                uint32_t nslots, const uint32_t m[2], uint8_t* inc, RectModel* models,
                                const ScoreOut& out, WgBest* wg, size_t wg_cap, BatchRecord* rec,
                                hipEvent_t ev0, hipEvent_t ev1, hipStream_t stream, const GenChain& chain = {});
+// Deferred selection of `count` consecutive fused batches in one launch (one
+// workgroup per batch): batch i's workgroup records at wg + i * wg_stride,
+// its models at models + i * nslots, its slots from slot0 + i * nslots, its
+// record to rec[i].  Same reduction as the per-launch k_select_wg.
+hipError_t launch_select_batches(const WgBest* wg, size_t wg_stride, const RectModel* models, uint64_t slot0,
+                                 uint32_t nslots, uint32_t count, BatchRecord* rec, hipStream_t stream);
 // true when launch_verify_fused at this batch size uses the chained kernel
 bool verify_chains(uint32_t nslots);
 

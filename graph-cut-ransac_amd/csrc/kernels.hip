@@ -2720,9 +2720,17 @@ __global__ void k_qr_update(double* c, const double* e, uint64_t lo, uint64_t hi
 
 // workgroup records -> one BatchRecord: first strict best over workgroups in
 // order (= slots in order), ties to the lower slot
+// Workgroup b of the launch reduces batch b (deferred selection: records at
+// wg + b * wg_stride, models at models + b * nslots, slots from
+// slot0 + b * nslots, record out[b]); a per-launch selection is one workgroup.
 __global__ __launch_bounds__(kSelectThreads) void k_select_wg(const WgBest* __restrict__ wg, uint32_t nwg,
                                                               const RectModel* __restrict__ models, uint64_t slot0,
-                                                              BatchRecord* out) {
+                                                              BatchRecord* out, uint32_t wg_stride = 0,
+                                                              uint32_t nslots = 0) {
+    wg += (size_t)blockIdx.x * wg_stride;
+    models += (size_t)blockIdx.x * nslots;
+    slot0 += (uint64_t)blockIdx.x * nslots;
+    out += blockIdx.x;
     __shared__ double s_val[kSelectThreads];
     __shared__ int32_t s_slot[kSelectThreads];
     __shared__ uint32_t s_n0[kSelectThreads], s_n1[kSelectThreads];
@@ -3134,7 +3142,20 @@ hipError_t launch_verify_fused(const DevProblem& p, const double T[2], uint64_t 
     else if (h == 16) launch_fused_t<16, 420>(p, T, nslots, out, g, stream);
     else launch_fused_t<4, 960>(p, T, nslots, out, g, stream);
     if (ev1) (void)hipEventRecord(ev1, stream);
-    hipLaunchKernelGGL(k_select_wg, dim3(1), dim3(kSelectThreads), 0, stream, wg, nwg, models, slot0, rec);
+    if (rec != nullptr)
+        hipLaunchKernelGGL(k_select_wg, dim3(1), dim3(kSelectThreads), 0, stream, wg, nwg, models, slot0, rec, 0u,
+                           0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_batches(const WgBest* wg, size_t wg_stride, const RectModel* models, uint64_t slot0,
+                                 uint32_t nslots, uint32_t count, BatchRecord* rec, hipStream_t stream) {
+    if (count == 0) return hipSuccess;
+    if (nslots == 0 || wg_stride < (size_t)(nslots + split_h(nslots) - 1) / split_h(nslots))
+        return hipErrorInvalidValue;
+    const uint32_t nwg = (nslots + split_h(nslots) - 1) / split_h(nslots);
+    hipLaunchKernelGGL(k_select_wg, dim3(count), dim3(kSelectThreads), 0, stream, wg, nwg, models, slot0, rec,
+                       (uint32_t)wg_stride, nslots);
     return hipGetLastError();
 }
 
