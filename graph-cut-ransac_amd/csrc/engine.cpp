@@ -221,6 +221,13 @@ struct Workspace {
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<WgBest> vb_wg;               // verify_batches: a ring of batches' workgroup bests and
     DevBuf<RectModel> vb_models;        // models, reduced by one deferred selection launch
+    // correspondence verify_batches with deferred selection: a ring of batch
+    // buffer sets, each array holding every set back to back (stride nh)
+    DevBuf<uint8_t> gr_inc;
+    DevBuf<GeoModel> gr_models;
+    DevBuf<uint32_t> gr_hmap, gr_hcount, gr_n0, gr_n1;
+    DevBuf<double> gr_v0, gr_v1, gr_tot;
+    hipEvent_t vb_flush = nullptr;
     DevBuf<uint32_t> rf_idx;            // GPU refit: inlier index lists
     PinBuf<uint32_t> rf_hidx;           // GPU refit: their pinned staging
     DevBuf<double> rf_A;                // GPU refit: A (3 columns) and b, column-major
@@ -243,7 +250,7 @@ struct Workspace {
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start})
+        for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start, vb_flush})
             if (e) (void)hipEventDestroy(e);
     }
 };
@@ -795,6 +802,12 @@ struct RectTraits {
     static constexpr bool kPipe = false;   // generation is fused into the scorer
     struct VBufs {};
     static VBufs vbufs(gcr_problem*, int, uint32_t) { return {}; }
+    static VBufs vbufs_ring(gcr_problem*, uint32_t, uint32_t, uint32_t) { return {}; }
+    static uint32_t select_ring(gcr_problem*, uint32_t) { return 1; }
+    static hipError_t select_ring_batches(gcr_problem*, const double*, uint64_t, uint32_t, const uint32_t*, uint32_t,
+                                          BatchRecord*, hipStream_t) {
+        return hipErrorNotSupported;
+    }
     static hipError_t verify_gen(gcr_problem*, uint64_t, uint64_t, uint32_t, const VBufs&, hipStream_t) {
         return hipErrorNotSupported;
     }
@@ -934,6 +947,7 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
         // multi-model slots are compacted by the scoring launch (verify_score)
         return launch_generate_geo(P->dp, seed, s0, n, b.inc, b.models, s);
     }
+    // rec == nullptr: score only (the ring's deferred selection reduces it)
     static hipError_t verify_score(gcr_problem* P, const double Tm[2], uint64_t s0, uint32_t n, const uint32_t m[2],
                                    BatchRecord* rec, hipEvent_t e0, hipEvent_t e1, const VBufs& b, hipStream_t s) {
         const uint32_t nh = n * (uint32_t)per(P);
@@ -942,7 +956,48 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
                                         b.hmap != nullptr);
         if (e != hipSuccess) return e;
         if (e1) (void)hipEventRecord(e1, s);
+        if (rec == nullptr) return hipSuccess;
         return launch_select_geo(P->solver, b.sb, b.inc, nh, s0, m[0], Tm[0], rec, s, b.hmap, b.hcount);
+    }
+    // deferred selection (GCR_VERIFY_DEFER, default on): the pipelined
+    // verify_batches scores batch b into ring set b % R and reduces a whole
+    // ring of batches in one launch; R up to 64, the ring held to 2^18
+    // hypotheses
+    static bool defer_on() {
+        const char* e = getenv("GCR_VERIFY_DEFER");
+        return !(e && e[0] == '0');
+    }
+    static uint32_t select_ring(gcr_problem* P, uint32_t n) {
+        const uint32_t nh = n * (uint32_t)per(P);
+        return std::max<uint32_t>(1u, std::min<uint32_t>(64u, (1u << 18) / nh));
+    }
+    static VBufs vbufs_ring(gcr_problem* P, uint32_t j, uint32_t R, uint32_t n) {
+        Workspace* w = P->w;
+        const size_t nh = (size_t)n * per(P);
+        w->gr_inc.ensure(R * nh);
+        w->gr_models.ensure(R * nh);
+        w->gr_n0.ensure(R * nh);
+        w->gr_n1.ensure(R * nh);
+        w->gr_v0.ensure(R * nh);
+        w->gr_v1.ensure(R * nh);
+        w->gr_tot.ensure(R * nh);
+        const bool cmp = per(P) > 1;
+        if (cmp) {
+            w->gr_hmap.ensure(R * nh);
+            w->gr_hcount.ensure(R);
+        }
+        const size_t o = j * nh;
+        return VBufs{w->gr_inc.p + o, w->gr_models.p + o, cmp ? w->gr_hmap.p + o : nullptr,
+                     cmp ? w->gr_hcount.p + j : nullptr,
+                     ScoreOut{w->gr_n0.p + o, w->gr_n1.p + o, w->gr_v0.p + o, w->gr_v1.p + o, w->gr_tot.p + o}};
+    }
+    // one launch for the `count` batches in ring sets 0 .. count - 1
+    static hipError_t select_ring_batches(gcr_problem* P, const double Tm[2], uint64_t s0_first, uint32_t n,
+                                          const uint32_t m[2], uint32_t count, BatchRecord* rec, hipStream_t s) {
+        const VBufs b0 = vbufs_ring(P, 0, 1, n);   // set 0 (already sized)
+        const uint32_t nh = n * (uint32_t)per(P);
+        return launch_select_geo_batches(P->solver, b0.sb, b0.inc, nh, nh, s0_first, m[0], Tm[0], count, rec, s,
+                                         b0.hmap, b0.hcount);
     }
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
@@ -1200,22 +1255,40 @@ public:
             Workspace* w = P_->w;
             for (hipEvent_t* e : {&w->vb_gen[0], &w->vb_gen[1], &w->vb_done[0], &w->vb_done[1], &w->vb_start})
                 if (*e == nullptr) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
-            const typename Tr::VBufs bufs[2] = {Tr::vbufs(P_, 0, nslots), Tr::vbufs(P_, 1, nslots)};
+            if (w->vb_flush == nullptr) HIPC(hipEventCreateWithFlags(&w->vb_flush, hipEventDisableTiming));
+            // deferred selection: batch b in ring set b % R, one selection
+            // launch per ring (after its last batch); otherwise two buffer
+            // sets and a selection launch per batch
+            const bool ring = Tr::defer_on();
+            const uint32_t R = ring ? Tr::select_ring(P_, nslots) : 2u;
+            std::vector<typename Tr::VBufs> bufs(R);
+            for (uint32_t j = 0; j < R; ++j)
+                bufs[j] = ring ? Tr::vbufs_ring(P_, j, R, nslots) : Tr::vbufs(P_, (int)j, nslots);
             hipStream_t side = P_->ctx->side;
             HIPC(hipEventRecord(w->vb_start, s_));
             HIPC(hipStreamWaitEvent(side, w->vb_start, 0));
             for (uint32_t b = 0; b < nb; ++b) {
-                const int k = (int)(b & 1u);
+                const int e = (int)(b & 1u);
+                const uint32_t k = b % R;
                 const uint64_t s0 = slot0 + (uint64_t)b * nslots;
-                const bool t = b % stride == 0;
-                if (b >= 2) HIPC(hipStreamWaitEvent(side, w->vb_done[k], 0));
+                const bool t = b % stride == 0 && !(ring && b > 0 && k == 0) && timed < ntimed;
+                // generation of batch b overlaps the scoring of batch b - 1
+                // only (not further ahead), and reuses a ring set only once
+                // the ring's selection has read it
+                if (b >= 2) HIPC(hipStreamWaitEvent(side, w->vb_done[e], 0));
+                if (ring && b >= R && k == 0) HIPC(hipStreamWaitEvent(side, w->vb_flush, 0));
                 HIPC(Tr::verify_gen(P_, prm_.seed, s0, nslots, bufs[k], side));
-                HIPC(hipEventRecord(w->vb_gen[k], side));
-                HIPC(hipStreamWaitEvent(s_, w->vb_gen[k], 0));
-                HIPC(Tr::verify_score(P_, Tm_, s0, nslots, m32, P_->w->recs.p + b,
+                HIPC(hipEventRecord(w->vb_gen[e], side));
+                HIPC(hipStreamWaitEvent(s_, w->vb_gen[e], 0));
+                HIPC(Tr::verify_score(P_, Tm_, s0, nslots, m32, ring ? nullptr : P_->w->recs.p + b,
                                       t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr,
                                       bufs[k], s_));
-                HIPC(hipEventRecord(w->vb_done[k], s_));
+                HIPC(hipEventRecord(w->vb_done[e], s_));
+                if (ring && (k == R - 1 || b + 1 == nb)) {
+                    HIPC(Tr::select_ring_batches(P_, Tm_, s0 - (uint64_t)k * nslots, nslots, m32, k + 1,
+                                                 P_->w->recs.p + (b - k), s_));
+                    HIPC(hipEventRecord(w->vb_flush, s_));
+                }
                 timed += t;
             }
         } else {

@@ -232,6 +232,12 @@ hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule,
 hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint64_t slot0,
                              uint32_t m, double Tm, BatchRecord* out, hipStream_t stream,
                              const uint32_t* hmap = nullptr, const uint32_t* hcount = nullptr);
+// deferred selection of `count` consecutive batches in one launch (one
+// workgroup per batch): batch b's score arrays, inc, hmap at offset b * stride,
+// its hcount at hcount + b, its slots from slot0 + b * nh / per, its record out[b]
+hipError_t launch_select_geo_batches(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint32_t stride,
+                                     uint64_t slot0, uint32_t m, double Tm, uint32_t count, BatchRecord* out,
+                                     hipStream_t stream, const uint32_t* hmap, const uint32_t* hcount);
 // order-preserving list of live hypotheses (inc <= 101): map[0 .. *count)
 // budget cut of a prefetched chunk: slots whose preceding increments reach
 // `budget` get inc = 255 (no model)

@@ -1925,7 +1925,18 @@ __global__ __launch_bounds__(kSelectThreads) void k_select(int solver, ScoreOut 
                                                            uint64_t slot0, uint32_t m0, uint32_t m1, double Tm0,
                                                            double Tm1, BatchRecord* out, uint32_t per = 1,
                                                            const uint32_t* __restrict__ hmap = nullptr,
-                                                           const uint32_t* __restrict__ hcount = nullptr) {
+                                                           const uint32_t* __restrict__ hcount = nullptr,
+                                                           uint32_t stride = 0) {
+    // deferred selection of consecutive batches: workgroup b reduces the
+    // batch whose arrays start `stride` hypotheses after batch b - 1's
+    if (stride != 0) {
+        const size_t o = (size_t)blockIdx.x * stride;
+        sc.n0 += o; sc.n1 += o; sc.v0 += o; sc.v1 += o; sc.tot += o;
+        inc += o;
+        if (hmap != nullptr) { hmap += o; hcount += blockIdx.x; }
+        slot0 += (uint64_t)blockIdx.x * (n / per);
+        out += blockIdx.x;
+    }
     __shared__ double s_val[kSelectThreads];
     __shared__ uint32_t s_idx[kSelectThreads];
     __shared__ unsigned long long s_models[kSelectThreads], s_its[kSelectThreads];
@@ -3355,6 +3366,17 @@ hipError_t launch_select_geo(int solver, const ScoreOut& sc, const uint8_t* inc,
     hipLaunchKernelGGL(k_select<GeoModel>, dim3(1), dim3(kSelectThreads), 0, stream, solver, sc, inc,
                        (const GeoModel*)nullptr, nh, slot0, m, 0u, Tm, 0.0, out, solver == 4 ? kFModels : 1u, hmap,
                        hcount);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_geo_batches(int solver, const ScoreOut& sc, const uint8_t* inc, uint32_t nh, uint32_t stride,
+                                     uint64_t slot0, uint32_t m, double Tm, uint32_t count, BatchRecord* out,
+                                     hipStream_t stream, const uint32_t* hmap, const uint32_t* hcount) {
+    if (count == 0) return hipSuccess;
+    if (stride < nh || stride == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_select<GeoModel>, dim3(count), dim3(kSelectThreads), 0, stream, solver, sc, inc,
+                       (const GeoModel*)nullptr, nh, slot0, m, 0u, Tm, 0.0, out, solver == 4 ? kFModels : 1u, hmap,
+                       hcount, stride);
     return hipGetLastError();
 }
 

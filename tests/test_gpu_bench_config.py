@@ -218,3 +218,31 @@ def test_deferred_selection_equals_per_batch(kind, nslots, nb, monkeypatch):
     assert outs[0] == outs[1]
     assert all(o[2] >= 0 for o in outs[0])
     assert len({o[2] for o in outs[0]}) > 1          # distinct batches, distinct bests
+
+
+@pytest.mark.parametrize("solver,nslots,nb", [(N.SOLVER_HOMOGRAPHY4, 4096, 70), (N.SOLVER_FUNDAMENTAL7, 3712, 30),
+                                              (N.SOLVER_HOMOGRAPHY4, 2048, 3)])
+def test_correspondence_deferred_selection_equals_per_batch(solver, nslots, nb, monkeypatch):
+    # the pipelined correspondence verify_batches scores batch b into ring set
+    # b % R (R = 64 at 4096 homography slots, 23 at 3712 fundamental-matrix
+    # slots = 11136 hypotheses) and reduces a whole ring in one launch;
+    # GCR_VERIFY_DEFER=0 (two buffer sets, a selection per batch) and the
+    # one-stream path must give the same records batch for batch
+    if solver == N.SOLVER_HOMOGRAPHY4:
+        corr, _, _, thr = S.problem_h(5000, 0.5, seed=SEED)
+    else:
+        corr, _, _, thr = S.problem_f(10_000, 0.8, seed=SEED)
+    prob = CorrProblem(solver, corr)
+    p = N.default_params()
+    p.scale_residual_thresh, p.seed = thr, SEED
+    outs = []
+    for defer, pipe in (("1", "1"), ("0", "1"), ("1", "0")):
+        monkeypatch.setenv("GCR_VERIFY_DEFER", defer)
+        monkeypatch.setenv("GCR_VERIFY_PIPE", pipe)
+        res = (N.BatchResult * nb)()
+        N.check(N.lib.gcr_problem_verify_batches(prob.h, C.byref(p), SLOT0, nslots, nb, res, None))
+        outs.append([(r.models, r.iterations, r.best_slot, bits(r.best_score).item(), r.best_inliers[0])
+                     for r in res])
+    assert outs[0] == outs[1] == outs[2]
+    assert all(o[2] >= 0 for o in outs[0])
+    assert len({o[2] for o in outs[0]}) > 1
