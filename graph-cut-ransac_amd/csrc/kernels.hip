@@ -3256,8 +3256,10 @@ hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot
     // 0.37 / 0.34 / 0.36 ms per 4096-slot step.  Widening groups (F bench line,
     // 3712 slots, two-stream pipeline, profiles/r2_v8_fwiden.txt): G = 4 / 8 /
     // 16 / 32 / 64 -> 0.173 / 0.143 / 0.126 / 0.139 / 0.159 ms per step, fixed
-    // G = 32 0.138 ms
-    int g = p.solver == 4 ? (nslots <= 8192 ? 16 : nslots <= 32768 ? 8 : 2)
+    // G = 32 0.138 ms.  The replay path's large chunks (F wall time to 0.99,
+    // every launch forced, profiles/r2_v13_bconc.txt): G = 2 / 4 / 8 / 16 ->
+    // 8.08 / 7.77 / 7.38 / 7.43 ms
+    int g = p.solver == 4 ? (nslots <= 8192 ? 16 : 8)
                           : (nslots <= 8192 ? 16 : nslots <= 32768 ? 4 : 1);
     if (env_g == 1 || env_g == 2 || env_g == 4 || env_g == 8 || env_g == 16 || env_g == 32 || env_g == 64) g = env_g;
     switch (g) {
