@@ -302,10 +302,24 @@ static bool faithful_subset(const std::vector<size_t>& indices, size_t N, std::v
 // block partials sequentially within aligned super-blocks of 65536 rows, then
 // the super-block partials sequentially -- what the GPU refit reproduces
 // bitwise.
+//
+// QR_ORDER_FROZEN (oracle_set_qr_order(1)) replaces every such reduction by the
+// plain sequential sum `s += f(i)` in row order -- the round-0 order, the
+// closest stand-in for Eigen's (unpinned) order.  It is FROZEN: never changed
+// to follow the product.  Tests check the product's results against it with a
+// tolerance (masks identical, models within 1e-6 relative), so a change of the
+// product's reduction order can no longer silently redefine the oracle.
 static constexpr size_t kSumBlockRows = 1024;
 static constexpr size_t kSumSuperRows = 64 * kSumBlockRows;
+enum QrOrder { QR_ORDER_BLOCKED = 0, QR_ORDER_FROZEN = 1 };
+static int g_qr_order = QR_ORDER_BLOCKED;
 template <class F>
 static double bsum(size_t lo, size_t hi, F f) {
+    if (g_qr_order == QR_ORDER_FROZEN) {
+        double s = 0.0;
+        for (size_t i = lo; i < hi; ++i) s += f(i);
+        return s;
+    }
     double total = 0.0;
     for (size_t u0 = lo; u0 < hi;) {
         const size_t u1 = std::min(hi, (u0 / kSumSuperRows + 1) * kSumSuperRows);
@@ -2393,6 +2407,13 @@ int oracle_lstsq3(const double* A_rowmajor, size_t m, const double* b, double* x
 double oracle_weighted_mode(const double* angles, const double* weights, size_t n, double bw) {
     std::vector<double> a(angles, angles + n), w(weights, weights + n);
     return Solver<2>::findWeightedMode(a, w, bw);
+}
+// reduction order of the least-squares fits: 0 = the engine's blocked order
+// (bitwise comparisons), 1 = the frozen sequential order (tolerance pin)
+int oracle_set_qr_order(int order) {
+    const int prev = g_qr_order;
+    g_qr_order = order == QR_ORDER_FROZEN ? QR_ORDER_FROZEN : QR_ORDER_BLOCKED;
+    return prev;
 }
 
 }  // extern "C"

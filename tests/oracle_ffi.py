@@ -107,8 +107,29 @@ def lib():
         L.oracle_lstsq3.argtypes = [dp, C.c_size_t, dp, dp]
         L.oracle_weighted_mode.argtypes = [dp, dp, C.c_size_t, C.c_double]
         L.oracle_weighted_mode.restype = C.c_double
+        L.oracle_set_qr_order.argtypes = [C.c_int]
         _lib = L
     return _lib
+
+
+QR_BLOCKED, QR_FROZEN = 0, 1
+
+
+class qr_order:
+    """Context manager: run the oracle's least-squares fits in `order`
+    (QR_FROZEN = the frozen sequential reduction order, never changed to follow
+    the product; QR_BLOCKED = the engine's blocked order, the default)."""
+
+    def __init__(self, order):
+        self.order = order
+
+    def __enter__(self):
+        self.prev = lib().oracle_set_qr_order(self.order)
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_qr_order(self.prev)
+        return False
 
 
 def _dp(a):

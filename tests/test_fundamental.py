@@ -245,6 +245,25 @@ def test_end_to_end_matches_oracle(gpu, n, outl, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("problem_seed,seed,kw", [
+    # the verdict's configs[3] case: 100 000-iteration cap, confidence 0.99
+    (304, 4, dict(min_it=50, max_it=100000)),
+    # bench.py's F latency call exactly: problem seed 20251121, seed 100,
+    # min_iters 0, max_iters 1e7 (terminates on confidence, ~700k iterations)
+    (20251121, 100, dict(min_it=0, max_it=10**7)),
+])
+def test_full_size_graph_cut_lo_matches_oracle(gpu, problem_seed, seed, kw):
+    """configs[3] at full size with the default graph-cut LO: N = 10 000, 80 %
+    outliers, spatial_coherence_weight 0.975, neighborhood_size 8 (labeling
+    GCRANSAC.h:759-870 inside LO :873-1062), bitwise against the oracle's
+    whole-graph BK: mask, F, iteration / LO / graph-cut counts, score."""
+    corr, truth, Fgt, thr = S.problem_f(10_000, 0.8, seed=problem_seed)
+    F, mask, st = _assert_same(corr, thr, seed, lam=0.975, **kw)
+    assert st["graph_cut_number"] > 0
+    assert (mask & truth).sum() / max(mask.sum(), 1) > 0.95
+
+
+@pytest.mark.gpu
 def test_spatial_weight_and_lo_budget_match_oracle(gpu):
     corr, _, _, thr = S.problem_f(800, 0.5, seed=9)
     _assert_same(corr, thr, 3, lam=0.975)
