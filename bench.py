@@ -48,6 +48,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector fp64 spec
 N_SIMD = 256 * 4               # CUs x SIMDs
 CLOCK_GHZ = 2.4                # MI355X peak engine clock (spec)
+# VALU issue ceiling: one wave64 VALU instruction per SIMD every 4 cycles (16
+# lanes per cycle; full-rate fp64 on CDNA4), in G wave-instructions/s
+VALU_ISSUE_PEAK = N_SIMD * CLOCK_GHZ / 4.0
 
 
 def score_kernel_name(kind, slots):
@@ -68,25 +71,30 @@ def score_kernel_name(kind, slots):
     return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, {fused}>"
 
 
-def traffic_per_launch(kernel, slots):
-    """HBM bytes per launch of `kernel` at this batch size from the committed
-    rocprofv3 PMC summary (profiles/pmc_traffic.json, written by
-    tools/pmc_summary.py from separate --pmc passes: 2 x FETCH_SIZE + WRITE_SIZE
-    per dispatch, the gfx950 correction of MI355X_MICROARCH.md); None if that
-    kernel/batch was not profiled."""
-    ent = pmc_entry(kernel, slots)
+def traffic_per_launch(ent):
+    """HBM bytes per launch from a PMC entry (profiles/pmc_traffic.json, written
+    by tools/pmc_summary.py from separate --pmc passes: 2 x FETCH_SIZE +
+    WRITE_SIZE per dispatch, the gfx950 correction of MI355X_MICROARCH.md);
+    None if this kernel/batch/build was not profiled."""
     return None if ent is None else ent.get("hbm_bytes_per_launch")
 
 
-def pmc_entry(kernel, slots):
-    """The committed PMC summary of `kernel` at this batch size, or None."""
+def pmc_entry(kernel, slots, build_id=None):
+    """The committed PMC summary of `kernel` at this batch size, or None.  An
+    entry counts only if it was collected from the kernels this process runs:
+    its `kernel_build_id` (tools/pmc_summary.py) must equal the loaded
+    library's gcr_kernel_build_id() (SHA-256 of the kernels' sources and
+    flags); counters of an older build are never reused."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             table = json.load(f)
     except (OSError, ValueError):
         return None
-    return table.get(f"{kernel}@{slots}")
+    ent = table.get(f"{kernel}@{slots}")
+    if ent is None or build_id is None or ent.get("kernel_build_id") != build_id:
+        return None
+    return ent
 
 
 # The fundamental matrix yields 1-3 models per 7-point sample (≈1.07 live per
@@ -119,6 +127,9 @@ def parse(argv=None):
                          "batch: configs[4] mixed H / F / rectification problems, full estimator calls")
     ap.add_argument("--problems", type=int, default=1024, help="batch workload: problems in the whole job")
     ap.add_argument("--concurrency", type=int, default=8, help="batch workload: host threads per GPU")
+    ap.add_argument("--batch-lambda", type=float, default=None,
+                    help="batch workload: spatial_coherence_weight of the H / F problems (default: the entry "
+                         "points' 0.975, graph-cut LO with pairwise terms; 0 isolates the graph-cut share)")
     ap.add_argument("--slots", type=int, default=None,
                     help="outer-iteration slots per launch (default 4096; f: 3712, see F_SLOTS)")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
@@ -268,6 +279,15 @@ def cpu_baseline(args):
                        f"ranges), CPU oracle (glibc math, {smp_text}, g++ -O3), {wall:.1f} s wall"),
                single_thread=dict(value=n1 / s1, cores=1, seconds=s1, calibration_rate=rate),
                cpu=info)
+    # the whole host (P = nproc).  The GPU box caps a one-GPU job
+    # at its 16-thread CPU share, so the full-host figure is the measured
+    # per-process rate of the P-process leg times the usable cores -- a
+    # projection (perfect scaling, no turbo loss), labelled as such
+    per_proc = nP / wall / P
+    cpu["full_host"] = dict(value=per_proc * info["usable_cores"], cores=info["usable_cores"],
+                            kind="projection", note=(f"{P}-process measured rate / {P} x {info['usable_cores']} "
+                                                     "usable cores; not run (the box limits a one-GPU job to "
+                                                     f"{CPU_SHARE} host threads)"))
     if not args.no_latency and kind != 4:
         t1 = time.perf_counter()
         kw = dict(min_it=0, max_it=10**7, lo=50, confidence=0.99, seed=100, math_mode=O.MATH_GLIBC, sampler=smp)
@@ -424,7 +444,8 @@ def main():
     # (SQ_ACTIVE_INST_VALU counts quad-cycles): the fraction of the 1024 SIMDs'
     # cycles spent issuing VALU during one launch -- the bound the algorithmic
     # HBM figure above does not see (the features are L2-resident)
-    pmc = pmc_entry(kernel_name, args.slots)
+    build_id = N.lib.gcr_kernel_build_id().decode()
+    pmc = pmc_entry(kernel_name, args.slots, build_id)
     if pmc and "SQ_ACTIVE_INST_VALU" in pmc and avg_kernel_s > 0:
         simd_cycles = N_SIMD * avg_kernel_s * CLOCK_GHZ * 1e9
         valu = dict(valu or {})
@@ -446,7 +467,8 @@ def main():
                       "frac": floor_s / avg_kernel_s, "clock_ghz": CLOCK_GHZ,
                       "wait_frac": (pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
                                     if pmc.get("SQ_WAVE_CYCLES") and pmc.get("SQ_WAIT_ANY") else None),
-                      "source": "profiles/pmc_traffic.json"}
+                      "rocprof_avg_ms": pmc.get("rocprof_avg_ms"),
+                      "source": f"profiles/pmc_traffic.json ({pmc.get('source')}, kernel build {build_id})"}
 
     # wall time to 0.99 confidence: full estimator call (incl. upload, LO, refit)
     latency = None
@@ -513,27 +535,40 @@ def main():
                 "collective_backend": backend if world > 1 else None,
             },
             "roofline": {
-                # the measured limiter: the features are L2-resident, so the
-                # nearest ceiling is fp64 VALU issue, not HBM (see valu_issue)
-                "bound": "valu" if valu_issue is not None else "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic_per_launch(kernel_name, args.slots),
-                "measured_peak": hbm_meas,
-                "frac_of_measured_peak": (achieved / hbm_meas) if hbm_meas else None,
+                # the measured limiter: the features are L2-resident (traffic is
+                # <1 % of the algorithmic bytes), so the ceiling that bounds the
+                # dominant kernel is fp64 VALU issue, not HBM
+                "bound": "valu",
+                "achieved": (valu_issue["insts_per_launch"] / avg_kernel_s / 1e9) if valu_issue else None,
+                "peak": VALU_ISSUE_PEAK,
+                "unit": "G wave-instructions/s",
+                "frac": valu_issue["frac"] if valu_issue else None,
+                "traffic": traffic_per_launch(pmc),
                 "valu_issue": valu_issue,
                 "kernel": kernel_name,
-                "bytes_per_hypothesis": bytes_per_feature * n_total,
+                "kernel_build_id": build_id,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
+                "avg_kernel_ms_note": ("HIP events on the engine's stream around every 4th launch "
+                                       "(GCR_TIMING_STRIDE), never the launch right after a deferred-selection "
+                                       "flush; the sampled mean is extrapolated to all launches. The whole "
+                                       "queue, selections included, is ms_per_step"),
                 "hypotheses_per_launch": models_per_launch,
-                "note": ("achieved/frac: ALGORITHMIC bytes (one pass over the feature SoA per hypothesis, "
-                         "the reference's f64 rows) / the kernel's live average duration, against the 8 TB/s "
-                         "spec and the box's measured copy bandwidth (measured_peak).  The features (<= 400 KB) "
-                         "stay L2/LDS-resident: real HBM traffic per launch is `traffic` (PMC), so HBM is not "
-                         "the limiter.  valu_issue.frac = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x clock x "
-                         "kernel time) is the honest bound; the rest of the time is latency (wait_frac)"),
+                "algorithmic_hbm": {
+                    "achieved_gbs": achieved,
+                    "peak_gbs": HBM_PEAK_GBS,
+                    "ratio": achieved / HBM_PEAK_GBS,
+                    "measured_peak_gbs": hbm_meas,
+                    "ratio_to_measured_peak": (achieved / hbm_meas) if hbm_meas else None,
+                    "bytes_per_hypothesis": bytes_per_feature * n_total,
+                    "note": ("ALGORITHMIC bytes (one pass over the feature rows per hypothesis, SURVEY §8(d)) / "
+                             "the kernel's live average duration. NOT a roofline fraction: the features stay "
+                             "L2/LDS-resident, so the ratio can exceed 1; real HBM bytes are `traffic`"),
+                },
+                "note": ("achieved/frac: SQ_INSTS_VALU of the dominant kernel (rocprofv3 --pmc pass of this "
+                         "same kernel build, profiles/pmc_traffic.json) / its live average duration, against "
+                         "the issue ceiling of 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction. null "
+                         "when no PMC pass exists for this kernel build; the rest of the time is latency "
+                         "(valu_issue.wait_frac)"),
             },
             "valu": valu,
             "cpu_baseline": cpu,
@@ -624,7 +659,7 @@ def bench_strong(args, rank, world, dist, device, coll_dev, backend):
         dist.destroy_process_group()
 
 
-def batch_problems(n, seed=20251121):
+def batch_problems(n, seed=20251121, lam=None):
     """BASELINE configs[4]: `n` independent problems, kinds cycling over
     homography / fundamental / hybrid rectification / scale-only, sizes
     U{1000 .. 10000}, 50 % outliers, confidence 0.99 (full estimator calls,
@@ -638,12 +673,13 @@ def batch_problems(n, seed=20251121):
         size = int(rng.integers(1000, 10001))
         k = i % 4
         common = dict(seed=i, confidence=0.99, min_iteration_number=0, max_iteration_number=10000)
+        corr = dict(common) if lam is None else dict(common, spatial_coherence_weight=lam)
         if k == 0:
             c, _, _, thr = S.problem_h(size, 0.5, seed=seed + i)
-            out.append(dict(kind="homography", correspondences=c, threshold=thr, **common))
+            out.append(dict(kind="homography", correspondences=c, threshold=thr, **corr))
         elif k == 1:
             c, _, _, thr = S.problem_f(size, 0.5, seed=seed + i)
-            out.append(dict(kind="fundamental", correspondences=c, threshold=thr, **common))
+            out.append(dict(kind="fundamental", correspondences=c, threshold=thr, **corr))
         elif k == 2:
             fs, fo, _, _, ts, to = S.problem_m2(size // 2, size - size // 2, seed=seed + i)
             out.append(dict(kind="sift", scale_features=fs, orientation_features=fo, scale_residual_thresh=ts,
@@ -660,7 +696,7 @@ def bench_batch(args, rank, world, dist, device, coll_dev):
     from pygcransac import distributed as D
     from pygcransac import _native as N
 
-    problems = batch_problems(args.problems)
+    problems = batch_problems(args.problems, lam=args.batch_lambda)
     solve_many = D.batch_solver(device, args.concurrency)
     shares = D.assign_lpt([D.problem_cost(p) for p in problems], world)
     warm = [problems[i] for i in shares[rank][:max(1, args.warmup // 50)]]
@@ -685,6 +721,22 @@ def bench_batch(args, rank, world, dist, device, coll_dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     solved = sum(1 for r in recs if r is not None)
+    # this rank's per-phase times summed over its problems, per kind (the
+    # engine's gcr_stats of each call; wall time overlaps across the
+    # concurrent solving threads, so the sums exceed the elapsed time)
+    phase_keys = ("ms_setup", "ms_generate", "ms_score", "ms_score_kernel", "ms_replay", "ms_lo", "ms_lo_lists",
+                  "ms_lo_fit", "ms_lo_score", "ms_refit_fit", "ms_refit", "ms_total")
+    phases = {}
+    for i, res in local.items():
+        kind = problems[i]["kind"]
+        agg = phases.setdefault(kind, dict(problems=0, hypotheses=0, graph_cut_number=0,
+                                           **{k: 0.0 for k in phase_keys}))
+        st = res["stats"]
+        agg["problems"] += 1
+        agg["hypotheses"] += int(st["hypotheses"])
+        agg["graph_cut_number"] += int(st["graph_cut_number"])
+        for k in phase_keys:
+            agg[k] += float(st[k])
     if rank == 0:
         print(json.dumps({
             "metric": METRIC,
@@ -703,7 +755,9 @@ def bench_batch(args, rank, world, dist, device, coll_dev):
                                    "(homography / fundamental / hybrid / scale-only, N ~ U{1000..10000}, "
                                    "50% outliers, confidence 0.99, full estimator calls)",
                        "parallelism": f"LPT problem sharding x{world}, {args.concurrency} host threads per GPU",
-                       "problems_per_s": len(problems) / elapsed, "solved": solved},
+                       "problems_per_s": len(problems) / elapsed, "solved": solved,
+                       "spatial_coherence_weight_hf": 0.975 if args.batch_lambda is None else args.batch_lambda,
+                       "rank0_phase_ms_sums": phases},
             "roofline": None,
             "cpu_baseline": None,
         }))

@@ -248,9 +248,20 @@ struct Workspace {
     DevBuf<uint32_t> pf_hmap, pf_hcount;   // verify_batches: the second batch's compaction
     hipEvent_t vb_gen[2] = {nullptr, nullptr}, vb_done[2] = {nullptr, nullptr}, vb_start = nullptr;
     std::vector<hipEvent_t> evs;        // score-kernel brackets, 2 per batch
+    // summary replay (RunnerT::replay_summaries): per chunk buffer set (set 0
+    // = inc / models / sb / hmap, set 1 = the pf_ arrays) its summary scratch,
+    // device summary, pinned summaries of every rank, the small-scorer pair
+    // buffers of a short chunk, and its completion / score-kernel events
+    DevBuf<uint8_t> sum_scr[2];
+    DevBuf<BlockSummary> dsum[2];
+    PinBuf<BlockSummary> hsum[2];       // [0] this rank's, then the all-gathered ones
+    DevBuf<double> cs_vals[2];
+    DevBuf<uint64_t> cs_bits[2];
+    hipEvent_t sum_done[2] = {nullptr, nullptr}, sum_k0[2] = {nullptr, nullptr}, sum_k1[2] = {nullptr, nullptr};
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
-        for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start, vb_flush})
+        for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start, vb_flush, sum_done[0],
+                             sum_done[1], sum_k0[0], sum_k0[1], sum_k1[0], sum_k1[1]})
             if (e) (void)hipEventDestroy(e);
     }
 };
@@ -1033,6 +1044,12 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
 
 struct FundTraits : GeoTraits {     // up to kFModels models per sample
     static constexpr size_t kPer = kFModels;
+    // summary replay: the live hypotheses of `nh` positions compacted on the
+    // device (hmap / hcount), the scorer sized by nh and cut at *hcount
+    static hipError_t score_compact(gcr_problem* P, const double T[2], const Model* m, const uint8_t* inc, uint32_t nh,
+                                    uint32_t* hmap, uint32_t* hcount, const ScoreOut& out, hipStream_t s) {
+        return launch_score_geo(P->dp, T[0], m, inc, nh, out, s, hmap, hcount, true);
+    }
 };
 
 constexpr int kMaxLOSample = 64;     // largest LO sample: 7 x the largest minimal sample (7)
@@ -1073,9 +1090,15 @@ public:
         compact_ = false;         // fixed-size per-hypothesis records cross the exchange
     }
 
-    // Full GCRANSAC::run; fills outputs, returns total inlier count.
-    int run(uint8_t* mask0, uint8_t* mask1, double* H, gcr_rect_model* model_out) {
-        const auto t_all = Clock::now();
+    // GCR_REPLAY=slots: the per-slot replay of round 2 (every chunk's
+    // per-hypothesis records copied back and walked on the host), kept as the
+    // A/B reference of the summary replay
+    static bool summary_replay_on() {
+        const char* e = getenv("GCR_REPLAY");              // read per run (tests switch it)
+        return !(e && e[0] == 's');
+    }
+
+    void replay_slots() {
         const uint64_t ones[2] = {1, 1};
         uint64_t max_iteration = iteration_number(ones);
         const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
@@ -1146,6 +1169,342 @@ public:
         replay_ms += ms_since(t_rep);
         st_.slots = slot;
         st_.ms_replay = replay_ms;
+    }
+
+    // ---- summary replay (the default) ------------------------------------
+    // Each chunk of slots is generated, scored and SUMMARISED on the device
+    // (summary.h): its prefix-maximum chain of finished scores with the
+    // iteration / hypothesis counts before each member, the totals, and the
+    // last live hypothesis.  Only those records come back (a few KB per chunk,
+    // one copy into pinned memory), and the replay walks the chain instead of
+    // every slot: a strict new best (GCRANSAC.h:440-446) is always a chain
+    // member, max_iteration and LO change only there (:467-483), and the loop
+    // condition (:286-287) is monotone in the iteration count, so the stop
+    // slot is located on the device once the last threshold is known.  A
+    // hypothesis-sharded run all-gathers these fixed-size records (SURVEY.md
+    // §8(e) row 2) instead of per-hypothesis data.  Chunks run on the side
+    // stream (low priority) into two buffer sets, the next one issued before
+    // the current one is replayed whenever the loop is certain to reach it
+    // (GCR_PREFETCH=0: never), so LO / refit kernels on the replay stream do
+    // not queue behind them.
+    struct Chunk {
+        uint64_t s0 = 0;          // first slot
+        uint32_t B = 0;           // slots of the chunk
+        uint32_t per = 0;         // slots per rank block
+        uint64_t it_lo = 0;       // iterations before the chunk (exact, or a lower bound when issued ahead)
+        int set = 0;              // buffer set
+        double bar = 0.0;         // the best score when issued (members beat it)
+    };
+    uint64_t rank_slot0(const Chunk& c, int r) const { return c.s0 + (uint64_t)r * c.per; }
+    uint32_t rank_nslots(const Chunk& c, int r) const {
+        const uint64_t b = (uint64_t)r * c.per;
+        return b >= c.B ? 0u : (uint32_t)std::min<uint64_t>(c.per, c.B - b);
+    }
+    DevBuf<uint8_t>& set_inc(int set) { return set ? P_->w->pf_inc : P_->w->inc; }
+    DevBuf<Model>& set_models(int set) { return set ? Tr::pf_dmodels(P_->w) : Tr::dmodels(P_->w); }
+    ScoreBufs& set_sb(int set) { return set ? P_->w->pf_sb : P_->w->sb; }
+    DevBuf<uint32_t>& set_hmap(int set) { return set ? P_->w->pf_hmap : P_->w->hmap; }
+    DevBuf<uint32_t>& set_hcount(int set) { return set ? P_->w->pf_hcount : P_->w->hcount; }
+
+    // summary launch of this rank's block of chunk c (mode chain or locate)
+    hipError_t launch_summary(const Chunk& c, double bar, uint32_t from_pos, uint64_t target, bool parts_ready,
+                              hipStream_t s) {
+        Workspace* w = P_->w;
+        const uint32_t n = rank_nslots(c, rank_);
+        const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
+        return launch_block_summary(P_->solver, set_inc(c.set).p, set_models(c.set).p, set_sb(c.set).dev(),
+                                    kP > 1 ? set_hmap(c.set).p : nullptr, n, (uint32_t)kP, m32, Tm_, bar, from_pos,
+                                    target, w->sum_scr[c.set].p, w->dsum[c.set].p, s, parts_ready);
+    }
+
+    // generate + score + summarise this rank's block of chunk c on stream s
+    void issue_chunk(const Chunk& c, hipStream_t s) {
+        Workspace* w = P_->w;
+        for (int k = 0; k < 2; ++k) {
+            for (hipEvent_t* e : {&w->sum_done[k]})
+                if (*e == nullptr) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            for (hipEvent_t* e : {&w->sum_k0[k], &w->sum_k1[k]})
+                if (*e == nullptr) HIPC(hipEventCreate(e));
+        }
+        const int set = c.set;
+        w->hsum[set].ensure((size_t)world_ + 1);
+        w->dsum[set].ensure(1);
+        const uint32_t n = rank_nslots(c, rank_);
+        if (n == 0) {                                     // an empty block (more ranks than slots)
+            HIPC(hipEventRecord(w->sum_done[set], s));
+            return;
+        }
+        const size_t np = (size_t)n * kP;
+        set_inc(set).ensure(np);
+        set_models(set).ensure(np);
+        set_sb(set).ensure(np);
+        w->sum_scr[set].ensure(summary_scratch_bytes((uint32_t)np, (uint32_t)kP));
+        HIPC(Tr::generate(P_, prm_.seed, rank_slot0(c, rank_), n, set_inc(set).p, set_models(set).p, s));
+        HIPC(hipEventRecord(w->sum_k0[set], s));
+        if constexpr (kP > 1) {
+            // multi-model slots: the live hypotheses compacted on the device
+            // (k_compact / the scorer's prologue), scores at the live rank
+            set_hmap(set).ensure(np);
+            set_hcount(set).ensure(1);
+            HIPC(Tr::score_compact(P_, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np, set_hmap(set).p,
+                                   set_hcount(set).p, set_sb(set).dev(), s));
+        } else {
+            if (np <= kSmallScore && small_score_on()) {
+                const size_t pairs = small_score_pairs(P_->dp);
+                w->cs_vals[set].ensure(pairs * np);
+                w->cs_bits[set].ensure(pairs * np / 64);
+                HIPC(launch_score_small(P_->dp, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np,
+                                        set_sb(set).dev(), w->cs_vals[set].p, w->cs_bits[set].p, s));
+            } else {
+                HIPC(Tr::score(P_, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np, true, set_sb(set).dev(),
+                               s));
+            }
+        }
+        HIPC(hipEventRecord(w->sum_k1[set], s));
+        HIPC(launch_summary(c, c.bar, 0, ~0ull, false, s));
+        HIPC(hipMemcpyAsync(w->hsum[set].p, w->dsum[set].p, sizeof(BlockSummary), hipMemcpyDeviceToHost, s));
+        HIPC(hipEventRecord(w->sum_done[set], s));
+        st_.launches += 5;
+        st_.hypotheses_computed += np;
+    }
+
+    // every rank's summary of its block (this rank's: `mine`, the others':
+    // the all-gather) into `all` (world records)
+    void gather_summaries(const BlockSummary& mine, BlockSummary* all) {
+        if (world_ == 1) {
+            all[0] = mine;
+            return;
+        }
+        const auto t0 = Clock::now();
+        if (xfn_(xuser_, &mine, all, sizeof(BlockSummary)) != 0) throw std::runtime_error("all-gather callback failed");
+        st_.ms_score += ms_since(t0);
+    }
+
+    static BlockSummary empty_summary() {
+        BlockSummary b;
+        std::memset(&b, 0, sizeof(b));
+        return b;
+    }
+
+    // chunk c's summaries of every rank into `all` (waits for this rank's)
+    void collect_chunk(const Chunk& c, BlockSummary* all) {
+        Workspace* w = P_->w;
+        const auto t0 = Clock::now();
+        HIPC(hipEventSynchronize(w->sum_done[c.set]));
+        st_.ms_score += ms_since(t0);
+        BlockSummary mine = empty_summary();
+        if (rank_nslots(c, rank_) > 0) {
+            mine = w->hsum[c.set].p[0];
+            float kms = 0;
+            HIPC(hipEventElapsedTime(&kms, w->sum_k0[c.set], w->sum_k1[c.set]));
+            st_.ms_score_kernel += kms;
+        }
+        gather_summaries(mine, all);
+    }
+
+    // a collective re-summary of chunk c (every rank calls it) into `all`:
+    // the chain of `owner`'s block continued from (from_pos, bar), or
+    // (target != null) the locate of target[rank] on every block
+    void resummarise(const Chunk& c, int owner, uint32_t from_pos, double bar, const uint64_t* target,
+                     BlockSummary* all) {
+        Workspace* w = P_->w;
+        BlockSummary mine = empty_summary();
+        if (rank_nslots(c, rank_) > 0 && (target != nullptr || owner == rank_)) {
+            HIPC(launch_summary(c, bar, target ? 0u : from_pos, target ? target[rank_] : ~0ull, target != nullptr,
+                                s_));
+            HIPC(hipMemcpyAsync(w->hsum[c.set].p, w->dsum[c.set].p, sizeof(BlockSummary), hipMemcpyDeviceToHost, s_));
+            HIPC(hipStreamSynchronize(s_));
+            st_.launches += 2;
+            mine = w->hsum[c.set].p[0];
+        }
+        gather_summaries(mine, all);
+    }
+
+    // the model of a summarised hypothesis
+    static Model model_of(const SumHyp& h) {
+        Model m;
+        std::memcpy(&m, h.m, sizeof(Model));
+        return m;
+    }
+
+    // the hypothesis the inlier buffer holds when the loop leaves a stretch of
+    // slots: the last one processed, if it came after the last new best
+    // (otherwise the buffer still holds what that new best -- or its LO --
+    // left there; GCRANSAC.h:460 writes every hypothesis, :440-446 flips)
+    uint64_t ord_last_best_ = 0;          // ordinal + 1 of the last strict new best (0: none)
+    void hold_last(const SumHyp& h, uint64_t ord) {
+        if (ord + 1 > ord_last_best_) bufs_[off_] = Buffer{true, model_of(h), {h.n0, h.n1}};
+    }
+
+    void replay_summaries() {
+        const uint64_t ones[2] = {1, 1};
+        uint64_t max_iteration = iteration_number(ones);
+        const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
+        const uint64_t L = std::max(min_it, max_it);
+        auto thr = [&]() { return std::max(min_it, std::min(max_iteration, max_it)); };
+        const bool ahead_ok = prefetch_on();
+        Workspace* w = P_->w;
+        double replay_ms = 0;
+        uint64_t hyps = 0;                 // live hypotheses before the current chunk
+        uint64_t next_slot = 0, chunk_no = 0, last_B = 0;
+        std::vector<Chunk> q;              // issued, not yet replayed (at most 2: one per buffer set)
+        int next_set = 0;
+        std::vector<BlockSummary> S(world_), X(world_);
+        std::vector<SumHyp> lasts(world_);
+        std::vector<uint8_t> has_last(world_);
+        std::vector<uint64_t> itb(world_ + 1), hb(world_ + 1), tgt(world_);
+        // plan + issue the chunk after the last issued one; `it_lo`: iterations
+        // before it (exact, or a lower bound: every slot adds at least one)
+        auto issue = [&](uint64_t it_lo) -> bool {
+            if (it_lo >= L) return false;
+            Chunk c;
+            c.B = (uint32_t)plan_chunk(chunk_no, last_B, it_lo, L);
+            c.s0 = next_slot;
+            c.per = (uint32_t)((c.B + world_ - 1) / world_);
+            c.it_lo = it_lo;
+            c.set = next_set;
+            c.bar = best_.sum;
+            issue_chunk(c, P_->ctx->side);
+            next_set ^= 1;
+            next_slot += c.B;
+            last_B = c.B;
+            ++chunk_no;
+            q.push_back(c);
+            return true;
+        };
+        while (min_it > it_ || it_ < std::min(max_iteration, max_it)) {
+            if (q.empty() && !issue(it_)) break;
+            const Chunk c = q.front();
+            // the chunk after it goes ahead (before this one is replayed) when
+            // the loop certainly reaches it: the iteration floor min_it alone
+            // keeps the loop going, and every slot adds at least one iteration
+            if (ahead_ok && q.size() == 1 && c.it_lo + c.B < min_it && issue(c.it_lo + c.B)) ++st_.prefetched_chunks;
+            collect_chunk(c, S.data());
+            const auto t_rep = Clock::now();
+            itb[0] = it_;
+            hb[0] = hyps;
+            for (int r = 0; r < world_; ++r) {
+                itb[r + 1] = itb[r] + S[r].inc_total;
+                hb[r + 1] = hb[r] + S[r].hyps_total;
+                lasts[r] = S[r].last;
+                has_last[r] = S[r].has_last ? 1 : 0;
+            }
+            // with this chunk's totals known the next one may be certain
+            if (ahead_ok && q.size() == 1 && itb[world_] < min_it && issue(itb[world_])) ++st_.prefetched_chunks;
+            bool stopped = false;
+            // LO runs once per slot, after all of the slot's models (the
+            // last new best of the slot decides, GCRANSAC.h:440-515), before
+            // the next slot's loop condition
+            uint64_t cur_slot = ~0ull;
+            bool slot_lo = false;
+            auto flush_lo = [&]() {
+                if (do_lo_ && slot_lo) {
+                    ++lo_number_;
+                    local_optimization(bufs_[off_]);
+                    max_iteration = iteration_number(best_.n);
+                }
+                slot_lo = false;
+            };
+            for (int r = 0; r < world_ && !stopped; ++r) {
+                uint32_t k = 0;
+                while (true) {
+                    if (k == S[r].ncand) {
+                        if (!S[r].overflow) break;
+                        // more members than one summary holds: the owner
+                        // continues the chain from the last one (collective)
+                        resummarise(c, r, S[r].resume_pos, S[r].resume_bar, nullptr, X.data());
+                        S[r] = X[r];
+                        k = 0;
+                        continue;
+                    }
+                    const SumHyp& h = S[r].cand[k++];
+                    const uint64_t gslot = rank_slot0(c, r) + h.pos / kP;
+                    if (gslot != cur_slot) {
+                        flush_lo();
+                        cur_slot = gslot;
+                        const uint64_t it_before = itb[r] + h.it_before;
+                        if (!(min_it > it_before || it_before < std::min(max_iteration, max_it))) {
+                            stopped = true;             // the loop ends at or before this member's slot
+                            break;
+                        }
+                        it_ = it_before + h.inc;
+                    }
+                    const Model model = model_of(h);
+                    const uint32_t rn[2] = {h.n0, h.n1};
+                    const HScore cur = finish(rn, h.v0, h.v1, h.tot);
+                    bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
+                    if (best_.sum < cur.sum && valid_model(model)) {
+                        off_ = 1 - off_;
+                        best_model_ = model;
+                        best_ = cur;
+                        ord_last_best_ = hb[r] + h.hyps_before + 1;
+                        bool nonmin = false;
+                        for (int cc = 0; cc < K_; ++cc) if (best_.n[cc] > m_[cc]) { nonmin = true; break; }
+                        slot_lo = (it_ > 20) && nonmin;
+                        max_iteration = iteration_number(best_.n);
+                    }
+                }
+            }
+            if (!stopped) flush_lo();
+            // past the last member the threshold is fixed: the loop ends in
+            // this chunk iff its iterations reach it
+            if (!stopped && itb[world_] >= thr()) stopped = true;
+            if (stopped) {
+                // the first slot after the last member processed whose
+                // iterations-before reach the threshold (located on every
+                // rank's block, the first rank's wins).  Earlier slots passed
+                // the condition under the thresholds of their time, which can
+                // be higher (a better score with fewer inliers in one class
+                // raises max_iteration); it_ is the count before that first
+                // slot and the counts increase strictly, so target max(thr, it_)
+                const uint64_t T = std::max(thr(), it_);
+                for (int r = 0; r < world_; ++r) tgt[r] = T > itb[r] ? T - itb[r] : 0;
+                resummarise(c, -1, 0, 0.0, tgt.data(), X.data());
+                int rs = -1;
+                for (int r = 0; r < world_; ++r)
+                    if (X[r].stop_found) { rs = r; break; }
+                if (rs < 0) throw std::runtime_error("summary replay: stop slot not located");
+                it_ = itb[rs] + X[rs].stop_it_before;
+                st_.slots = rank_slot0(c, rs) + X[rs].stop_slot;
+                st_.hypotheses = hb[rs] + X[rs].stop_hyps_before;
+                // the last hypothesis processed: before the stop in its block,
+                // else the last one of an earlier block of the chunk (earlier
+                // chunks were settled at their ends)
+                if (X[rs].has_last) {
+                    hold_last(X[rs].last, hb[rs] + X[rs].last.hyps_before);
+                } else {
+                    for (int r = rs - 1; r >= 0; --r)
+                        if (has_last[r]) {
+                            hold_last(lasts[r], hb[r] + lasts[r].hyps_before);
+                            break;
+                        }
+                }
+                replay_ms += ms_since(t_rep);
+                break;
+            }
+            // the whole chunk was processed
+            it_ = itb[world_];
+            hyps = hb[world_];
+            st_.hypotheses = hyps;
+            st_.slots = c.s0 + c.B;
+            for (int r = world_ - 1; r >= 0; --r)
+                if (has_last[r]) {
+                    hold_last(lasts[r], hb[r] + lasts[r].hyps_before);
+                    break;
+                }
+            q.erase(q.begin());
+            replay_ms += ms_since(t_rep);
+        }
+        // chunks issued ahead that the loop never reached
+        for (const Chunk& c : q) HIPC(hipEventSynchronize(w->sum_done[c.set]));
+        st_.ms_replay = replay_ms;
+    }
+
+    // Full GCRANSAC::run; fills outputs, returns total inlier count.
+    int run(uint8_t* mask0, uint8_t* mask1, double* H, gcr_rect_model* model_out) {
+        const auto t_all = Clock::now();
+        if (summary_replay_on()) replay_summaries();
+        else replay_slots();
 
         int total = 0;
         Model out_model = Tr::def();
@@ -1544,6 +1903,7 @@ private:
         else if (min_it >= max_it) B = 65536;
         else B = chunk_no == 0 ? kSmallScore : std::min<uint64_t>(65536, last_chunk * 4);
         B = std::min<uint64_t>(B, L > it ? L - it : 0);
+        B = std::min<uint64_t>(B, (uint64_t)262144 * world_);      // a block summary covers <= 2^18 slots
         return std::max<uint64_t>(B, 1);
     }
 

@@ -7,6 +7,7 @@
 #include "fund.h"
 #include "geo.h"
 #include "rect.h"
+#include "summary.h"
 
 namespace gcr {
 
@@ -282,6 +283,20 @@ struct WarpMap {
 };
 hipError_t launch_warp(const void* src, int sh, int sw, int ch, int dtype, const WarpMap& M, void* dst, int dh,
                        int dw, int border_mode, hipStream_t stream);
+// Summary of a scored block of `nslots` slots (summary.h, summary.hip): per =
+// hypotheses per slot, positions slot * per + q; scores at the position, or
+// at its live rank when hmap != null (compacted launch).  target == ~0: the
+// chain of hypotheses beating `bar` (from position from_pos on), totals and
+// the block's last live hypothesis; otherwise locate the first slot whose
+// iterations-before reach `target` (block-relative) -- parts_ready: the
+// per-part totals of an earlier summary of the same block are reused.
+// scratch: summary_scratch_bytes(nslots * per, per) bytes of device memory.
+size_t summary_scratch_bytes(uint32_t npos, uint32_t per);
+hipError_t launch_block_summary(int solver, const uint8_t* inc, const void* models, const ScoreOut& sc,
+                                const uint32_t* hmap, uint32_t nslots, uint32_t per, const uint32_t m[2],
+                                const double Tm[2], double bar, uint32_t from_pos, uint64_t target, void* scratch,
+                                BlockSummary* out, hipStream_t stream, bool parts_ready = false);
+
 // streaming copy of `bytes` (a multiple of 16) for the HBM peak probe
 hipError_t launch_hbm_copy(const void* src, void* dst, size_t bytes, int nontemporal, hipStream_t stream);
 

@@ -1301,41 +1301,68 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
         if (wave == kW) {
             // ------------------------------------------ look-ahead generator
             // the next batch's slots of this workgroup (blockIdx.x * H + sl,
-            // slot index slot0 + nh + ...), 64 / H lanes per slot trying
-            // attempts r G + g; the lowest success wins (k_generate's rule).
+            // slot index slot0 + nh + ...), k_generate_fw's widening lane
+            // groups: the H slots start with 64 / H lanes each, and after
+            // every round the unfinished ones share the whole wave (64 /
+            // pow2ceil(k) lanes for k left) from one wave-uniform lowest
+            // untried attempt, so each slot's result is still its lowest
+            // successful attempt (k_generate's rule).  ~4 attempts per slot at
+            // 50 % outliers: fixed groups of 4 lanes needed 3-5 rounds of
+            // attempt latency for the slowest of 16 slots, widening ~2-3.
             // Overlaps the rounds below; no barrier follows.
             if (gen.chain.next_inc == nullptr) return;
-            constexpr int G = 64 / H;
-            const int sl = lane / G, g = lane % G;
-            const uint32_t hs = blockIdx.x * H + sl;
-            const bool act = hs < nh;
-            bool open = act;
-            int won = -1;
-            RectModel best = default_model();
-            for (uint32_t rr = 0; rr * G < 101; ++rr) {
-                if (__ballot(open) == 0) break;
-                const uint32_t a = rr * G + g;
-                RectModel m = default_model();
-                bool ok = false;
-                if (open && a < 101)
-                    ok = (gen.probe & 8u) ? a == 0 : attempt<KIND>(p, gen.seed, gen.slot0 + nh + hs, a, m);
-                const uint64_t bm = __ballot(ok);
-                const uint64_t grp = (bm >> (sl * G)) & ((G == 64) ? ~0ull : ((1ull << G) - 1ull));
-                if (open && grp != 0) {
-                    open = false;
-                    if (g == __builtin_ctzll(grp)) {
-                        won = (int)a;
-                        best = m;
+            const uint32_t hs0 = blockIdx.x * H;
+            const uint32_t live = hs0 < nh ? min((uint32_t)H, nh - hs0) : 0u;
+            uint64_t pend = live >= 64u ? ~0ull : (1ull << live) - 1ull;
+            uint32_t nx = 0;                    // wave-uniform lowest untried attempt
+            while (pend) {
+                const int k = __builtin_popcountll(pend);
+                const int lw = 6 - (k == 1 ? 0 : 32 - __builtin_clz((uint32_t)(k - 1)));
+                const int j = lane >> lw;
+                const uint32_t a = nx + (uint32_t)(lane & ((1 << lw) - 1));
+                int si = -1;                    // this lane's slot: the j-th unfinished one
+                {
+                    uint64_t m = pend;
+                    for (int c = 0; m; ++c) {
+                        const int i = __builtin_ctzll(m);
+                        m &= m - 1;
+                        si = c == j ? i : si;
                     }
                 }
-            }
-            if (act && won >= 0) {
-                gen.chain.next_inc[hs] = (uint8_t)(won + 1);
-                gen.chain.next_models[hs] = best;
-            } else if (act && g == 0 && open) {
-                // every attempt failed (inc 102, no model)
-                gen.chain.next_inc[hs] = 102;
-                gen.chain.next_models[hs] = default_model();
+                RectModel m = default_model();
+                bool ok = false;
+                if (si >= 0 && a < 101)
+                    ok = (gen.probe & 8u) ? a == 0
+                                          : attempt<KIND>(p, gen.seed, gen.slot0 + nh + hs0 + (uint32_t)si, a, m);
+                const uint64_t mask = __ballot(ok);
+                nx += 1u << lw;
+                const bool out_of_attempts = nx >= 101;
+                uint64_t np = out_of_attempts ? 0ull : pend;
+                bool win = false;
+                {
+                    uint64_t mm = pend;
+                    for (int c = 0; mm; ++c) {
+                        const int i = __builtin_ctzll(mm);
+                        mm &= mm - 1;
+                        const uint64_t grp = lw == 6 ? mask : (mask >> (c << lw)) & ((1ull << (1 << lw)) - 1ull);
+                        if (grp) {
+                            np &= ~(1ull << i);
+                            win |= lane == (c << lw) + __builtin_ctzll(grp);
+                        }
+                    }
+                }
+                const uint64_t gm = lw == 6 ? ~0ull : ((1ull << (1 << lw)) - 1ull);
+                const bool fail = out_of_attempts && si >= 0 && !((mask >> (j << lw)) & gm) &&
+                                  (lane & ((1 << lw) - 1)) == 0;
+                pend = np;
+                const uint32_t hs = hs0 + (uint32_t)si;
+                if (win) {
+                    gen.chain.next_inc[hs] = (uint8_t)(a + 1);
+                    gen.chain.next_models[hs] = m;
+                } else if (fail) {              // every attempt failed (inc 102, no model)
+                    gen.chain.next_inc[hs] = 102;
+                    gen.chain.next_models[hs] = default_model();
+                }
             }
             return;
         }
@@ -3400,33 +3427,28 @@ namespace gcr {
 
 // --------------------------------------------------------- HBM peak probe ----
 // Streaming copy used by bench.py to measure the box's achievable HBM
-// bandwidth (the roofline's measured peak beside the 8 TB/s spec).  16-byte
-// loads and stores, a grid-stride loop with 8 independent strips per thread in
-// flight; NT = nontemporal hints (the probe reports the better of the two).
+// bandwidth (the roofline's measured peak beside the 8 TB/s spec).  One 16-byte
+// load and store per lane and one 4 KB tile per workgroup, a grid of n / 256
+// workgroups (no grid-stride loop): the hardware keeps every CU's queue full.
+// Measured on MI355X (tools/micro/hbm_copy.hip, 2 GiB, read + write bytes):
+// this shape 6.24 TB/s; grid-stride loops with 2-8 strips in flight per lane
+// 4.6-5.5 TB/s; tiles of 2-8 strips per lane 5.4-5.9 TB/s.  NT = nontemporal
+// hints (the probe reports the better of the two).
 typedef double hbm_v2d __attribute__((ext_vector_type(2)));
 template <bool NT>
 __global__ __launch_bounds__(256) void k_hbm_copy(const hbm_v2d* __restrict__ src, hbm_v2d* __restrict__ dst,
                                                   size_t n) {
-    constexpr int U = 8;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + (U - 1) * stride < n; i += U * stride) {
-        hbm_v2d v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + u * stride) : src[i + u * stride];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (NT) __builtin_nontemporal_store(v[u], dst + i + u * stride);
-            else dst[i + u * stride] = v[u];
-        }
-    }
-    for (; i < n; i += stride) dst[i] = src[i];
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    if (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    else dst[i] = src[i];
 }
 
 hipError_t launch_hbm_copy(const void* src, void* dst, size_t bytes, int nontemporal, hipStream_t stream) {
     const size_t n = bytes / sizeof(hbm_v2d);
     if (n == 0) return hipSuccess;
-    const dim3 grid(256 * 8), block(256);
+    if ((n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
     if (nontemporal)
         hipLaunchKernelGGL(k_hbm_copy<true>, grid, block, 0, stream, static_cast<const hbm_v2d*>(src),
                            static_cast<hbm_v2d*>(dst), n);

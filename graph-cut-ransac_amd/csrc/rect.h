@@ -99,9 +99,19 @@ GCR_HD double orient_sq_residual(double x, double y, double ct, double st, const
         px = m.s * (x - m.x0 * 1.0);
         py = m.s * (y - m.y0 * 1.0);
     }
-    const double th = rectified_angle(px, py, ct, st, m.h7, m.h8);
-    const double c0 = dm::clip_angle_small(th);                // th in [0, 2 pi]
-    const double c1 = dm::clip_angle_small(th - kPi);
+    // rectifiedAngle's clipAngle(atan2) and linesAnglesDiff's clipAngle(th),
+    // clipAngle(th - pi), with the ranges known: atan2 lies in [-pi, pi] (or is
+    // NaN), so th = clipAngle(atan2) is one conditional + 2 pi and lies in
+    // [0, 2 pi]; clipAngle(th) is th except 0 for th == 2 pi (a tiny negative
+    // atan2 rounds up to it); th - pi lies in [-pi, pi].  The same values as
+    // clip_angle_small on each (NaN stays NaN), with fewer operations.
+    const double numer = (-px * st + py * ct) * m.h7 + st;
+    const double denom = (px * st - py * ct) * m.h8 + ct;
+    const double a = dm::dm_atan2(numer, denom);
+    const double th = a < 0.0 ? a + kTwoPi : a;
+    const double c0 = th == kTwoPi ? 0.0 : th;
+    const double dpi = th - kPi;
+    const double c1 = dpi < 0.0 ? dpi + kTwoPi : dpi;
     const double l1 = __builtin_fmin(min_angle_diff_c(oc.cphi, c0), min_angle_diff_c(oc.cphi, c1));
     const double l2 = __builtin_fmin(min_angle_diff_c(oc.cphi2, c0), min_angle_diff_c(oc.cphi2, c1));
     const double r = __builtin_fmin(l1, l2);

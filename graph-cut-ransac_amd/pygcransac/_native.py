@@ -117,6 +117,7 @@ def _load():
     L.gcr_last_error.restype = C.c_char_p
     L.gcr_abi_version.restype = C.c_int
     L.gcr_device_count.restype = C.c_int
+    L.gcr_kernel_build_id.restype = C.c_char_p
     L.gcr_create.argtypes = [C.c_int, C.POINTER(vp)]
     L.gcr_synchronize.argtypes = [vp]
     L.gcr_destroy.argtypes = [vp]

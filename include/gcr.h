@@ -113,6 +113,9 @@ typedef struct gcr_stats {
 const char* gcr_last_error(void);
 int gcr_abi_version(void);
 int gcr_device_count(void);
+/* SHA-256 prefix (16 hex) of the sources the GPU code object was built from
+ * (kernels.hip + device headers + build flags); profiles are keyed by it */
+const char* gcr_kernel_build_id(void);
 int gcr_create(int device, gcr_ctx** out);
 void gcr_destroy(gcr_ctx* ctx);
 /* hipDeviceSynchronize on the context's device */

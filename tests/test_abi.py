@@ -54,6 +54,11 @@ def test_errors_cross_the_abi_as_codes_not_exceptions():
     assert rc == N.GCR_EINVAL
 
 
+def test_kernel_build_id_is_the_source_hash():
+    bid = N.lib.gcr_kernel_build_id().decode()
+    assert len(bid) == 16 and int(bid, 16) >= 0
+
+
 def test_host_hooks_need_no_gpu():
     assert N.lib.gcr_host_log(1.0) == 0.0
     assert N.lib.gcr_host_pow_m3(2.0) == 0.125

@@ -39,8 +39,10 @@ def _digest(res):
                 hyp=st["hypotheses"], score=bits(st["score"]).tolist(), rec=bits(rec).tolist())
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, env=None):
     import torch.distributed as dist
+
+    os.environ.update(env or {})
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -61,17 +63,34 @@ def _free_port():
 
 
 @pytest.mark.timeout(600)
-def test_sharded_problem_equals_single_rank(tmp_path):
+@pytest.mark.parametrize("world,env", [
+    (2, {}),
+    # a two-member summary cap: chains continue on the owner's device, every
+    # rank joins each continuation exchange
+    (2, {"GCR_SUMMARY_CAP": "2"}),
+    # three ranks, the per-slot exchange of round 2 (GCR_REPLAY=slots) as reference
+    (3, {}),
+])
+def test_sharded_problem_equals_single_rank(tmp_path, world, env):
     if N.lib.gcr_device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
-    world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), env), nprocs=world, join=True)
     outs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
-    for name, solver, f0, f1, prm in _cases():
-        ref = json.loads(json.dumps(_digest(D.run_problem_sharded(solver, f0, f1, prm, device=0))))
-        assert outs[0][name] == ref, name
-        assert outs[1][name] == ref, name
-        assert ref["H"] is not None and ref["hyp"] > 0
+    saved = {k: os.environ.get(k) for k in ("GCR_REPLAY",)}
+    try:
+        if world == 3:
+            os.environ["GCR_REPLAY"] = "slots"
+        for name, solver, f0, f1, prm in _cases():
+            ref = json.loads(json.dumps(_digest(D.run_problem_sharded(solver, f0, f1, prm, device=0))))
+            for r in range(world):
+                assert outs[r][name] == ref, (name, r)
+            assert ref["H"] is not None and ref["hyp"] > 0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def test_single_rank_entry_equals_public_api():

@@ -1,7 +1,13 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc passes: mean counter value per dispatch, per kernel.
 
-usage: tools/pmc_summary.py gpurun_out/pmc [--slots N --traffic-json profiles/pmc_traffic.json] > profiles/<name>.csv
+usage: tools/pmc_summary.py gpurun_out/pmc [--slots N --traffic-json profiles/pmc_traffic.json
+                                           --stats <rocprofv3 kernel_stats.csv of the same command>]
+                                           > profiles/<name>.csv
+
+Each traffic-json entry records the kernel build it was collected from
+(`kernel_build_id`, read from the bench JSON line the passes printed), so
+bench.py never reuses counters of an older build of the kernels.
 
 FETCH_SIZE is reported as measured (KiB) and corrected: MI355X_MICROARCH.md's
 HBM section notes gfx950 under-reports wide streaming reads by 2x, so the
@@ -20,7 +26,34 @@ def short(name):
     return m.group(1) if m else name[:60]
 
 
-def main(root, slots=None, traffic_json=None):
+def build_id_of(root):
+    """kernel_build_id of the bench line printed by the passes (all must agree)."""
+    import json
+    ids = set()
+    for path in glob.glob(os.path.join(root, "pass*.log")):
+        with open(path) as f:
+            for ln in f:
+                if ln.startswith("{") and "kernel_build_id" in ln:
+                    try:
+                        ids.add(json.loads(ln)["roofline"]["kernel_build_id"])
+                    except (ValueError, KeyError, TypeError):
+                        pass
+    if len(ids) != 1:
+        raise SystemExit(f"expected one kernel_build_id in {root}/pass*.log, found {sorted(ids)}")
+    return ids.pop()
+
+
+def stats_avg_ms(stats_csv):
+    """kernel -> average duration (ms) from a rocprofv3 --stats kernel_stats.csv."""
+    out = {}
+    if stats_csv:
+        with open(stats_csv) as f:
+            for row in csv.DictReader(f):
+                out[short(row["Name"])] = float(row["AverageNs"]) / 1e6
+    return out
+
+
+def main(root, slots=None, traffic_json=None, stats_csv=None):
     vals = defaultdict(lambda: defaultdict(list))
     for path in sorted(glob.glob(os.path.join(root, "pass*", "*counter_collection.csv"))):
         with open(path) as f:
@@ -42,6 +75,8 @@ def main(root, slots=None, traffic_json=None):
                 table = json.load(f)
         except (OSError, ValueError):
             table = {}
+        bid = build_id_of(root)
+        avg = stats_avg_ms(stats_csv)
         for k in vals:
             if "FETCH_SIZE" not in vals[k] or not k.startswith("k_score"):
                 continue
@@ -49,7 +84,9 @@ def main(root, slots=None, traffic_json=None):
             wr = vals[k].get("WRITE_SIZE")
             wrb = 1024 * sum(wr) / len(wr) if wr else 0.0
             ent = {"hbm_bytes_per_launch": rd + wrb, "read_bytes": rd, "write_bytes": wrb,
-                   "source": os.path.normpath(root)}
+                   "source": os.path.normpath(root), "kernel_build_id": bid}
+            if k in avg:
+                ent["rocprof_avg_ms"] = avg[k]
             # VALU view (bench.py "valu"): instructions issued and active VALU
             # quad-cycles per launch, when that pass was collected
             for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
@@ -66,5 +103,6 @@ if __name__ == "__main__":
     ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
     ap.add_argument("--slots", type=int)
     ap.add_argument("--traffic-json")
+    ap.add_argument("--stats")
     a = ap.parse_args()
-    main(a.root, a.slots, a.traffic_json)
+    main(a.root, a.slots, a.traffic_json, a.stats)
