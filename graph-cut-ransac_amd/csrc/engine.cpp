@@ -236,6 +236,8 @@ struct Workspace {
     DevBuf<QRFState> rf_qrf;            // GPU refit: fused-pass QR driver state
     PinBuf<double> rf_hpart;
     PinBuf<double> rf_htop;             // GPU refit: async upload ring
+    DevBuf<DD> rf_gram;                 // GPU refit (Gram path): per-tile double-double sums
+    PinBuf<DD> rf_hgram;                //   and their pinned host image
     // the next chunk of slots, generated and scored on the side stream while
     // the host replays the current one (RunnerT prefetch); swapped in whole
     DevBuf<uint8_t> pf_inc;
@@ -473,6 +475,31 @@ struct GpuSiftSolver final : SiftSystemSolver {
         st.prepare();
         qr3_solve(st, rows, x);
         HIPC(hipStreamSynchronize(s));          // the pinned ring must outlive its uploads
+    }
+    // the double-double Gram matrix of the same rows (gram.h): one kernel
+    // builds every row once and reduces it in its tile, the tiles come back
+    // through pinned memory and are added here in order
+    bool gram(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows, DD g[kGramN]) override {
+        hipStream_t s = P->ctx->stream;
+        const size_t ns = si.size(), no = oi.size();
+        const size_t all_s = P->dp.cls[0].n, all_o = P->dp.cls[1].n;
+        const size_t rows_max = std::max(rows, all_s + all_o * (all_o - (all_o > 0)) / 2);
+        const size_t tiles_max = (rows_max + kGramTile - 1) / kGramTile, tiles = (rows + kGramTile - 1) / kGramTile;
+        P->w->rf_idx.ensure(all_s + all_o);
+        P->w->rf_hidx.ensure(all_s + all_o);
+        P->w->rf_gram.ensure(tiles_max * kGramN);
+        P->w->rf_hgram.ensure(tiles_max * kGramN);
+        std::memcpy(P->w->rf_hidx.p, si.data(), ns * sizeof(uint32_t));
+        std::memcpy(P->w->rf_hidx.p + ns, oi.data(), no * sizeof(uint32_t));
+        HIPC(hipMemcpyAsync(P->w->rf_idx.p, P->w->rf_hidx.p, (ns + no) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIPC(launch_sift_gram(P->dp.cls[0], P->dp.cls[1], P->w->rf_idx.p, (uint32_t)ns, P->w->rf_idx.p + ns,
+                              (uint32_t)no, rows, P->w->rf_gram.p, s));
+        HIPC(hipMemcpyAsync(P->w->rf_hgram.p, P->w->rf_gram.p, tiles * kGramN * sizeof(DD), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        for (int k = 0; k < kGramN; ++k) g[k] = DD{0.0, 0.0};
+        for (size_t t = 0; t < tiles; ++t)
+            for (int k = 0; k < kGramN; ++k) g[k] = dd_add(g[k], P->w->rf_hgram.p[t * kGramN + k]);
+        return true;
     }
     void for_ranges(size_t n, const std::function<void(size_t, size_t)>& fn) override;
 };
@@ -1397,11 +1424,14 @@ public:
             // the next slot's loop condition
             uint64_t cur_slot = ~0ull;
             bool slot_lo = false;
+            double lo_ms = 0.0;               // LO time inside this chunk's replay (reported as ms_lo)
             auto flush_lo = [&]() {
                 if (do_lo_ && slot_lo) {
+                    const auto t_lo = Clock::now();
                     ++lo_number_;
                     local_optimization(bufs_[off_]);
                     max_iteration = iteration_number(best_.n);
+                    lo_ms += ms_since(t_lo);
                 }
                 slot_lo = false;
             };
@@ -1479,7 +1509,7 @@ public:
                             break;
                         }
                 }
-                replay_ms += ms_since(t_rep);
+                replay_ms += ms_since(t_rep) - lo_ms;
                 break;
             }
             // the whole chunk was processed
@@ -1493,7 +1523,7 @@ public:
                     break;
                 }
             q.erase(q.begin());
-            replay_ms += ms_since(t_rep);
+            replay_ms += ms_since(t_rep) - lo_ms;
         }
         // chunks issued ahead that the loop never reached
         for (const Chunk& c : q) HIPC(hipEventSynchronize(w->sum_done[c.set]));

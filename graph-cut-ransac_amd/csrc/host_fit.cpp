@@ -181,6 +181,98 @@ void sift_rows_host(const HostClass& sc, const HostClass& oc, const std::vector<
     }
 }
 
+}  // namespace
+
+bool gram_refit_on() {
+    const char* e = getenv("GCR_REFIT");              // read per fit (tests switch it)
+    return !(e && e[0] == 'q');
+}
+
+void gram_sift_host(const HostClass& sc, const HostClass& oc, const std::vector<uint32_t>& si,
+                    const std::vector<uint32_t>& oi, size_t rows, DD g[kGramN]) {
+    const size_t ns = si.size(), no = oi.size();
+    for (int k = 0; k < kGramN; ++k) g[k] = DD{0.0, 0.0};
+    std::vector<DD> lane((size_t)kGramLanes * kGramN);
+    for (size_t base = 0; base < rows; base += kGramTile) {
+        for (auto& v : lane) v = DD{0.0, 0.0};
+        for (int l = 0; l < kGramLanes; ++l) {
+            DD* acc = &lane[(size_t)l * kGramN];
+            for (size_t u = 0; u < kGramTile / kGramLanes; ++u) {
+                const size_t r = base + (size_t)l + (size_t)kGramLanes * u;
+                if (r >= rows) break;
+                double row[4];
+                if (r < ns) {
+                    const uint32_t j = si[r];
+                    const double w = 1.0;
+                    row[0] = w * sc.x[j];
+                    row[1] = w * sc.y[j];
+                    row[2] = w * sc.c0[j];
+                    row[3] = w;
+                } else {
+                    uint64_t i, j;
+                    pair_of(r - ns, no, i, j);
+                    const uint32_t a = oi[i], c = oi[j];
+                    sift_pair_row(oc.x[a], oc.y[a], oc.c0[a], oc.c1[a], oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], row);
+                }
+                gram_add_row(acc, row);
+            }
+        }
+        for (int h = kGramLanes / 2; h >= 1; h >>= 1)
+            for (int l = 0; l < h; ++l)
+                for (int k = 0; k < kGramN; ++k)
+                    lane[(size_t)l * kGramN + k] = dd_add(lane[(size_t)l * kGramN + k], lane[(size_t)(l + h) * kGramN + k]);
+        for (int k = 0; k < kGramN; ++k) g[k] = dd_add(g[k], lane[k]);
+    }
+}
+
+void gram_solve3(const DD g[kGramN], size_t rows, double x[3]) {
+    // S: the Gram matrix of [A | b], updated to its Schur complements
+    DD S[4][4];
+    for (int a = 0; a < 4; ++a)
+        for (int b = 0; b < 4; ++b) S[a][b] = g[gram_index(a, b)];
+    int ord[3] = {0, 1, 2};                  // pivot order: stored column of step k
+    const double eps = std::numeric_limits<double>::epsilon();
+    double maxn = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const double nk = dd_sqrt(S[k][k]).hi;
+        if (k == 0 || maxn < nk) maxn = nk;
+    }
+    const double thr_helper = ((maxn * eps) * (maxn * eps)) / (double)rows;
+    int nonzero = 3;
+    DD R[3][4];                              // R[k][c]: row k of R at stored column c (c = 3: Q^T b)
+    for (int k = 0; k < 3; ++k) {
+        // the largest remaining squared column norm, first on ties
+        int big = k;
+        for (int j = k + 1; j < 3; ++j)
+            if (dd_lt(S[ord[big]][ord[big]], S[ord[j]][ord[j]])) big = j;
+        const double big_sq = S[ord[big]][ord[big]].hi;
+        if (nonzero == 3 && big_sq < thr_helper * (double)(rows - (size_t)k)) nonzero = k;
+        std::swap(ord[k], ord[big]);
+        const int p = ord[k];
+        const DD rkk = dd_sqrt(S[p][p]);
+        R[k][p] = rkk;
+        int rest[3], nr = 0;                 // the remaining stored columns and b
+        for (int j = k + 1; j < 3; ++j) rest[nr++] = ord[j];
+        rest[nr++] = 3;
+        for (int q = 0; q < nr; ++q) R[k][rest[q]] = rkk.hi > 0.0 ? dd_div(S[p][rest[q]], rkk) : DD{0.0, 0.0};
+        // Schur complement of the remaining columns and b
+        for (int a = 0; a < nr; ++a)
+            for (int b = a; b < nr; ++b) {
+                const int ca = rest[a], cb = rest[b];
+                S[ca][cb] = dd_sub(S[ca][cb], dd_mul(R[k][ca], R[k][cb]));
+                S[cb][ca] = S[ca][cb];
+            }
+    }
+    DD c[3] = {R[0][3], R[1][3], R[2][3]};
+    for (int jj = nonzero - 1; jj >= 0; --jj) {
+        c[jj] = dd_div(c[jj], R[jj][ord[jj]]);
+        for (int i = 0; i < jj; ++i) c[i] = dd_sub(c[i], dd_mul(c[jj], R[i][ord[jj]]));
+    }
+    for (int k = 0; k < 3; ++k) x[ord[k]] = k < nonzero ? c[k].hi : 0.0;
+}
+
+namespace {
+
 bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectModel& out, SiftSystemSolver* big,
                 size_t big_rows) {
     const HostClass& sc = cls[0];
@@ -199,7 +291,11 @@ bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectMode
     }
     const size_t rows = ns + npairs;
     double sol[3];
-    if (big && rows >= big_rows) {
+    if (rows >= kGramRows && gram_refit_on()) {
+        DD g[kGramN];
+        if (!(big && big->gram(si, oi, rows, g))) gram_sift_host(sc, oc, si, oi, rows, g);
+        gram_solve3(g, rows, sol);
+    } else if (big && rows >= big_rows) {
         big->solve(si, oi, rows, sol);
     } else {
         std::vector<double> A(rows * 3), b(rows);

@@ -11,6 +11,7 @@
 
 #include "fund.h"
 #include "geo.h"
+#include "gram.h"
 #include "rect.h"
 
 namespace gcr {
@@ -36,6 +37,10 @@ struct SiftSystemSolver {
     virtual ~SiftSystemSolver() = default;
     virtual void solve(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows,
                        double x[3]) = 0;
+    // the double-double Gram matrix of the same rows (gram.h order), ten
+    // entries; false: not available here (the host computes it)
+    virtual bool gram(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows,
+                      DD g[kGramN]) { return false; }
     // fn(lo, hi) over [0, n) in disjoint ranges, possibly in parallel (the
     // per-inlier work around a big solve); the default runs it in one piece
     virtual void for_ranges(size_t n, const std::function<void(size_t, size_t)>& fn) { fn(0, n); }
@@ -67,6 +72,16 @@ void jacobi_eigen(double (&a)[N][N], double (&v)[N][N], double (&d)[N]);
 
 // findWeightedMode (two_sift.hpp:354-394), libstdc++ unordered_map order.
 double weighted_mode(const std::vector<double>& angles, const std::vector<double>& weights, double bin_width);
+
+// The hybrid system's Gram matrix on the host, in gram.h's order (tiles,
+// 256 lanes, halving tree, tiles in order): bit-identical to the GPU kernel.
+void gram_sift_host(const HostClass& sc, const HostClass& oc, const std::vector<uint32_t>& si,
+                    const std::vector<uint32_t>& oi, size_t rows, DD g[kGramN]);
+// min |A x - b| from the Gram matrix of [A | b] (gram.h): column-pivoted
+// Cholesky in double-double with Eigen's pivot rule and rank threshold.
+void gram_solve3(const DD g[kGramN], size_t rows, double x[3]);
+// GCR_REFIT=qr: big hybrid systems by Householder QR (round 2) instead
+bool gram_refit_on();
 
 // RectifyingHomography::getHomography (model.h:211-226), row-major, / H22.
 void homography_of(const RectModel& m, double H[9]);

@@ -6,6 +6,7 @@
 
 #include "fund.h"
 #include "geo.h"
+#include "gram.h"
 #include "rect.h"
 #include "summary.h"
 
@@ -101,6 +102,11 @@ hipError_t launch_select(int solver, const ScoreOut& sc, const uint8_t* inc, con
 hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns,
                             const uint32_t* oi, uint32_t no, size_t rows, double* A0, double* A1, double* A2,
                             double* b, hipStream_t stream);
+// The hybrid system's double-double Gram matrix in gram.h's order: tile t's
+// kGramN entries at tiles[t * kGramN ..] (ceil(rows / kGramTile) tiles); the
+// caller adds the tiles in order.
+hipError_t launch_sift_gram(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns, const uint32_t* oi,
+                            uint32_t no, size_t rows, DD* tiles, hipStream_t stream);
 // Block partials of sum_{i in [lo, hi)} a[i] * c[i] for the aligned blocks of
 // kSumBlock (qr3.h) rows that intersect [lo, hi), each summed in row order;
 // partials[0 .. nblocks) in block order.  Returns the block count via nblocks.

@@ -2072,6 +2072,73 @@ __device__ __forceinline__ void sift_row_at(const DevClass& sc, const DevClass& 
     sift_pair_row(oc.x[a], oc.y[a], oc.c0[a], oc.c1[a], oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], out);
 }
 
+// The hybrid system's double-double Gram matrix (gram.h): one workgroup per
+// tile of kGramTile rows, lane l accumulating rows tile + l + 256 u; each
+// lane's pair index advances by 256 pairs per step (a carry into the next
+// first index when it runs past the end of a row), so the pair decode runs
+// once per lane; the first index's feature stays in registers.  The 256 lane
+// sums are combined by gram.h's halving tree in LDS.
+constexpr int kGramBlock = kGramLanes;
+__global__ __launch_bounds__(kGramBlock) void k_sift_gram(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
+                                                          uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no,
+                                                          uint64_t rows, DD* __restrict__ tiles) {
+    __shared__ DD red[kGramN][kGramBlock];
+    const int l = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * kGramTile;
+    DD acc[kGramN];
+#pragma unroll
+    for (int k = 0; k < kGramN; ++k) acc[k] = DD{0.0, 0.0};
+    bool have = false;
+    uint64_t pi = 0, pj = 0, ci = ~0ull;
+    double xi = 0.0, yi = 0.0, cosi = 0.0, sini = 0.0;
+    for (uint32_t u = 0; u < (uint32_t)(kGramTile / kGramLanes); ++u) {
+        const uint64_t r = base + (uint64_t)l + (uint64_t)kGramLanes * u;
+        if (r >= rows) break;
+        double row[4];
+        if (r < ns) {
+            const uint32_t j = si[r];
+            const double w = 1.0;
+            row[0] = w * sc.x[j];
+            row[1] = w * sc.y[j];
+            row[2] = w * sc.c0[j];
+            row[3] = w;
+        } else {
+            if (!have) {
+                pair_of(r - ns, no, pi, pj);
+                have = true;
+            } else {
+                pj += kGramLanes;
+                while (pj >= no) {
+                    pj = pj - no + pi + 2;
+                    ++pi;
+                }
+            }
+            if (pi != ci) {
+                const uint32_t a = oi[pi];
+                xi = oc.x[a];
+                yi = oc.y[a];
+                cosi = oc.c0[a];
+                sini = oc.c1[a];
+                ci = pi;
+            }
+            const uint32_t c = oi[pj];
+            sift_pair_row(xi, yi, cosi, sini, oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], row);
+        }
+        gram_add_row(acc, row);
+    }
+#pragma unroll
+    for (int k = 0; k < kGramN; ++k) red[k][l] = acc[k];
+    __syncthreads();
+    for (int h = kGramBlock / 2; h >= 1; h >>= 1) {
+        if (l < h) {
+#pragma unroll
+            for (int k = 0; k < kGramN; ++k) red[k][l] = dd_add(red[k][l], red[k][l + h]);
+        }
+        __syncthreads();
+    }
+    if (l < kGramN) tiles[(size_t)blockIdx.x * kGramN + l] = red[l][0];
+}
+
 __global__ __launch_bounds__(kRowBlock) void k_sift_rows(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
                                                          uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no,
                                                          uint64_t rows, double* A0, double* A1, double* A2,
@@ -3017,6 +3084,14 @@ hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32
     if (rows == 0) return hipSuccess;
     hipLaunchKernelGGL(k_sift_rows, dim3((unsigned)((rows + kRowBlock - 1) / kRowBlock)), dim3(kRowBlock), 0, stream,
                        sc, oc, si, ns, oi, no, (uint64_t)rows, A0, A1, A2, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_sift_gram(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns, const uint32_t* oi,
+                            uint32_t no, size_t rows, DD* tiles, hipStream_t stream) {
+    if (rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sift_gram, dim3((unsigned)((rows + kGramTile - 1) / kGramTile)), dim3(kGramBlock), 0, stream,
+                       sc, oc, si, ns, oi, no, (uint64_t)rows, tiles);
     return hipGetLastError();
 }
 

@@ -396,16 +396,20 @@ def test_gpu_solver_records_match_direct_calls():
 
 # ------------------------------------------------------------ GPU refit ----
 @pytest.mark.parametrize("ks,ko", [(40, 46), (800, 120), (2000, 260), (2500, 2500), (0, 300), (3, 1200)])
-@pytest.mark.parametrize("qr_mode", ["fused", "device", "host"])
-def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko, qr_mode, monkeypatch):
-    # the hybrid least-squares system (ns + C(no,2) rows, up to 3.1 M) built and
-    # solved on the GPU equals the host path and the oracle bit for bit, with
-    # the QR driver on the device in fused passes (launch_qr_fused), on the
-    # device one pass per step (launch_qr_device) or on the host.  ks = 0:
-    # column 2 is all zeros (pair rows have no scale term), so step 2 takes
-    # the rank-deficient branches (nonzero = 2, tau = 0)
-    monkeypatch.setenv("GCR_QR_DEVICE", "0" if qr_mode == "host" else "1")
-    monkeypatch.setenv("GCR_QR_FUSED", "1" if qr_mode == "fused" else "0")
+@pytest.mark.parametrize("refit", ["gram", "qr-fused", "qr-device", "qr-host"])
+def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko, refit, monkeypatch):
+    # the hybrid least-squares system (ns + C(no,2) rows, up to 3.1 M) solved
+    # on the GPU equals the host path bit for bit.  Default ("gram", systems
+    # of >= 32768 rows): the double-double Gram matrix built by one kernel
+    # (gram.h), solved by pivoted Cholesky -- also equal to the oracle's
+    # restatement.  GCR_REFIT=qr: the Householder QR of round 2 with its
+    # driver on the device in fused passes, one pass per step, or on the host.
+    # ks = 0: column 2 is all zeros (pair rows have no scale term), the
+    # rank-deficient branches (nonzero = 2)
+    if refit != "gram":
+        monkeypatch.setenv("GCR_REFIT", "qr")
+    monkeypatch.setenv("GCR_QR_DEVICE", "0" if refit == "qr-host" else "1")
+    monkeypatch.setenv("GCR_QR_FUSED", "1" if refit == "qr-fused" else "0")
     fs, fo, ts, to, _, _ = S.problem_m2(5000, 5000, seed=ks + 3 * ko)
     rng = np.random.default_rng(ks + ko)
     i0 = np.sort(rng.choice(np.flatnonzero(ts), size=ks, replace=False)).astype(np.uint32)
@@ -423,9 +427,16 @@ def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko, qr_mode, monkeypatch)
     if ks > 0:
         assert rcs[0] == 1
     assert np.array_equal(bits(out[0]), bits(out[1]))
-    if ko <= 300 and rcs[0] == 1:
+    rows = ks + ko * (ko - 1) // 2
+    if ko <= 300 and rcs[0] == 1 and (refit == "gram" or rows < 32768):
         exp = O.fit_nonminimal(N.SOLVER_SIFT22, fs, fo, i0, i1)
         assert np.array_equal(bits(out[0]), bits(exp))
+    if rcs[0] == 1:
+        # either solve within the frozen pin's tolerance of the sequential
+        # Householder order
+        with O.qr_order(O.QR_FROZEN):
+            frz = O.fit_nonminimal(N.SOLVER_SIFT22, fs, fo, i0, i1)
+        assert np.all(np.abs(out[0] - frz) <= 1e-6 * np.maximum(np.abs(frz), 1e-12))
 
 
 # --------------------------------------------- band prefilter, adversarial ----

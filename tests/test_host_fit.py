@@ -46,9 +46,12 @@ def test_scale_fit_matches_oracle_bitwise(kind, k):
         assert np.array_equal(got.view(np.uint64), exp.view(np.uint64))
 
 
-@pytest.mark.parametrize("ks,ko", [(2, 2), (3, 2), (14, 14), (60, 45), (500, 46), (800, 120), (2000, 260)])
+@pytest.mark.parametrize("ks,ko", [(2, 2), (3, 2), (14, 14), (60, 45), (500, 46), (800, 120), (2000, 260),
+                                   (0, 300), (3, 600)])
 def test_sift_fit_matches_oracle_bitwise(ks, ko):
-    # ko = 46 -> 1035 pair rows (blocked order starts); 260 -> 33 670 rows
+    # ko = 46 -> 1035 pair rows (blocked order starts); 260 -> 33 670 rows:
+    # >= 32768 rows take the double-double Gram path (gram.h); (0, 300): no
+    # scale rows, the rank-deficient pivot branch
     fs, fo, ts, to, _, _ = S.problem_m2(5000, 3000, seed=ks + ko)
     rng = np.random.default_rng(ks * 7 + ko)
     i0 = np.sort(rng.choice(np.flatnonzero(ts), size=ks, replace=False))
@@ -59,6 +62,10 @@ def test_sift_fit_matches_oracle_bitwise(ks, ko):
         assert got is None
     else:
         assert np.array_equal(got.view(np.uint64), exp.view(np.uint64))
+        # and within the frozen pin's tolerance of the sequential Householder order
+        with O.qr_order(O.QR_FROZEN):
+            frz = O.fit_nonminimal(N.SOLVER_SIFT22, fs, fo, i0, i1)
+        assert np.all(np.abs(got - frz) <= 1e-6 * np.maximum(np.abs(frz), 1e-12))
 
 
 def test_weighted_mode_matches_oracle_including_ties():
