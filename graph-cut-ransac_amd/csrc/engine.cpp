@@ -36,6 +36,7 @@
 #include <string>
 #include <vector>
 #include <thread>
+#include <map>
 #include <mutex>
 #include <atomic>
 #include <exception>
@@ -260,6 +261,7 @@ struct Workspace {
     DevBuf<double> cs_vals[2];
     DevBuf<uint64_t> cs_bits[2];
     hipEvent_t sum_done[2] = {nullptr, nullptr}, sum_k0[2] = {nullptr, nullptr}, sum_k1[2] = {nullptr, nullptr};
+    bool spec_pending[2] = {false, false};   // a speculative chunk of this set may still run
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
         for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start, vb_flush, sum_done[0],
@@ -509,6 +511,10 @@ struct GpuSiftSolver final : SiftSystemSolver {
 // does not depend on the scheduling).  Size: GCR_HOST_THREADS, default
 // min(16, hardware threads) -- one GPU's CPU share on an MI355X node; the
 // 50 LO fits of a graph-cut round take 42 us on 16 threads, 70 on 8.
+// host threads currently solving problems inside gcr_solve_batch (the pool's
+// workers do not spin while several of them share the cores)
+std::atomic<int> g_solving{0};
+
 class HostPool {
 public:
     explicit HostPool(unsigned n) {
@@ -571,20 +577,30 @@ private:
             next_.store(n_);                      // stop handing out work
         }
     }
-    // A worker polls for the next job for ~kSpinUs after finishing one (the
+    // A worker polls for the next job for ~spin_us() after finishing one (the
     // LO rounds call the pool every ~100 us: a condition-variable wake-up of
-    // 15 threads costs tens of us per call), then blocks.
-    static constexpr int64_t kSpinUs = 300;
+    // 15 threads costs tens of us per call), then blocks.  GCR_POOL_SPIN_US
+    // sets the window (default 300, 0 = always block); while more than one
+    // thread of gcr_solve_batch is solving, workers block at once (their
+    // spinning would take cores from those threads).
+    static int64_t spin_us() {
+        static const int64_t us = [] {
+            const char* e = getenv("GCR_POOL_SPIN_US");
+            return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)300;
+        }();
+        return g_solving.load(std::memory_order_relaxed) > 1 ? 0 : us;
+    }
     void loop() {
         uint64_t seen = 0;
         for (;;) {
             uint64_t g = gen_.load(std::memory_order_acquire);
             if (g == seen) {
                 const auto t0 = Clock::now();
+                const int64_t window = spin_us();
                 unsigned k = 0;
-                while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+                while (window > 0 && (g = gen_.load(std::memory_order_acquire)) == seen) {
                     if ((++k & 255) == 0 &&
-                        std::chrono::duration_cast<std::chrono::microseconds>(Clock::now() - t0).count() > kSpinUs)
+                        std::chrono::duration_cast<std::chrono::microseconds>(Clock::now() - t0).count() > window)
                         break;
 #if defined(__x86_64__)
                     __builtin_ia32_pause();
@@ -1213,7 +1229,13 @@ public:
     // stream (low priority) into two buffer sets, the next one issued before
     // the current one is replayed whenever the loop is certain to reach it
     // (GCR_PREFETCH=0: never), so LO / refit kernels on the replay stream do
-    // not queue behind them.
+    // not queue behind them.  Adaptive runs also issue it speculatively while
+    // the current chunk's iterations stay below the stop threshold known
+    // before its replay (GCR_SPECULATE=0: never): the device computes the next
+    // chunk while the host replays and runs LO on this one, and a chunk the
+    // loop never reaches is simply not replayed (slots are pure functions of
+    // (seed, slot): results are identical).  Its completion is awaited at the
+    // next run's start, not at this run's end.
     struct Chunk {
         uint64_t s0 = 0;          // first slot
         uint32_t B = 0;           // slots of the chunk
@@ -1364,6 +1386,13 @@ public:
     }
 
     void replay_summaries() {
+        // speculative chunks a previous run left in flight (their pinned
+        // summary buffers are rewritten below)
+        for (int k = 0; k < 2; ++k)
+            if (P_->w->spec_pending[k]) {
+                HIPC(hipEventSynchronize(P_->w->sum_done[k]));
+                P_->w->spec_pending[k] = false;
+            }
         const uint64_t ones[2] = {1, 1};
         uint64_t max_iteration = iteration_number(ones);
         const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
@@ -1382,10 +1411,11 @@ public:
         std::vector<uint64_t> itb(world_ + 1), hb(world_ + 1), tgt(world_);
         // plan + issue the chunk after the last issued one; `it_lo`: iterations
         // before it (exact, or a lower bound: every slot adds at least one)
+        const bool spec_ok = ahead_ok && speculate_on() && min_it < max_it && prm_.batch_slots == 0;
         auto issue = [&](uint64_t it_lo) -> bool {
             if (it_lo >= L) return false;
             Chunk c;
-            c.B = (uint32_t)plan_chunk(chunk_no, last_B, it_lo, L);
+            c.B = (uint32_t)plan_chunk(chunk_no, last_B, it_lo, L, thr(), next_slot);
             c.s0 = next_slot;
             c.per = (uint32_t)((c.B + world_ - 1) / world_);
             c.it_lo = it_lo;
@@ -1416,8 +1446,12 @@ public:
                 lasts[r] = S[r].last;
                 has_last[r] = S[r].has_last ? 1 : 0;
             }
-            // with this chunk's totals known the next one may be certain
-            if (ahead_ok && q.size() == 1 && itb[world_] < min_it && issue(itb[world_])) ++st_.prefetched_chunks;
+            // with this chunk's totals known the next one may be certain, or
+            // (adaptive runs) likely: below the threshold known before this
+            // chunk's replay, which only its new bests can lower
+            if (ahead_ok && q.size() == 1 && (itb[world_] < min_it || (spec_ok && itb[world_] < thr())) &&
+                issue(itb[world_]))
+                ++st_.prefetched_chunks;
             bool stopped = false;
             // LO runs once per slot, after all of the slot's models (the
             // last new best of the slot decides, GCRANSAC.h:440-515), before
@@ -1525,8 +1559,9 @@ public:
             q.erase(q.begin());
             replay_ms += ms_since(t_rep) - lo_ms;
         }
-        // chunks issued ahead that the loop never reached
-        for (const Chunk& c : q) HIPC(hipEventSynchronize(w->sum_done[c.set]));
+        // chunks issued ahead that the loop never reached: awaited by the
+        // next run (above) or the workspace's release
+        for (const Chunk& c : q) w->spec_pending[c.set] = true;
         st_.ms_replay = replay_ms;
     }
 
@@ -1926,12 +1961,27 @@ private:
     // adaptive run starts with kSmallScore slots (the small-batch scorer; a
     // 0.99-confidence run at 50 % outliers needs 35-90) and grows x4; never
     // past the budget L from iteration count `it`.
-    uint64_t plan_chunk(uint64_t chunk_no, uint64_t last_chunk, uint64_t it, uint64_t L) const {
+    // `thr`: the loop's current stop threshold, `slots_done`: slots before
+    // the chunk (summary replay; 0 = no estimate)
+    uint64_t plan_chunk(uint64_t chunk_no, uint64_t last_chunk, uint64_t it, uint64_t L, uint64_t thr = ~0ull,
+                        uint64_t slots_done = 0) const {
         const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
         uint64_t B;
         if (prm_.batch_slots) B = prm_.batch_slots;
         else if (min_it >= max_it) B = 65536;
         else B = chunk_no == 0 ? kSmallScore : std::min<uint64_t>(65536, last_chunk * 4);
+        // adaptive runs: no more slots than the current threshold is expected
+        // to need (iterations per slot so far, + 25 %), so the chunk that ends
+        // the run does not compute tens of thousands of slots past the stop
+        // (F at configs[3]: ~8 iterations a slot, the last 4x-grown chunk was
+        // 65536 slots for ~20 000 needed).  The threshold only falls as bests
+        // improve (barring rare rises, which another chunk absorbs).
+        // GCR_CHUNK_CAP=0 disables.
+        if (!prm_.batch_slots && min_it < max_it && slots_done > 0 && it > 0 && thr > it && chunk_cap_on()) {
+            const double per = (double)it / (double)slots_done;
+            const double need = (double)(thr - it) / per * 1.25 + 64.0;
+            if (need < (double)B) B = std::max<uint64_t>((uint64_t)need, kSmallScore);
+        }
         B = std::min<uint64_t>(B, L > it ? L - it : 0);
         B = std::min<uint64_t>(B, (uint64_t)262144 * world_);      // a block summary covers <= 2^18 slots
         return std::max<uint64_t>(B, 1);
@@ -1951,6 +2001,14 @@ private:
 
     static bool prefetch_on() {
         const char* e = getenv("GCR_PREFETCH");              // read per run (tests switch it)
+        return !(e && e[0] == '0');
+    }
+    static bool speculate_on() {
+        const char* e = getenv("GCR_SPECULATE");
+        return !(e && e[0] == '0');
+    }
+    static bool chunk_cap_on() {
+        const char* e = getenv("GCR_CHUNK_CAP");
         return !(e && e[0] == '0');
     }
     // GCR_VERIFY_PIPE=0: verify_batches on one stream (A/B of the pipeline)
@@ -2354,6 +2412,22 @@ void fill_stats(gcr_stats* out, const gcr_stats& st) {
 }
 }  // namespace
 
+// The batch entry point's solving contexts (a stream pair and a workspace
+// each, with its pinned staging buffers) outlive the call: the next call on the
+// device takes them back instead of creating and warming new ones (a fresh
+// context's first problem pays its pinned allocations), as a persistent
+// service would hold them.  Kept for the process lifetime.
+namespace {
+struct BatchCtxPool {
+    std::mutex mu;
+    std::map<int, std::vector<gcr_ctx*>> free;
+};
+BatchCtxPool& batch_ctx_pool() {
+    static BatchCtxPool* p = new BatchCtxPool();   // never destroyed (HIP may be gone at exit)
+    return *p;
+}
+}  // namespace
+
 extern "C" {
 
 const char* gcr_last_error(void) { return g_err.c_str(); }
@@ -2531,16 +2605,41 @@ int gcr_solve_batch(int device, gcr_batch_item* items, size_t n, int concurrency
     if (concurrency < 1) concurrency = 1;
     if ((size_t)concurrency > n) concurrency = (int)std::max<size_t>(n, 1);
     std::vector<gcr_ctx*> ctxs((size_t)concurrency, nullptr);
+    {
+        std::lock_guard<std::mutex> lk(batch_ctx_pool().mu);
+        auto& fr = batch_ctx_pool().free[device];
+        for (auto& c : ctxs)
+            if (!fr.empty()) {
+                c = fr.back();
+                fr.pop_back();
+            }
+    }
+    auto release = [&]() {
+        std::lock_guard<std::mutex> lk(batch_ctx_pool().mu);
+        auto& fr = batch_ctx_pool().free[device];
+        for (auto*& c : ctxs)
+            if (c) {
+                if (fr.size() < 64) fr.push_back(c);
+                else gcr_destroy(c);
+                c = nullptr;
+            }
+    };
     for (auto& c : ctxs)
-        if (int rc = gcr_create(device, &c); rc != GCR_OK) {
-            for (auto* d : ctxs) gcr_destroy(d);
-            return rc;
-        }
+        if (c == nullptr)
+            if (int rc = gcr_create(device, &c); rc != GCR_OK) {
+                c = nullptr;
+                release();
+                return rc;
+            }
     std::atomic<size_t> next{0};
     std::atomic<int> first_err{GCR_OK};
     std::mutex err_mu;
     std::string err_text;
     auto worker = [&](gcr_ctx* ctx) {
+        g_solving.fetch_add(1, std::memory_order_relaxed);
+        struct Leave {
+            ~Leave() { g_solving.fetch_sub(1, std::memory_order_relaxed); }
+        } leave;
         for (size_t i; (i = next.fetch_add(1)) < n;) {
             gcr_batch_item& it = items[i];
             it.result = run_oneshot(ctx, it.solver, it.f0, it.n0, it.f1, it.n1, &it.params, it.mask0_out,
@@ -2558,7 +2657,7 @@ int gcr_solve_batch(int device, gcr_batch_item* items, size_t n, int concurrency
     for (int t = 1; t < concurrency; ++t) pool.emplace_back(worker, ctxs[(size_t)t]);
     worker(ctxs[0]);
     for (auto& th : pool) th.join();
-    for (auto* c : ctxs) gcr_destroy(c);
+    release();
     if (first_err.load() != GCR_OK) return set_err(first_err.load(), "%s", err_text.c_str());
     return GCR_OK;
 }

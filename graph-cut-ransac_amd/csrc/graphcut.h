@@ -425,8 +425,79 @@ struct CellScratch {
     std::vector<int32_t> local;
 };
 
-inline void graphcut_cell(const double* q, const double* r2, double sqt, double lambda, const uint32_t* nodes,
-                          uint32_t k, CellScratch& cs, uint8_t* seg) {
+// A two-point cell in closed form: the same unary / pairwise arithmetic as
+// add_term1 / add_term2 (energy.h:204-245, graph.h:405-452), then BK's
+// result without running it.  With at most one s-t path (s -> i -> j -> t
+// needs tr_i > 0 > tr_j) BK augments it once by f = min(arc cap, tr_i, -tr_j)
+// and stops; the SINK nodes are those that still reach t in the residual
+// graph: j iff -tr_j > f, i iff its arc keeps capacity (cap > f) and j is
+// SINK; without a path, a node is SINK iff tr < 0, or tr == 0 and its arc
+// leads to a node with tr < 0.  (Comparisons replace BK's subtractions: for
+// floats, x - f > 0 exactly when x > f.)  Returns false (BK decides) when a
+// term is not a number.  tests/cpp/gc_pair.cpp checks it against
+// graphcut_cell_bk.
+inline bool graphcut_pair(const double* q, const double* r2, double sqt, double lambda, const uint32_t* nodes,
+                          uint8_t* seg) {
+    const double oml = 1.0 - lambda;
+    double tr[2] = {0.0, 0.0};
+    // Graph::add_tweights on a node whose tr may be nonzero
+    auto tweights = [&](int i, double cs, double ck) {
+        const double delta = tr[i];
+        if (delta > 0) cs += delta;
+        else ck -= delta;
+        tr[i] = cs - ck;
+    };
+    for (int a = 0; a < 2; ++a) {
+        const uint32_t i = nodes[a];
+        const double energy = 1.0 - q[i];
+        if (r2[i] <= sqt) tweights(a, 0.0, oml * energy);      // add_term1(a, oml energy, 0)
+        else tweights(a, oml * (1.0 - energy), 0.0);           // add_term1(a, 0, oml (1 - energy))
+    }
+    // add_term2(0, 1, A = e00 lambda, B = C = lambda, D = 0)
+    const double e00 = 0.5 * (q[nodes[0]] + q[nodes[1]]);
+    double A = e00 * lambda, B = lambda, C = lambda, D = 0.0 * lambda;
+    tweights(0, D, A);
+    B -= A;
+    C -= D;
+    double c01, c10;                                           // arc 0 -> 1, arc 1 -> 0
+    if (B < 0) {
+        tweights(0, 0, B);
+        tweights(1, 0, -B);
+        c01 = 0;
+        c10 = B + C;
+    } else if (C < 0) {
+        tweights(0, 0, -C);
+        tweights(1, 0, C);
+        c01 = B + C;
+        c10 = 0;
+    } else {
+        c01 = B;
+        c10 = C;
+    }
+    if (tr[0] != tr[0] || tr[1] != tr[1] || c01 != c01 || c10 != c10) return false;
+    bool sink[2];
+    auto path = [&](int i, int j, double cap) {                // s -> i -> j -> t
+        double f = cap;
+        if (f > tr[i]) f = tr[i];
+        if (f > -tr[j]) f = -tr[j];
+        sink[j] = -tr[j] > f;
+        sink[i] = cap > f && sink[j];
+    };
+    if (tr[0] > 0 && tr[1] < 0 && c01 != 0.0) {
+        path(0, 1, c01);
+    } else if (tr[1] > 0 && tr[0] < 0 && c10 != 0.0) {
+        path(1, 0, c10);
+    } else {
+        sink[0] = tr[0] < 0 || (tr[0] == 0 && c01 != 0.0 && tr[1] < 0);
+        sink[1] = tr[1] < 0 || (tr[1] == 0 && c10 != 0.0 && tr[0] < 0);
+    }
+    seg[nodes[0]] = sink[0] ? 1 : 0;
+    seg[nodes[1]] = sink[1] ? 1 : 0;
+    return true;
+}
+
+inline void graphcut_cell_bk(const double* q, const double* r2, double sqt, double lambda, const uint32_t* nodes,
+                             uint32_t k, CellScratch& cs, uint8_t* seg) {
     const double oml = 1.0 - lambda;
     MaxFlow& g = cs.g;
     g.reset(k, (size_t)k * (k - 1) / 2);
@@ -444,6 +515,12 @@ inline void graphcut_cell(const double* q, const double* r2, double sqt, double 
         }
     g.maxflow();
     for (uint32_t a = 0; a < k; ++a) seg[nodes[a]] = g.is_sink((int32_t)a) ? 1 : 0;
+}
+
+inline void graphcut_cell(const double* q, const double* r2, double sqt, double lambda, const uint32_t* nodes,
+                          uint32_t k, CellScratch& cs, uint8_t* seg) {
+    if (k == 2 && graphcut_pair(q, r2, sqt, lambda, nodes, seg)) return;
+    graphcut_cell_bk(q, r2, sqt, lambda, nodes, k, cs, seg);
 }
 
 template <class ForCells>

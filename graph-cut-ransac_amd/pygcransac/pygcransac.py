@@ -373,16 +373,20 @@ def grid_cell_sizes(correspondences, h1, w1, h2, w2, neighborhood_size):
     GridNeighborhoodGraph<4> over {w1, h1, w2, h2} / cells).  An image size
     <= 0 (unknown) is replaced by the correspondences' extent along that axis
     (max coordinate + 1, at least 1 px)."""
-    f = np.asarray(correspondences, dtype=np.float64)
     k = float(neighborhood_size)
-    out = []
-    for col, size in zip(range(4), (w1, h1, w2, h2)):
-        size = float(size)
-        if not size > 0.0 or not math.isfinite(size):
-            finite = f[:, col][np.isfinite(f[:, col])] if f.size else np.zeros(0)
-            size = max(1.0, float(finite.max()) + 1.0) if finite.size else 1.0
-        out.append(size / k)
-    return out
+    sizes = [float(v) for v in (w1, h1, w2, h2)]
+    known = [v > 0.0 and math.isfinite(v) for v in sizes]
+    if not all(known):
+        # the extents of every unknown axis in one pass (finite values only)
+        f = np.asarray(correspondences, dtype=np.float64)
+        if f.size:
+            fin = np.isfinite(f[:, :4])
+            top = np.where(fin, f[:, :4], -np.inf).max(axis=0)
+            has = fin.any(axis=0)
+        for col in range(4):
+            if not known[col]:
+                sizes[col] = max(1.0, float(top[col]) + 1.0) if f.size and has[col] else 1.0
+    return [v / k for v in sizes]
 
 
 def _set_grid(p, correspondences, h1, w1, h2, w2, neighborhood_size):

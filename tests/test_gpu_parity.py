@@ -132,13 +132,14 @@ def test_score_kernel_matches_oracle_bitwise(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("nh", [1, 37, 256])
-def test_small_batch_scorer_matches_oracle_bitwise(kind, nh, monkeypatch):
+@pytest.mark.parametrize("nh,nf", [(1, 1337), (37, 1337), (256, 1337), (37, 5000)])
+def test_small_batch_scorer_matches_oracle_bitwise(kind, nh, nf, monkeypatch):
     # launch_score_small (LO trials, refits, short replay chunks): every pair in
     # parallel, then one wave per model adds its inliers in order; ragged class
-    # tails (n not a multiple of 64) exercise the padded layout
+    # tails (n not a multiple of 64) exercise the padded layout, nf = 5000 two
+    # 8192-value blocks of k_lo_chain (the class boundary inside the first)
     monkeypatch.setenv("GCR_DEBUG_SCORER", "small")
-    f0, f1, thr0, thr1 = _problem_data(kind, 1337, seed=61 + kind)
+    f0, f1, thr0, thr1 = _problem_data(kind, nf, seed=61 + kind)
     prob = Problem(kind, f0, f1)
     inc, models = prob.generate(19, 0, 256)
     uniq = models[inc <= 101][:96]

@@ -245,3 +245,42 @@ def test_labeling_without_edges_is_the_terminal_test():
         q = np.clip(r2 / sqt, 0, 1)
         tr = np.where(r2 <= sqt, 0.0 - (1 - lam) * (1 - q), (1 - lam) * (1 - (1 - q)) - 0.0)
         assert np.array_equal(got, tr < 0)
+
+
+def test_grid_cell_sizes_unknown_image_sizes():
+    # an image size <= 0 (or not finite) falls back to that axis's extent of
+    # the finite coordinates (max + 1, at least 1 px), divided by the cells
+    from pygcransac import pygcransac as P
+
+    rng = np.random.default_rng(5)
+    corr = rng.uniform(0, 500, (300, 4))
+    corr[7, 1] = np.nan
+    corr[9, 2] = np.inf
+    corr[:, 3] = -5.0                                        # no positive extent: 1 px
+    got = P.grid_cell_sizes(corr, 0, 640, -1, float("nan"), 8)
+
+    def ref(col, size):
+        if size > 0 and np.isfinite(size):
+            return size / 8
+        v = corr[:, col][np.isfinite(corr[:, col])]
+        return max(1.0, float(v.max()) + 1.0) / 8 if v.size else 1.0 / 8
+
+    assert got == [ref(0, 640), ref(1, 0), ref(2, float("nan")), ref(3, -1)]
+    assert P.grid_cell_sizes(np.zeros((0, 4)), 0, 0, 0, 0, 4) == [0.25] * 4
+
+
+def test_two_point_cells_closed_form_equals_bk(tmp_path):
+    # graphcut.h graphcut_pair (two-point cells, ~45 % of the cells at
+    # configs[3]) decides BK's labeling without running it; checked against
+    # graphcut_cell_bk on 2 M random cells with deliberate ties (residuals at
+    # the truncated threshold, equal points, q in {0, 1/2, 1}, lambda 0 / 1)
+    import os
+    import subprocess
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = str(tmp_path / "gc_pair")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                           os.path.join(here, "cpp", "gc_pair.cpp"), "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches 0" in out.stdout
