@@ -113,21 +113,34 @@ inline void grid_edges(const double* const* coords, int dims, size_t n, const do
 // Boykov-Kolmogorov max-flow, Graph<double,double,double> semantics.
 class MaxFlow {
 public:
+    // storage grows to the largest graph seen and is reused (no per-graph
+    // allocation or vector bookkeeping: the cells are mostly 2-4 nodes)
     void reset(size_t n_nodes, size_t n_edges) {
         n_ = n_nodes;
-        first_.assign(n_, kNone);
-        parent_.assign(n_, kNone);
-        next_.assign(n_, kNone);
-        ts_.assign(n_, 0);
-        dist_.assign(n_, 0);
-        sink_.assign(n_, 0);
-        tr_.assign(n_, 0.0);
-        head_.clear();
-        anext_.clear();
-        rcap_.clear();
-        head_.reserve(2 * n_edges);
-        anext_.reserve(2 * n_edges);
-        rcap_.reserve(2 * n_edges);
+        if (first_.size() < n_) {
+            first_.resize(n_);
+            parent_.resize(n_);
+            next_.resize(n_);
+            ts_.resize(n_);
+            dist_.resize(n_);
+            sink_.resize(n_);
+            tr_.resize(n_);
+        }
+        for (size_t i = 0; i < n_; ++i) {
+            first_[i] = kNone;
+            parent_[i] = kNone;
+            next_[i] = kNone;
+            ts_[i] = 0;
+            dist_[i] = 0;
+            sink_[i] = 0;
+            tr_[i] = 0.0;
+        }
+        if (head_.size() < 2 * n_edges) {
+            head_.resize(2 * n_edges);
+            anext_.resize(2 * n_edges);
+            rcap_.resize(2 * n_edges);
+        }
+        na_ = 0;
     }
     // Graph::add_tweights (graph.h:405-418)
     void add_tweights(int32_t i, double cap_source, double cap_sink) {
@@ -138,15 +151,21 @@ public:
     }
     // Graph::add_edge (graph.h:420-452): arc 2k = i -> j, arc 2k+1 = j -> i
     void add_edge(int32_t i, int32_t j, double cap, double rev_cap) {
-        const int32_t a = (int32_t)head_.size();
-        head_.push_back(j);
-        anext_.push_back(first_[i]);
-        rcap_.push_back(cap);
+        const int32_t a = na_;
+        if ((size_t)a + 2 > head_.size()) {                  // more edges than reset() was told
+            head_.resize((size_t)a + 2);
+            anext_.resize((size_t)a + 2);
+            rcap_.resize((size_t)a + 2);
+        }
+        head_[a] = j;
+        anext_[a] = first_[i];
+        rcap_[a] = cap;
         first_[i] = a;
-        head_.push_back(i);
-        anext_.push_back(first_[j]);
-        rcap_.push_back(rev_cap);
+        head_[a + 1] = i;
+        anext_[a + 1] = first_[j];
+        rcap_[a + 1] = rev_cap;
         first_[j] = a + 1;
+        na_ = a + 2;
     }
     // Energy::add_term1 / add_term2 (energy.h:204-245)
     void add_term1(int32_t x, double A, double B) { add_tweights(x, B, A); }
@@ -251,6 +270,7 @@ private:
     static constexpr int32_t kNone = -1, kTerminal = -2, kOrphan = -3;
     static constexpr int kInfD = 0x7fffffff;
     size_t n_ = 0;
+    int32_t na_ = 0;                                          // arcs in use
     std::vector<int32_t> first_, parent_, next_;
     std::vector<int> ts_, dist_;
     std::vector<uint8_t> sink_;
@@ -528,15 +548,21 @@ inline void graphcut_labeling(const double* r2, size_t n, double sqt, double lam
                               std::vector<double>& q, std::vector<uint8_t>& seg, ForCells&& for_cells) {
     const double oml = 1.0 - lambda;
     q.resize(n);
-    seg.assign(n, 0);
+    seg.resize(n);
+    double* qp = q.data();
+    uint8_t* sp = seg.data();
     for (size_t i = 0; i < n; ++i) {
-        const double qq = std::clamp(r2[i] / sqt, 0.0, 1.0);
-        q[i] = qq;
+        // std::clamp(r2 / sqt, 0, 1), NaN passing through, as selects
+        const double v = r2[i] / sqt;
+        const double lo = v < 0.0 ? 0.0 : v;
+        const double qq = 1.0 < lo ? 1.0 : lo;
+        qp[i] = qq;
         // the terminal test (a node without pairwise terms): SINK iff its
         // terminal residual capacity is < 0
         const double energy = 1.0 - qq;
-        const double tr = (r2[i] <= sqt) ? (0.0 - oml * energy) : (oml * (1.0 - energy) - 0.0);
-        seg[i] = tr < 0 ? 1 : 0;
+        const double tin = 0.0 - oml * energy, tout = oml * (1.0 - energy) - 0.0;
+        const double tr = (r2[i] <= sqt) ? tin : tout;
+        sp[i] = tr < 0 ? 1 : 0;
     }
     if (!(lambda > 0) || edges.off.size() < 2) return;
     const size_t ncells = edges.off.size() - 1;

@@ -404,6 +404,124 @@ __global__ __launch_bounds__(kSumFinalThreads) void k_sum_final(SumArgs a) {
     }
 }
 
+// ---- one-part summaries (npos <= pp: LO-sized and early adaptive chunks):
+// A, B and C fused into one wave, no scratch round trip and one launch
+// instead of three (the 1024-thread final pass alone cost ~25 us)
+template <class M>
+__global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
+    const int lane = threadIdx.x;
+    const uint32_t end = a.npos;
+    const bool locate = a.target != ~0ull;
+    const int K = a.solver == 2 ? 2 : 1;
+    const M* models = static_cast<const M*>(a.models);
+    BlockSummary* out = a.out;
+    uint32_t coff = 0, loff = 0, nc = 0, over = 0;
+    int32_t lastp = -1;
+    uint32_t last_it = 0, last_hb = 0;
+    uint32_t stop_p = 0xffffffffu, stop_it = 0, stop_hb = 0;
+    double run = a.bar;
+    for (uint32_t o = 0; o < end; o += 64) {
+        const uint32_t p = o + lane;
+        const uint32_t in = p < end ? a.inc[p] : 255u;
+        const uint32_t c = contrib_of(in);
+        const bool l = in <= 101;
+        const uint32_t cs = wave_incl_sum(c, lane), ls = wave_incl_sum(l ? 1u : 0u, lane);
+        const uint32_t excl = coff + cs - c;                   // iterations before p's slot (q = 0)
+        const uint32_t hb = loff + ls - (l ? 1u : 0u);          // live hypotheses before p
+        uint32_t lim = 64u;                                     // positions of this 64 before the stop
+        if (locate) {
+            if (stop_p == 0xffffffffu) {
+                const bool start = p < end && (p % a.per) == 0;
+                const uint64_t hit = __ballot(start && (uint64_t)excl >= a.target);
+                if (hit) {
+                    lim = (uint32_t)__builtin_ctzll(hit);
+                    stop_p = o + lim;
+                    stop_it = __shfl(excl, (int)lim);
+                    stop_hb = __shfl(hb, (int)lim);
+                }
+            } else {
+                lim = 0u;                                       // past the stop: totals only
+            }
+        }
+        const uint64_t bl = __ballot(l) & (lim >= 64u ? ~0ull : ((1ull << lim) - 1ull));
+        if (bl) {
+            const int hl = 63 - __builtin_clzll(bl);
+            const uint32_t q = (o + (uint32_t)hl) % a.per;
+            const uint32_t own = q > 0 ? contrib_of(a.inc[o + hl - q]) : 0u;
+            lastp = (int32_t)(o + (uint32_t)hl);
+            last_it = __shfl(excl, hl) - own;
+            last_hb = __shfl(hb, hl);
+        }
+        if (!locate) {
+            double val = -1.0;
+            if (l && p >= a.from_pos) {
+                const uint32_t j = a.hmap != nullptr ? hb : p;
+                val = finish_at(a.sc, j, K, a.m0, a.m1, a.Tm0, a.Tm1);
+                if constexpr (std::is_same<M, RectModel>::value)
+                    if (a.solver == 2 && !valid_model_sift22(models[p])) val = -1.0;
+            }
+            const double im = wave_incl_max(val, lane);
+            const double before = __shfl_up(im, 1);
+            const double bar = lane == 0 ? run : (run < before ? before : run);
+            const bool cand = val >= 0.0 && val > bar;
+            const uint64_t bc = __ballot(cand);
+            if (cand) {
+                const uint32_t r = nc + (uint32_t)__builtin_popcountll(bc & ((1ull << lane) - 1ull));
+                if (r < a.cap) {
+                    const uint32_t q = p % a.per;
+                    const uint32_t own = q > 0 ? contrib_of(a.inc[p - q]) : 0u;
+                    fill_hyp<M>(a, p, excl - own, hb, out->cand[r]);
+                    if (r + 1 == a.cap) {                      // the last member a full summary holds
+                        out->resume_pos = p + 1;
+                        out->resume_bar = val;
+                    }
+                }
+            }
+            const uint32_t add = (uint32_t)__builtin_popcountll(bc);
+            if (nc + add > a.cap) over = 1;
+            nc = min(nc + add, a.cap);
+            const double wm = __shfl(im, 63);
+            run = run < wm ? wm : run;
+        }
+        coff += __shfl(cs, 63);
+        loff += __shfl(ls, 63);
+    }
+    if (lane != 0) return;
+    if (!locate) {
+        out->inc_total = coff;
+        out->hyps_total = loff;
+        out->ncand = nc;
+        out->overflow = over;
+        out->stop_found = 0;
+    } else {
+        out->inc_total = coff;
+        out->hyps_total = loff;
+        out->ncand = 0;
+        out->overflow = 0;
+        if (a.target == 0) {                                 // before slot 0
+            out->stop_found = 1;
+            out->stop_slot = 0;
+            out->stop_it_before = 0;
+            out->stop_hyps_before = 0;
+            out->has_last = 0;
+            return;
+        }
+        if (stop_p == 0xffffffffu && (uint64_t)coff >= a.target) {   // the last slot reaches it
+            stop_p = end;
+            stop_it = coff;
+            stop_hb = loff;
+        }
+        out->stop_found = stop_p != 0xffffffffu ? 1u : 0u;
+        if (stop_p != 0xffffffffu) {
+            out->stop_slot = stop_p / a.per;
+            out->stop_it_before = stop_it;
+            out->stop_hyps_before = stop_hb;
+        }
+    }
+    out->has_last = lastp >= 0 ? 1u : 0u;
+    if (lastp >= 0) fill_hyp<M>(a, (uint32_t)lastp, last_it, last_hb, out->last);
+}
+
 }  // namespace
 
 size_t summary_scratch_bytes(uint32_t npos, uint32_t per) {
@@ -445,6 +563,15 @@ hipError_t launch_block_summary(int solver, const uint8_t* inc, const void* mode
     a.out = out;
     if (a.npos == 0 || a.nparts > (uint32_t)kSumFinalThreads) return hipErrorInvalidValue;
     const bool rect = solver <= 2;
+    // GCR_SUMMARY_ONE=0: one-part summaries through the three launches too
+    // (read per launch: tests switch it)
+    const char* e1 = getenv("GCR_SUMMARY_ONE");
+    const bool one_on = !(e1 && e1[0] == '0');
+    if (a.nparts == 1 && one_on) {
+        if (rect) hipLaunchKernelGGL(k_sum_one<RectModel>, dim3(1), dim3(64), 0, stream, a);
+        else hipLaunchKernelGGL(k_sum_one<GeoModel>, dim3(1), dim3(64), 0, stream, a);
+        return hipGetLastError();
+    }
     if (!parts_ready) hipLaunchKernelGGL(k_sum_parts, dim3(a.nparts), dim3(64), 0, stream, a);
     if (target == ~0ull) {
         if (rect) hipLaunchKernelGGL(k_sum_chain<RectModel>, dim3(a.nparts), dim3(64), 0, stream, a);

@@ -377,15 +377,19 @@ def grid_cell_sizes(correspondences, h1, w1, h2, w2, neighborhood_size):
     sizes = [float(v) for v in (w1, h1, w2, h2)]
     known = [v > 0.0 and math.isfinite(v) for v in sizes]
     if not all(known):
-        # the extents of every unknown axis in one pass (finite values only)
         f = np.asarray(correspondences, dtype=np.float64)
-        if f.size:
-            fin = np.isfinite(f[:, :4])
-            top = np.where(fin, f[:, :4], -np.inf).max(axis=0)
-            has = fin.any(axis=0)
         for col in range(4):
-            if not known[col]:
-                sizes[col] = max(1.0, float(top[col]) + 1.0) if f.size and has[col] else 1.0
+            if known[col]:
+                continue
+            if not f.size:
+                sizes[col] = 1.0
+                continue
+            c = f[:, col]
+            top = float(c.max())                    # NaN / inf present: the finite values only
+            if not math.isfinite(top):
+                fin = c[np.isfinite(c)]
+                top = float(fin.max()) if fin.size else None
+            sizes[col] = max(1.0, top + 1.0) if top is not None else 1.0
     return [v / k for v in sizes]
 
 

@@ -6,8 +6,9 @@ strict new bests).  Both must give identical runs -- masks, model bits,
 iteration / hypothesis / LO / graph-cut counts, slots, score -- for every
 estimator, fixed and adaptive budgets, tiny chunks, a one-member summary cap
 (every chunk overflows and is continued on the device) and with the next chunk
-issued ahead or not.  The oracle parity of the default path is tested
-everywhere else (golden, end-to-end, bench-config tests)."""
+issued ahead or not, and one-part blocks summarised by the fused one-wave
+kernel (k_sum_one) or the three launches.  The oracle parity of the default
+path is tested everywhere else (golden, end-to-end, bench-config tests)."""
 import ctypes as C
 
 import numpy as np
@@ -77,3 +78,6 @@ def test_summary_replay_equals_slot_replay(kind, budget, monkeypatch):
     assert _run(kind, budget, monkeypatch, {"GCR_SUMMARY_CAP": "1"}) == ref
     # no chunk issued ahead of the replay
     assert _run(kind, budget, monkeypatch, {"GCR_PREFETCH": "0", "GCR_SUMMARY_CAP": "3"}) == ref
+    # one-part blocks through the three-launch summary instead of k_sum_one
+    assert _run(kind, budget, monkeypatch, {"GCR_SUMMARY_ONE": "0"}) == ref
+    assert _run(kind, budget, monkeypatch, {"GCR_SUMMARY_ONE": "0", "GCR_SUMMARY_CAP": "1"}) == ref
