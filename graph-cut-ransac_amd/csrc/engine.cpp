@@ -116,6 +116,20 @@ struct Ptr {
     T* p = nullptr;
 };
 
+// the device address of pinned (hipHostMalloc) host memory: kernels write
+// small results straight into it (no copy-back launch) and read small inputs
+// from it (GCR_ZEROCOPY=0: staged copies instead)
+template <class T>
+T* dev_view(T* host) {
+    void* d = nullptr;
+    HIPC(hipHostGetDevicePointer(&d, host, 0));
+    return static_cast<T*>(d);
+}
+inline bool zerocopy_on() {
+    const char* e = getenv("GCR_ZEROCOPY");              // read per call (tests switch it)
+    return !(e && e[0] == '0');
+}
+
 template <class B>
 void swap_buf(B& a, B& b) {
     std::swap(a.p, b.p);
@@ -149,6 +163,13 @@ struct ScoreBufs {
         carve(hblk.p, hn0, hn1, hv0, hv1, htot);
     }
     ScoreOut dev() const { return ScoreOut{n0.p, n1.p, v0.p, v1.p, tot.p}; }
+    // the pinned mirror as kernels see it (results written in place)
+    ScoreOut host_dev() const {
+        double* b = dev_view(hblk.p);
+        const ptrdiff_t d = reinterpret_cast<char*>(b) - reinterpret_cast<char*>(hblk.p);
+        auto at = [d](auto* h) { return reinterpret_cast<decltype(h)>(reinterpret_cast<char*>(h) + d); };
+        return ScoreOut{at(hn0.p), at(hn1.p), at(hv0.p), at(hv1.p), at(htot.p)};
+    }
     void swap(ScoreBufs& o) {
         std::swap(dblk.p, o.dblk.p); std::swap(dblk.cap, o.dblk.cap);
         std::swap(hblk.p, o.hblk.p); std::swap(hblk.cap, o.hblk.cap);
@@ -212,6 +233,8 @@ struct Workspace {
     PinBuf<double> h_r2;
     DevBuf<double> sm_vals;             // launch_score_small: pair values
     DevBuf<uint64_t> sm_bits;           // launch_score_small: inlier bitmasks
+    PinBuf<RectModel> h_lorect;         // score_models: small batches' models, read in place
+    PinBuf<GeoModel> h_logeo;
     PinBuf<uint64_t> h_lbits;           // launch_score_small: LO list bits (ListBits), written by
                                         // the kernel straight into this mapped pinned buffer
     PinBuf<uint8_t> h_mask_all;
@@ -833,6 +856,7 @@ struct RectTraits {
     static DevBuf<Model>& pf_dmodels(Workspace* w) { return w->pf_models; }
     static PinBuf<Model>& pf_hmodels(Workspace* w) { return w->pf_h_models; }
     static DevBuf<Model>& lomodels(Workspace* w) { return w->lo_models; }
+    static PinBuf<Model>& hlomodels(Workspace* w) { return w->h_lorect; }
     static bool identity(const Model& m) { return identity_norm(m); }
     static bool valid(int solver, const Model& m) { return solver == 2 ? valid_model_sift22(m) : true; }
     static hipError_t generate(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, uint8_t* inc, Model* m,
@@ -948,6 +972,7 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     static DevBuf<Model>& pf_dmodels(Workspace* w) { return w->pf_gmodels; }
     static PinBuf<Model>& pf_hmodels(Workspace* w) { return w->pf_h_gmodels; }
     static DevBuf<Model>& lomodels(Workspace* w) { return w->lo_gmodels; }
+    static PinBuf<Model>& hlomodels(Workspace* w) { return w->h_logeo; }
     static bool identity(const Model&) { return true; }
     static bool valid(int, const Model&) { return true; }
     static hipError_t generate(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, uint8_t* inc, Model* m,
@@ -1257,13 +1282,13 @@ public:
 
     // summary launch of this rank's block of chunk c (mode chain or locate)
     hipError_t launch_summary(const Chunk& c, double bar, uint32_t from_pos, uint64_t target, bool parts_ready,
-                              hipStream_t s) {
+                              BlockSummary* out, hipStream_t s) {
         Workspace* w = P_->w;
         const uint32_t n = rank_nslots(c, rank_);
         const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
         return launch_block_summary(P_->solver, set_inc(c.set).p, set_models(c.set).p, set_sb(c.set).dev(),
                                     kP > 1 ? set_hmap(c.set).p : nullptr, n, (uint32_t)kP, m32, Tm_, bar, from_pos,
-                                    target, w->sum_scr[c.set].p, w->dsum[c.set].p, s, parts_ready);
+                                    target, w->sum_scr[c.set].p, out, s, parts_ready);
     }
 
     // generate + score + summarise this rank's block of chunk c on stream s
@@ -1310,8 +1335,10 @@ public:
             }
         }
         HIPC(hipEventRecord(w->sum_k1[set], s));
-        HIPC(launch_summary(c, c.bar, 0, ~0ull, false, s));
-        HIPC(hipMemcpyAsync(w->hsum[set].p, w->dsum[set].p, sizeof(BlockSummary), hipMemcpyDeviceToHost, s));
+        const bool zc = zerocopy_on();
+        HIPC(launch_summary(c, c.bar, 0, ~0ull, false, zc ? dev_view(w->hsum[set].p) : w->dsum[set].p, s));
+        if (!zc)
+            HIPC(hipMemcpyAsync(w->hsum[set].p, w->dsum[set].p, sizeof(BlockSummary), hipMemcpyDeviceToHost, s));
         HIPC(hipEventRecord(w->sum_done[set], s));
         st_.launches += 5;
         st_.hypotheses_computed += np;
@@ -1359,9 +1386,12 @@ public:
         Workspace* w = P_->w;
         BlockSummary mine = empty_summary();
         if (rank_nslots(c, rank_) > 0 && (target != nullptr || owner == rank_)) {
+            const bool zc = zerocopy_on();
             HIPC(launch_summary(c, bar, target ? 0u : from_pos, target ? target[rank_] : ~0ull, target != nullptr,
-                                s_));
-            HIPC(hipMemcpyAsync(w->hsum[c.set].p, w->dsum[c.set].p, sizeof(BlockSummary), hipMemcpyDeviceToHost, s_));
+                                zc ? dev_view(w->hsum[c.set].p) : w->dsum[c.set].p, s_));
+            if (!zc)
+                HIPC(hipMemcpyAsync(w->hsum[c.set].p, w->dsum[c.set].p, sizeof(BlockSummary), hipMemcpyDeviceToHost,
+                                    s_));
             HIPC(hipStreamSynchronize(s_));
             st_.launches += 2;
             mine = w->hsum[c.set].p[0];
@@ -2149,9 +2179,21 @@ private:
         P_->w->lo_sb.ensure(n);
         bool identity = true;
         for (uint32_t i = 0; i < n; ++i) identity = identity && Tr::identity(models[i]);
-        HIPC(hipMemcpyAsync(lm.p, models, n * sizeof(Model), hipMemcpyHostToDevice, s_));
+        const bool small = identity && n <= kSmallScore && small_score_on();
+        // small batches: models read from pinned memory and results written
+        // into the pinned mirror by the kernels (no copy launches either way)
+        const bool zc = small && zerocopy_on();
+        const Model* dmodels = lm.p;
+        if (zc) {
+            auto& hm = Tr::hlomodels(P_->w);
+            hm.ensure(kSmallScore);                  // sized once (a pinned reallocation costs milliseconds)
+            std::memcpy(hm.p, models, n * sizeof(Model));
+            dmodels = dev_view(hm.p);
+        } else {
+            HIPC(hipMemcpyAsync(lm.p, models, n * sizeof(Model), hipMemcpyHostToDevice, s_));
+        }
         bool lists = false;
-        if (identity && n <= kSmallScore && small_score_on()) {
+        if (small) {
             // a few models: all pairs in parallel, then one wave per model
             // adds its inliers in order (no ~90 us batch-scorer chain)
             const size_t pairs = small_score_pairs(P_->dp);
@@ -2171,12 +2213,13 @@ private:
                 lb.rule = req->rule;
                 lb.bits = static_cast<uint64_t*>(dptr);
             }
-            HIPC(launch_score_small(P_->dp, Tm_, lm.p, nullptr, n, P_->w->lo_sb.dev(), P_->w->sm_vals.p,
+            HIPC(launch_score_small(P_->dp, Tm_, dmodels, nullptr, n,
+                                    zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev(), P_->w->sm_vals.p,
                                     P_->w->sm_bits.p, s_, lists ? &lb : nullptr));
         } else {
             HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
         }
-        P_->w->lo_sb.d2h(n, s_);
+        if (!zc) P_->w->lo_sb.d2h(n, s_);
         HIPC(hipStreamSynchronize(s_));
         st_.launches += 1;
         for (uint32_t i = 0; i < n; ++i) {
