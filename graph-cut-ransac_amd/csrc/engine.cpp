@@ -81,6 +81,11 @@ inline double ms_since(Clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
 }
 
+// host threads currently solving problems inside gcr_solve_batch (the pool's
+// workers do not spin while several of them share the cores)
+std::atomic<int> g_solving{0};
+
+
 template <class T>
 struct DevBuf {
     T* p = nullptr;
@@ -534,9 +539,6 @@ struct GpuSiftSolver final : SiftSystemSolver {
 // does not depend on the scheduling).  Size: GCR_HOST_THREADS, default
 // min(16, hardware threads) -- one GPU's CPU share on an MI355X node; the
 // 50 LO fits of a graph-cut round take 42 us on 16 threads, 70 on 8.
-// host threads currently solving problems inside gcr_solve_batch (the pool's
-// workers do not spin while several of them share the cores)
-std::atomic<int> g_solving{0};
 
 class HostPool {
 public:
@@ -2261,8 +2263,12 @@ private:
             const size_t n = N_[0];
             P_->w->r2.ensure(n);
             P_->w->h_r2.ensure(n);
-            HIPC(Tr::sqres(P_, model, P_->w->r2.p, s_));
-            HIPC(hipMemcpyAsync(P_->w->h_r2.p, P_->w->r2.p, n * sizeof(double), hipMemcpyDeviceToHost, s_));
+            if (zerocopy_on()) {                                 // written straight into pinned memory
+                HIPC(Tr::sqres(P_, model, dev_view(P_->w->h_r2.p), s_));
+            } else {
+                HIPC(Tr::sqres(P_, model, P_->w->r2.p, s_));
+                HIPC(hipMemcpyAsync(P_->w->h_r2.p, P_->w->r2.p, n * sizeof(double), hipMemcpyDeviceToHost, s_));
+            }
             HIPC(hipStreamSynchronize(s_));
             st_.launches += 1;
             lists[0].clear();
@@ -2285,10 +2291,12 @@ private:
         const size_t tot = N_[0] + (K_ == 2 ? N_[1] : 0);
         P_->w->mask_all.ensure(tot);
         P_->w->h_mask_all.ensure(tot);
+        // the masks written straight into pinned memory (zero-copy)
+        const bool zc = zerocopy_on();
+        uint8_t* mk = zc ? dev_view(P_->w->h_mask_all.p) : P_->w->mask_all.p;
         for (int c = 0; c < K_; ++c)
-            HIPC(Tr::mask(P_, c, model, rule, T[c], prm_.spatial_coherence_weight,
-                          P_->w->mask_all.p + (c ? N_[0] : 0), s_));
-        HIPC(hipMemcpyAsync(P_->w->h_mask_all.p, P_->w->mask_all.p, tot, hipMemcpyDeviceToHost, s_));
+            HIPC(Tr::mask(P_, c, model, rule, T[c], prm_.spatial_coherence_weight, mk + (c ? N_[0] : 0), s_));
+        if (!zc) HIPC(hipMemcpyAsync(P_->w->h_mask_all.p, P_->w->mask_all.p, tot, hipMemcpyDeviceToHost, s_));
         HIPC(hipStreamSynchronize(s_));
         st_.launches += K_;
         for (int c = 0; c < 2; ++c) {
