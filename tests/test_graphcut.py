@@ -284,3 +284,30 @@ def test_two_point_cells_closed_form_equals_bk(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "mismatches 0" in out.stdout
+
+
+def test_frozen_tie_fixtures():
+    # tests/golden/graphcut_ties.json (tools/gen_gc_ties.py, written once, never
+    # regenerated): labeling() calls whose energies tie on purpose (residuals
+    # exactly at the truncated threshold, equal residuals, dyadic lambda); the
+    # expected SINK sets come from the reference's reading rule (what_segment
+    # with default SOURCE, GCRANSAC.h:865, graph.h:115-117) as the intersection
+    # of all optimal labelings' sink sets over an exhaustive enumeration, with
+    # no BK code involved.  Both BK implementations must return exactly them.
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "graphcut_ties.json")) as f:
+        cases = json.load(f)["cases"]
+    assert sum(c["optimal_labelings"] >= 2 for c in cases) >= 15
+    for c in cases:
+        r2 = np.asarray(c["r2"], dtype=np.float64)
+        pts = np.asarray(c["points"], dtype=np.float64)
+        edges = np.asarray(c["edges"], dtype=np.uint32).reshape(-1, 2)
+        assert np.array_equal(product_edges(pts, c["cell_size"], c["cells"]), edges), c["name"]
+        expect = np.asarray(c["sink"], dtype=bool)
+        got = product_labeling(r2, c["sqt"], c["lambda"], pts, c["cell_size"], c["cells"])
+        assert np.array_equal(got, expect), c["name"]
+        unary, pair = labeling_energy(r2, c["sqt"], c["lambda"], edges)
+        assert np.array_equal(O.bk_energy(unary, edges, pair)[0], expect), c["name"]
+        assert np.array_equal(product_bk(unary, edges, pair), expect), c["name"]
