@@ -1779,6 +1779,110 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
 // scan), and wave 0 folds them: lane 0 the class sum, lane 1 (KIND 2) the
 // running total.  Blocks alternate between two sets of LDS buffers, so the
 // next block's loads are issued while wave 0 still folds.
+// fold_exact_wave: the in-order running sum run += v[k], k = b .. e-1, by one
+// whole wave, bit-identical to the sequential fp64 loop (MSAC_scoring_function
+// .hpp:53-107 adds the inliers' terms one by one).  While the running sum s
+// stays in one binade [2^E, 2^(E+1)) its ulp U is fixed and s is a multiple of
+// U, so fl(s + v) = s + U * rint(v / U) unless v / U ends in exactly .5 (a
+// tie, whose rounding depends on the parity of s / U).  So 256 values at a
+// time (4 consecutive ones per lane): each value is scaled by 1/U (exact: a
+// power of two) and rounded to an integer, the lane adds its four in order,
+// an inclusive DPP scan over the lanes adds the lane totals to s / U, and the
+// first value that ties, is positive, too large or leaves the binade ends the
+// step's fast part.  The values are all <= 0 (MSAC terms -r^2; the sum only
+// grows in magnitude), so every partial sum before that value is an integer
+// below 2^53 in magnitude: all of this integer arithmetic in fp64 is exact.
+// The first bad value is added with one ordinary fp64 addition (the
+// sequential rule itself), and the next step starts after it in the new
+// binade; a zero, subnormal or non-finite running sum also takes the ordinary
+// addition.  In a long sum only the few binade crossings and the early ties
+// (values as large as the sum) are added one by one: ~5000 dependent adds
+// become ~40 wave steps.  All lanes of the wave call it; `v` may be LDS or
+// global memory.  GCR_LO_FOLD=wide selects it in k_lo_chain (A/B).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double x) {      // DPP move of an fp64 value, 0 where nothing moves in
+    const uint64_t u = as_u64(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROWS, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROWS, 0xf, true);
+    return as_f64(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+__device__ __forceinline__ double wave_incl_scan_f64(double x) {
+    x = x + dpp_f64<0x111, 0xf>(x);     // row_shr:1
+    x = x + dpp_f64<0x112, 0xf>(x);     // row_shr:2
+    x = x + dpp_f64<0x114, 0xf>(x);     // row_shr:4
+    x = x + dpp_f64<0x118, 0xf>(x);     // row_shr:8
+    x = x + dpp_f64<0x142, 0xa>(x);     // row_bcast:15 into rows 1, 3
+    x = x + dpp_f64<0x143, 0xc>(x);     // row_bcast:31 into rows 2, 3
+    return x;
+}
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const uint64_t u = as_u64(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return as_f64(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double fold_exact_wave(const double* __restrict__ v, uint32_t k, const uint32_t e,
+                                                  double run, const int lane) {
+    constexpr int kPer = 4;                       // consecutive values per lane
+    while (k < e) {
+        const uint32_t n = min(64u * kPer, e - k);
+        const int be = (int)((as_u64(run) >> 52) & 0x7ffu);
+        if (be < 53 || be == 0x7ff || !(run < 0.0)) {   // zero / tiny / subnormal / positive / inf / NaN sum
+            run = run + v[k];
+            ++k;
+            continue;
+        }
+        const double U = as_f64((uint64_t)(be - 52) << 52);        // ulp of the binade
+        const double iU = as_f64((uint64_t)(2098 - be) << 52);     // 1 / U
+        const uint32_t p0 = (uint32_t)lane * kPer;
+        double pre[kPer];
+        bool ok[kPer];
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const double x0 = p0 + j < n ? v[k + p0 + j] : 0.0;
+            const double t = x0 * iU;
+            const double ni = __builtin_rint(t);
+            ok[j] = !(x0 > 0.0) && __builtin_fabs(t) < 0x1p53 && __builtin_fabs(t - ni) != 0.5;
+            acc = acc + ni;
+            pre[j] = acc;                         // lane-local inclusive partial sums
+        }
+        const double S0 = run * iU;               // s / U, an integer in (-2^53, -2^52]
+        // the state before this lane's first value: the previous lane's
+        // inclusive scan value (wave_shr:1), S0 for lane 0
+        const double X = wave_incl_scan_f64(lane == 0 ? S0 + acc : acc);
+        const double Xp = dpp_f64<0x138, 0xf>(X);
+        const double B = lane == 0 ? S0 : Xp;
+        int fb = kPer;                            // this lane's first bad value
+#pragma unroll
+        for (int j = kPer - 1; j >= 0; --j) {
+            const double q = B + pre[j];
+            const bool good = (ok[j] && q > -0x1p53 && q <= -0x1p52) || p0 + j >= n;
+            fb = good ? fb : j;
+        }
+        const uint64_t bad = __ballot(fb < kPer);
+        uint32_t f = n;
+        if (bad) {
+            const int L = __builtin_ctzll(bad);
+            f = min(n, (uint32_t)L * kPer + (uint32_t)__builtin_amdgcn_readlane(fb, L));
+        }
+        if (f > 0) {
+            const uint32_t g = f - 1;             // the state after value g
+            const int jj = (int)(g % kPer);
+            const double qs = B + (jj == 0 ? pre[0] : jj == 1 ? pre[1] : jj == 2 ? pre[2] : pre[3]);
+            run = readlane_f64(qs, (int)(g / kPer)) * U;            // exact: an integer times a power of two
+        }
+        if (f < n) {
+            run = run + v[k + f];                                   // the sequential rule for this value
+            k += f + 1;
+        } else {
+            k += n;
+        }
+    }
+    return run;
+}
+
 constexpr uint32_t kLoBlock = 8192;                    // features per block (128 chunks of 64)
 constexpr uint32_t kLoChunks = kLoBlock / 64;
 constexpr int kLoThreads = 1024;
@@ -1787,7 +1891,7 @@ constexpr int kLoPer = kLoChunks / (kLoThreads / 64); // chunks per wave per blo
 template <int KIND>
 __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t ntot,
                                                         const double* __restrict__ vals,
-                                                        const uint64_t* __restrict__ bits, ScoreOut out) {
+                                                        const uint64_t* __restrict__ bits, ScoreOut out, int wide) {
     __shared__ double cbuf[2][kLoBlock];
     __shared__ uint32_t ccnt[2][kLoChunks];                // inliers per chunk
     __shared__ uint32_t coff[2][kLoChunks + 1];            // exclusive prefix; [kLoChunks] = block total
@@ -1893,6 +1997,23 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
             }
             for (; k < e; ++k) run += cb[k];
         };
+        if (wide) {
+            // whole-wave exact folds: the class sum (lane 0's chain) and, for
+            // KIND 2 after the class boundary, the running total (lane 1's)
+            const double r0 = __shfl(run, 0), r1 = __shfl(run, 1);
+            const double c = fold_exact_wave(cb, 0, bpos, r0, lane);
+            // before the class boundary both chains hold the same sum: one fold
+            double tt = (KIND == 2 && as_u64(r1) != as_u64(r0)) ? fold_exact_wave(cb, 0, bpos, r1, lane) : c;
+            double cc = c;
+            if (KIND == 2 && has_b) {
+                hold = c;                                    // lane 0 keeps it (uniform value)
+                cc = 0.0;
+            }
+            cc = fold_exact_wave(cb, bpos, total, cc, lane);
+            if (KIND == 2) tt = fold_exact_wave(cb, bpos, total, tt, lane);
+            run = (KIND == 2 && lane == 1) ? tt : cc;
+            continue;
+        }
         fold(0, bpos);
         if (KIND == 2 && has_b && lane == 0) {
             hold = run;
@@ -3273,6 +3394,14 @@ hipError_t launch_select_batches(const WgBest* wg, size_t wg_stride, const RectM
 }
 
 
+// GCR_LO_FOLD=wide: k_lo_chain folds with the wave-parallel exact fold
+// instead of one lane per chain (read per launch; measured no faster, see
+// DESIGN.md)
+bool lo_fold_wide() {
+    const char* e = getenv("GCR_LO_FOLD");
+    return e && e[0] == 'w';
+}
+
 size_t small_score_pairs(const DevProblem& p) {
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t pad1 = (p.solver == 2) ? ((p.cls[1].n + 63u) & ~63u) : 0u;
@@ -3293,7 +3422,8 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         using M = typename ModelOf<KIND>::type;
         hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), inc, T[0], T[1],
                            pad0, ntot, vals, bits, lb);
-        hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits, out);
+        hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits, out,
+                           lo_fold_wide() ? 1 : 0);
     };
     switch (p.solver) {
         case 0: go(std::integral_constant<int, 0>{}); break;
@@ -3318,8 +3448,26 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
     return hipGetLastError();
 }
 
+// op 7 of gcr_debug_math: out[0] = fold_exact_wave over a[0, n) from +0.0,
+// out[1] = the same sum by one lane's sequential loop (one wave)
+__global__ __launch_bounds__(64) void k_fold_test(const double* __restrict__ a, uint32_t n, double* out) {
+    const int lane = threadIdx.x;
+    const double w = fold_exact_wave(a, 0, n, 0.0, lane);
+    if (lane == 0) {
+        double s = 0.0;
+        for (uint32_t k = 0; k < n; ++k) s = s + a[k];
+        out[0] = w;
+        out[1] = s;
+    }
+}
+
 hipError_t launch_math(int op, const double* a, const double* b, size_t n, double* out, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    if (op == 7) {
+        if (n < 2 || n > 0xffffffffull) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_fold_test, dim3(1), dim3(64), 0, stream, a, (uint32_t)n, out);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_math, dim3(blocks_for(n, 256)), dim3(256), 0, stream, op, a, b, n, out);
     return hipGetLastError();
 }

@@ -281,7 +281,10 @@ double gcr_host_atan2(double y, double x);
 int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls, uint64_t n,
                     uint32_t m, uint32_t* out);
 /* device evaluation of the same primitives over arrays (GPU parity tests):
- * op 0 log(a), 1 pow_m3(a), 2 atan2(a, b), 3 a / b, 4 sqrt(a) */
+ * op 0 log(a), 1 pow_m3(a), 2 atan2(a, b), 3 a / b, 4 sqrt(a),
+ * 5 clip_angle_small(a), 6 clip_angle(a);
+ * op 7 (n >= 2): out[0] = the wave-parallel exact in-order sum of a[0, n)
+ * (k_lo_chain's fold), out[1] = the same sum by a sequential loop */
 int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out);
 /* perspective_warp's resampling (examples/utils.py:92-123, cv2.warpPerspective
  * with INTER_LINEAR): dst pixel (x, y) <- bilinear sample of src at

@@ -1,0 +1,91 @@
+"""Device check of k_lo_chain's wave-parallel exact fold (fold_exact_wave,
+gcr_debug_math op 7) against the sequential fp64 sum on adversarial sequences
+(ties at every scale, binade crossings, zeros, subnormals, huge values, inf,
+NaN, lengths around the 64-lane batch), and the small-batch scorer with the
+wide fold (GCR_LO_FOLD=wide) against the default one-lane fold on every estimator."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from fold_cases import cases, sequential
+from gcr_testutil import CorrProblem, Problem
+from pygcransac import _native as N
+from pygcransac import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _fold(v):
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    out = np.zeros(max(2, v.size))
+    dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    N.check(N.lib.gcr_debug_math(N.context(0), 7, dp(v), None, v.size, dp(out)))
+    return out[0], out[1]
+
+
+def _same(a, b):
+    return np.float64(a).tobytes() == np.float64(b).tobytes() or (a != a and b != b)
+
+
+@pytest.mark.parametrize("name", sorted(cases()))
+def test_device_fold_equals_sequential_sum(name):
+    v = cases()[name]
+    wide, seq = _fold(v)
+    ref = sequential(v)
+    assert _same(seq, ref), (seq, ref)
+    assert _same(wide, ref), (wide, ref)
+
+
+def test_device_fold_random():
+    rng = np.random.default_rng(5)
+    for _ in range(60):
+        n = int(rng.integers(2, 20000))
+        scale = 10.0 ** rng.uniform(-8, 8)
+        v = -rng.uniform(0, scale, n)
+        if rng.random() < 0.5:
+            v = np.round(v / scale * 64) * scale / 64
+        wide, _ = _fold(v)
+        assert _same(wide, sequential(v))
+
+
+def _small_scores(kind, fold, monkeypatch):
+    monkeypatch.setenv("GCR_DEBUG_SCORER", "small")
+    if fold:
+        monkeypatch.setenv("GCR_LO_FOLD", fold)
+    else:
+        monkeypatch.delenv("GCR_LO_FOLD", raising=False)
+    if kind >= N.SOLVER_HOMOGRAPHY4:
+        c, _, H, thr = (S.problem_h(3000, 0.5, seed=31) if kind == N.SOLVER_HOMOGRAPHY4
+                        else S.problem_f(3000, 0.6, seed=32))
+        prob = CorrProblem(kind, c)
+        p = N.default_params()
+        p.scale_residual_thresh = thr
+        rng = np.random.default_rng(3)
+        Hs = np.ascontiguousarray(np.repeat(np.asarray(H, float).reshape(1, 9), 40, 0)
+                                  * (1.0 + 1e-4 * rng.standard_normal((40, 9))))
+        n0 = np.zeros(40, np.uint32)
+        v0 = np.zeros(40)
+        tot = np.zeros(40)
+        dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        N.check(N.lib.gcr_debug_score_h(prob.h, C.byref(p), dp(Hs), 40, n0.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                        dp(v0), dp(tot)))
+        return n0.tobytes() + v0.tobytes() + tot.tobytes()
+    if kind == N.SOLVER_SIFT22:
+        fs, fo, _, _, t0, t1 = S.problem_m2(5000, 4000, seed=33)
+        prob = Problem(kind, fs, fo)
+    else:
+        fs, _, t0 = S.problem_m1(9000, seed=34 + kind)
+        fo, t1 = None, 0.0
+        prob = Problem(kind, fs, fo)
+    inc, models = prob.generate(23, 0, 256)
+    uniq = models[inc <= 101][:50]
+    return b"".join(np.asarray(a).tobytes() for a in prob.score_raw(uniq, t0, t1))
+
+
+@pytest.mark.parametrize("kind", [N.SOLVER_SCALE3, N.SOLVER_SCALE3_ORIGINAL, N.SOLVER_SIFT22,
+                                  N.SOLVER_HOMOGRAPHY4, N.SOLVER_FUNDAMENTAL7])
+def test_small_scorer_wide_fold_equals_one_lane_fold(kind, monkeypatch):
+    a = _small_scores(kind, "wide", monkeypatch)
+    b = _small_scores(kind, None, monkeypatch)
+    assert a == b
