@@ -1160,6 +1160,13 @@ public:
         compact_ = false;         // fixed-size per-hypothesis records cross the exchange
     }
 
+    // GCR_SPEC_TRIM=0: speculate even when the chunk's best member already
+    // ends the run inside it
+    static bool spec_trim_on() {
+        const char* e = getenv("GCR_SPEC_TRIM");           // read per run
+        return !(e && e[0] == '0');
+    }
+
     // GCR_REPLAY=slots: the per-slot replay of round 2 (every chunk's
     // per-hypothesis records copied back and walked on the host), kept as the
     // A/B reference of the summary replay
@@ -1481,7 +1488,24 @@ public:
             // with this chunk's totals known the next one may be certain, or
             // (adaptive runs) likely: below the threshold known before this
             // chunk's replay, which only its new bests can lower
-            if (ahead_ok && q.size() == 1 && (itb[world_] < min_it || (spec_ok && itb[world_] < thr())) &&
+            // A speculative chunk is skipped when this chunk's own best
+            // member already brings the threshold inside it (the usual end of
+            // a short run): its scoring would occupy the CUs that this
+            // chunk's LO and refit kernels need (a ~85 us scorer launch held
+            // the LO masks for 60-80 us).  LO rarely raises the threshold
+            // again; if it does, the next chunk is issued after the replay.
+            // Results are identical either way.
+            uint64_t spec_thr = thr();
+            if (spec_ok && spec_trim_on())
+                for (int r = 0; r < world_; ++r)
+                    if (S[r].ncand) {
+                        const SumHyp& h = S[r].cand[S[r].ncand - 1];
+                        const uint32_t rn[2] = {h.n0, h.n1};
+                        const HScore sc = finish(rn, h.v0, h.v1, h.tot);
+                        if (best_.sum < sc.sum)
+                            spec_thr = std::min(spec_thr, std::max(min_it, iteration_number(sc.n)));
+                    }
+            if (ahead_ok && q.size() == 1 && (itb[world_] < min_it || (spec_ok && itb[world_] < spec_thr)) &&
                 issue(itb[world_]))
                 ++st_.prefetched_chunks;
             bool stopped = false;

@@ -1823,14 +1823,16 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 }
 
 __device__ __forceinline__ double fold_exact_wave(const double* __restrict__ v, uint32_t k, const uint32_t e,
-                                                  double run, const int lane) {
+                                                  double run, const int lane, uint32_t* stats = nullptr) {
     constexpr int kPer = 4;                       // consecutive values per lane
     while (k < e) {
         const uint32_t n = min(64u * kPer, e - k);
         const int be = (int)((as_u64(run) >> 52) & 0x7ffu);
+        if (stats) ++stats[0];
         if (be < 53 || be == 0x7ff || !(run < 0.0)) {   // zero / tiny / subnormal / positive / inf / NaN sum
             run = run + v[k];
             ++k;
+            if (stats) ++stats[1];
             continue;
         }
         const double U = as_f64((uint64_t)(be - 52) << 52);        // ulp of the binade
@@ -1876,6 +1878,7 @@ __device__ __forceinline__ double fold_exact_wave(const double* __restrict__ v, 
         if (f < n) {
             run = run + v[k + f];                                   // the sequential rule for this value
             k += f + 1;
+            if (stats) ++stats[1];
         } else {
             k += n;
         }
@@ -1888,10 +1891,48 @@ constexpr uint32_t kLoChunks = kLoBlock / 64;
 constexpr int kLoThreads = 1024;
 constexpr int kLoPer = kLoChunks / (kLoThreads / 64); // chunks per wave per block
 
-template <int KIND>
+// The one-lane in-order fold of k_lo_chain: ping-pong batches of 16 LDS
+// reads, the next batch in flight during the current batch's dependent adds
+// (sched_barrier keeps the scheduler from sinking the reads back next to
+// their adds).
+__device__ __forceinline__ double fold_seq_lane(const double* __restrict__ cb, uint32_t k, const uint32_t e,
+                                                double run) {
+    if (k + 32 <= e) {
+        double ta[16], tb[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) ta[u] = cb[k + u];
+#pragma unroll 1
+        for (; k + 32 <= e; k += 32) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) tb[u] = cb[k + 16 + u];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) run += ta[u];
+            __builtin_amdgcn_sched_barrier(0);
+            // the batch after next (clamped inside the buffer: a clamped
+            // batch lies past e and is never added)
+            const uint32_t nx = min(k + 32, kLoBlock - 16);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) ta[u] = cb[nx + u];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) run += tb[u];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (k + 16 <= e) {                         // ta = cb[k, k + 16)
+#pragma unroll
+            for (int u = 0; u < 16; ++u) run += ta[u];
+            k += 16;
+        }
+    }
+    for (; k < e; ++k) run += cb[k];
+    return run;
+}
+
+template <int KIND, bool kWide>
 __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t ntot,
                                                         const double* __restrict__ vals,
-                                                        const uint64_t* __restrict__ bits, ScoreOut out, int wide) {
+                                                        const uint64_t* __restrict__ bits, ScoreOut out) {
     __shared__ double cbuf[2][kLoBlock];
     __shared__ uint32_t ccnt[2][kLoChunks];                // inliers per chunk
     __shared__ uint32_t coff[2][kLoChunks + 1];            // exclusive prefix; [kLoChunks] = block total
@@ -1961,65 +2002,73 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
         const uint32_t bpos = cb0 < ch0 ? 0u : (has_b ? co[cb0 - ch0] : total);   // values before class 1
         cnt0 += bpos;
         cntall += total;
-        auto fold = [&](uint32_t k, uint32_t e) {
-            if (lane >= kChains) return;
-            if (k + 32 <= e) {
-                // ping-pong batches of 16: the next batch's reads are in
-                // flight during the current batch's dependent adds
-                // (sched_barrier keeps the scheduler from sinking the reads
-                // back next to their adds)
-                double ta[16], tb[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) ta[u] = cb[k + u];
+        if constexpr (kWide) {
+            // whole-wave exact folds, one call site (register pressure): the
+            // class sum (lane 0's chain) and, for KIND 2, the running total
+            // (lane 1's), which before the class boundary is the same sum
+            double cc = __shfl(run, 0), tt = __shfl(run, 1);
+            const bool same = as_u64(cc) == as_u64(tt);
 #pragma unroll 1
-                for (; k + 32 <= e; k += 32) {
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) tb[u] = cb[k + 16 + u];
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) run += ta[u];
-                    __builtin_amdgcn_sched_barrier(0);
-                    // the batch after next (clamped inside the buffer: a
-                    // clamped batch lies past e and is never added)
-                    const uint32_t nx = min(k + 32, kLoBlock - 16);
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) ta[u] = cb[nx + u];
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) run += tb[u];
-                    __builtin_amdgcn_sched_barrier(0);
+            for (int ps = 0; ps < 4; ++ps) {
+                // 0: class-0 part of the class chain; 1: of the total (KIND 2,
+                // when it differs); 2: class-1 part of the class chain (after
+                // the boundary's restart); 3: of the total (KIND 2)
+                if ((ps == 1 || ps == 3) && KIND != 2) continue;
+                if (ps == 1 && same) { tt = cc; continue; }
+                if (ps == 2 && KIND == 2 && has_b) {
+                    hold = cc;                       // lane 0 keeps it (uniform value)
+                    cc = 0.0;
                 }
-                if (k + 16 <= e) {                         // ta = cb[k, k + 16)
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) run += ta[u];
-                    k += 16;
-                }
+                const uint32_t kb = ps < 2 ? 0u : bpos, ke = ps < 2 ? bpos : total;
+                const double r = fold_exact_wave(cb, kb, ke, (ps & 1) ? tt : cc, lane);
+                if (ps & 1) tt = r; else cc = r;
             }
-            for (; k < e; ++k) run += cb[k];
-        };
-        if (wide) {
-            // whole-wave exact folds: the class sum (lane 0's chain) and, for
-            // KIND 2 after the class boundary, the running total (lane 1's)
-            const double r0 = __shfl(run, 0), r1 = __shfl(run, 1);
-            const double c = fold_exact_wave(cb, 0, bpos, r0, lane);
-            // before the class boundary both chains hold the same sum: one fold
-            double tt = (KIND == 2 && as_u64(r1) != as_u64(r0)) ? fold_exact_wave(cb, 0, bpos, r1, lane) : c;
-            double cc = c;
-            if (KIND == 2 && has_b) {
-                hold = c;                                    // lane 0 keeps it (uniform value)
-                cc = 0.0;
-            }
-            cc = fold_exact_wave(cb, bpos, total, cc, lane);
-            if (KIND == 2) tt = fold_exact_wave(cb, bpos, total, tt, lane);
             run = (KIND == 2 && lane == 1) ? tt : cc;
-            continue;
+        } else {
+            // one-lane folds: lane 0 the class sum, lane 1 (KIND 2) the total
+            auto fold = [&](uint32_t k, uint32_t e) {
+                if (lane >= kChains) return;
+                if (k + 32 <= e) {
+                    // ping-pong batches of 16: the next batch's reads are in
+                    // flight during the current batch's dependent adds
+                    // (sched_barrier keeps the scheduler from sinking the reads
+                    // back next to their adds)
+                    double ta[16], tb[16];
+    #pragma unroll
+                    for (int u = 0; u < 16; ++u) ta[u] = cb[k + u];
+    #pragma unroll 1
+                    for (; k + 32 <= e; k += 32) {
+    #pragma unroll
+                        for (int u = 0; u < 16; ++u) tb[u] = cb[k + 16 + u];
+                        __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                        for (int u = 0; u < 16; ++u) run += ta[u];
+                        __builtin_amdgcn_sched_barrier(0);
+                        // the batch after next (clamped inside the buffer: a
+                        // clamped batch lies past e and is never added)
+                        const uint32_t nx = min(k + 32, kLoBlock - 16);
+    #pragma unroll
+                        for (int u = 0; u < 16; ++u) ta[u] = cb[nx + u];
+                        __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                        for (int u = 0; u < 16; ++u) run += tb[u];
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    if (k + 16 <= e) {                         // ta = cb[k, k + 16)
+    #pragma unroll
+                        for (int u = 0; u < 16; ++u) run += ta[u];
+                        k += 16;
+                    }
+                }
+                for (; k < e; ++k) run += cb[k];
+            };
+            fold(0, bpos);
+            if (KIND == 2 && has_b && lane == 0) {
+                hold = run;
+                run = 0.0;
+            }
+            fold(bpos, total);
         }
-        fold(0, bpos);
-        if (KIND == 2 && has_b && lane == 0) {
-            hold = run;
-            run = 0.0;
-        }
-        fold(bpos, total);
     }
     if (wave == 0) {
         const double tot = KIND == 2 ? __shfl(run, 1) : run;
@@ -3422,8 +3471,12 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         using M = typename ModelOf<KIND>::type;
         hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), inc, T[0], T[1],
                            pad0, ntot, vals, bits, lb);
-        hipLaunchKernelGGL(k_lo_chain<KIND>, dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits, out,
-                           lo_fold_wide() ? 1 : 0);
+        if (lo_fold_wide())
+            hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits,
+                               out);
+        else
+            hipLaunchKernelGGL((k_lo_chain<KIND, false>), dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals,
+                               bits, out);
     };
     switch (p.solver) {
         case 0: go(std::integral_constant<int, 0>{}); break;
@@ -3449,15 +3502,36 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
 }
 
 // op 7 of gcr_debug_math: out[0] = fold_exact_wave over a[0, n) from +0.0,
-// out[1] = the same sum by one lane's sequential loop (one wave)
+// out[1] = the same sum by one lane's sequential loop (one wave).  For
+// n <= kLoBlock both run over an LDS copy (as in k_lo_chain) and out[2..5] =
+// cycles of the wave fold, cycles of the sequential fold, wave steps, values
+// added one by one (n >= 6).
 __global__ __launch_bounds__(64) void k_fold_test(const double* __restrict__ a, uint32_t n, double* out) {
+    __shared__ double buf[kLoBlock];
     const int lane = threadIdx.x;
-    const double w = fold_exact_wave(a, 0, n, 0.0, lane);
+    const bool lds = n <= kLoBlock;
+    if (lds)
+        for (uint32_t i = lane; i < n; i += 64) buf[i] = a[i];
+    __syncthreads();
+    const double* v = lds ? buf : a;
+    uint32_t st[2] = {0, 0};
+    const uint64_t t0 = __builtin_readcyclecounter();
+    const double w = fold_exact_wave(v, 0, n, 0.0, lane, st);
+    const uint64_t t1 = __builtin_readcyclecounter();
+    double s = 0.0;
+    if (lane == 0) s = lds ? fold_seq_lane(buf, 0, n, 0.0) : 0.0;
+    if (lane == 0 && !lds)
+        for (uint32_t k = 0; k < n; ++k) s = s + v[k];
+    const uint64_t t2 = __builtin_readcyclecounter();
     if (lane == 0) {
-        double s = 0.0;
-        for (uint32_t k = 0; k < n; ++k) s = s + a[k];
         out[0] = w;
         out[1] = s;
+        if (lds && n >= 6) {
+            out[2] = (double)(t1 - t0);
+            out[3] = (double)(t2 - t1);
+            out[4] = st[0];
+            out[5] = st[1];
+        }
     }
 }
 

@@ -45,21 +45,51 @@ struct PartCand {
     double val;
 };
 
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(v, d);
-        if (lane >= d) v += o;
-    }
+// Wave scans by DPP (row shifts, then the two row broadcasts): the lanes
+// exchange through the VALU's data-parallel moves instead of ds_bpermute
+// round trips through the LDS (a scan step ~10 cycles instead of ~100; the
+// one-wave summary k_sum_one runs three scans per 64 positions).  Integer sums
+// and maxima: the results do not depend on the combination order.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double old, double v) {
+    const uint64_t o = __builtin_bit_cast(uint64_t, old), u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = dpp_u32<CTRL, ROWS>((uint32_t)o, (uint32_t)u);
+    const uint32_t hi = dpp_u32<CTRL, ROWS>((uint32_t)(o >> 32), (uint32_t)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, int) {
+    v += dpp_u32<0x111, 0xf>(0u, v);     // row_shr:1
+    v += dpp_u32<0x112, 0xf>(0u, v);     // row_shr:2
+    v += dpp_u32<0x114, 0xf>(0u, v);     // row_shr:4
+    v += dpp_u32<0x118, 0xf>(0u, v);     // row_shr:8
+    v += dpp_u32<0x142, 0xa>(0u, v);     // row_bcast:15 into rows 1, 3
+    v += dpp_u32<0x143, 0xc>(0u, v);     // row_bcast:31 into rows 2, 3
     return v;
 }
-__device__ __forceinline__ double wave_incl_max(double v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const double o = __shfl_up(v, d);
-        if (lane >= d) v = v < o ? o : v;
-    }
+__device__ __forceinline__ double dmax(double v, double o) { return v < o ? o : v; }
+__device__ __forceinline__ double wave_incl_max(double v, int) {
+    constexpr double ninf = -__builtin_huge_val();
+    v = dmax(v, dpp_f64<0x111, 0xf>(ninf, v));
+    v = dmax(v, dpp_f64<0x112, 0xf>(ninf, v));
+    v = dmax(v, dpp_f64<0x114, 0xf>(ninf, v));
+    v = dmax(v, dpp_f64<0x118, 0xf>(ninf, v));
+    v = dmax(v, dpp_f64<0x142, 0xa>(ninf, v));
+    v = dmax(v, dpp_f64<0x143, 0xc>(ninf, v));
     return v;
+}
+// the previous lane's value (wave_shr:1); lane 0 gets `old`
+__device__ __forceinline__ double prev_lane_f64(double old, double v) { return dpp_f64<0x138, 0xf>(old, v); }
+// a lane's value, wave-uniform index
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ double lane_f64(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    return __builtin_bit_cast(double, ((uint64_t)lane_u32((uint32_t)(u >> 32), l) << 32) | lane_u32((uint32_t)u, l));
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -122,12 +152,12 @@ __global__ __launch_bounds__(64) void k_sum_parts(SumArgs a) {
             // iterations before that position's slot: the exclusive prefix at
             // the position minus its slot's own inc when q > 0
             const uint32_t q = (base + o + hl) % a.per;
-            const uint32_t excl = __shfl(cs - c, hl);
+            const uint32_t excl = lane_u32(cs - c, hl);
             const uint32_t own = q > 0 ? (uint32_t)contrib_of(a.inc[base + o + hl - q]) : 0u;
             last = (int32_t)(base + o + hl);
             last_it = contrib + excl - own;
         }
-        contrib += __shfl(cs, 63);
+        contrib += lane_u32(cs, 63);
         live += (uint32_t)__builtin_popcountll(bl);
     }
     if (lane == 0) {
@@ -171,7 +201,7 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
                 if (a.solver == 2 && !valid_model_sift22(models[p])) val = -1.0;
         }
         const double im = wave_incl_max(val, lane);
-        const double before = __shfl_up(im, 1);
+        const double before = prev_lane_f64(run, im);
         const double bar = lane == 0 ? run : (run < before ? before : run);
         const bool cand = val >= 0.0 && val > bar;
         const uint64_t bc = __ballot(cand);
@@ -190,11 +220,11 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
         const uint32_t add = (uint32_t)__builtin_popcountll(bc);
         if (nc + add > a.cap) over = 1;
         nc = min(nc + add, a.cap);
-        const double wm = __shfl(im, 63);
+        const double wm = lane_f64(im, 63);
         run = run < wm ? wm : run;
         pmax = pmax < wm ? wm : pmax;
-        coff += __shfl(cs, 63);
-        loff += __shfl(ls, 63);
+        coff += lane_u32(cs, 63);
+        loff += lane_u32(ls, 63);
     }
     if (lane == 0) {
         SumPart& s = a.parts[k];
@@ -368,16 +398,16 @@ __global__ __launch_bounds__(kSumFinalThreads) void k_sum_final(SumArgs a) {
             const uint32_t q = (base + o + (uint32_t)hl) % a.per;
             const uint32_t own = q > 0 ? contrib_of(a.inc[base + o + hl - q]) : 0u;
             lastp = (int32_t)(base + o + (uint32_t)hl);
-            last_it = __shfl(excl, hl) - own;
-            last_hb = __shfl(lexcl, hl);
+            last_it = lane_u32(excl, hl) - own;
+            last_hb = lane_u32(lexcl, hl);
         }
         if (hit) {
             stop_p = base + o + lim;
-            stop_it = __shfl(excl, (int)lim);
-            stop_hb = __shfl(lexcl, (int)lim);
+            stop_it = lane_u32(excl, (int)lim);
+            stop_hb = lane_u32(lexcl, (int)lim);
         }
-        run += __shfl(cs, 63);
-        lrun += __shfl(ls, 63);
+        run += lane_u32(cs, 63);
+        lrun += lane_u32(ls, 63);
     }
     if (lane == 0) {
         if (stop_p == 0xffffffffu) {
@@ -436,8 +466,8 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
                 if (hit) {
                     lim = (uint32_t)__builtin_ctzll(hit);
                     stop_p = o + lim;
-                    stop_it = __shfl(excl, (int)lim);
-                    stop_hb = __shfl(hb, (int)lim);
+                    stop_it = lane_u32(excl, (int)lim);
+                    stop_hb = lane_u32(hb, (int)lim);
                 }
             } else {
                 lim = 0u;                                       // past the stop: totals only
@@ -449,8 +479,8 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
             const uint32_t q = (o + (uint32_t)hl) % a.per;
             const uint32_t own = q > 0 ? contrib_of(a.inc[o + hl - q]) : 0u;
             lastp = (int32_t)(o + (uint32_t)hl);
-            last_it = __shfl(excl, hl) - own;
-            last_hb = __shfl(hb, hl);
+            last_it = lane_u32(excl, hl) - own;
+            last_hb = lane_u32(hb, hl);
         }
         if (!locate) {
             double val = -1.0;
@@ -461,7 +491,7 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
                     if (a.solver == 2 && !valid_model_sift22(models[p])) val = -1.0;
             }
             const double im = wave_incl_max(val, lane);
-            const double before = __shfl_up(im, 1);
+            const double before = prev_lane_f64(run, im);
             const double bar = lane == 0 ? run : (run < before ? before : run);
             const bool cand = val >= 0.0 && val > bar;
             const uint64_t bc = __ballot(cand);
@@ -480,11 +510,11 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
             const uint32_t add = (uint32_t)__builtin_popcountll(bc);
             if (nc + add > a.cap) over = 1;
             nc = min(nc + add, a.cap);
-            const double wm = __shfl(im, 63);
+            const double wm = lane_f64(im, 63);
             run = run < wm ? wm : run;
         }
-        coff += __shfl(cs, 63);
-        loff += __shfl(ls, 63);
+        coff += lane_u32(cs, 63);
+        loff += lane_u32(ls, 63);
     }
     if (lane != 0) return;
     if (!locate) {

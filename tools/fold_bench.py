@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Cycle counts of k_lo_chain's two in-order folds over an LDS copy of one
+value sequence (gcr_debug_math op 7): the wave-parallel exact fold and the
+one-lane batched fold, on MSAC-like sequences (-r^2 of inliers)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "graph-cut-ransac_amd"))
+from pygcransac import _native as N  # noqa: E402
+
+
+def run(v):
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    out = np.zeros(max(8, v.size))
+    dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    N.check(N.lib.gcr_debug_math(N.context(0), 7, dp(v), None, v.size, dp(out)))
+    return out[:6]
+
+
+rng = np.random.default_rng(1)
+cases = {
+    "scale r^2, thr 0.05": -(rng.uniform(0, 1, 5000) * 0.05) ** 2 * 2.25,
+    "orient r^2, 1 deg": -(rng.uniform(0, 1, 5000) * np.radians(1.0)) ** 2 * 2.25,
+    "uniform [0, 2.25]": -rng.uniform(0, 2.25, 5000),
+    "2500 values": -rng.uniform(0, 2.25, 2500),
+    "8000 values": -rng.uniform(0, 2.25, 8000),
+}
+for name, v in cases.items():
+    for _ in range(2):
+        o = run(v)
+    same = o[0].tobytes() == o[1].tobytes()
+    print(f"{name:22s} n={v.size:5d} wide {o[2]:9.0f} cyc  seq {o[3]:9.0f} cyc  ratio {o[3] / o[2]:5.2f}  "
+          f"steps {o[4]:4.0f}  one-by-one {o[5]:4.0f}  equal {same}")
