@@ -1779,26 +1779,7 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
 // scan), and wave 0 folds them: lane 0 the class sum, lane 1 (KIND 2) the
 // running total.  Blocks alternate between two sets of LDS buffers, so the
 // next block's loads are issued while wave 0 still folds.
-// fold_exact_wave: the in-order running sum run += v[k], k = b .. e-1, by one
-// whole wave, bit-identical to the sequential fp64 loop (MSAC_scoring_function
-// .hpp:53-107 adds the inliers' terms one by one).  While the running sum s
-// stays in one binade [2^E, 2^(E+1)) its ulp U is fixed and s is a multiple of
-// U, so fl(s + v) = s + U * rint(v / U) unless v / U ends in exactly .5 (a
-// tie, whose rounding depends on the parity of s / U).  So 256 values at a
-// time (4 consecutive ones per lane): each value is scaled by 1/U (exact: a
-// power of two) and rounded to an integer, the lane adds its four in order,
-// an inclusive DPP scan over the lanes adds the lane totals to s / U, and the
-// first value that ties, is positive, too large or leaves the binade ends the
-// step's fast part.  The values are all <= 0 (MSAC terms -r^2; the sum only
-// grows in magnitude), so every partial sum before that value is an integer
-// below 2^53 in magnitude: all of this integer arithmetic in fp64 is exact.
-// The first bad value is added with one ordinary fp64 addition (the
-// sequential rule itself), and the next step starts after it in the new
-// binade; a zero, subnormal or non-finite running sum also takes the ordinary
-// addition.  In a long sum only the few binade crossings and the early ties
-// (values as large as the sum) are added one by one: ~5000 dependent adds
-// become ~40 wave steps.  All lanes of the wave call it; `v` may be LDS or
-// global memory.  GCR_LO_FOLD=wide selects it in k_lo_chain (A/B).
+// DPP helpers of the exact folds below (fp64 moves, wave scan, readlane)
 template <int CTRL, int ROWS>
 __device__ __forceinline__ double dpp_f64(double x) {      // DPP move of an fp64 value, 0 where nothing moves in
     const uint64_t u = as_u64(x);
@@ -1820,70 +1801,6 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
     return as_f64(((uint64_t)hi << 32) | lo);
-}
-
-__device__ __forceinline__ double fold_exact_wave(const double* __restrict__ v, uint32_t k, const uint32_t e,
-                                                  double run, const int lane, uint32_t* stats = nullptr) {
-    constexpr int kPer = 4;                       // consecutive values per lane
-    while (k < e) {
-        const uint32_t n = min(64u * kPer, e - k);
-        const int be = (int)((as_u64(run) >> 52) & 0x7ffu);
-        if (stats) ++stats[0];
-        if (be < 53 || be == 0x7ff || !(run < 0.0)) {   // zero / tiny / subnormal / positive / inf / NaN sum
-            run = run + v[k];
-            ++k;
-            if (stats) ++stats[1];
-            continue;
-        }
-        const double U = as_f64((uint64_t)(be - 52) << 52);        // ulp of the binade
-        const double iU = as_f64((uint64_t)(2098 - be) << 52);     // 1 / U
-        const uint32_t p0 = (uint32_t)lane * kPer;
-        double pre[kPer];
-        bool ok[kPer];
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const double x0 = p0 + j < n ? v[k + p0 + j] : 0.0;
-            const double t = x0 * iU;
-            const double ni = __builtin_rint(t);
-            ok[j] = !(x0 > 0.0) && __builtin_fabs(t) < 0x1p53 && __builtin_fabs(t - ni) != 0.5;
-            acc = acc + ni;
-            pre[j] = acc;                         // lane-local inclusive partial sums
-        }
-        const double S0 = run * iU;               // s / U, an integer in (-2^53, -2^52]
-        // the state before this lane's first value: the previous lane's
-        // inclusive scan value (wave_shr:1), S0 for lane 0
-        const double X = wave_incl_scan_f64(lane == 0 ? S0 + acc : acc);
-        const double Xp = dpp_f64<0x138, 0xf>(X);
-        const double B = lane == 0 ? S0 : Xp;
-        int fb = kPer;                            // this lane's first bad value
-#pragma unroll
-        for (int j = kPer - 1; j >= 0; --j) {
-            const double q = B + pre[j];
-            const bool good = (ok[j] && q > -0x1p53 && q <= -0x1p52) || p0 + j >= n;
-            fb = good ? fb : j;
-        }
-        const uint64_t bad = __ballot(fb < kPer);
-        uint32_t f = n;
-        if (bad) {
-            const int L = __builtin_ctzll(bad);
-            f = min(n, (uint32_t)L * kPer + (uint32_t)__builtin_amdgcn_readlane(fb, L));
-        }
-        if (f > 0) {
-            const uint32_t g = f - 1;             // the state after value g
-            const int jj = (int)(g % kPer);
-            const double qs = B + (jj == 0 ? pre[0] : jj == 1 ? pre[1] : jj == 2 ? pre[2] : pre[3]);
-            run = readlane_f64(qs, (int)(g / kPer)) * U;            // exact: an integer times a power of two
-        }
-        if (f < n) {
-            run = run + v[k + f];                                   // the sequential rule for this value
-            k += f + 1;
-            if (stats) ++stats[1];
-        } else {
-            k += n;
-        }
-    }
-    return run;
 }
 
 constexpr uint32_t kLoBlock = 8192;                    // features per block (128 chunks of 64)
@@ -1927,6 +1844,127 @@ __device__ __forceinline__ double fold_seq_lane(const double* __restrict__ cb, u
     }
     for (; k < e; ++k) run += cb[k];
     return run;
+}
+
+// fold_seq_lane with batches of 8 (fewer registers; for the short flagged
+// segments of fold_exact_seg)
+__device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, uint32_t k, const uint32_t e,
+                                                 double run) {
+    for (; k + 8 <= e; k += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = cb[k + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) run += t[u];
+    }
+    for (; k < e; ++k) run += cb[k];
+    return run;
+}
+
+// fold_exact_seg: the same in-order sum (bit-identical to the sequential
+// loop) by segments.  Lane l takes the l-th of 64 contiguous segments.
+//  1. Approximate segment sums and a DPP scan give every segment an
+//     approximate start value and so its binade E (ulp U); a segment whose
+//     approximate end lies in another binade, or that starts at a zero /
+//     positive / tiny sum, is flagged.
+//  2. Each lane adds rint(v / U) over its segment (four independent integer
+//     accumulators: integer sums below 2^53 are exact in any order) and flags
+//     ties (a fraction of exactly .5), positive and too large values.
+//  3. Lane 0 walks the segments in order: an unflagged segment whose exact
+//     start s lies in its binade E and whose end s / U + I stays in it is one
+//     exact fp64 addition (s + U I: both multiples of U, the result in the
+//     binade); any other segment is folded value by value (fold_seq_lane).
+// While s stays in one binade, fl(s + v) = s + U rint(v / U) except at ties,
+// so the result equals the sequential sum.  Only the segments where the sum
+// crosses a binade (about one per doubling of the sum) and the first ones
+// (values as large as the sum: ties) are folded value by value.  All lanes
+// call it; returns the sum on every lane.  GCR_LO_FOLD=wide selects it in k_lo_chain (A/B).
+__device__ __forceinline__ double fold_exact_seg(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
+                                                 double run, const int lane, uint32_t* stats = nullptr) {
+    const uint32_t n = e - k;
+    if (n < 512) return fold_seq_lane8(cb, k, e, run);   // short: every lane alike
+    // an odd segment length: the 64 lanes' LDS reads (stride 2L dwords) hit
+    // distinct banks
+    const uint64_t tp0 = stats ? __builtin_readcyclecounter() : 0;
+    const uint32_t L = ((n + 63) / 64) | 1u;
+    const uint32_t b = min(e, k + (uint32_t)lane * L), ee = min(e, b + L);
+    // 1. approximate sums, approximate starts
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    uint32_t i = b;
+    for (; i + 4 <= ee; i += 4) {
+        a0 += cb[i];
+        a1 += cb[i + 1];
+        a2 += cb[i + 2];
+        a3 += cb[i + 3];
+    }
+    for (; i < ee; ++i) a0 += cb[i];
+    const double a = (a0 + a1) + (a2 + a3);
+    const double X = wave_incl_scan_f64(a);
+    const double g = run + (X - a);                       // approximate start
+    const int be = (int)((as_u64(g) >> 52) & 0x7ffu);
+    const int be2 = (int)((as_u64(g + a) >> 52) & 0x7ffu);
+    bool flag = !(g < 0.0) || be < 53 || be == 0x7ff || be2 != be;
+    const int bs = flag ? 1075 : be;                      // a harmless scale for flagged segments
+    const double iU = as_f64((uint64_t)(2098 - bs) << 52);
+    // 2. integer increments
+    double i0 = 0.0, i1 = 0.0, i2 = 0.0, i3 = 0.0;
+    bool bad = false;
+    i = b;
+    for (; i + 4 <= ee; i += 4) {
+        const double v0 = cb[i], v1 = cb[i + 1], v2 = cb[i + 2], v3 = cb[i + 3];
+        const double t0 = v0 * iU, t1 = v1 * iU, t2 = v2 * iU, t3 = v3 * iU;
+        const double n0 = __builtin_rint(t0), n1 = __builtin_rint(t1), n2 = __builtin_rint(t2), n3 = __builtin_rint(t3);
+        bad |= (v0 > 0.0) | (v1 > 0.0) | (v2 > 0.0) | (v3 > 0.0);
+        bad |= !(__builtin_fabs(t0) < 0x1p53) | !(__builtin_fabs(t1) < 0x1p53) | !(__builtin_fabs(t2) < 0x1p53) |
+               !(__builtin_fabs(t3) < 0x1p53);
+        bad |= (__builtin_fabs(t0 - n0) == 0.5) | (__builtin_fabs(t1 - n1) == 0.5) | (__builtin_fabs(t2 - n2) == 0.5) |
+               (__builtin_fabs(t3 - n3) == 0.5);
+        i0 += n0;
+        i1 += n1;
+        i2 += n2;
+        i3 += n3;
+    }
+    for (; i < ee; ++i) {
+        const double v0 = cb[i], t0 = v0 * iU, n0 = __builtin_rint(t0);
+        bad |= (v0 > 0.0) | !(__builtin_fabs(t0) < 0x1p53) | (__builtin_fabs(t0 - n0) == 0.5);
+        i0 += n0;
+    }
+    flag = flag || bad;
+    const double I = flag ? 0.0 : (i0 + i1) + (i2 + i3);
+    const int E = flag ? 0 : be;
+    // 3. the in-order walk over the segments, by every lane alike (the
+    //    segments' records by readlane: cross-lane reads stay in uniform
+    //    control flow, and the result is the same on every lane)
+    double s = run;
+    const uint64_t tp1 = stats ? __builtin_readcyclecounter() : 0;
+    {
+        uint32_t folded = 0;
+        for (int l = 0; l < 64; ++l) {
+            const uint32_t sb = min(e, k + (uint32_t)l * L), se = min(e, sb + L);
+            if (sb >= se) break;
+            const int el = __builtin_amdgcn_readlane(E, l);
+            const int es = (int)((as_u64(s) >> 52) & 0x7ffu);
+            if (el != 0 && es == el && s < 0.0) {
+                const double Ul = as_f64((uint64_t)(el - 52) << 52), iUl = as_f64((uint64_t)(2098 - el) << 52);
+                const double S = s * iUl + readlane_f64(I, l);      // exact when it stays below 2^53
+                if (S > -0x1p53 && S <= -0x1p52) {
+                    s = S * Ul;
+                    continue;
+                }
+            }
+            const uint64_t tf0 = stats ? __builtin_readcyclecounter() : 0;
+            s = fold_seq_lane8(cb, sb, se, s);
+            ++folded;
+            if (stats) stats[4] += (uint32_t)(__builtin_readcyclecounter() - tf0);
+        }
+        if (stats) {
+            stats[0] += 64;
+            stats[1] += folded;
+            stats[2] += (uint32_t)(tp1 - tp0);
+            stats[3] += (uint32_t)(__builtin_readcyclecounter() - tp1);
+        }
+    }
+    return s;
 }
 
 template <int KIND, bool kWide>
@@ -2020,7 +2058,7 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
                     cc = 0.0;
                 }
                 const uint32_t kb = ps < 2 ? 0u : bpos, ke = ps < 2 ? bpos : total;
-                const double r = fold_exact_wave(cb, kb, ke, (ps & 1) ? tt : cc, lane);
+                const double r = fold_exact_seg(cb, kb, ke, (ps & 1) ? tt : cc, lane);
                 if (ps & 1) tt = r; else cc = r;
             }
             run = (KIND == 2 && lane == 1) ? tt : cc;
@@ -3501,11 +3539,12 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
     return hipGetLastError();
 }
 
-// op 7 of gcr_debug_math: out[0] = fold_exact_wave over a[0, n) from +0.0,
+// op 7 of gcr_debug_math: out[0] = fold_exact_seg over a[0, n) from +0.0,
 // out[1] = the same sum by one lane's sequential loop (one wave).  For
 // n <= kLoBlock both run over an LDS copy (as in k_lo_chain) and out[2..5] =
-// cycles of the wave fold, cycles of the sequential fold, wave steps, values
-// added one by one (n >= 6).
+// cycles of the segment fold, cycles of the one-lane fold, segments, segments
+// folded value by value, cycles of the parallel part, of the walk, of the
+// walk's value-by-value folds (n >= 9).
 __global__ __launch_bounds__(64) void k_fold_test(const double* __restrict__ a, uint32_t n, double* out) {
     __shared__ double buf[kLoBlock];
     const int lane = threadIdx.x;
@@ -3514,9 +3553,9 @@ __global__ __launch_bounds__(64) void k_fold_test(const double* __restrict__ a, 
         for (uint32_t i = lane; i < n; i += 64) buf[i] = a[i];
     __syncthreads();
     const double* v = lds ? buf : a;
-    uint32_t st[2] = {0, 0};
+    uint32_t st[5] = {0, 0, 0, 0, 0};
     const uint64_t t0 = __builtin_readcyclecounter();
-    const double w = fold_exact_wave(v, 0, n, 0.0, lane, st);
+    const double w = fold_exact_seg(v, 0, n, 0.0, lane, st);
     const uint64_t t1 = __builtin_readcyclecounter();
     double s = 0.0;
     if (lane == 0) s = lds ? fold_seq_lane(buf, 0, n, 0.0) : 0.0;
@@ -3526,11 +3565,14 @@ __global__ __launch_bounds__(64) void k_fold_test(const double* __restrict__ a, 
     if (lane == 0) {
         out[0] = w;
         out[1] = s;
-        if (lds && n >= 6) {
+        if (lds && n >= 9) {                  // out holds n doubles
             out[2] = (double)(t1 - t0);
             out[3] = (double)(t2 - t1);
             out[4] = st[0];
             out[5] = st[1];
+            out[6] = st[2];
+            out[7] = st[3];
+            out[8] = st[4];
         }
     }
 }

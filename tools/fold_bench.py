@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Cycle counts of k_lo_chain's two in-order folds over an LDS copy of one
-value sequence (gcr_debug_math op 7): the wave-parallel exact fold and the
+value sequence (gcr_debug_math op 7): the segment-parallel exact fold and the
 one-lane batched fold, on MSAC-like sequences (-r^2 of inliers)."""
 import ctypes as C
 import os
@@ -14,10 +14,10 @@ from pygcransac import _native as N  # noqa: E402
 
 def run(v):
     v = np.ascontiguousarray(v, dtype=np.float64)
-    out = np.zeros(max(8, v.size))
+    out = np.zeros(max(16, v.size))
     dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
     N.check(N.lib.gcr_debug_math(N.context(0), 7, dp(v), None, v.size, dp(out)))
-    return out[:6]
+    return out[:9]
 
 
 rng = np.random.default_rng(1)
@@ -33,4 +33,5 @@ for name, v in cases.items():
         o = run(v)
     same = o[0].tobytes() == o[1].tobytes()
     print(f"{name:22s} n={v.size:5d} wide {o[2]:9.0f} cyc  seq {o[3]:9.0f} cyc  ratio {o[3] / o[2]:5.2f}  "
-          f"steps {o[4]:4.0f}  one-by-one {o[5]:4.0f}  equal {same}")
+          f"segments {o[4]:4.0f}  folded one by one {o[5]:4.0f}  parallel {o[6]:7.0f} cyc  walk {o[7]:7.0f} cyc (folds {o[8]:7.0f})  "
+          f"equal {same}")
