@@ -1,0 +1,67 @@
+"""RCCL on the box: the "nccl" backend (RCCL on ROCm) with one rank per GPU.
+The one-GPU box cannot host two RCCL ranks (one GPU per rank), so this runs a
+world of 1 in a child process: process-group init over RCCL, the all-gather
+callback of gcr_problem_run_sharded (distributed.make_allgather) on device
+tensors, called the way the engine calls it, and bench.py's collectives
+(all_reduce MAX / SUM, all_gather) on device tensors.  The two-rank exchange
+itself is covered with gloo in test_gpu_sharded.py and test_distributed.py."""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from pygcransac import _native as N
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(os.path.dirname(HERE), "graph-cut-ransac_amd")
+
+CHILD = textwrap.dedent("""
+    import ctypes as C, os, sys
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.environ["GCR_PKG"])
+    from pygcransac import distributed as D
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + os.environ["GCR_PORT"], rank=0, world_size=1)
+    try:
+        assert dist.get_backend() == "nccl"
+        dev = torch.device("cuda", 0)
+        cb = D.make_allgather(dist, 1, dev)
+        send = np.arange(5000, dtype=np.uint8) * 7
+        recv = np.zeros_like(send)
+        rc = cb(None, send.ctypes.data, recv.ctypes.data, send.size)
+        assert rc == 0 and np.array_equal(send, recv), rc
+        t = torch.tensor([1.5], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        m = torch.tensor([3.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(m, op=dist.ReduceOp.SUM)
+        outs = [torch.empty(5, dtype=torch.float64, device=dev)]
+        dist.all_gather(outs, torch.arange(5, dtype=torch.float64, device=dev))
+        torch.cuda.synchronize()
+        assert t.item() == 1.5 and m.item() == 3.0 and outs[0].tolist() == [0, 1, 2, 3, 4]
+        dist.barrier()
+        print("RCCL OK")
+    finally:
+        dist.destroy_process_group()
+""")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(300)
+def test_rccl_world1_allgather_callback_and_bench_collectives():
+    if N.lib.gcr_device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    env = dict(os.environ, GCR_PKG=PKG, GCR_PORT=str(_free_port()), MASTER_ADDR="127.0.0.1")
+    out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and "RCCL OK" in out.stdout, out.stdout[-2000:] + out.stderr[-3000:]
