@@ -240,6 +240,7 @@ struct Workspace {
     DevBuf<uint64_t> sm_bits;           // launch_score_small: inlier bitmasks
     PinBuf<RectModel> h_lorect;         // score_models: small batches' models, read in place
     PinBuf<GeoModel> h_logeo;
+    PinBuf<uint64_t> h_mbits;           // launch_score_small: MSAC inlier ballots (ListBits.mbits)
     PinBuf<uint64_t> h_lbits;           // launch_score_small: LO list bits (ListBits), written by
                                         // the kernel straight into this mapped pinned buffer
     PinBuf<uint8_t> h_mask_all;
@@ -1160,6 +1161,12 @@ public:
         compact_ = false;         // fixed-size per-hypothesis records cross the exchange
     }
 
+    // GCR_LO_REUSE=0: the final refit always rescores the buffer model
+    static bool lo_reuse_on() {
+        const char* e = getenv("GCR_LO_REUSE");            // read per run
+        return !(e && e[0] == '0');
+    }
+
     // GCR_SPEC_TRIM=0: speculate even when the chunk's best member already
     // ends the run inside it
     static bool spec_trim_on() {
@@ -1649,7 +1656,19 @@ public:
             const ListReq msac{{Tm_[0], Tm_[1]}, 0};
             std::vector<uint32_t> lists[2];
             bool have_lists = false;
-            if (diff) {
+            // the adopted LO winner's own scoring launch already gave its
+            // score, raw counts and MSAC lists (the launch scores with Tm and
+            // mirrored its MSAC ballots): the rescore below would repeat that
+            // launch bit for bit
+            const bool cached = diff && lo_cache_.valid && lo_reuse_on() &&
+                                std::memcmp(&lo_cache_.model, &best_model_, sizeof(Model)) == 0;
+            if (cached) {
+                best_ = lo_cache_.score;
+                lists[0] = lo_cache_.lists[0];
+                lists[1] = lo_cache_.lists[1];
+                have_lists = true;
+                bufs_[off_] = Buffer{true, best_model_, {lo_cache_.raw[0], lo_cache_.raw[1]}};
+            } else if (diff) {
                 HScore s;
                 uint32_t rn[2];
                 if (score_models(&best_model_, 1, &s, rn, &msac)) {
@@ -1821,6 +1840,18 @@ private:
     Buffer bufs_[2];
     int off_ = 0;
     uint64_t lo_number_ = 0, gc_number_ = 0;
+    // the last adopted LO winner: its score, raw counts and the inlier lists
+    // of its scoring launch (LO rule 0 with Tlo, two-class problems), so the
+    // final refit need not rescore it when Tlo equals the MSAC threshold
+    struct LoCache {
+        bool valid = false;
+        Model model{};
+        HScore score{};
+        uint32_t raw[2] = {0, 0};
+        std::vector<uint32_t> lists[2];
+    } lo_cache_;
+    bool lo_lists_from_bits_ = false;     // the current LO winner's lists came from its scoring launch
+    std::vector<uint32_t> lo_msac_lists_[2];   // its MSAC lists (ListBits.mbits)
 
     bool valid_model(const Model& m) const { return Tr::valid(P_->solver, m); }
 
@@ -2197,6 +2228,7 @@ private:
     struct ListReq {
         double T[2];
         int rule;
+        bool msac = false;        // also the MSAC ballots (mlist_of)
     };
     bool score_models(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */,
                       const ListReq* req = nullptr) {
@@ -2227,7 +2259,7 @@ private:
             P_->w->sm_bits.ensure(pairs * n / 64);
             // the graph-cut labeling with pairwise terms needs the residuals
             lists = req != nullptr && !(req->rule == 2 && use_graph());
-            ListBits lb{{0.0, 0.0}, 0, prm_.spatial_coherence_weight, nullptr};
+            ListBits lb{{0.0, 0.0}, 0, prm_.spatial_coherence_weight, nullptr, nullptr};
             if (lists) {
                 // sized once for the largest small-scorer launch (a pinned
                 // reallocation costs milliseconds)
@@ -2238,6 +2270,13 @@ private:
                 lb.T[1] = req->T[1];
                 lb.rule = req->rule;
                 lb.bits = static_cast<uint64_t*>(dptr);
+                if (req->msac) {
+                    // the MSAC ballots as well (the final refit's lists of an
+                    // adopted LO winner, without rescoring it)
+                    P_->w->h_mbits.ensure(pairs * kSmallScore / 64);
+                    HIPC(hipHostGetDevicePointer(&dptr, P_->w->h_mbits.p, 0));
+                    lb.mbits = static_cast<uint64_t*>(dptr);
+                }
             }
             HIPC(launch_score_small(P_->dp, Tm_, dmodels, nullptr, n,
                                     zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev(), P_->w->sm_vals.p,
@@ -2259,10 +2298,10 @@ private:
 
     // model q's inlier lists from the bits of the last score_models(req) call
     // (small scorer pair layout: class 0 at [0, pad0), class 1 after it)
-    void list_of(uint32_t q, std::vector<uint32_t> lists[2]) const {
+    void list_of(uint32_t q, std::vector<uint32_t> lists[2], bool msac = false) const {
         const size_t pairs = small_score_pairs(P_->dp);
         const size_t pad0 = (N_[0] + 63) & ~(size_t)63;
-        const uint64_t* w = P_->w->h_lbits.p + q * (pairs / 64);
+        const uint64_t* w = (msac ? P_->w->h_mbits.p : P_->w->h_lbits.p) + q * (pairs / 64);
         for (int c = 0; c < 2; ++c) {
             lists[c].clear();
             if (c >= K_) continue;
@@ -2342,6 +2381,7 @@ private:
         static_assert(kMaxLOSample >= 7 * 7, "LO sample buffer");
 
         ++lo_number_;
+        lo_lists_from_bits_ = false;
         std::vector<uint32_t> inl[2];
         std::vector<std::array<std::vector<uint32_t>, 2>> trial_samples;
         std::vector<Model> trial_fit;
@@ -2353,7 +2393,7 @@ private:
         // the LO lists (threshold (1.5 thr)^2, labeling rule) of the round's
         // winner come back with the trial scores, so the next round starts
         // without its own mask launch + synchronisation
-        const ListReq lreq{{Tlo_[0], Tlo_[1]}, K_ == 2 ? 0 : 2};
+        const ListReq lreq{{Tlo_[0], Tlo_[1]}, K_ == 2 ? 0 : 2, lo_reuse_on()};
         bool have_inl = false;
         while (++gc_number_ < 10) {
             bool updated = false;
@@ -2427,9 +2467,11 @@ private:
                         lo_buf = Buffer{true, trial_models[q], {trial_raw[2 * q], trial_raw[2 * q + 1]}};
                     }
                 }
+                if (updated) lo_lists_from_bits_ = bits && lreq.msac;
                 if (updated && bits) {
                     list_of((uint32_t)win, inl);
                     have_inl = true;
+                    if (lreq.msac) list_of((uint32_t)win, lo_msac_lists_, true);
                 }
             }
             if (!updated) break;
@@ -2439,6 +2481,18 @@ private:
             best_ = max_score;
             best_model_ = lo_model;
             sfb_buf = lo_buf;
+            // lo_msac_lists_ holds lo_model's MSAC lists from its own
+            // scoring launch (the round that adopted it; later rounds only
+            // score other models)
+            lo_cache_.valid = lo_lists_from_bits_;
+            if (lo_cache_.valid) {
+                lo_cache_.model = lo_model;
+                lo_cache_.score = max_score;
+                lo_cache_.raw[0] = lo_buf.n[0];
+                lo_cache_.raw[1] = lo_buf.n[1];
+                lo_cache_.lists[0].swap(lo_msac_lists_[0]);
+                lo_cache_.lists[1].swap(lo_msac_lists_[1]);
+            }
             return true;
         }
         return false;

@@ -267,6 +267,7 @@ struct ListBits {
     int rule;
     double lambda;
     uint64_t* bits;
+    uint64_t* mbits;         // optional: the MSAC inlier ballots too (r^2 <= the scoring threshold)
 };
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
                               uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream,

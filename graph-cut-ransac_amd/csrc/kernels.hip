@@ -1767,6 +1767,7 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
         if ((threadIdx.x & 63) == 0) {
             bits[((size_t)mi * ntot + j) / 64] = b;
             if (lb.bits != nullptr) lb.bits[((size_t)mi * ntot + j) / 64] = lbw;
+            if (lb.mbits != nullptr) lb.mbits[((size_t)mi * ntot + j) / 64] = b;
         }
     }
 }
@@ -3498,7 +3499,7 @@ size_t small_score_pairs(const DevProblem& p) {
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
                               uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream,
                               const ListBits* lists) {
-    const ListBits lb = lists ? *lists : ListBits{{0.0, 0.0}, 0, 0.0, nullptr};
+    const ListBits lb = lists ? *lists : ListBits{{0.0, 0.0}, 0, 0.0, nullptr, nullptr};
     if (nm == 0) return hipSuccess;
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t ntot = (uint32_t)small_score_pairs(p);
