@@ -289,6 +289,7 @@ struct Workspace {
     PinBuf<BlockSummary> hsum[2];       // [0] this rank's, then the all-gathered ones
     DevBuf<double> cs_vals[2];
     DevBuf<uint64_t> cs_bits[2];
+    PinBuf<uint64_t> h_cbits[2];        // small-scored chunks: every slot's LO list bits (ListBits)
     hipEvent_t sum_done[2] = {nullptr, nullptr}, sum_k0[2] = {nullptr, nullptr}, sum_k1[2] = {nullptr, nullptr};
     bool spec_pending[2] = {false, false};   // a speculative chunk of this set may still run
     ~Workspace() {
@@ -1161,6 +1162,13 @@ public:
         compact_ = false;         // fixed-size per-hypothesis records cross the exchange
     }
 
+    // GCR_CHUNK_LISTS=0: small-scored chunks write no LO list bits (every
+    // LO's first round launches its own masks)
+    static bool chunk_lists_on() {
+        const char* e = getenv("GCR_CHUNK_LISTS");         // read per run
+        return !(e && e[0] == '0');
+    }
+
     // GCR_LO_REUSE=0: the final refit always rescores the buffer model
     static bool lo_reuse_on() {
         const char* e = getenv("GCR_LO_REUSE");            // read per run
@@ -1317,6 +1325,7 @@ public:
                 if (*e == nullptr) HIPC(hipEventCreate(e));
         }
         const int set = c.set;
+        if (lo_row_ >= 0 && lo_row_set_ == set) lo_row_ = -1;   // its list bits are about to be rewritten
         w->hsum[set].ensure((size_t)world_ + 1);
         w->dsum[set].ensure(1);
         const uint32_t n = rank_nslots(c, rank_);
@@ -1343,9 +1352,22 @@ public:
                 const size_t pairs = small_score_pairs(P_->dp);
                 w->cs_vals[set].ensure(pairs * np);
                 w->cs_bits[set].ensure(pairs * np / 64);
+                // every slot's LO lists (Tlo, LO rule) into pinned memory: an LO
+                // triggered by one of these models starts without its own mask
+                // launch and synchronisation
+                ListBits lb{{Tlo_[0], Tlo_[1]}, K_ == 2 ? 0 : 2, prm_.spatial_coherence_weight, nullptr, nullptr};
+                const bool cl = chunk_lists_on() && world_ == 1 && !(lb.rule == 2 && use_graph());
+                if (cl) {
+                    w->h_cbits[set].ensure(pairs * kSmallScore / 64);    // sized once
+                    void* dptr = nullptr;
+                    HIPC(hipHostGetDevicePointer(&dptr, w->h_cbits[set].p, 0));
+                    lb.bits = static_cast<uint64_t*>(dptr);
+                }
+                chunk_lists_[set] = cl;
                 HIPC(launch_score_small(P_->dp, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np,
-                                        set_sb(set).dev(), w->cs_vals[set].p, w->cs_bits[set].p, s));
+                                        set_sb(set).dev(), w->cs_vals[set].p, w->cs_bits[set].p, s, cl ? &lb : nullptr));
             } else {
+                chunk_lists_[set] = false;
                 HIPC(Tr::score(P_, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np, true, set_sb(set).dev(),
                                s));
             }
@@ -1565,6 +1587,10 @@ public:
                         best_model_ = model;
                         best_ = cur;
                         ord_last_best_ = hb[r] + h.hyps_before + 1;
+                        // its LO lists are in the chunk's list bits (small-scored chunks)
+                        lo_row_ = (kP == 1 && chunk_lists_[c.set]) ? (int64_t)h.pos : -1;
+                        lo_row_set_ = c.set;
+                        lo_row_model_ = model;
                         bool nonmin = false;
                         for (int cc = 0; cc < K_; ++cc) if (best_.n[cc] > m_[cc]) { nonmin = true; break; }
                         slot_lo = (it_ > 20) && nonmin;
@@ -1850,6 +1876,10 @@ private:
         uint32_t raw[2] = {0, 0};
         std::vector<uint32_t> lists[2];
     } lo_cache_;
+    bool chunk_lists_[2] = {false, false};    // the set's chunk was small-scored with LO list bits
+    int64_t lo_row_ = -1;                       // the last new best's row in those bits (-1: none)
+    int lo_row_set_ = 0;
+    Model lo_row_model_{};
     bool lo_lists_from_bits_ = false;     // the current LO winner's lists came from its scoring launch
     std::vector<uint32_t> lo_msac_lists_[2];   // its MSAC lists (ListBits.mbits)
 
@@ -2299,9 +2329,14 @@ private:
     // model q's inlier lists from the bits of the last score_models(req) call
     // (small scorer pair layout: class 0 at [0, pad0), class 1 after it)
     void list_of(uint32_t q, std::vector<uint32_t> lists[2], bool msac = false) const {
+        decode_lists(msac ? P_->w->h_mbits.p : P_->w->h_lbits.p, q, lists);
+    }
+    // row q of a small-scorer bit array (pair layout: class 0 at [0, pad0),
+    // class 1 after it) as inlier index lists
+    void decode_lists(const uint64_t* bits, uint32_t q, std::vector<uint32_t> lists[2]) const {
         const size_t pairs = small_score_pairs(P_->dp);
         const size_t pad0 = (N_[0] + 63) & ~(size_t)63;
-        const uint64_t* w = (msac ? P_->w->h_mbits.p : P_->w->h_lbits.p) + q * (pairs / 64);
+        const uint64_t* w = bits + q * (pairs / 64);
         for (int c = 0; c < 2; ++c) {
             lists[c].clear();
             if (c >= K_) continue;
@@ -2398,7 +2433,15 @@ private:
         while (++gc_number_ < 10) {
             bool updated = false;
             auto tp = Clock::now();
-            if (!have_inl) inlier_lists(lo_model, Tlo_, lreq.rule, inl);
+            if (!have_inl) {
+                if (lo_row_ >= 0 && std::memcmp(&lo_row_model_, &lo_model, sizeof(Model)) == 0) {
+                    // the triggering model's lists from its chunk's scoring launch
+                    decode_lists(P_->w->h_cbits[lo_row_set_].p, (uint32_t)lo_row_, inl);
+                } else {
+                    inlier_lists(lo_model, Tlo_, lreq.rule, inl);
+                }
+            }
+            lo_row_ = -1;
             have_inl = false;
             st_.ms_lo_lists += ms_since(tp);
             tp = Clock::now();

@@ -1,4 +1,4 @@
-"""The final refit reuses the adopted LO winner's score, raw counts and
+"""Reuse of scoring launches.  The final refit reuses the adopted LO winner's score, raw counts and
 inlier lists from its own scoring launch when the LO lists used the MSAC
 threshold itself (two-class problems: Tlo = (1.5 thr)^2 and Tm = (2.25 thr)
 thr rounding alike, rule 0), instead of rescoring it (GCRANSAC.h:628-675).
@@ -30,3 +30,17 @@ def test_refit_reuse_equals_rescore(n, seed, conf, monkeypatch):
     b = _run(fs, fo, ts, to, seed, conf)
     assert a == b
     assert a[0] is not None and a[4] > 0
+
+
+@pytest.mark.parametrize("budget", ["fixed", "adaptive", "tiny", "floor"])
+def test_chunk_list_bits_equal_mask_launches(budget, monkeypatch):
+    # small-scored chunks write every slot's LO lists into pinned memory and
+    # the LO of a new best from such a chunk starts from them instead of a
+    # mask launch (GCR_CHUNK_LISTS=0): identical runs for every estimator and
+    # budget ("tiny": 37-slot chunks, the two buffer sets reused many times)
+    from test_gpu_summary import SOLVERS, _run as run_problem
+
+    for kind in SOLVERS:
+        a = run_problem(kind, budget, monkeypatch, {})
+        b = run_problem(kind, budget, monkeypatch, {"GCR_CHUNK_LISTS": "0"})
+        assert a == b, kind
