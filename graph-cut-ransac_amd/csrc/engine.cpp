@@ -2086,7 +2086,7 @@ private:
         uint64_t B;
         if (prm_.batch_slots) B = prm_.batch_slots;
         else if (min_it >= max_it) B = 65536;
-        else B = chunk_no == 0 ? kSmallScore : std::min<uint64_t>(65536, last_chunk * 4);
+        else B = chunk_no == 0 ? first_chunk() : std::min<uint64_t>(65536, last_chunk * 4);
         // adaptive runs: no more slots than the current threshold is expected
         // to need (iterations per slot so far, + 25 %), so the chunk that ends
         // the run does not compute tens of thousands of slots past the stop
@@ -2116,6 +2116,16 @@ private:
     bool pf_active_ = false;
     uint64_t pf_s0_ = 0, pf_B_ = 0;
 
+    // slots of an adaptive run's first chunk: 128 (GCR_FIRST_CHUNK=n, 1 ..
+    // 256).  The bench problems end within 13-83 slots; against 256, the
+    // small scorer's pair launch halves (M2 / M1 / H latency to 0.99 -10 to
+    // -40 us per seed, tools/lat_seeds.py, profiles/r3_fc_seeds_*.log), and
+    // long runs (F) take one more, speculatively issued, chunk
+    static uint64_t first_chunk() {
+        const char* e = getenv("GCR_FIRST_CHUNK");           // read per run
+        const long v = e ? atol(e) : 0;
+        return (v >= 1 && v <= (long)kSmallScore) ? (uint64_t)v : (uint64_t)128;
+    }
     static bool prefetch_on() {
         const char* e = getenv("GCR_PREFETCH");              // read per run (tests switch it)
         return !(e && e[0] == '0');
