@@ -300,6 +300,22 @@ struct Workspace {
     }
 };
 
+namespace {
+// A run can end with a speculative chunk of the summary replay still running
+// on the side stream (RunnerT::replay_summaries leaves it in flight so the
+// run returns sooner).  It writes set 0 / 1's chunk buffers and reads the
+// feature SoA, so everything that reuses the workspace -- the next run's
+// replay (either path), verify_batches, the debug entry points, the upload
+// of the next problem into a recycled workspace -- waits for it first.
+void await_spec(Workspace* w) {
+    for (int k = 0; k < 2; ++k)
+        if (w->spec_pending[k]) {
+            HIPC(hipEventSynchronize(w->sum_done[k]));
+            w->spec_pending[k] = false;
+        }
+}
+}  // namespace
+
 struct gcr_ctx {
     int device = 0;
     hipStream_t stream = nullptr;       // the replay's stream: LO, refit, fetched chunks (high priority)
@@ -809,6 +825,7 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
         if (!P->own) P->own.reset(new Workspace());
         P->w = P->own.get();
     }
+    await_spec(P->w);                   // a recycled workspace: its last speculative chunk reads feat
     P->w->feat.ensure(total);
     // the whole SoA image (pads zeroed) is staged in pinned memory and goes
     // up in ONE copy (ten pageable copies cost ~150 us of a one-shot call)
@@ -1456,11 +1473,7 @@ public:
     void replay_summaries() {
         // speculative chunks a previous run left in flight (their pinned
         // summary buffers are rewritten below)
-        for (int k = 0; k < 2; ++k)
-            if (P_->w->spec_pending[k]) {
-                HIPC(hipEventSynchronize(P_->w->sum_done[k]));
-                P_->w->spec_pending[k] = false;
-            }
+        await_spec(P_->w);
         const uint64_t ones[2] = {1, 1};
         uint64_t max_iteration = iteration_number(ones);
         const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
@@ -1657,6 +1670,7 @@ public:
     // Full GCRANSAC::run; fills outputs, returns total inlier count.
     int run(uint8_t* mask0, uint8_t* mask1, double* H, gcr_rect_model* model_out) {
         const auto t_all = Clock::now();
+        await_spec(P_->w);                // either replay path reuses set 0 / 1's buffers
         if (summary_replay_on()) replay_summaries();
         else replay_slots();
 
@@ -1750,6 +1764,7 @@ public:
         static_assert(sizeof(BatchRecord) == sizeof(gcr_batch_result), "record layout");
         static_assert(offsetof(BatchRecord, best_model) == offsetof(gcr_batch_result, best_model), "record layout");
         const auto t0 = Clock::now();
+        await_spec(P_->w);
         P_->w->inc.ensure(nslots * kP); Tr::dmodels(P_->w).ensure(nslots * kP); P_->w->sb.ensure(nslots * kP);
         // record buffers sized once for up to 4096 batches: a reallocation
         // (device + pinned) inside a timed call costs milliseconds
@@ -2892,6 +2907,7 @@ int gcr_debug_generate_h(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint3
         return set_err(GCR_EINVAL, "not a correspondence (homography / fundamental) problem");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
         const size_t nh = (size_t)nslots * GeoTraits::per(prob);
         prob->w->inc.ensure(nh);
         prob->w->gmodels.ensure(nh);
@@ -2911,6 +2927,7 @@ int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double*
         return set_err(GCR_EINVAL, "not a correspondence (homography / fundamental) problem");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
         hipStream_t s = prob->ctx->stream;
         const double thr = params->scale_residual_thresh;
         const double T = (2.25 * thr) * thr;
@@ -2942,6 +2959,7 @@ int gcr_debug_mask_h(gcr_problem* prob, const gcr_params* params, const double* 
         return set_err(GCR_EINVAL, "not a correspondence (homography / fundamental) problem");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
         hipStream_t s = prob->ctx->stream;
         const double thr = params->scale_residual_thresh;
         double T;
@@ -2980,6 +2998,7 @@ int gcr_debug_generate(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_
     if (!prob || !inc_out || !models_out) return set_err(GCR_EINVAL, "null argument");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
         prob->w->inc.ensure(nslots);
         prob->w->models.ensure(nslots);
         hipStream_t s = prob->ctx->stream;
@@ -2996,6 +3015,7 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
     if (!prob || !params || !models) return set_err(GCR_EINVAL, "null argument");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
         hipStream_t s = prob->ctx->stream;
         double T[2];
         const double thr[2] = {params->scale_residual_thresh, params->orientation_residual_thresh};
@@ -3036,6 +3056,7 @@ int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_m
     if (cls < 0 || cls >= prob->K) return set_err(GCR_EINVAL, "class %d out of range", cls);
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
         hipStream_t s = prob->ctx->stream;
         const double thr = cls == 0 ? params->scale_residual_thresh : params->orientation_residual_thresh;
         double T;
@@ -3077,6 +3098,7 @@ int gcr_debug_fit_nonminimal(gcr_problem* prob, const uint32_t* idx0, size_t k0,
     if (!prob || !idx0 || !model_out || (prob->solver == 2 && !idx1)) return set_err(GCR_EINVAL, "bad arguments");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
         std::vector<uint32_t> lists[2];
         lists[0].assign(idx0, idx0 + k0);
         if (prob->solver == 2) lists[1].assign(idx1, idx1 + k1);

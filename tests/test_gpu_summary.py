@@ -81,3 +81,15 @@ def test_summary_replay_equals_slot_replay(kind, budget, monkeypatch):
     # one-part blocks through the three-launch summary instead of k_sum_one
     assert _run(kind, budget, monkeypatch, {"GCR_SUMMARY_ONE": "0"}) == ref
     assert _run(kind, budget, monkeypatch, {"GCR_SUMMARY_ONE": "0", "GCR_SUMMARY_CAP": "1"}) == ref
+
+
+def test_slot_replay_after_speculative_chunks_on_recycled_workspace(monkeypatch):
+    """An adaptive F run can return with a speculative chunk still running on
+    the side stream; the next problem reuses the workspace (last in, first
+    out).  The per-slot replay and the upload of the next problem must wait
+    for it (engine.cpp await_spec) instead of racing it on set 0's buffers."""
+    kind = N.SOLVER_FUNDAMENTAL7
+    ref = _run(kind, "adaptive", monkeypatch, {"GCR_REPLAY": "slots"})
+    for _ in range(3):
+        assert _run(kind, "adaptive", monkeypatch, {}) == ref
+        assert _run(kind, "adaptive", monkeypatch, {"GCR_REPLAY": "slots"}) == ref
