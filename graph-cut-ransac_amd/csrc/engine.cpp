@@ -142,38 +142,41 @@ void swap_buf(B& a, B& b) {
 }
 
 // Score arrays for `cap` hypotheses, device and pinned host mirrors, each set
-// in one allocation laid out n0 | n1 | v0 | v1 | tot (capacity-sized fields),
-// so that a small batch comes back in one copy instead of five (every copy
-// is a ~5 us blit on the stream).
+// in one allocation laid out n0 | n1 | v0 | v1 | tot | fl | lfl
+// (capacity-sized fields; fl / lfl: the flagged decisions of exact.h), so that
+// a small batch comes back in one copy instead of seven (every copy is a ~5 us
+// blit on the stream).
 struct ScoreBufs {
     DevBuf<double> dblk;
     PinBuf<double> hblk;
     size_t cap = 0;
-    Ptr<uint32_t> n0, n1, hn0, hn1;
+    Ptr<uint32_t> n0, n1, hn0, hn1, fl, lfl, hfl, hlfl;
     Ptr<double> v0, v1, tot, hv0, hv1, htot;
     void ensure(size_t n) {
         if (n <= cap) return;
-        dblk.ensure(4 * n);
-        hblk.ensure(4 * n);
+        dblk.ensure(5 * n);
+        hblk.ensure(5 * n);
         cap = n;
         auto carve = [n](double* b, Ptr<uint32_t>& a0, Ptr<uint32_t>& a1, Ptr<double>& b0, Ptr<double>& b1,
-                         Ptr<double>& b2) {
+                         Ptr<double>& b2, Ptr<uint32_t>& f0, Ptr<uint32_t>& f1) {
             a0.p = reinterpret_cast<uint32_t*>(b);
             a1.p = a0.p + n;
             b0.p = b + n;
             b1.p = b + 2 * n;
             b2.p = b + 3 * n;
+            f0.p = reinterpret_cast<uint32_t*>(b + 4 * n);
+            f1.p = f0.p + n;
         };
-        carve(dblk.p, n0, n1, v0, v1, tot);
-        carve(hblk.p, hn0, hn1, hv0, hv1, htot);
+        carve(dblk.p, n0, n1, v0, v1, tot, fl, lfl);
+        carve(hblk.p, hn0, hn1, hv0, hv1, htot, hfl, hlfl);
     }
-    ScoreOut dev() const { return ScoreOut{n0.p, n1.p, v0.p, v1.p, tot.p}; }
+    ScoreOut dev() const { return ScoreOut{n0.p, n1.p, v0.p, v1.p, tot.p, fl.p, lfl.p}; }
     // the pinned mirror as kernels see it (results written in place)
     ScoreOut host_dev() const {
         double* b = dev_view(hblk.p);
         const ptrdiff_t d = reinterpret_cast<char*>(b) - reinterpret_cast<char*>(hblk.p);
         auto at = [d](auto* h) { return reinterpret_cast<decltype(h)>(reinterpret_cast<char*>(h) + d); };
-        return ScoreOut{at(hn0.p), at(hn1.p), at(hv0.p), at(hv1.p), at(htot.p)};
+        return ScoreOut{at(hn0.p), at(hn1.p), at(hv0.p), at(hv1.p), at(htot.p), at(hfl.p), at(hlfl.p)};
     }
     void swap(ScoreBufs& o) {
         std::swap(dblk.p, o.dblk.p); std::swap(dblk.cap, o.dblk.cap);
@@ -182,9 +185,10 @@ struct ScoreBufs {
         std::swap(n0, o.n0); std::swap(n1, o.n1); std::swap(hn0, o.hn0); std::swap(hn1, o.hn1);
         std::swap(v0, o.v0); std::swap(v1, o.v1); std::swap(tot, o.tot);
         std::swap(hv0, o.hv0); std::swap(hv1, o.hv1); std::swap(htot, o.htot);
+        std::swap(fl, o.fl); std::swap(lfl, o.lfl); std::swap(hfl, o.hfl); std::swap(hlfl, o.hlfl);
     }
     void d2h(size_t n, hipStream_t s) {
-        const size_t span = (3 * cap + n) * sizeof(double);    // n0 .. tot[n)
+        const size_t span = 4 * cap * sizeof(double) + (cap + n) * sizeof(uint32_t);    // n0 .. lfl[n)
         if (span <= (size_t)256 * 1024 || 2 * n >= cap) {
             HIPC(hipMemcpyAsync(hblk.p, dblk.p, span, hipMemcpyDeviceToHost, s));
             return;
@@ -194,6 +198,8 @@ struct ScoreBufs {
         HIPC(hipMemcpyAsync(hv0.p, v0.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPC(hipMemcpyAsync(hv1.p, v1.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPC(hipMemcpyAsync(htot.p, tot.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(hfl.p, fl.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(hlfl.p, lfl.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     }
 };
 
@@ -211,6 +217,14 @@ struct BufferT {             // one of temp_inner_inliers[2]
     bool has = false;
     M model{};
     uint64_t n[2] = {0, 0};  // list sizes (raw inlier counts of `model`)
+    // rectification, resolved when the buffer is read (RunnerT::resolve):
+    // inc 1..101: `model` is slot `slot`'s generated model with the twin phi
+    // of the 2-SIFT minimal solver (the glibc phi is computed on demand);
+    // exact: n are the reference's counts (false: flagged decisions, or a
+    // model exact.h's bound does not cover, still to recheck)
+    uint64_t slot = 0;
+    uint32_t inc = 0;
+    bool exact = true;
 };
 
 }  // namespace
@@ -339,7 +353,73 @@ struct gcr_problem {
     DevProblem dp{};
     std::unique_ptr<Workspace> own;     // gcr_problem_create: private buffers
     Workspace* w = nullptr;             // own.get() or &ctx->shared
+    bool scales_ok = true;              // exact.h scales_in_range over the scale features
 };
+
+namespace {
+
+// ---------------------------------------- decisions in glibc (exact.h) ----
+// The kernels evaluate the detmath twins and flag every decision whose twin
+// residual lies within the proven twin-glibc bound of its threshold; these
+// host routines take those decisions (and every decision of a model the bound
+// does not cover, scale_unsafe) in the reference's arithmetic.
+
+// one pair's squared residual under model m with the twins (TwinMath: the
+// values the kernels fold) or glibc (GlibcMath: the reference's decision)
+template <class M>
+double host_r2(const gcr_problem* P, int cls, size_t i, const RectModel& m) {
+    const HostClass& h = P->hc[cls];
+    if (cls == 0) {
+        const double ac = alpha_cube(m);
+        return P->solver == 1 ? scale_sq_residual<true, false, M>(h.x[i], h.y[i], h.a[i], m, ac)
+                              : scale_sq_residual<false, false, M>(h.x[i], h.y[i], h.a[i], m, ac);
+    }
+    return orient_sq_residual<false, M>(h.x[i], h.y[i], h.c0[i], h.c1[i], m, orient_const(m));
+}
+
+struct ExactCount {
+    uint64_t models = 0;       // models whose decisions went through the host
+    uint64_t pairs = 0;        // pairs decided with glibc
+    uint64_t flips = 0;        // ... whose decision differs from the twin's
+    double ms = 0.0;
+};
+
+// GCR_EXACT=0: decisions stay the twins' (no host recheck, no glibc phi):
+// the A/B switch of the rechecks' cost; read per call
+bool exact_on() {
+    const char* e = getenv("GCR_EXACT");
+    return !(e && e[0] == '0');
+}
+
+bool model_unsafe(const gcr_problem* P, const RectModel& m, double T0) {
+    return P->solver <= 2 && scale_unsafe(P->solver, m.alpha, T0, P->scales_ok);
+}
+
+// The MSAC accumulators of one model with every decision in the reference's
+// arithmetic (the oracle's TWIN-mode getScore): pair i of class c is an
+// inlier iff its glibc r^2 under md is <= T[c] (MSAC_scoring_function.hpp:
+// 53-107), and then adds -(its twin r^2 under mv) -- the value the kernels
+// fold; mv differs from md only in a generated 2-SIFT model's phi.  Sums in
+// feature order, class 0 then 1, the total running across classes.  Pairs in
+// parallel on the host pool, the sums sequential.  `lists`: the MSAC inlier
+// lists too.
+void exact_accumulate(const gcr_problem* P, const RectModel& mv, const RectModel& md, const double T[2],
+                      uint32_t n[2], double v[2], double& tot, std::vector<uint32_t>* lists, ExactCount& ec);
+
+// k_mask bytes of one class (bit 0 the twin decision, bit 1 flagged) turned
+// into the reference's decisions under md: flagged pairs -- every pair when
+// `all` -- decided with glibc (mask_rule on the glibc r^2)
+void exact_mask(const gcr_problem* P, int cls, const RectModel& md, int rule, double T, double lambda, uint8_t* mk,
+                bool all, ExactCount& ec);
+
+// The glibc phi of slot `slot`'s generated 2-SIFT model (successful attempt
+// a): the reference's atan2 of the sample's vanishing point (two_sift.hpp:
+// 341); the generators evaluate the twin.  The sample is redrawn on the host
+// from the same Philox stream as kernels.hip attempt<2>; its h7, h8, alpha
+// must equal the device model's bit for bit.
+RectModel glibc_minimal_model(const gcr_problem* P, uint64_t seed, uint64_t slot, uint32_t a, const RectModel& dev);
+
+}  // namespace
 
 namespace {
 
@@ -682,6 +762,113 @@ HostPool& host_pool() {
     return pool;
 }
 
+// ---------------------------------------- decisions in glibc: bodies ----
+void exact_accumulate(const gcr_problem* P, const RectModel& mv, const RectModel& md, const double T[2],
+                      uint32_t n[2], double v[2], double& tot, std::vector<uint32_t>* lists, ExactCount& ec) {
+    const auto t0 = Clock::now();
+    thread_local std::vector<double> val;
+    thread_local std::vector<uint8_t> dec;
+    n[0] = n[1] = 0;
+    v[0] = v[1] = 0.0;
+    tot = 0.0;
+    for (int c = 0; c < 2; ++c) {
+        if (lists) lists[c].clear();
+        if (c >= P->K) continue;
+        const size_t N = P->hc[c].n;
+        val.resize(N);
+        dec.resize(N);
+        // the caller's thread_local scratch (the pool's workers have their own)
+        double* const vp = val.data();
+        uint8_t* const dp = dec.data();
+        std::atomic<uint64_t> flips{0};
+        auto body = [&](size_t lo, size_t hi) {
+            uint64_t f = 0;
+            for (size_t i = lo; i < hi; ++i) {
+                const double rv = host_r2<TwinMath>(P, c, i, mv);
+                const bool d = host_r2<GlibcMath>(P, c, i, md) <= T[c];
+                vp[i] = rv;
+                dp[i] = d ? 1 : 0;
+                f += (rv <= T[c]) != d ? 1u : 0u;
+            }
+            flips.fetch_add(f, std::memory_order_relaxed);
+        };
+        const size_t parts = N >= 4096 ? 16 : 1, step = (N + parts - 1) / parts;
+        host_pool().parallel_for(parts, [&](size_t q) { body(std::min(N, q * step), std::min(N, (q + 1) * step)); });
+        for (size_t i = 0; i < N; ++i)
+            if (dec[i]) {
+                ++n[c];
+                v[c] += -val[i];
+                tot += -val[i];
+                if (lists) lists[c].push_back((uint32_t)i);
+            }
+        ec.pairs += N;
+        ec.flips += flips.load();
+    }
+    ++ec.models;
+    ec.ms += ms_since(t0);
+}
+
+void exact_mask(const gcr_problem* P, int cls, const RectModel& md, int rule, double T, double lambda, uint8_t* mk,
+                bool all, ExactCount& ec) {
+    const size_t N = P->hc[cls].n;
+    if (!all) {
+        for (size_t i = 0; i < N; ++i) {
+            if (!(mk[i] & 2)) {
+                mk[i] &= 1;
+                continue;
+            }
+            const uint8_t d = mask_rule(host_r2<GlibcMath>(P, cls, i, md), rule, T, lambda) ? 1 : 0;
+            ++ec.pairs;
+            ec.flips += (mk[i] & 1) != d ? 1u : 0u;
+            mk[i] = d;
+        }
+        return;
+    }
+    const auto t0 = Clock::now();
+    std::atomic<uint64_t> flips{0};
+    auto body = [&](size_t lo, size_t hi) {
+        uint64_t f = 0;
+        for (size_t i = lo; i < hi; ++i) {
+            const uint8_t d = mask_rule(host_r2<GlibcMath>(P, cls, i, md), rule, T, lambda) ? 1 : 0;
+            f += (mk[i] & 1) != d ? 1u : 0u;
+            mk[i] = d;
+        }
+        flips.fetch_add(f, std::memory_order_relaxed);
+    };
+    const size_t parts = N >= 4096 ? 16 : 1, step = (N + parts - 1) / parts;
+    host_pool().parallel_for(parts, [&](size_t q) { body(std::min(N, q * step), std::min(N, (q + 1) * step)); });
+    ec.pairs += N;
+    ec.flips += flips.load();
+    ec.ms += ms_since(t0);
+}
+
+RectModel glibc_minimal_model(const gcr_problem* P, uint64_t seed, uint64_t slot, uint32_t a, const RectModel& dev) {
+    const HostClass& sc = P->hc[0];
+    const HostClass& oc = P->hc[1];
+    uint32_t si[2], oi[2];
+    WordStream ws0(seed, slot, a, kStreamMain, 0);
+    WordStream ws1(seed, slot, a, kStreamMain, 1);
+    RectModel m = default_model();
+    bool ok = sample_distinct<2>(ws0, sc.n, 2, si) && sample_distinct<2>(ws1, oc.n, 2, oi);
+    if (ok) {
+        double sx[2], sy[2], sp[2], ox[2], oy[2], oco[2], osi[2];
+        for (int j = 0; j < 2; ++j) {
+            sx[j] = sc.x[si[j]];
+            sy[j] = sc.y[si[j]];
+            sp[j] = sc.c0[si[j]];
+            ox[j] = oc.x[oi[j]];
+            oy[j] = oc.y[oi[j]];
+            oco[j] = oc.c0[oi[j]];
+            osi[j] = oc.c1[oi[j]];
+        }
+        ok = valid_sample_sift22(sx, sy, ox, oy, oco, osi) && solve_sift22<GlibcMath>(sx, sy, sp, ox, oy, oco, osi, m);
+    }
+    if (!ok || as_u64(m.h7) != as_u64(dev.h7) || as_u64(m.h8) != as_u64(dev.h8) ||
+        as_u64(m.alpha) != as_u64(dev.alpha))
+        throw std::runtime_error("host redraw of a generated 2-SIFT slot disagrees with the generator");
+    return m;
+}
+
 // LO trials, refits and reconciliations of at most kSmallScore models use
 // launch_score_small; GCR_SMALL_SCORE=0 routes them through the batch scorers
 constexpr uint32_t kSmallScore = 256;
@@ -807,6 +994,7 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     P->K = K;
     const size_t ns[2] = {n0, K == 2 ? n1 : 0};
     fill_host_classes(solver, f0, n0, f1, n1, P->hc);
+    if (solver <= 2) P->scales_ok = scales_in_range(P->hc[0].a.data(), P->hc[0].n);
     // SoA, every array padded to an even length (zeros) so that 16-byte
     // LDS-DMA strips (k_score_split staging) are aligned and in bounds
     const size_t np[2] = {(ns[0] + 1) & ~size_t(1), (ns[1] + 1) & ~size_t(1)};
@@ -1163,6 +1351,7 @@ public:
             const double t = 1.5 * thr_[c];                 // GCRANSAC.h:207-208
             Tlo_[c] = t * t;
         }
+        Tu_ = std::max(Tm_[0], Tlo_[0]);
         N_[0] = P->hc[0].n;
         N_[1] = K_ == 2 ? P->hc[1].n : 0;
         log_prob_ = std::log(1.0 - prm.confidence);
@@ -1250,13 +1439,17 @@ public:
                 const size_t si = compact_ ? cursor_++ : hj;
                 const Model& model = Tr::hmodels(P_->w).p[hj];
                 const uint32_t rn[2] = {P_->w->sb.hn0.p[si], P_->w->sb.hn1.p[si]};
-                const HScore cur = kP == 1 ? chunk_sc_[j]
-                                           : finish(rn, P_->w->sb.hv0.p[si], P_->w->sb.hv1.p[si], P_->w->sb.htot.p[si]);
-                bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
+                HScore cur = kP == 1 ? chunk_sc_[j]
+                                     : finish(rn, P_->w->sb.hv0.p[si], P_->w->sb.hv1.p[si], P_->w->sb.htot.p[si]);
+                Buffer b = gen_buf(model, chunk_begin + j, inc, rn, kRect ? P_->w->sb.hfl.p[si] : 0u);
+                if (!b.exact) resolve(b, &cur);         // flagged: the reference's score
+                bufs_[off_] = b;
                 ++st_.hypotheses;
                 if (best_.sum < cur.sum && valid_model(model)) {
+                    resolve(bufs_[off_]);               // the glibc phi of a generated 2-SIFT model
+                    best_model_ = bufs_[off_].model;
+                    best_val_ = model;
                     off_ = 1 - off_;
-                    best_model_ = model;
                     best_ = cur;
                     bool nonmin = false;
                     for (int c = 0; c < K_; ++c) if (best_.n[c] > m_[c]) { nonmin = true; break; }
@@ -1327,7 +1520,9 @@ public:
         Workspace* w = P_->w;
         const uint32_t n = rank_nslots(c, rank_);
         const uint32_t m32[2] = {(uint32_t)m_[0], (uint32_t)m_[1]};
-        return launch_block_summary(P_->solver, set_inc(c.set).p, set_models(c.set).p, set_sb(c.set).dev(),
+        ScoreOut sc = set_sb(c.set).dev();
+        if (!chunk_lists_[c.set]) sc.lfl = nullptr;      // list flags exist with the chunk's list bits only
+        return launch_block_summary(P_->solver, set_inc(c.set).p, set_models(c.set).p, sc,
                                     kP > 1 ? set_hmap(c.set).p : nullptr, n, (uint32_t)kP, m32, Tm_, bar, from_pos,
                                     target, w->sum_scr[c.set].p, out, s, parts_ready);
     }
@@ -1368,7 +1563,7 @@ public:
             if (np <= kSmallScore && small_score_on()) {
                 const size_t pairs = small_score_pairs(P_->dp);
                 w->cs_vals[set].ensure(pairs * np);
-                w->cs_bits[set].ensure(pairs * np / 64);
+                w->cs_bits[set].ensure(3 * pairs * np / 64);   // ballots + two flag planes
                 // every slot's LO lists (Tlo, LO rule) into pinned memory: an LO
                 // triggered by one of these models starts without its own mask
                 // launch and synchronisation
@@ -1466,8 +1661,9 @@ public:
     // (otherwise the buffer still holds what that new best -- or its LO --
     // left there; GCRANSAC.h:460 writes every hypothesis, :440-446 flips)
     uint64_t ord_last_best_ = 0;          // ordinal + 1 of the last strict new best (0: none)
-    void hold_last(const SumHyp& h, uint64_t ord) {
-        if (ord + 1 > ord_last_best_) bufs_[off_] = Buffer{true, model_of(h), {h.n0, h.n1}};
+    void hold_last(const SumHyp& h, uint64_t ord, uint64_t slot) {
+        const uint32_t rn[2] = {h.n0, h.n1};
+        if (ord + 1 > ord_last_best_) bufs_[off_] = gen_buf(model_of(h), slot, h.inc, rn, h.fl);
     }
 
     void replay_summaries() {
@@ -1593,17 +1789,22 @@ public:
                     }
                     const Model model = model_of(h);
                     const uint32_t rn[2] = {h.n0, h.n1};
-                    const HScore cur = finish(rn, h.v0, h.v1, h.tot);
-                    bufs_[off_] = Buffer{true, model, {rn[0], rn[1]}};
+                    HScore cur = finish(rn, h.v0, h.v1, h.tot);
+                    Buffer b = gen_buf(model, gslot, h.inc, rn, h.fl);
+                    if (!b.exact) resolve(b, &cur);     // flagged: the reference's score
+                    bufs_[off_] = b;
                     if (best_.sum < cur.sum && valid_model(model)) {
+                        resolve(bufs_[off_]);           // the glibc phi of a generated 2-SIFT model
+                        best_model_ = bufs_[off_].model;
+                        best_val_ = model;
                         off_ = 1 - off_;
-                        best_model_ = model;
                         best_ = cur;
                         ord_last_best_ = hb[r] + h.hyps_before + 1;
                         // its LO lists are in the chunk's list bits (small-scored chunks)
                         lo_row_ = (kP == 1 && chunk_lists_[c.set]) ? (int64_t)h.pos : -1;
                         lo_row_set_ = c.set;
-                        lo_row_model_ = model;
+                        lo_row_model_ = best_model_;
+                        lo_row_lfl_ = h.lfl;
                         bool nonmin = false;
                         for (int cc = 0; cc < K_; ++cc) if (best_.n[cc] > m_[cc]) { nonmin = true; break; }
                         slot_lo = (it_ > 20) && nonmin;
@@ -1637,11 +1838,11 @@ public:
                 // else the last one of an earlier block of the chunk (earlier
                 // chunks were settled at their ends)
                 if (X[rs].has_last) {
-                    hold_last(X[rs].last, hb[rs] + X[rs].last.hyps_before);
+                    hold_last(X[rs].last, hb[rs] + X[rs].last.hyps_before, rank_slot0(c, rs) + X[rs].last.pos / kP);
                 } else {
                     for (int r = rs - 1; r >= 0; --r)
                         if (has_last[r]) {
-                            hold_last(lasts[r], hb[r] + lasts[r].hyps_before);
+                            hold_last(lasts[r], hb[r] + lasts[r].hyps_before, rank_slot0(c, r) + lasts[r].pos / kP);
                             break;
                         }
                 }
@@ -1655,7 +1856,7 @@ public:
             st_.slots = c.s0 + c.B;
             for (int r = world_ - 1; r >= 0; --r)
                 if (has_last[r]) {
-                    hold_last(lasts[r], hb[r] + lasts[r].hyps_before);
+                    hold_last(lasts[r], hb[r] + lasts[r].hyps_before, rank_slot0(c, r) + lasts[r].pos / kP);
                     break;
                 }
             q.erase(q.begin());
@@ -1686,6 +1887,8 @@ public:
                 local_optimization(bufs_[off_]);
             }
             const auto t_ref = Clock::now();
+            resolve(bufs_[0]);            // the reference's counts and models in both buffers
+            resolve(bufs_[1]);
             bool diff = false;
             for (int c = 0; c < K_; ++c) if (bufs_[off_].n[c] != best_.n[c]) diff = true;
             if (diff) off_ = 1 - off_;
@@ -1711,7 +1914,7 @@ public:
             } else if (diff) {
                 HScore s;
                 uint32_t rn[2];
-                if (score_models(&best_model_, 1, &s, rn, &msac)) {
+                if (score_models(&best_val_, 1, &s, rn, &msac, &best_model_) && !sm_lbad_[0]) {
                     list_of(0, lists);
                     have_lists = true;
                 }
@@ -1728,11 +1931,12 @@ public:
             if (fitted) {
                 HScore s;
                 uint32_t rn[2];
-                const bool rl = score_models(&refit, 1, &s, rn, &msac);
+                const bool rl = score_models(&refit, 1, &s, rn, &msac) && !sm_lbad_[0];
                 const int idx = 1 - off_;
                 bufs_[idx] = Buffer{true, refit, {rn[0], rn[1]}};
                 if (best_.sum < s.sum) {
                     best_model_ = refit;
+                    best_val_ = refit;
                     off_ = idx;
                     if (rl) list_of(0, lists);
                     else inlier_lists(bufs_[off_].model, Tm_, 0, lists);
@@ -1750,6 +1954,10 @@ public:
         st_.iteration_number = it_;
         st_.local_optimization_number = lo_number_;
         st_.graph_cut_number = gc_number_;
+        st_.exact_models = ec_.models;
+        st_.exact_pairs = ec_.pairs;
+        st_.exact_flips = ec_.flips;
+        st_.ms_exact = ec_.ms;
         st_.ms_total = ms_since(t_all);
         return total;
     }
@@ -1900,6 +2108,84 @@ private:
 
     bool valid_model(const Model& m) const { return Tr::valid(P_->solver, m); }
 
+    // ---- decisions in the reference's arithmetic (exact.h) ---------------
+    // The kernels decide with the detmath twins and flag every decision within
+    // the twin-glibc bound of its threshold (ScoreOut::fl / lfl, k_mask bit
+    // 1, SumHyp::fl).  Every hypothesis the replay acts on -- chain members,
+    // the buffers, LO winners, the refit -- is then taken in glibc: a flagged
+    // score is recounted on the host (exact_score), flagged lists rechecked
+    // (exact_mask), and a generated 2-SIFT model carries the glibc phi of its
+    // sample (dec_of) wherever the reference would use the model.  The twin
+    // phi stays the hypothesis's VALUE model (best_val_): what its MSAC sums
+    // were folded with.
+    static constexpr bool kRect = std::is_same<Model, RectModel>::value;
+    ExactCount ec_;
+    double Tu_ = 0.0;                     // the larger scale threshold (scale_unsafe)
+    Model best_val_ = Tr::def();          // best_model_ as the kernels score it
+    std::vector<uint8_t> sm_mbad_, sm_lbad_;  // score_models: model q's MSAC / list bits need the host
+    uint32_t lo_row_lfl_ = 0;             // flagged list decisions of the lo_row_ model in its chunk bits
+
+    const bool exact_ = exact_on();       // GCR_EXACT=0: the twins' decisions throughout (A/B)
+    bool unsafe(const Model& m) const {
+        if constexpr (kRect) return exact_ && model_unsafe(P_, m, Tu_);
+        else return false;
+    }
+    // a hypothesis of a generated chunk as an inlier buffer, its decisions
+    // resolved when the buffer is read
+    Buffer gen_buf(const Model& m, uint64_t slot, uint32_t inc, const uint32_t rn[2], uint32_t fl) const {
+        Buffer b{true, m, {rn[0], rn[1]}};
+        if constexpr (kRect) {
+            if (!exact_) return b;
+            b.slot = slot;
+            b.inc = (P_->solver == 2 && inc >= 1 && inc <= 101) ? inc : 0;
+            b.exact = fl == 0 && !unsafe(m);
+        }
+        return b;
+    }
+    // the model the reference holds for a generated hypothesis (glibc phi)
+    Model dec_of(const Model& m, uint64_t slot, uint32_t inc) const {
+        if constexpr (kRect) {
+            if (P_->solver == 2 && inc >= 1 && inc <= 101) return glibc_minimal_model(P_, prm_.seed, slot, inc - 1, m);
+        }
+        return m;
+    }
+    // the score of value model mv with decision model md's glibc decisions
+    HScore exact_score(const Model& mv, const Model& md, uint32_t raw[2], std::vector<uint32_t>* lists = nullptr) {
+        if constexpr (kRect) {
+            uint32_t n[2];
+            double v[2], tot;
+            exact_accumulate(P_, mv, md, Tm_, n, v, tot, lists, ec_);
+            raw[0] = n[0];
+            raw[1] = K_ == 2 ? n[1] : 0;
+            return finish(n, v[0], v[1], tot);
+        } else {
+            (void)mv; (void)md; (void)raw; (void)lists;
+            throw std::logic_error("exact_score: rectification solvers only");
+        }
+    }
+    // buffer b with its decisions resolved: a generated model's glibc phi,
+    // the reference's counts (*sc: the finished score when recounted)
+    void resolve(Buffer& b, HScore* sc = nullptr) {
+        if constexpr (kRect) {
+            if (!b.has) return;
+            const Model mv = b.model;
+            if (b.inc) {
+                b.model = dec_of(b.model, b.slot, b.inc);
+                b.inc = 0;
+            }
+            if (!b.exact) {
+                uint32_t raw[2];
+                const HScore s = exact_score(mv, b.model, raw);
+                b.n[0] = raw[0];
+                b.n[1] = raw[1];
+                b.exact = true;
+                if (sc) *sc = s;
+            }
+        } else {
+            (void)b; (void)sc;
+        }
+    }
+
     // neighbourhood graph (homography / fundamental matrix with a grid and
     // lambda > 0): the grid's edges are built once per run, on first use
     NeighbourEdges edges_;
@@ -1958,7 +2244,7 @@ private:
         double v0, v1, tot;
         uint32_t n0, n1;
         uint32_t inc;
-        uint32_t pad;
+        uint32_t fl;
     };
 
     // Sharded chunk: rank r generates and scores slots [s0 + r per, s0 + (r+1) per)
@@ -1990,7 +2276,7 @@ private:
         const ScoreBufs& sb = P_->w->sb;
         for (size_t i = 0; i < nh; ++i)
             send[i] = HypRec{Tr::hmodels(P_->w).p[i], sb.hv0.p[i], sb.hv1.p[i], sb.htot.p[i],
-                             sb.hn0.p[i], sb.hn1.p[i], P_->w->h_inc.p[i], 0u};
+                             sb.hn0.p[i], sb.hn1.p[i], P_->w->h_inc.p[i], kRect ? sb.hfl.p[i] : 0u};
         t0 = Clock::now();
         if (xfn_(xuser_, send.data(), recv.data(), nh * sizeof(HypRec)) != 0)
             throw std::runtime_error("all-gather callback failed");
@@ -2003,6 +2289,7 @@ private:
             Tr::hmodels(P_->w).p[i] = r.m;
             P_->w->sb.hn0.p[i] = r.n0; P_->w->sb.hn1.p[i] = r.n1;
             P_->w->sb.hv0.p[i] = r.v0; P_->w->sb.hv1.p[i] = r.v1; P_->w->sb.htot.p[i] = r.tot;
+            P_->w->sb.hfl.p[i] = r.fl;
         }
         const uint64_t Bw = (uint64_t)per * world_;
         uint64_t itp = it_, cnt = 0;
@@ -2067,7 +2354,7 @@ private:
             // wave per model (the batch scorers' chain would dominate)
             const size_t pairs = small_score_pairs(P_->dp);
             P_->w->sm_vals.ensure(pairs * nh);
-            P_->w->sm_bits.ensure(pairs * nh / 64);
+            P_->w->sm_bits.ensure(3 * pairs * nh / 64);
             HIPC(launch_score_small(P_->dp, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(),
                                     P_->w->sm_vals.p, P_->w->sm_bits.p, s_));
         } else {
@@ -2196,11 +2483,14 @@ private:
         if (kP != 1 || world_ > 1 || chunk_no < 2 || cnt != B || !prefetch_on()) return;
         double run = best_.sum;
         int64_t trig = -1;
-        for (uint64_t j = 0; j < cnt; ++j)
-            if (run < chunk_sc_[j].sum && chunk_ok_[j]) {
-                run = chunk_sc_[j].sum;
+        for (uint64_t j = 0; j < cnt; ++j) {
+            // a flagged slot may be a new best whatever its twin score (exact.h)
+            const bool fl = kRect && exact_ && P_->w->sb.hfl.p[j] != 0;
+            if ((run < chunk_sc_[j].sum || fl) && chunk_ok_[j]) {
+                if (!fl) run = chunk_sc_[j].sum;
                 trig = (int64_t)j;
             }
+        }
         pf_pending_ = true;
         pf_trigger_ = trig;
         pf_chunk_no_ = chunk_no;
@@ -2285,8 +2575,13 @@ private:
         int rule;
         bool msac = false;        // also the MSAC ballots (mlist_of)
     };
+    // `decs` (rectification): each model's decision model when it differs
+    // from the one scored (a generated 2-SIFT model's glibc phi); a model with
+    // flagged decisions, or one exact.h's bound does not cover, is rescored in
+    // the reference's decisions on the host, and its list / MSAC bits marked
+    // unusable (sm_lbad_ / sm_mbad_)
     bool score_models(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */,
-                      const ListReq* req = nullptr) {
+                      const ListReq* req = nullptr, const Model* decs = nullptr) {
         auto& lm = Tr::lomodels(P_->w);
         lm.ensure(n);
         P_->w->lo_sb.ensure(n);
@@ -2311,7 +2606,7 @@ private:
             // adds its inliers in order (no ~90 us batch-scorer chain)
             const size_t pairs = small_score_pairs(P_->dp);
             P_->w->sm_vals.ensure(pairs * n);
-            P_->w->sm_bits.ensure(pairs * n / 64);
+            P_->w->sm_bits.ensure(3 * pairs * n / 64);
             // the graph-cut labeling with pairwise terms needs the residuals
             lists = req != nullptr && !(req->rule == 2 && use_graph());
             ListBits lb{{0.0, 0.0}, 0, prm_.spatial_coherence_weight, nullptr, nullptr};
@@ -2342,11 +2637,26 @@ private:
         if (!zc) P_->w->lo_sb.d2h(n, s_);
         HIPC(hipStreamSynchronize(s_));
         st_.launches += 1;
+        sm_mbad_.assign(n, 0);
+        sm_lbad_.assign(n, 0);
         for (uint32_t i = 0; i < n; ++i) {
             const uint32_t rn[2] = {P_->w->lo_sb.hn0.p[i], P_->w->lo_sb.hn1.p[i]};
             out[i] = finish(rn, P_->w->lo_sb.hv0.p[i], P_->w->lo_sb.hv1.p[i], P_->w->lo_sb.htot.p[i]);
             raw_n[2 * i] = rn[0];
             raw_n[2 * i + 1] = K_ == 2 ? rn[1] : 0;
+            if constexpr (kRect) {
+                if (!exact_) continue;
+                const Model& md = decs ? decs[i] : models[i];
+                const bool bad = unsafe(md);
+                if (P_->w->lo_sb.hfl.p[i] != 0 || bad) {
+                    uint32_t raw[2];
+                    out[i] = exact_score(models[i], md, raw);
+                    raw_n[2 * i] = raw[0];
+                    raw_n[2 * i + 1] = raw[1];
+                    sm_mbad_[i] = 1;
+                }
+                if (lists && (P_->w->lo_sb.hlfl.p[i] != 0 || bad)) sm_lbad_[i] = 1;
+            }
         }
         return lists;
     }
@@ -2425,9 +2735,15 @@ private:
         for (int c = 0; c < 2; ++c) {
             lists[c].clear();
             if (c >= K_) continue;
-            const uint8_t* mk = P_->w->h_mask_all.p + (c ? N_[0] : 0);
+            uint8_t* mk = P_->w->h_mask_all.p + (c ? N_[0] : 0);
+            // flagged decisions (bit 1; every scale pair of a model the bound
+            // does not cover) in glibc
+            if constexpr (kRect)
+                if (exact_)
+                    exact_mask(P_, c, model, rule, T[c], prm_.spatial_coherence_weight, mk, c == 0 && unsafe(model),
+                               ec_);
             for (uint64_t i = 0; i < N_[c]; ++i)
-                if (mk[i]) lists[c].push_back((uint32_t)i);
+                if (mk[i] & 1) lists[c].push_back((uint32_t)i);
         }
     }
 
@@ -2459,7 +2775,8 @@ private:
             bool updated = false;
             auto tp = Clock::now();
             if (!have_inl) {
-                if (lo_row_ >= 0 && std::memcmp(&lo_row_model_, &lo_model, sizeof(Model)) == 0) {
+                if (lo_row_ >= 0 && std::memcmp(&lo_row_model_, &lo_model, sizeof(Model)) == 0 &&
+                    (lo_row_lfl_ == 0 || !exact_) && !unsafe(lo_model)) {
                     // the triggering model's lists from its chunk's scoring launch
                     decode_lists(P_->w->h_cbits[lo_row_set_].p, (uint32_t)lo_row_, inl);
                 } else {
@@ -2535,11 +2852,15 @@ private:
                         lo_buf = Buffer{true, trial_models[q], {trial_raw[2 * q], trial_raw[2 * q + 1]}};
                     }
                 }
-                if (updated) lo_lists_from_bits_ = bits && lreq.msac;
+                if (updated) lo_lists_from_bits_ = bits && lreq.msac && !sm_mbad_[win];
                 if (updated && bits) {
-                    list_of((uint32_t)win, inl);
-                    have_inl = true;
-                    if (lreq.msac) list_of((uint32_t)win, lo_msac_lists_, true);
+                    // bits with flagged decisions: the next round relabels
+                    // through inlier_lists (exact_mask) instead
+                    if (!sm_lbad_[win]) {
+                        list_of((uint32_t)win, inl);
+                        have_inl = true;
+                    }
+                    if (lo_lists_from_bits_) list_of((uint32_t)win, lo_msac_lists_, true);
                 }
             }
             if (!updated) break;
@@ -2548,6 +2869,7 @@ private:
         if (best_.sum < max_score.sum) {
             best_ = max_score;
             best_model_ = lo_model;
+            best_val_ = lo_model;
             sfb_buf = lo_buf;
             // lo_msac_lists_ holds lo_model's MSAC lists from its own
             // scoring launch (the round that adopted it; later rounds only
@@ -2938,7 +3260,7 @@ int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double*
             const double Tt[2] = {T, 0.0};
             const size_t pairs = small_score_pairs(prob->dp);
             prob->w->sm_vals.ensure(pairs * nmodels);
-            prob->w->sm_bits.ensure(pairs * nmodels / 64);
+            prob->w->sm_bits.ensure(3 * pairs * nmodels / 64);
             HIPC(launch_score_small(prob->dp, Tt, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(),
                                     prob->w->sm_vals.p, prob->w->sm_bits.p, s));
         } else {
@@ -3033,7 +3355,7 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
         if (identity && debug_small_scorer(nmodels)) {
             const size_t pairs = small_score_pairs(prob->dp);
             prob->w->sm_vals.ensure(pairs * nmodels);
-            prob->w->sm_bits.ensure(pairs * nmodels / 64);
+            prob->w->sm_bits.ensure(3 * pairs * nmodels / 64);
             HIPC(launch_score_small(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, prob->w->lo_sb.dev(),
                                     prob->w->sm_vals.p, prob->w->sm_bits.p, s));
         } else {
@@ -3046,6 +3368,21 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
         std::memcpy(v0, prob->w->lo_sb.hv0.p, nmodels * sizeof(double));
         std::memcpy(v1, prob->w->lo_sb.hv1.p, nmodels * sizeof(double));
         std::memcpy(tot, prob->w->lo_sb.htot.p, nmodels * sizeof(double));
+        // flagged decisions (or a model exact.h does not cover): the
+        // reference's decisions, the twin values (the oracle's TWIN mode)
+        if (exact_on()) {
+            ExactCount ec;
+            for (uint32_t i = 0; i < nmodels; ++i)
+                if (prob->w->lo_sb.hfl.p[i] != 0 || model_unsafe(prob, hm[i], T[0])) {
+                    uint32_t n[2];
+                    double v[2];
+                    exact_accumulate(prob, hm[i], hm[i], T, n, v, tot[i], nullptr, ec);
+                    n0[i] = n[0];
+                    n1[i] = prob->K == 2 ? n[1] : 0;
+                    v0[i] = v[0];
+                    v1[i] = prob->K == 2 ? v[1] : 0.0;
+                }
+        }
         return GCR_OK;
     });
 }
@@ -3069,6 +3406,12 @@ int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_m
                          prob->w->mask[cls].p, s));
         HIPC(hipMemcpyAsync(mask_out, prob->w->mask[cls].p, n, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
+        // flagged decisions in glibc (GCR_EXACT=0: the twin's)
+        ExactCount ec;
+        if (exact_on())
+            exact_mask(prob, cls, m, rule == 2 ? 2 : 0, T, params->spatial_coherence_weight, mask_out,
+                       cls == 0 && model_unsafe(prob, m, T), ec);
+        for (size_t i = 0; i < n; ++i) mask_out[i] &= 1;
         return GCR_OK;
     });
 }

@@ -1,0 +1,129 @@
+// exact.h -- inlier decisions in the reference's arithmetic (glibc).
+//
+// The reference evaluates std::log, std::pow(t, -3.0) and std::atan2 from glibc
+// inside every residual (solver_rectifying_homography_three_sift.hpp:293-317,
+// ..._two_sift.hpp:621-665, model.h:156-204) and in the 2-SIFT minimal solver's
+// phi (..._two_sift.hpp:341), and decides with them: MSAC `r^2 <= 2.25 thr^2`
+// (MSAC_scoring_function.hpp:53-107), the LO relabel `r^2 <= (1.5 thr)^2`
+// (GCRANSAC.h:921-942), the 1-class labeling's `fl(r^2 / T) < 1`
+// (GCRANSAC.h:789-870) and the final masks.  The kernels evaluate the detmath
+// twins (detmath.h), whose results can differ from glibc's in the last bits.
+//
+// The twins' deviation from glibc is bounded.  For the residual r (r^2 the
+// squared residual) of one (feature, model) pair,
+//   scale:        |r_twin - r_glibc| <= 9.2e-16 + 2.9e-16 r
+//     (dm_pow_m3 < 1.5 ulp and glibc pow < 0.52 ulp: rs within 2.1 ulp, the
+//     two products round alike -> arg within 4.2 ulp = 9.2e-16 relative ->
+//     log(arg) within 9.2e-16 absolute; dm_log <= 0.77 ulp and glibc log
+//     <= 0.52 ulp of r -> 1.3 ulp(r) <= 2.9e-16 r), valid while rs, arg and
+//     t^-3 are normal numbers and rs is not at the 1e-9 cut (scale_unsafe);
+//   orientation:  |r_twin - r_glibc| <= 8e-15
+//     (dm_atan2 <= 1.8 ulp and glibc atan2 <= 1 ulp of |a| <= pi: 1.25e-15;
+//     the model's phi, when it is a minimal model's twin phi against the glibc
+//     one, as much again plus the phi + pi/2 rounding; th, c0, c1 and the two
+//     minAngleDiff steps add at most 4 roundings of ulp(2 pi) / 2 on each side:
+//     3.6e-15).
+// tests/test_exact.py measures the deviations on random pairs (max 8.9e-16
+// scale, 1.3e-15 orientation) far inside these bounds.
+//
+// The kernels therefore flag every pair whose twin r^2 lies within the band
+// [lo, hi] = [((sqrt(T) - D)(1 - 1e-12))^2, ((sqrt(T) + D)(1 + 1e-12))^2]
+// around a decision threshold T, with D = kDevScale / kDevOrient (the bounds
+// above with a 4-5x margin; the 1e-12 relative margin covers the relative
+// term, sqrt's and the squares' roundings).  Outside the band the twin and the
+// glibc residual fall on the same side of T (and of fl(r^2 / T) < 1, which
+// only differs from r^2 < T within 2^-53 T).  Inside it the host recomputes
+// the pair with glibc (engine.cpp, RunnerT::exact_*).  The conservative
+// prefilters of the batch scorers keep every flagged pair: their slack is
+// >= 1e-9 absolute in log scale and tan(1.5 thr) 1e-6 + 1e-12 in angle.
+//
+// Values: the MSAC running sums add the twin r^2 of the pairs the glibc
+// decision makes inliers (a definition, restated by the oracle's TWIN mode);
+// a pair whose decision the recheck flips makes the host re-fold that model's
+// sums in that definition.  A flip moves the finished score by
+// |1 - r^2 / T| <= (hi - lo) / T (r^2 is inside the band), i.e. by ~1e-13 at
+// the bench thresholds: score comparisons between different hypotheses are
+// unaffected unless their scores tie to that level.
+#pragma once
+
+#include "gcr_hd.h"
+
+namespace gcr {
+
+constexpr double kDevScale = 4e-15;      // bound on |r_twin - r_glibc|, scale class (absolute part)
+constexpr double kDevScaleRel = 1e-12;   // ... its relative part (and the band's rounding margin)
+constexpr double kDevOrient = 4e-14;     // orientation class (radians)
+
+// Per class c: a pair is flagged iff |r2 - mid[c]| <= half[c].
+struct FlagBand {
+    double mid[2];
+    double half[2];
+};
+
+GCR_HD bool in_flag_band(double r2, double mid, double half) { return __builtin_fabs(r2 - mid) <= half; }
+
+// The inlier rule of a squared residual (k_mask, the LO lists, the host's
+// glibc recheck): rule 0 r^2 <= T (MSAC_scoring_function.hpp:64-66, the LO
+// relabel GCRANSAC.h:921-942); rule 2 the 1-class labeling of an empty
+// neighbourhood graph (GCRANSAC.h:789-811, gcransac_python.cpp:63-68): SINK iff
+// the terminal capacity of add_term1(clamp(r^2 / T) energies) is < 0.
+GCR_HD bool mask_rule(double r2, int rule, double T, double lambda) {
+    if (rule == 2) {
+        const double oml = 1.0 - lambda;
+        double q = r2 / T;
+        q = (q < 0.0) ? 0.0 : ((1.0 < q) ? 1.0 : q);      // std::clamp
+        const double energy = 1.0 - q;
+        const double tr = (r2 <= T) ? (0.0 - oml * energy) : (oml * (1.0 - energy) - 0.0);
+        return tr < 0.0;
+    }
+    return r2 <= T;
+}
+
+// host-side helpers (launchers and engine)
+// the band around threshold T (squared) of class c (0 scale, 1 orientation)
+inline void flag_band_1(double T, int c, double& mid, double& half) {
+    const double D = c == 0 ? kDevScale : kDevOrient;
+    const double rT = sqrt(T);
+    double rlo = (rT - D) * (1.0 - kDevScaleRel), rhi = (rT + D) * (1.0 + kDevScaleRel);
+    if (!(rlo > 0.0)) rlo = 0.0;
+    const double lo = rlo * rlo, hi = rhi * rhi;
+    mid = 0.5 * (lo + hi);
+    half = 0.5 * (hi - lo) * (1.0 + 1e-9) + 1e-300;
+    if (!(T >= 0.0)) {                   // NaN threshold: nothing is an inlier on either side
+        mid = 0.0;
+        half = -1.0;
+    }
+}
+inline FlagBand flag_band(const double T[2]) {
+    FlagBand b;
+    for (int c = 0; c < 2; ++c) flag_band_1(T[c], c, b.mid[c], b.half[c]);
+    return b;
+}
+
+// A rectification model whose scale residuals the bound above does not cover:
+// sqrt(T) >= 60 (arguments of log near the ends of the normal range),
+// alpha^3 outside [2^-200, 2^200], a problem with a positive finite scale
+// outside [2^-200, 2^200] (`scales_ok` false) -- with both in range, log's
+// argument within [e^-60, e^60] keeps t^-3 and rs normal, so the error
+// analysis holds; other features give inf / NaN on both sides -- or the
+// rectified-scale cut rs < 1e-9 (scale_sq_residual) inside the inlier band
+// (|log(alpha^3 1e-9)| close to sqrt(T): the twin and glibc rs can fall on
+// either side of the cut).  The engine decides every pair of such a model on
+// the host.  `solver`: 0, 1 (original: arg = rs / alpha^3) or 2.
+inline bool scale_unsafe(int solver, double alpha, double T0, bool scales_ok) {
+    const double rT = sqrt(T0);
+    if (!(rT < 60.0) || !scales_ok) return true;
+    const double ac = (alpha * alpha) * alpha;
+    if (!(ac >= 0x1p-200 && ac <= 0x1p200)) return true;
+    const double at_cut = fabs(log(solver == 1 ? 1e-9 / ac : ac * 1e-9));
+    return !(at_cut > rT + 1e-3);
+}
+// the problem-level half of it: every positive finite scale feature in
+// [2^-200, 2^200]
+inline bool scales_in_range(const double* s, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (s[i] > 0.0 && s[i] < HUGE_VAL && !(s[i] >= 0x1p-200 && s[i] <= 0x1p200)) return false;
+    return true;
+}
+
+}  // namespace gcr

@@ -6,6 +6,8 @@
 // (findWeightedMode), :423-579 (non-minimal), :715-848 (normalizePoints, whose
 // transform is reset to identity), and Eigen's ColPivHouseholderQR for the
 // least-squares solve.  Weights are always empty on the Python path, i.e. 1.0.
+// Models are the reference's: the rectified angles of the mode (and the
+// minimal 2-SIFT phi) use glibc's atan2 (GlibcMath), as the reference does.
 #include "host_fit.h"
 #include "qr3.h"
 
@@ -287,7 +289,7 @@ bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectMode
         const double sp[2] = {sc.c0[si[0]], sc.c0[si[1]]};
         const double ox[2] = {oc.x[oi[0]], oc.x[oi[1]]}, oy[2] = {oc.y[oi[0]], oc.y[oi[1]]};
         const double ocs[2] = {oc.c0[oi[0]], oc.c0[oi[1]]}, osn[2] = {oc.c1[oi[0]], oc.c1[oi[1]]};
-        return solve_sift22(sx, sy, sp, ox, oy, ocs, osn, out);
+        return solve_sift22<GlibcMath>(sx, sy, sp, ox, oy, ocs, osn, out);
     }
     const size_t rows = ns + npairs;
     double sol[3];
@@ -310,7 +312,7 @@ bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectMode
     auto angles = [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; ++i) {
             const uint32_t j = oi[i];
-            ang[i] = rectified_angle(oc.x[j], oc.y[j], oc.c0[j], oc.c1[j], out.h7, out.h8);
+            ang[i] = rectified_angle<GlibcMath>(oc.x[j], oc.y[j], oc.c0[j], oc.c1[j], out.h7, out.h8);
         }
     };
     if (big && rows >= big_rows) big->for_ranges(no, angles);

@@ -1,7 +1,7 @@
 // host_fit.h -- host-side model fitting for local optimisation and the final
 // refit (the parts north_star keeps in host C++).  Per-feature constants come
 // from the problem's precomputed SoA arrays; hypothesis-dependent angles use
-// detmath so the results match what the kernels would compute.
+// glibc, as the reference's fits do (models are never twin arithmetic).
 #pragma once
 
 #include <cstddef>

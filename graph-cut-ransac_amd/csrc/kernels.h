@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "exact.h"
 #include "fund.h"
 #include "geo.h"
 #include "gram.h"
@@ -53,12 +54,18 @@ struct DevProblem {
 
 // Raw MSAC accumulators per hypothesis (host finishes the score exactly as
 // MSACScoringFunction::getScore does, MSAC_scoring_function.hpp:108-127).
+// fl (rectification scorers, optional): the hypothesis's pairs whose twin
+// r^2 lies in the flag band of the MSAC threshold (exact.h) -- decisions the
+// host rechecks with glibc; lfl (small scorer with ListBits, optional): the
+// same for the list predicate.  Correspondence scorers leave them alone.
 struct ScoreOut {
     uint32_t* n0;
     uint32_t* n1;
     double* v0;
     double* v1;
     double* tot;
+    uint32_t* fl = nullptr;
+    uint32_t* lfl = nullptr;
 };
 
 // Draw + validate + solve `nslots` outer-iteration slots [slot0, slot0+nslots).
@@ -253,8 +260,10 @@ hipError_t launch_sqres_geo(const DevProblem& p, const GeoModel& model, double* 
 hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_t* count, hipStream_t stream);
 
 // Low-latency scoring of a few models (LO trials, refits): every pair in
-// parallel into vals / bits (small_score_pairs(p) doubles and /64 words per
-// model), then one wave per model adds the inlier values in feature order.
+// parallel into vals / bits (small_score_pairs(p) doubles and 3 x /64 words
+// per model: the inlier ballots, then the MSAC and the list predicate's flag
+// ballots, exact.h), then one wave per model adds the inlier values in
+// feature order and counts the flags (out.fl, out.lfl).
 // Same raw accumulators as launch_score / launch_score_geo.  `models` points
 // to RectModel (solvers 0-2) or GeoModel (3, 4), identity normalisation only;
 // models with inc > 101 (inc may be null) score zeros.
@@ -273,7 +282,9 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
                               uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream,
                               const ListBits* lists = nullptr);
 
-// Per-feature inlier mask of one model for class `cls`.
+// Per-feature inlier mask of one model for class `cls`: bit 0 the decision,
+// bit 1 set when the pair's twin r^2 lies in the flag band of T (exact.h:
+// the host rechecks it with glibc).
 // rule 0: r^2 <= T (T = MSAC 2.25 thr^2 or LO (1.5 thr)^2 as passed)
 // rule 2: 1-class graph-cut labeling with weight lambda, T = (1.5 thr)^2
 hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int rule, double T, double lambda,

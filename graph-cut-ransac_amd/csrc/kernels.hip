@@ -304,22 +304,24 @@ __global__ __launch_bounds__(kGenBlock) void k_generate_fw(DevProblem p, uint64_
 
 // ---------------------------------------------------------------- score ----
 template <int KIND, bool kIdentity>
-__global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, double T1,
+__global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, double T1, FlagBand fb,
                                                        const RectModel* __restrict__ models,
                                                        const uint8_t* __restrict__ inc, uint32_t nh, ScoreOut out) {
     const uint32_t h = blockIdx.x * kScoreBlock + threadIdx.x;
     if (h >= nh) return;
     if (inc != nullptr && inc[h] > 101) {
         out.n0[h] = 0; out.n1[h] = 0; out.v0[h] = 0.0; out.v1[h] = 0.0; out.tot[h] = 0.0;
+        if (out.fl) out.fl[h] = 0;
         return;
     }
     const RectModel m = models[h];
     const DevClass c0 = p.cls[0];
     const double ac = alpha_cube(m);
-    uint32_t cnt0 = 0;
+    uint32_t cnt0 = 0, nfl = 0;
     double acc0 = 0.0;
     for (uint32_t i = 0; i < c0.n; ++i) {
         const double r2 = scale_sq_residual<KIND == 1, kIdentity>(c0.x[i], c0.y[i], c0.a[i], m, ac);
+        nfl += in_flag_band(r2, fb.mid[0], fb.half[0]) ? 1u : 0u;
         if (r2 <= T0) {
             cnt0 += 1;
             acc0 += -r2;
@@ -332,6 +334,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, 
         const OrientConst oc = orient_const(m);
         for (uint32_t i = 0; i < c1.n; ++i) {
             const double r2 = orient_sq_residual<kIdentity>(c1.x[i], c1.y[i], c1.c0[i], c1.c1[i], m, oc);
+            nfl += in_flag_band(r2, fb.mid[1], fb.half[1]) ? 1u : 0u;
             if (r2 <= T1) {
                 cnt1 += 1;
                 acc1 += -r2;
@@ -344,6 +347,7 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, 
     out.v0[h] = acc0;
     out.v1[h] = acc1;
     out.tot[h] = tot;
+    if (out.fl) out.fl[h] = nfl;
 }
 
 // ------------------------------------------------------- split scoring ----
@@ -469,7 +473,7 @@ struct GenArgs {
 
 template <int KIND, int H, int R, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, double T0, double T1, double band0,
-                                                               double tan_tau1,
+                                                               double tan_tau1, FlagBand fband,
                                                                const typename ModelOf<KIND>::type* __restrict__ models,
                                                                const uint8_t* __restrict__ inc, uint32_t nh_in,
                                                                ScoreOut out, GenArgs gen) {
@@ -500,6 +504,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     __shared__ uint16_t queue[kComputeWaves][kPack ? 1 : kPer * 64];
     __shared__ HypConst hyp[H];
     __shared__ uint32_t cnt_sh[2][H];
+    __shared__ uint32_t fl_sh[H];                     // flagged pairs (exact.h), rectification solvers
     // KIND >= 3: per round buffer, compute wave and hypothesis, the number of
     // inlier values the wave packed (in feature order) into its tile segment
     __shared__ uint32_t seg_cnt[2][kPack ? kComputeWaves : 1][kPack ? H : 1];
@@ -626,6 +631,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
         hyp[h] = q;
     }
     if (t < 2 * H) cnt_sh[t / H][t % H] = 0;
+    if (t < H) fl_sh[t] = 0;
     stage(0, 0, t, kSplitThreads);
     __syncthreads();
 
@@ -741,6 +747,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         tl[hh * kRP + il] = -r2;
                         atomicAdd(&cnt_sh[cls][hh], 1u);
                     }
+                    if (KIND <= 2 && in_flag_band(r2, fband.mid[cls], fband.half[cls])) atomicAdd(&fl_sh[hh], 1u);
                 }
                 }   // band path (KIND <= 3)
             }
@@ -827,6 +834,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
             out.v0[hg] = valid_h ? acc0 : 0.0;
             out.v1[hg] = valid_h ? acc1 : 0.0;
             out.tot[hg] = valid_h ? tot : 0.0;
+            if (KIND <= 2 && out.fl) out.fl[hg] = valid_h ? fl_sh[h] : 0u;
             if constexpr (kGen) {
                 // MSACScoringFunction::getScore finish (MSAC_scoring_function.hpp:108-127)
                 double sum = 0.0;
@@ -1126,7 +1134,7 @@ __device__ __forceinline__ void pb_test(const HPairBand& b, float x1, float y1, 
 
 template <int KIND, int H, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(KIND >= 3 ? 8 : 1))) void k_score_fm(DevProblem p, double T0, double T1, double band0,
-                                                            double tan_tau1,
+                                                            double tan_tau1, FlagBand fband,
                                                             const typename ModelOf<KIND>::type* __restrict__ models,
                                                             const uint8_t* __restrict__ inc, uint32_t nh,
                                                             ScoreOut out, GenArgs gen) {
@@ -1156,6 +1164,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     __shared__ HypConst hyp[H];
     __shared__ uint32_t hval[H];
     __shared__ uint32_t cnt_sh[2][H];
+    __shared__ uint32_t fl_sh[H];                       // flagged pairs (exact.h), rectification solvers
     using PairBand = std::conditional_t<KIND == 3, HPairBand, FPairBand>;
     __shared__ PairBand fpb[KIND >= 3 ? (H + 1) / 2 : 1];
     __shared__ int gen_a[kGen ? H : 1];
@@ -1280,6 +1289,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
         hval[t] = v ? 1u : 0u;
         cnt_sh[0][t] = 0;
         cnt_sh[1][t] = 0;
+        fl_sh[t] = 0;
     }
     if constexpr (KIND == 4) {
         if ((H & 1) && t == H) fpb_setup(fpb, t, hyp[0].g, false, T0, p.cls[0]);   // odd H: inert pad
@@ -1563,6 +1573,8 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                     }
                     ow[q * kReg + k] = inl ? -r2 : 0.0;
                     if (inl) atomicAdd(&cnt_sh[cls][q], 1u);
+                    // a decision the host rechecks with glibc (exact.h); rare
+                    if (KIND <= 2 && in_flag_band(r2, fband.mid[cls], fband.half[cls])) atomicAdd(&fl_sh[q], 1u);
                 }
                 cur = nxt_s;
             }
@@ -1660,6 +1672,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             out.v0[hg] = valid_h ? acc0 : 0.0;
             out.v1[hg] = valid_h ? acc1 : 0.0;
             out.tot[hg] = valid_h ? tot : 0.0;
+            if (KIND <= 2 && out.fl) out.fl[hg] = valid_h ? fl_sh[h] : 0u;
             if constexpr (kGen) {
                 // MSACScoringFunction::getScore finish (MSAC_scoring_function.hpp:108-127)
                 double sum = 0.0;
@@ -1718,25 +1731,14 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
 //
 // Layout per model: class 0 at [0, pad0), class 1 at [pad0, pad0 + pad1),
 // pad_c = n_c rounded up to 64 (unused pairs: value 0, bit 0).
-// mask rule of k_mask / launch_mask on a residual (rule 0: threshold; rule 2:
-// the 1-class labeling without pairwise edges)
-__device__ __forceinline__ bool mask_rule(double r2, int rule, double T, double lambda) {
-    if (rule == 2) {
-        const double oml = 1.0 - lambda;
-        double q = r2 / T;
-        q = (q < 0.0) ? 0.0 : ((1.0 < q) ? 1.0 : q);      // std::clamp
-        const double energy = 1.0 - q;
-        const double tr = (r2 <= T) ? (0.0 - oml * energy) : (oml * (1.0 - energy) - 0.0);
-        return tr < 0.0;
-    }
-    return r2 <= T;
-}
+// mask rule of k_mask / launch_mask on a residual: mask_rule, exact.h
 
 template <int KIND>
 __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
                                                   const uint8_t* __restrict__ inc, double T0, double T1,
                                                   uint32_t pad0, uint32_t ntot, double* __restrict__ vals,
-                                                  uint64_t* __restrict__ bits, ListBits lb) {
+                                                  uint64_t* __restrict__ bits, ListBits lb, FlagBand fbm,
+                                                  FlagBand fbl) {
     const uint32_t mi = blockIdx.y;
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (blockIdx.x * 256 >= ntot) return;                // whole block (ntot is a multiple of 64)
@@ -1762,12 +1764,20 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
     const bool lin = lb.bits != nullptr && live && j < ntot && i < c.n &&
                      mask_rule(r2, lb.rule, cls == 0 ? lb.T[0] : lb.T[1], lb.lambda);
     const uint64_t lbw = __ballot(lin);
+    // decisions within the twin-glibc bound of their threshold (exact.h): the
+    // MSAC test's and the list predicate's, counted by k_lo_chain
+    const bool ev = live && j < ntot && i < c.n && KIND <= 2;
+    const uint64_t fw = __ballot(ev && in_flag_band(r2, fbm.mid[cls], fbm.half[cls]));
+    const uint64_t lfw = __ballot(ev && lb.bits != nullptr && in_flag_band(r2, fbl.mid[cls], fbl.half[cls]));
     if (j < ntot) {
         vals[(size_t)mi * ntot + j] = inl ? -r2 : 0.0;
         if ((threadIdx.x & 63) == 0) {
-            bits[((size_t)mi * ntot + j) / 64] = b;
-            if (lb.bits != nullptr) lb.bits[((size_t)mi * ntot + j) / 64] = lbw;
-            if (lb.mbits != nullptr) lb.mbits[((size_t)mi * ntot + j) / 64] = b;
+            const size_t wi = ((size_t)mi * ntot + j) / 64, plane = (size_t)gridDim.y * ntot / 64;
+            bits[wi] = b;
+            bits[plane + wi] = fw;
+            bits[2 * plane + wi] = lfw;
+            if (lb.bits != nullptr) lb.bits[wi] = lbw;
+            if (lb.mbits != nullptr) lb.mbits[wi] = b;
         }
     }
 }
@@ -1986,6 +1996,22 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
     const uint32_t nblk = (nchunks + kLoChunks - 1) / kLoChunks;
     double run = 0.0, hold = 0.0;
     uint32_t cnt0 = 0, cntall = 0;
+    // flagged decisions (k_lo_values' flag planes: MSAC, list predicate),
+    // counted before the fold (the block loop's barriers order them)
+    __shared__ uint32_t fcnt[2];
+    if (t < 2) fcnt[t] = 0;
+    __syncthreads();
+    {
+        const size_t plane = (size_t)gridDim.x * ntot / 64;
+        const uint64_t* fw = bits + plane + (size_t)mi * ntot / 64;
+        uint32_t a = 0, l = 0;
+        for (uint32_t c = (uint32_t)t; c < nchunks; c += kLoThreads) {
+            a += (uint32_t)__builtin_popcountll(fw[c]);
+            l += (uint32_t)__builtin_popcountll(fw[plane + c]);
+        }
+        if (a) atomicAdd(&fcnt[0], a);
+        if (l) atomicAdd(&fcnt[1], l);
+    }
     for (uint32_t b = 0; b < nblk; ++b) {
         const uint32_t ch0 = b * kLoChunks;
         const uint32_t nch = min(kLoChunks, nchunks - ch0);
@@ -2117,6 +2143,8 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
             out.v0[mi] = KIND == 2 ? hold : run;
             out.v1[mi] = KIND == 2 ? run : 0.0;
             out.tot[mi] = tot;
+            if (out.fl) out.fl[mi] = fcnt[0];
+            if (out.lfl) out.lfl[mi] = fcnt[1];
         }
     }
 }
@@ -3096,7 +3124,8 @@ __global__ __launch_bounds__(kSelectThreads) void k_select_wg(const WgBest* __re
 // ----------------------------------------------------------------- mask ----
 template <int KIND>
 __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, typename ModelOf<KIND>::type m, int rule,
-                                                     double T, double lambda, uint8_t* __restrict__ mask) {
+                                                     double T, double lambda, double fmid, double fhalf,
+                                                     uint8_t* __restrict__ mask) {
     const uint32_t i = blockIdx.x * kMaskBlock + threadIdx.x;
     if (i >= c.n) return;
     double r2;
@@ -3104,8 +3133,11 @@ __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, typena
     else if (cls == 0) r2 = scale_sq_residual<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
     else r2 = orient_sq_residual<false>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
     // rule 2: labeling(), BK max-flow with no pairwise edges (empty grid
-    // graph, gcransac_python.cpp:63-68) -> SINK iff terminal capacity < 0
-    mask[i] = mask_rule(r2, rule, T, lambda) ? 1 : 0;
+    // graph, gcransac_python.cpp:63-68) -> SINK iff terminal capacity < 0;
+    // bit 1: a decision within the twin-glibc bound (exact.h), rechecked by
+    // the host
+    const bool flag = KIND <= 2 && in_flag_band(r2, fmid, fhalf);
+    mask[i] = (uint8_t)((mask_rule(r2, rule, T, lambda) ? 1 : 0) | (flag ? 2 : 0));
 }
 
 // ----------------------------------------------------------------- math ----
@@ -3159,9 +3191,9 @@ void launch_score_t(const DevProblem& p, const double T[2], const RectModel* mod
                     const ScoreOut& out, hipStream_t stream) {
     const dim3 grid(blocks_for(nh, kScoreBlock)), block(kScoreBlock);
     switch (p.solver) {
-        case 0: hipLaunchKernelGGL((k_score<0, kIdentity>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
-        case 1: hipLaunchKernelGGL((k_score<1, kIdentity>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
-        default: hipLaunchKernelGGL((k_score<2, kIdentity>), grid, block, 0, stream, p, T[0], T[1], models, inc, nh, out); break;
+        case 0: hipLaunchKernelGGL((k_score<0, kIdentity>), grid, block, 0, stream, p, T[0], T[1], flag_band(T), models, inc, nh, out); break;
+        case 1: hipLaunchKernelGGL((k_score<1, kIdentity>), grid, block, 0, stream, p, T[0], T[1], flag_band(T), models, inc, nh, out); break;
+        default: hipLaunchKernelGGL((k_score<2, kIdentity>), grid, block, 0, stream, p, T[0], T[1], flag_band(T), models, inc, nh, out); break;
     }
 }
 
@@ -3171,7 +3203,8 @@ void launch_score_t(const DevProblem& p, const double T[2], const RectModel* mod
 void band_consts(const double T[2], double& band0, double& tan_tau1) {
     band0 = exp(sqrt(T[0] / 2.25) * 1.5) * (1.0 + 1e-9);
     const double tau1 = sqrt(T[1]);
-    tan_tau1 = (tau1 < 0.7) ? tan(tau1) * (1.0 + 1e-6) + 1e-300 : HUGE_VAL;
+    // + 1e-12: the flag band of exact.h reaches kDevOrient = 4e-14 past sqrt(T)
+    tan_tau1 = (tau1 < 0.7) ? tan(tau1) * (1.0 + 1e-6) + 1e-12 : HUGE_VAL;
 }
 
 template <int H, int R>
@@ -3181,9 +3214,9 @@ void launch_split_t(const DevProblem& p, const double T[2], const RectModel* mod
     double band0, tan_tau1;
     band_consts(T, band0, tan_tau1);
     switch (p.solver) {
-        case 0: hipLaunchKernelGGL((k_score_split<0, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, GenArgs{}); break;
-        case 1: hipLaunchKernelGGL((k_score_split<1, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, GenArgs{}); break;
-        default: hipLaunchKernelGGL((k_score_split<2, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, GenArgs{}); break;
+        case 0: hipLaunchKernelGGL((k_score_split<0, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), models, inc, nh, out, GenArgs{}); break;
+        case 1: hipLaunchKernelGGL((k_score_split<1, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), models, inc, nh, out, GenArgs{}); break;
+        default: hipLaunchKernelGGL((k_score_split<2, H, R, false>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), models, inc, nh, out, GenArgs{}); break;
     }
 }
 
@@ -3204,9 +3237,9 @@ void launch_fm_t(const DevProblem& p, const double T[2], uint32_t nh, const Scor
     double band0, tan_tau1;
     band_consts(T, band0, tan_tau1);
     switch (p.solver) {
-        case 0: hipLaunchKernelGGL((k_score_fm<0, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, g); break;
-        case 1: hipLaunchKernelGGL((k_score_fm<1, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, g); break;
-        default: hipLaunchKernelGGL((k_score_fm<2, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, models, inc, nh, out, g); break;
+        case 0: hipLaunchKernelGGL((k_score_fm<0, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), models, inc, nh, out, g); break;
+        case 1: hipLaunchKernelGGL((k_score_fm<1, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), models, inc, nh, out, g); break;
+        default: hipLaunchKernelGGL((k_score_fm<2, H, kGen>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), models, inc, nh, out, g); break;
     }
 }
 
@@ -3416,9 +3449,9 @@ void launch_fused_t(const DevProblem& p, const double T[2], uint32_t nh, const S
     double band0, tan_tau1;
     band_consts(T, band0, tan_tau1);
     switch (p.solver) {
-        case 0: hipLaunchKernelGGL((k_score_split<0, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, nullptr, nullptr, nh, out, g); break;
-        case 1: hipLaunchKernelGGL((k_score_split<1, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, nullptr, nullptr, nh, out, g); break;
-        default: hipLaunchKernelGGL((k_score_split<2, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, nullptr, nullptr, nh, out, g); break;
+        case 0: hipLaunchKernelGGL((k_score_split<0, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), nullptr, nullptr, nh, out, g); break;
+        case 1: hipLaunchKernelGGL((k_score_split<1, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), nullptr, nullptr, nh, out, g); break;
+        default: hipLaunchKernelGGL((k_score_split<2, H, R, true>), grid, block, 0, stream, p, T[0], T[1], band0, tan_tau1, flag_band(T), nullptr, nullptr, nh, out, g); break;
     }
 }
 
@@ -3509,7 +3542,7 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         constexpr int KIND = decltype(ktag)::value;
         using M = typename ModelOf<KIND>::type;
         hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), inc, T[0], T[1],
-                           pad0, ntot, vals, bits, lb);
+                           pad0, ntot, vals, bits, lb, flag_band(T), flag_band(lb.T));
         if (lo_fold_wide())
             hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits,
                                out);
@@ -3532,10 +3565,12 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
     const DevClass& c = p.cls[cls];
     if (c.n == 0) return hipSuccess;
     const dim3 grid(blocks_for(c.n, kMaskBlock)), block(kMaskBlock);
+    double fmid, fhalf;
+    flag_band_1(T, cls, fmid, fhalf);
     switch (p.solver) {
-        case 0: hipLaunchKernelGGL(k_mask<0>, grid, block, 0, stream, c, cls, model, rule, T, lambda, mask); break;
-        case 1: hipLaunchKernelGGL(k_mask<1>, grid, block, 0, stream, c, cls, model, rule, T, lambda, mask); break;
-        default: hipLaunchKernelGGL(k_mask<2>, grid, block, 0, stream, c, cls, model, rule, T, lambda, mask); break;
+        case 0: hipLaunchKernelGGL(k_mask<0>, grid, block, 0, stream, c, cls, model, rule, T, lambda, fmid, fhalf, mask); break;
+        case 1: hipLaunchKernelGGL(k_mask<1>, grid, block, 0, stream, c, cls, model, rule, T, lambda, fmid, fhalf, mask); break;
+        default: hipLaunchKernelGGL(k_mask<2>, grid, block, 0, stream, c, cls, model, rule, T, lambda, fmid, fhalf, mask); break;
     }
     return hipGetLastError();
 }
@@ -3663,7 +3698,7 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
         constexpr int KIND = decltype(ktag)::value, H = decltype(htag)::value, R = decltype(rtag)::value;
         const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;     // h_band slack
         hipLaunchKernelGGL((k_score_split<KIND, H, R, false>), dim3((nh + H - 1) / H), dim3(kSplitThreads), 0,
-                           stream, p, T, 0.0, sb * sb, 0.0, models, inc, nh, out, ga);
+                           stream, p, T, 0.0, sb * sb, 0.0, FlagBand{}, models, inc, nh, out, ga);
     };
     auto by_h = [&](auto ktag) {
         const int h = split_h(nh);
@@ -3685,11 +3720,11 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
         (void)attr;
         if (p.solver == 4) {
             hipLaunchKernelGGL((k_score_fm<4, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), dyn, stream, p,
-                               T, 0.0, T * (1.0 + 1e-9), 0.0, models, inc, nh, out, ga);
+                               T, 0.0, T * (1.0 + 1e-9), 0.0, FlagBand{}, models, inc, nh, out, ga);
         } else {
             const double sb = sqrt(T) * (1.0 + 1e-7) + 1e-7;
             hipLaunchKernelGGL((k_score_fm<3, 16, false>), dim3((nh + 15) / 16), dim3(kSplitThreads), dyn, stream, p,
-                               T, 0.0, sb * sb, 0.0, models, inc, nh, out, ga);
+                               T, 0.0, sb * sb, 0.0, FlagBand{}, models, inc, nh, out, ga);
         }
     } else if (p.solver == 4) {
         by_h(std::integral_constant<int, 4>{});
@@ -3705,9 +3740,9 @@ hipError_t launch_mask_geo(const DevProblem& p, const GeoModel& model, int rule,
     if (c.n == 0) return hipSuccess;
     const dim3 grid(blocks_for(c.n, kMaskBlock)), block(kMaskBlock);
     if (p.solver == 4)
-        hipLaunchKernelGGL(k_mask<4>, grid, block, 0, stream, c, 0, model, rule, T, lambda, mask);
+        hipLaunchKernelGGL(k_mask<4>, grid, block, 0, stream, c, 0, model, rule, T, lambda, 0.0, -1.0, mask);
     else
-        hipLaunchKernelGGL(k_mask<3>, grid, block, 0, stream, c, 0, model, rule, T, lambda, mask);
+        hipLaunchKernelGGL(k_mask<3>, grid, block, 0, stream, c, 0, model, rule, T, lambda, 0.0, -1.0, mask);
     return hipGetLastError();
 }
 

@@ -32,6 +32,23 @@ constexpr double kPi2 = dm::cf(0x3ff921fb54442d18ull);     // M_PI_2
 constexpr double kTwoPi = 2.0 * dm::cf(0x400921fb54442d18ull);
 constexpr double kEps9 = 1e-9;                              // solvers' kEpsilon
 
+// The three hypothesis-dependent libm calls of the residuals and of the
+// 2-SIFT minimal solver, as a policy: TwinMath (detmath.h, host and device,
+// what every kernel evaluates) or, on the host only, GlibcMath -- the
+// reference's own std::log / std::pow(t, -3.0) / std::atan2, with which the
+// engine takes every decision and model (exact.h).  Same operations around
+// them either way.
+struct TwinMath {
+    static GCR_HD double log(double x) { return dm::dm_log(x); }
+    static GCR_HD double pm3(double t) { return dm::dm_pow_m3(t); }
+    static GCR_HD double atan2(double y, double x) { return dm::dm_atan2(y, x); }
+};
+struct GlibcMath {                       // host only (the engine's recheck, host fits)
+    static double log(double x) { return ::log(x); }
+    static double pm3(double t) { return ::pow(t, -3.0); }
+    static double atan2(double y, double x) { return ::atan2(y, x); }
+};
+
 // model.h: NormalizingTransform{x0,y0,s} + RectifyingHomography{h7,h8} +
 // ScaleBased{alpha} + OrientationBased{phi}.  56 bytes, POD on both sides.
 struct RectModel {
@@ -48,7 +65,7 @@ GCR_HD double alpha_cube(const RectModel& m) { return m.alpha * m.alpha * m.alph
 
 // r^2 of one scale feature (x, y, s); DBL_MAX*DBL_MAX (= +inf) for rectified
 // scales below 1e-9 as in the reference.  kOriginal selects log(rs/alpha^3).
-template <bool kOriginal, bool kIdentity>
+template <bool kOriginal, bool kIdentity, class M = TwinMath>
 GCR_HD double scale_sq_residual(double x, double y, double sc, const RectModel& m, double ac) {
     double px = x, py = y, ps = sc;
     if (!kIdentity) {
@@ -57,10 +74,10 @@ GCR_HD double scale_sq_residual(double x, double y, double sc, const RectModel& 
         ps = sc * m.s;
     }
     const double t = (-m.h7 * px - m.h8 * py) + 1.0;
-    const double rs = ps * dm::dm_pow_m3(t);
+    const double rs = ps * M::pm3(t);
     if (rs < kEps9) return DBL_MAX * DBL_MAX;
     const double arg = kOriginal ? rs / ac : ac * rs;
-    const double r = __builtin_fabs(dm::dm_log(arg));
+    const double r = __builtin_fabs(M::log(arg));
     return r * r;
 }
 
@@ -85,13 +102,14 @@ GCR_HD double min_angle_diff_c(double ca, double cb) {
 
 // RectifyingHomography::rectifiedAngle (model.h:156-165) with the feature's
 // cos/sin supplied; (px, py) are already normalised coordinates.
+template <class M = TwinMath>
 GCR_HD double rectified_angle(double px, double py, double ct, double st, double h7, double h8) {
     const double numer = (-px * st + py * ct) * h7 + st;
     const double denom = (px * st - py * ct) * h8 + ct;
-    return dm::clip_angle_small(dm::dm_atan2(numer, denom));   // |atan2| <= pi
+    return dm::clip_angle_small(M::atan2(numer, denom));   // |atan2| <= pi
 }
 
-template <bool kIdentity>
+template <bool kIdentity, class M = TwinMath>
 GCR_HD double orient_sq_residual(double x, double y, double ct, double st, const RectModel& m,
                                  const OrientConst& oc) {
     double px = x, py = y;
@@ -107,7 +125,7 @@ GCR_HD double orient_sq_residual(double x, double y, double ct, double st, const
     // clip_angle_small on each (NaN stays NaN), with fewer operations.
     const double numer = (-px * st + py * ct) * m.h7 + st;
     const double denom = (px * st - py * ct) * m.h8 + ct;
-    const double a = dm::dm_atan2(numer, denom);
+    const double a = M::atan2(numer, denom);
     const double th = a < 0.0 ? a + kTwoPi : a;
     const double c0 = th == kTwoPi ? 0.0 : th;
     const double dpi = th - kPi;
@@ -280,6 +298,7 @@ GCR_HD bool valid_sample_sift22(const double sx[2], const double sy[2], const do
     return !point_in_hull4(hxs, hys, vx, vy);
 }
 
+template <class M = TwinMath>
 GCR_HD bool solve_sift22(const double sx[2], const double sy[2], const double sp[2], const double ox[2],
                          const double oy[2], const double oc[2], const double os[2], RectModel& out) {
     double a[3][4];
@@ -307,7 +326,7 @@ GCR_HD bool solve_sift22(const double sx[2], const double sy[2], const double sp
     if (out.alpha < kEps9) return false;
     const double vz = (-out.h7 * vp[0] - out.h8 * vp[1]) + vp[2];   // rectifyPoint(vp)
     if (__builtin_fabs(vz) > kEps9) return false;
-    out.phi = dm::clip_angle_small(dm::dm_atan2(vp[1], vp[0]));
+    out.phi = dm::clip_angle_small(M::atan2(vp[1], vp[0]));
     return true;
 }
 

@@ -10,7 +10,11 @@
 //   - its prefix-maximum chain: the hypotheses whose finished MSAC score beats
 //     every earlier valid one of the block and a bar (the best known when the
 //     block was summarised).  Every strict new best of the replay is one of
-//     them, whatever LO does in between (LO only raises the bar);
+//     them, whatever LO does in between (LO only raises the bar).  A
+//     hypothesis with flagged decisions (exact.h: its score in the reference's
+//     arithmetic is only known after the host's recheck) is always a member
+//     and never raises the running maximum, so the chain still holds every
+//     possible new best;
 //   - the iteration and hypothesis totals, and for each chain member the
 //     iterations and hypotheses before it (prefix sums of inc);
 //   - the block's last live hypothesis (the buffer the replay holds at a
@@ -33,6 +37,8 @@ struct SumHyp {                        // one hypothesis of a block
     uint64_t it_before;                // sum of inc over the block's slots before its slot
     uint64_t hyps_before;              // live hypotheses before it in the block
     uint32_t n0, n1;                   // raw MSAC accumulators (ScoreOut)
+    uint32_t fl;                       // flagged MSAC decisions (exact.h): the host rechecks them
+    uint32_t lfl;                      // flagged list decisions (small-scored chunks with list bits)
     double v0, v1, tot;
     double m[9];                       // the model (RectModel: 7 doubles, GeoModel: 9)
 };

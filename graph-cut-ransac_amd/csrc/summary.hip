@@ -35,6 +35,8 @@ struct SumPart {
     uint32_t ncand;                     // B: chain members kept
     uint32_t over;                      // B: chain truncated at kPartCap
     double maxv;                        // B: largest eligible value of the part (-1: none)
+    uint32_t nflag;                     // B: flagged members of the part (exact.h)
+    uint32_t pad;
 };
 
 struct PartCand {
@@ -42,7 +44,8 @@ struct PartCand {
     uint32_t it_before;                 // block-relative
     uint32_t hyps_before;               // block-relative
     uint32_t pad;
-    double val;
+    double val;                         // its score (+inf: flagged, always a member)
+    double rb;                          // the part's running maximum including it
 };
 
 // Wave scans by DPP (row shifts, then the two row broadcasts): the lanes
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
     const int K = a.solver == 2 ? 2 : 1;
     const M* models = static_cast<const M*>(a.models);
     double run = a.bar, pmax = -1.0;
-    uint32_t nc = 0, over = 0;
+    uint32_t nc = 0, over = 0, nflag = 0;
     for (uint32_t o = 0; base + o < end; o += 64) {
         const uint32_t p = base + o + lane;
         const uint32_t in = p < end ? a.inc[p] : 255u;
@@ -194,16 +197,23 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
         const uint32_t cs = wave_incl_sum(c, lane), ls = wave_incl_sum(l ? 1u : 0u, lane);
         const uint32_t hb = loff + ls - (l ? 1u : 0u);          // live hypotheses before p
         double val = -1.0;
+        bool flagged = false;
         if (l && p >= a.from_pos) {
             const uint32_t j = a.hmap != nullptr ? hb : p;
             val = finish_at(a.sc, j, K, a.m0, a.m1, a.Tm0, a.Tm1);
             if constexpr (std::is_same<M, RectModel>::value)
-                if (a.solver == 2 && !valid_model_sift22(models[p])) val = -1.0;
+                if (a.solver == 2 && !valid_model_sift22(models[p])) val = -2.0;
+            // flagged decisions: its exact score is the host's to find (a
+            // member whatever its twin score, never the running maximum)
+            if (val > -2.0 && a.sc.fl != nullptr && a.sc.fl[j] != 0) {
+                flagged = true;
+                val = -1.0;
+            }
         }
         const double im = wave_incl_max(val, lane);
         const double before = prev_lane_f64(run, im);
         const double bar = lane == 0 ? run : (run < before ? before : run);
-        const bool cand = val >= 0.0 && val > bar;
+        const bool cand = (val >= 0.0 && val > bar) || flagged;
         const uint64_t bc = __ballot(cand);
         if (cand) {
             const uint32_t r = nc + (uint32_t)__builtin_popcountll(bc & ((1ull << lane) - 1ull));
@@ -214,9 +224,11 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
                 pc.pos = p;
                 pc.it_before = coff + cs - c - own;
                 pc.hyps_before = hb;
-                pc.val = val;
+                pc.val = flagged ? __builtin_huge_val() : val;
+                pc.rb = flagged ? bar : val;
             }
         }
+        nflag += (uint32_t)__builtin_popcountll(__ballot(flagged));
         const uint32_t add = (uint32_t)__builtin_popcountll(bc);
         if (nc + add > a.cap) over = 1;
         nc = min(nc + add, a.cap);
@@ -231,6 +243,7 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
         s.ncand = nc;
         s.over = over;
         s.maxv = pmax;
+        s.nflag = nflag;
     }
 }
 
@@ -244,6 +257,8 @@ __device__ void fill_hyp(const SumArgs& a, uint32_t p, uint64_t it_before, uint6
     h.hyps_before = hyps_before;
     h.n0 = a.sc.n0[j];
     h.n1 = a.sc.n1[j];
+    h.fl = a.sc.fl != nullptr ? a.sc.fl[j] : 0u;
+    h.lfl = a.sc.lfl != nullptr ? a.sc.lfl[j] : 0u;
     h.v0 = a.sc.v0[j];
     h.v1 = a.sc.v1[j];
     h.tot = a.sc.tot[j];
@@ -265,9 +280,9 @@ __global__ __launch_bounds__(kSumFinalThreads) void k_sum_final(SumArgs a) {
     const uint32_t np = a.nparts;            // <= kSumFinalThreads (launch checks)
     const bool mine = (uint32_t)t < np;
     const bool locate = a.target != ~0ull;
-    SumPart sp{0, 0, -1, 0, 0, 0, -1.0};
+    SumPart sp{0, 0, -1, 0, 0, 0, -1.0, 0, 0};
     if (mine) sp = a.parts[t];
-    if (locate) { sp.ncand = 0; sp.over = 0; sp.maxv = -1.0; }   // chain fields: not this launch's
+    if (locate) { sp.ncand = 0; sp.over = 0; sp.maxv = -1.0; sp.nflag = 0; }   // chain fields: not this launch's
     s_coff[t] = sp.contrib;
     s_loff[t] = sp.live;
     s_mx[t] = sp.maxv;
@@ -286,12 +301,13 @@ __global__ __launch_bounds__(kSumFinalThreads) void k_sum_final(SumArgs a) {
     const uint32_t coff = s_coff[t] - sp.contrib;             // exclusive prefixes
     const double mprev = t == 0 ? -1.0 : s_mx[t - 1];
     const double mb = a.bar < mprev ? mprev : a.bar;         // the maximum before part t
-    // this part's members that beat it (a suffix of its increasing chain);
-    // a truncated chain whose part maximum beats it has lost members
+    // this part's members that beat it (flagged ones always); a truncated
+    // chain whose part maximum beats it, or that holds flagged members, may
+    // have lost members
     uint32_t g = 0;
     if (mine) {
         for (uint32_t i = 0; i < sp.ncand; ++i) g += a.pcand[(size_t)t * kPartCap + i].val > mb ? 1u : 0u;
-        if (sp.over && sp.maxv > mb) atomicMin(&s_fail, (uint32_t)t);
+        if (sp.over && (sp.maxv > mb || sp.nflag > 0)) atomicMin(&s_fail, (uint32_t)t);
         if (sp.live > 0) atomicMax(&s_lastpart, t);
     }
     if (locate && mine && (uint64_t)coff < a.target && (uint64_t)coff + sp.contrib >= a.target)
@@ -319,7 +335,7 @@ __global__ __launch_bounds__(kSumFinalThreads) void k_sum_final(SumArgs a) {
                 fill_hyp<M>(a, pc.pos, pc.it_before, pc.hyps_before, out->cand[r]);
                 if (r + 1 == min(total, a.cap)) {                        // the last member emitted
                     out->resume_pos = pc.pos + 1;
-                    out->resume_bar = pc.val;
+                    out->resume_bar = mb < pc.rb ? pc.rb : mb;
                 }
                 ++r;
             }
@@ -484,16 +500,22 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
         }
         if (!locate) {
             double val = -1.0;
+            bool flagged = false;
             if (l && p >= a.from_pos) {
                 const uint32_t j = a.hmap != nullptr ? hb : p;
                 val = finish_at(a.sc, j, K, a.m0, a.m1, a.Tm0, a.Tm1);
                 if constexpr (std::is_same<M, RectModel>::value)
-                    if (a.solver == 2 && !valid_model_sift22(models[p])) val = -1.0;
+                    if (a.solver == 2 && !valid_model_sift22(models[p])) val = -2.0;
+                // flagged decisions (exact.h): always a member, never the maximum
+                if (val > -2.0 && a.sc.fl != nullptr && a.sc.fl[j] != 0) {
+                    flagged = true;
+                    val = -1.0;
+                }
             }
             const double im = wave_incl_max(val, lane);
             const double before = prev_lane_f64(run, im);
             const double bar = lane == 0 ? run : (run < before ? before : run);
-            const bool cand = val >= 0.0 && val > bar;
+            const bool cand = (val >= 0.0 && val > bar) || flagged;
             const uint64_t bc = __ballot(cand);
             if (cand) {
                 const uint32_t r = nc + (uint32_t)__builtin_popcountll(bc & ((1ull << lane) - 1ull));
@@ -503,7 +525,7 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
                     fill_hyp<M>(a, p, excl - own, hb, out->cand[r]);
                     if (r + 1 == a.cap) {                      // the last member a full summary holds
                         out->resume_pos = p + 1;
-                        out->resume_bar = val;
+                        out->resume_bar = flagged ? bar : val;
                     }
                 }
             }
@@ -593,6 +615,7 @@ hipError_t launch_block_summary(int solver, const uint8_t* inc, const void* mode
     a.out = out;
     if (a.npos == 0 || a.nparts > (uint32_t)kSumFinalThreads) return hipErrorInvalidValue;
     const bool rect = solver <= 2;
+    if (!rect) a.sc.fl = a.sc.lfl = nullptr;   // the correspondence scorers flag nothing (no libm in their residuals)
     // GCR_SUMMARY_ONE=0: one-part summaries through the three launches too
     // (read per launch: tests switch it)
     const char* e1 = getenv("GCR_SUMMARY_ONE");

@@ -68,6 +68,10 @@ class Stats(C.Structure):
         ("ms_lo_score", C.c_double),
         ("ms_refit_fit", C.c_double),
         ("prefetched_chunks", C.c_uint64),
+        ("exact_models", C.c_uint64),
+        ("exact_pairs", C.c_uint64),
+        ("exact_flips", C.c_uint64),
+        ("ms_exact", C.c_double),
     ]
 
     def as_dict(self):

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GCR_ABI_VERSION 2
+#define GCR_ABI_VERSION 3
 
 /* error codes */
 #define GCR_OK 0
@@ -107,6 +107,13 @@ typedef struct gcr_stats {
                                      buffer reconciliation, rescoring and lists      */
     uint64_t prefetched_chunks;   /* chunks generated + scored on the side stream
                                      while the host replayed the previous one        */
+    /* decisions in the reference's arithmetic (glibc; csrc/exact.h): the kernels
+     * flag every decision whose detmath residual lies within the proven
+     * twin-glibc bound of its threshold, and the host takes it with glibc */
+    uint64_t exact_models;        /* models rescored / relabelled on the host       */
+    uint64_t exact_pairs;         /* (feature, model) decisions taken with glibc    */
+    uint64_t exact_flips;         /* ... that differ from the detmath decision      */
+    double ms_exact;              /* host time of those recounts                    */
 } gcr_stats;
 
 /* ---- context ---------------------------------------------------------- */

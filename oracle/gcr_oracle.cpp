@@ -20,9 +20,20 @@
 //
 // Math modes:
 //   GLIBC (0): std::log / std::pow(t,-3.0) / std::atan2, exactly the reference.
-//   TWIN  (1): those three hypothesis-dependent functions come from the
-//              product's detmath.h so GPU results can be compared bitwise;
-//              tests cross-check TWIN against GLIBC.
+//   TWIN  (1): the product's arithmetic, restated so GPU results can be
+//              compared bitwise.  Every DECISION and every MODEL is the
+//              reference's (glibc): inlier tests r^2 <= T and the labeling
+//              rule, LO / refit / final lists, the minimal solver's phi, the
+//              fits' rectified angles.  The MSAC running sums add the
+//              residuals of the product's detmath.h twins instead (the GPU
+//              evaluates the twins and rechecks on the host every decision
+//              whose twin residual lies within the proven twin-glibc bound of
+//              the threshold: csrc/exact.h); a minimal 2-SIFT model's sums use
+//              its twin phi (phi_val, the value the generator kernel holds).
+//              Masks, counts and models therefore equal GLIBC mode; the score
+//              values differ from GLIBC's in the last bits only.
+//   PURE_TWIN (2): the round-3 definition, detmath for the three functions
+//              everywhere (decisions included); kept to show what TWIN fixes.
 // =============================================================================
 #include <algorithm>
 #include <array>
@@ -44,14 +55,25 @@
 namespace oracle {
 
 // ----------------------------------------------------------------- math ----
-enum MathMode { MATH_GLIBC = 0, MATH_TWIN = 1 };
+enum MathMode { MATH_GLIBC = 0, MATH_TWIN = 1, MATH_PURE_TWIN = 2 };
 static thread_local int g_math = MATH_GLIBC;
-
-static inline double m_log(double x) { return g_math == MATH_TWIN ? gcr::dm::dm_log(x) : std::log(x); }
-static inline double m_pow_m3(double t) { return g_math == MATH_TWIN ? gcr::dm::dm_pow_m3(t) : std::pow(t, -3.0); }
-static inline double m_atan2(double y, double x) {
-    return g_math == MATH_TWIN ? gcr::dm::dm_atan2(y, x) : std::atan2(y, x);
+// which implementation m_log / m_pow_m3 / m_atan2 call right now: 0 glibc,
+// 1 the detmath twins (TWIN mode switches to 1 only for the MSAC sums' values
+// and the minimal model's value phi)
+static thread_local int g_fn = 0;
+static inline void set_mode(int mode) {
+    g_math = mode;
+    g_fn = mode == MATH_PURE_TWIN ? 1 : 0;
 }
+struct FnScope {                       // the twins for one evaluation (TWIN mode's values)
+    int saved;
+    explicit FnScope(int fn) : saved(g_fn) { g_fn = fn; }
+    ~FnScope() { g_fn = saved; }
+};
+
+static inline double m_log(double x) { return g_fn ? gcr::dm::dm_log(x) : std::log(x); }
+static inline double m_pow_m3(double t) { return g_fn ? gcr::dm::dm_pow_m3(t) : std::pow(t, -3.0); }
+static inline double m_atan2(double y, double x) { return g_fn ? gcr::dm::dm_atan2(y, x) : std::atan2(y, x); }
 
 // ------------------------------------------------------ math_utils.hpp ----
 // (HDR/math_utils.hpp:45-321)
@@ -176,6 +198,15 @@ struct Model {
     double h7 = 0.0, h8 = 0.0;            // RectifyingHomography
     double alpha = 1.0;                    // ScaleBased
     double phi = 0.0;                      // OrientationBased
+    // TWIN mode: the phi a minimal 2-SIFT model's MSAC sums are evaluated with
+    // (the twin atan2 of its vanishing point, what the generator kernel
+    // stores); NaN: phi itself
+    double phi_val = std::numeric_limits<double>::quiet_NaN();
+    Model value_model() const {
+        Model v = *this;
+        if (!std::isnan(phi_val)) v.phi = phi_val;
+        return v;
+    }
 
     void normalize(double& x, double& y, double w) const { x = s * (x - x0 * w); y = s * (y - y0 * w); }
     void normalizeScale(double& sc) const { sc *= s; }
@@ -707,6 +738,10 @@ struct Solver {
         m.rectifyPoint3(vp);
         if (std::abs(vp[2]) > 1e-9) return false;
         m.phi = clipAngle(m_atan2(vp[1], vp[0]));
+        if (g_math == MATH_TWIN) {
+            FnScope tw(1);
+            m.phi_val = clipAngle(m_atan2(vp[1], vp[0]));
+        }
         models.push_back(m);
         return true;
     }
@@ -1344,6 +1379,10 @@ struct FSolver {
 };
 
 // --------------------------------------------------------------- MSAC ----
+static inline Model value_of(const Model& m) { return m.value_model(); }
+template <class M>
+static inline const M& value_of(const M& m) { return m; }
+
 template <class S>
 static Score<S::K> getScore(const S& solver, const Data<S::K>& data, const typename S::ModelT& m,
                             const double thr[S::K], Inliers<S::K>& inliers) {
@@ -1352,14 +1391,22 @@ static Score<S::K> getScore(const S& solver, const Data<S::K>& data, const typen
     double T[K];
     for (size_t c = 0; c < K; ++c) T[c] = (2.25 * thr[c]) * thr[c];
     for (auto& s : inliers) s.clear();
+    // TWIN mode: the decision by the glibc residual, the sum of the twin one
+    const bool twin_values = g_math == MATH_TWIN;
+    const typename S::ModelT mv = value_of(m);
     for (size_t c = 0; c < K; ++c) {
         const Features& f = *data[c];
         for (size_t i = 0; i < f.n; ++i) {
             const double r2 = solver.squaredResidual(c, f, i, m);
             if (r2 <= T[c]) {
+                double v2 = r2;
+                if (twin_values) {
+                    FnScope tw(1);
+                    v2 = solver.squaredResidual(c, f, i, mv);
+                }
                 inliers[c].emplace_back(i);
                 score.inc_n(c);
-                score.inc_v(c, -r2);
+                score.inc_v(c, -v2);
             }
         }
     }
@@ -2063,7 +2110,7 @@ static Model read_model(const double* m7) {
 template <int KIND>
 static int run_generic(const Data<Solver<KIND>::K>& data, const oracle_params* p, uint8_t** masks, double* H9,
                        double* model7, oracle_stats* st) {
-    g_math = p->math_mode;
+    set_mode(p->math_mode);
     GCRANSAC<Solver<KIND>> g;
     g.settings.threshold[0] = p->thr0;
     g.settings.threshold[1] = p->thr1;
@@ -2124,7 +2171,7 @@ int oracle_rect_sift(const double* sfeat, size_t ns, const double* ofeat, size_t
 // homography: correspondences N x 4, threshold in px
 int oracle_find_homography(const double* corr, size_t n, const oracle_params* p, uint8_t* mask, double* H9,
                            oracle_stats* st) {
-    g_math = p->math_mode;
+    set_mode(p->math_mode);
     Features f = make_features(corr, n, 4);
     GCRANSAC<HSolver> g;
     g.settings.threshold[0] = p->thr0;
@@ -2165,7 +2212,7 @@ int oracle_find_homography(const double* corr, size_t n, const oracle_params* p,
 // homography hooks: one slot (model9), score / residuals of a model9, fit
 int oracle_find_fundamental(const double* corr, size_t n, const oracle_params* p, uint8_t* mask, double* H9,
                            oracle_stats* st) {
-    g_math = p->math_mode;
+    set_mode(p->math_mode);
     Features f = make_features(corr, n, 4);
     GCRANSAC<FSolver> g;
     g.settings.threshold[0] = p->thr0;
@@ -2312,7 +2359,7 @@ int oracle_f_fit(const double* corr, size_t n, const uint64_t* idx, size_t k, do
 // every attempt failed), writes the model when valid.
 int oracle_slot(int kind, const double* f0, size_t n0, const double* f1, size_t n1, uint64_t seed, uint64_t slot,
                 int math_mode, double* model7) {
-    g_math = math_mode;
+    set_mode(math_mode);
     Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
     auto go = [&](auto solver, auto data) -> int {
         constexpr size_t K = decltype(solver)::K;
@@ -2329,7 +2376,8 @@ int oracle_slot(int kind, const double* f0, size_t n0, const double* f1, size_t 
             if (!solver.isValidSample(data, smp)) continue;
             if (solver.estimateModel(data, smp, models)) break;
         }
-        if (!models.empty()) fill_model(models[0], model7);
+        // TWIN mode: the value model (twin phi), what the generator kernel stores
+        if (!models.empty()) fill_model(models[0].value_model(), model7);
         return (int)umg;   // == inc
     };
     if (kind == 0) return go(Solver<0>{}, Data<1>{&a});
@@ -2341,7 +2389,7 @@ int oracle_slot(int kind, const double* f0, size_t n0, const double* f1, size_t 
 int oracle_score(int kind, const double* f0, size_t n0, const double* f1, size_t n1, const double* model7,
                  double thr0, double thr1, int math_mode, uint64_t* counts, double* values, double* value,
                  uint8_t* mask0, uint8_t* mask1) {
-    g_math = math_mode;
+    set_mode(math_mode);
     Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
     Model m = read_model(model7);
     const double thr[2] = {thr0, thr1};
@@ -2363,7 +2411,8 @@ int oracle_score(int kind, const double* f0, size_t n0, const double* f1, size_t
 
 // per-feature squared residuals of one model
 int oracle_residuals(int kind, int cls, const double* f, size_t n, const double* model7, int math_mode, double* r2) {
-    g_math = math_mode;
+    set_mode(math_mode);
+    if (math_mode == MATH_TWIN) g_fn = 1;          // the values the product's kernels compute
     Features a = make_features(f, n);
     Model m = read_model(model7);
     for (size_t i = 0; i < n; ++i) {
@@ -2390,7 +2439,7 @@ void oracle_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
 // non-minimal fit over explicit index lists (LO / final refit path)
 int oracle_fit_nonminimal(int kind, const double* f0, size_t n0, const double* f1, size_t n1, const uint64_t* i0,
                           size_t k0, const uint64_t* i1, size_t k1, int math_mode, double* model7) {
-    g_math = math_mode;
+    set_mode(math_mode);
     Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
     auto go = [&](auto solver, auto data) -> int {
         constexpr size_t K = decltype(solver)::K;
@@ -2415,7 +2464,7 @@ int oracle_fit_nonminimal(int kind, const double* f0, size_t n0, const double* f
 int64_t oracle_hot_batch(int kind, const double* f0, size_t n0, const double* f1, size_t n1, double thr0, double thr1,
                          uint64_t seed, uint64_t slot0, uint64_t nslots, int sampler, int math_mode, double* seconds,
                          double* best_value) {
-    g_math = math_mode;
+    set_mode(math_mode);
     // kind 3 (homography): f0 is N x 4 correspondences
     Features a = make_features(f0, n0, kind >= 3 ? 4 : 3), b = f1 ? make_features(f1, n1) : Features{};
     const double thr[2] = {thr0, thr1};
@@ -2489,7 +2538,7 @@ int oracle_point_in_polygon(double px, double py, const double* xy, size_t n) {
 }
 // model methods: op 0 rectifiedScale, 1 unrectifiedScale, 2 rectifiedAngle, 3 unrectifiedAngle
 double oracle_model_op(const double* model7, int op, double x, double y, double v, int math_mode) {
-    g_math = math_mode;
+    set_mode(math_mode);
     Model m = read_model(model7);
     switch (op) {
         case 0: return m.rectifiedScale(x, y, v);

@@ -142,3 +142,49 @@ class CorrProblem:
         m = np.ascontiguousarray(model, dtype=np.float64)
         N.check(N.lib.gcr_debug_mask_h(self.h, C.byref(p), dp(m), rule, out.ctypes.data_as(u8p)))
         return out.astype(bool)
+
+
+# ---------------------------------------------------------------------------
+# Thresholds at the boundary between the reference's arithmetic (glibc) and
+# the detmath twins: for a pair whose glibc and twin squared residuals differ,
+# a threshold whose MSAC T = (2.25 thr) thr lies between them makes the two
+# arithmetics decide that pair differently (csrc/exact.h; VERDICT round 3,
+# "What's weak" 1).
+def msac_T(thr):
+    return (2.25 * thr) * thr
+
+
+def thr_between(a, b):
+    """A threshold whose MSAC T lies in [min(a, b), max(a, b)), or None."""
+    lo, hi = min(a, b), max(a, b)
+    if not (lo < hi):
+        return None
+    t = float(np.sqrt(lo / 2.25))
+    for _ in range(400):
+        T = msac_T(t)
+        if lo <= T < hi:
+            return t
+        t = float(np.nextafter(t, np.inf if T < lo else -np.inf))
+    return None
+
+
+def boundary_thresholds(O, kind, f0, f1, thr0, thr1, model, per_class=4, window=0.3):
+    """(cls, feature, thr0, thr1) cases: for up to `per_class` features of each
+    class whose glibc and twin r^2 under `model` differ and lie within
+    `window` T of the class threshold, the thresholds with that class's moved
+    between the two residuals."""
+    out = []
+    classes = [(0, f0)] + ([(1, f1)] if kind == N.SOLVER_SIFT22 else [])
+    for cls, f in classes:
+        g = O.residuals(kind, cls, f, model, math_mode=O.MATH_GLIBC)
+        t = O.residuals(kind, cls, f, model, math_mode=O.MATH_TWIN)
+        T = msac_T(thr0 if cls == 0 else thr1)
+        idx = np.where((g != t) & np.isfinite(g) & (np.abs(g - T) < window * T))[0]
+        for i in idx[:per_class]:
+            x = thr_between(g[i], t[i])
+            if x is None:
+                continue
+            th = [thr0, thr1]
+            th[cls] = x
+            out.append((cls, int(i), th[0], th[1]))
+    return out

@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
 
-MATH_GLIBC, MATH_TWIN = 0, 1
+MATH_GLIBC, MATH_TWIN, MATH_PURE_TWIN = 0, 1, 2
 SAMPLER_PHILOX, SAMPLER_FAITHFUL = 0, 1
 KIND_SCALE3, KIND_SCALE3_ORIGINAL, KIND_SIFT22 = 0, 1, 2
 

@@ -1,6 +1,9 @@
 """Golden vectors (tests/golden/*.npz, made by tools/gen_golden.py): seeded
 synthetic problems at N = 50 / 500 / 2000 with the oracle's outputs in the
-reference's arithmetic (glibc) and in the GPU's (twin).
+reference's arithmetic (glibc) and in the GPU's (twin: glibc decisions and
+models, detmath values in the MSAC sums -- oracle/gcr_oracle.cpp's header).
+Every twin entry equals its glibc entry (regenerated in round 4 when twin mode
+took its decisions from glibc; only sift_n50's model moved, to the glibc one).
 
 CPU: the oracle still reproduces every fixture exactly (regression pin).
 GPU: the product reproduces the twin outputs bitwise (masks, H, model, run
@@ -87,6 +90,7 @@ def test_gpu_matches_golden(path):
         assert np.array_equal(a, b)
     for a, b in zip(got, _masks(d, "glibc", names, sizes)):
         assert np.array_equal(a, b)
+    assert [st[k] for k in STAT_KEYS] == d["glibc_stats"].tolist()
     exp_model = d["twin_model"]
     keys = MODEL_KEYS if _kind(path) == "sift" else MODEL_KEYS[:6]
     assert np.array_equal(np.array([getattr(model, k) for k in keys]), exp_model[:len(keys)])

@@ -6,7 +6,9 @@ The reference itself cannot be built here (Eigen/OpenCV absent) and holds no
 end-to-end fixtures, so the expected outputs are the oracle restatement's, in
 both math modes:
   glibc -- the reference's own libm for every call (its arithmetic);
-  twin  -- detmath for log / pow / atan2 (what the GPU reproduces bitwise).
+  twin  -- the product's arithmetic (what the GPU reproduces bitwise): every
+           decision and model as glibc, the MSAC sums over detmath residuals
+           (oracle/gcr_oracle.cpp, math modes).
 Each file holds the inputs, the parameters and, per mode, the masks, H, the
 model parameters and the run statistics.
 
