@@ -40,13 +40,14 @@ def _unrectified_angle(h7, h8, x, y, angle):
 
 
 def scale_features(n: int, outlier_ratio: float = 0.5, seed: int = DEFAULT_SEED,
-                   gt: GroundTruth = GroundTruth(), noise: float = 0.02):
+                   gt: GroundTruth = GroundTruth(), noise: float = 0.02, width: float = WIDTH,
+                   height: float = HEIGHT):
     """M1: n scale features (x, y, s); returns (features[n,3], inlier_mask)."""
     rng = np.random.default_rng(seed)
     n_out = int(round(n * outlier_ratio))
     n_in = n - n_out
-    x = rng.uniform(0.0, WIDTH, n)
-    y = rng.uniform(0.0, HEIGHT, n)
+    x = rng.uniform(0.0, width, n)
+    y = rng.uniform(0.0, height, n)
     t = 1.0 - gt.h7 * x[:n_in] - gt.h8 * y[:n_in]
     s_in = (t / gt.alpha) ** 3 * np.exp(rng.normal(0.0, noise, n_in))
     s_out = np.exp(rng.uniform(math.log(2.0), math.log(64.0), n_out))
@@ -59,13 +60,14 @@ def scale_features(n: int, outlier_ratio: float = 0.5, seed: int = DEFAULT_SEED,
 
 
 def orientation_features(n: int, outlier_ratio: float = 0.5, seed: int = DEFAULT_SEED + 1,
-                         gt: GroundTruth = GroundTruth(), noise_deg: float = 0.5):
+                         gt: GroundTruth = GroundTruth(), noise_deg: float = 0.5, width: float = WIDTH,
+                         height: float = HEIGHT):
     """M2 orientation part: n features (x, y, angle); returns (features, inlier_mask)."""
     rng = np.random.default_rng(seed)
     n_out = int(round(n * outlier_ratio))
     n_in = n - n_out
-    x = rng.uniform(0.0, WIDTH, n)
-    y = rng.uniform(0.0, HEIGHT, n)
+    x = rng.uniform(0.0, width, n)
+    y = rng.uniform(0.0, height, n)
     theta = np.empty(n)
     which = rng.integers(0, 2, n_in)
     noise = np.deg2rad(rng.normal(0.0, noise_deg, n_in))

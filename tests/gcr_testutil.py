@@ -188,3 +188,40 @@ def boundary_thresholds(O, kind, f0, f1, thr0, thr1, model, per_class=4, window=
             th[cls] = x
             out.append((cls, int(i), th[0], th[1]))
     return out
+
+
+def first_member_model(O, kind, f0, f1, thr0, thr1, seed, slots=64):
+    """The model of the first slot whose hypothesis is valid and scores > 0
+    (GLIBC mode, 2-SIFT: the glibc phi): every run with `seed` acts on it --
+    it is the first member of the first chunk's chain whatever the threshold
+    does to the counts of one pair -- so thresholds built from its residuals
+    put a decision of the run itself at the glibc/twin boundary."""
+    for s in range(slots):
+        inc, m = O.slot(kind, f0, f1, seed, s, math_mode=O.MATH_GLIBC)
+        if inc > 101:
+            continue
+        if kind == N.SOLVER_SIFT22 and not max(abs(m[3]), abs(m[4])) < 1e-3:
+            continue
+        sc = O.score(kind, f0, f1, m, thr0, thr1, math_mode=O.MATH_GLIBC)
+        if sc["value"] > 0:
+            return m
+    raise AssertionError("no positive valid hypothesis in the first slots")
+
+
+def best_minimal_model(O, kind, f0, f1, thr0, thr1, seed, budget):
+    """The best generated hypothesis of a fixed-budget run (min = max =
+    budget iterations, GLIBC mode; 2-SIFT: valid models only, the glibc phi):
+    with no LO trials (lo = 0) the final refit fits exactly its MSAC inlier
+    lists, so thresholds built from its residuals decide the refit's input."""
+    it = s = 0
+    best, bv = None, 0.0
+    while it < budget:
+        inc, m = O.slot(kind, f0, f1, seed, s, math_mode=O.MATH_GLIBC)
+        s += 1
+        it += inc
+        if inc > 101 or (kind == N.SOLVER_SIFT22 and not max(abs(m[3]), abs(m[4])) < 1e-3):
+            continue
+        v = O.score(kind, f0, f1, m, thr0, thr1, math_mode=O.MATH_GLIBC)["value"]
+        if bv < v:
+            bv, best = v, m
+    return best

@@ -28,13 +28,18 @@ import oracle_ffi as O
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLDEN = os.path.join(HERE, "golden")
 FROZEN = os.path.join(GOLDEN, "frozen")
-SMALL = sorted(p for p in glob.glob(os.path.join(FROZEN, "*.npz")) if not os.path.basename(p).startswith(("full_", "corr_")))
+SMALL = sorted(p for p in glob.glob(os.path.join(FROZEN, "*.npz"))
+               if not os.path.basename(p).startswith(("full_", "corr_", "refit_")))
 CORR = sorted(glob.glob(os.path.join(FROZEN, "corr_*.npz")))
 FULL_M2 = sorted(glob.glob(os.path.join(FROZEN, "full_m2_*.npz")))
 FULL_F = sorted(glob.glob(os.path.join(FROZEN, "full_f_*.npz")))
 MODEL_KEYS = ("x0", "y0", "s", "h7", "h8", "alpha", "phi")
 STAT_KEYS = ("iteration_number", "local_optimization_number", "graph_cut_number", "slots", "hypotheses")
 REL = 1e-6                       # north_star: models within 1e-6 relative
+# the golden-size fixtures (blocked order, product bitwise) sit within 6.8e-14
+# of the frozen order (sift_n500; measured over every fixture, round 4): held
+# to 1e-12, so a drift far below north_star's bound still shows
+REL_SMALL = 1e-12
 
 
 def _load(path):
@@ -54,16 +59,16 @@ def _kind(name):
     return "sift" if "sift" in name or "m2" in name else ("original" if "original" in name else "scale")
 
 
-def _within(model, ref):
+def _within(model, ref, rel=REL):
     model, ref = np.asarray(model, dtype=np.float64), np.asarray(ref, dtype=np.float64)
-    return bool(np.all(np.abs(model - ref) <= REL * np.maximum(np.abs(ref), 1e-12)))
+    return bool(np.all(np.abs(model - ref) <= rel * np.maximum(np.abs(ref), 1e-12)))
 
 
-def _matrix_within(M, ref):
+def _matrix_within(M, ref, rel=REL):
     """3 x 3 matrices (H normalised by H22, F by its own convention): entries
-    within 1e-6 of the largest entry's magnitude."""
+    within rel of the largest entry's magnitude."""
     M, ref = np.asarray(M, dtype=np.float64).ravel(), np.asarray(ref, dtype=np.float64).ravel()
-    return bool(np.max(np.abs(M - ref)) <= REL * np.max(np.abs(ref)))
+    return bool(np.max(np.abs(M - ref)) <= rel * np.max(np.abs(ref)))
 
 
 def _problem(d, name):
@@ -158,8 +163,8 @@ def test_blocked_order_fixtures_within_frozen_pin(path):
     for tag in ("glibc", "twin"):
         for nm, n in zip(names, sizes):
             assert np.array_equal(_unpack(g, f"{tag}_{nm}", n), _unpack(d, f"{tag}_{nm}", n))
-        assert _within(g[f"{tag}_model"], d[f"{tag}_model"])
-        assert _matrix_within(g[f"{tag}_H"], d[f"{tag}_H"])
+        assert _within(g[f"{tag}_model"], d[f"{tag}_model"], REL_SMALL)
+        assert _matrix_within(g[f"{tag}_H"], d[f"{tag}_H"], REL_SMALL)
 
 
 @pytest.mark.parametrize("path", CORR, ids=_ids(CORR))
@@ -168,7 +173,7 @@ def test_blocked_order_corr_fixtures_within_frozen_pin(path):
     g = _load(os.path.join(GOLDEN, str(d["source"])))
     n = g["correspondences"].shape[0]
     assert np.array_equal(_unpack(g, "mask", n), _unpack(d, "twin_mask", n))
-    assert _matrix_within(g["M"], d["twin_H"])
+    assert _matrix_within(g["M"], d["twin_H"], REL_SMALL)
 
 
 # ------------------------------------------------------------------- GPU ----
@@ -204,8 +209,9 @@ def test_gpu_within_frozen_pin(path):
             assert np.array_equal(m, _unpack(d, f"{tag}_{nm}", n)), (tag, nm)
     keys = MODEL_KEYS if kind == "sift" else MODEL_KEYS[:6]
     got = np.array([getattr(model, k) for k in keys])
-    assert _within(got, d["glibc_model"][:len(keys)])
-    assert _matrix_within(H, d["glibc_H"])
+    rel = REL if name.startswith("full_") else REL_SMALL    # full size: the Gram refit of 3.1 M rows
+    assert _within(got, d["glibc_model"][:len(keys)], rel)
+    assert _matrix_within(H, d["glibc_H"], rel)
 
 
 @pytest.mark.gpu
@@ -242,3 +248,68 @@ def test_gpu_full_size_fundamental_graph_cut_within_frozen_pin(path):
                                                min_iters=min_it, lo_number=lo, seed=seed, device=0)
     assert np.array_equal(mask, _unpack(d, "twin_mask", len(c)))
     assert _matrix_within(M, d["twin_H"])
+
+
+# ---------------------------------------------- ill-conditioned refits ----
+# tools/gen_frozen_refit.py: hybrid refits past the Gram threshold (>= 32768
+# rows) on ill-conditioned systems -- nearly parallel orientation lines
+# (vanishing points ~1e9 px out), 4k coordinates, two scale rows, and both --
+# in the frozen sequential Householder order.  The product's Gram refit (the
+# double-double normal equations, gram.h) must stay within north_star's 1e-6
+# and make the same rank decision (the same exactly-zero components).
+REFIT = sorted(glob.glob(os.path.join(FROZEN, "refit_*.npz")))
+
+
+def _refit_check(got, d):
+    exp = d["frozen_model"]
+    assert got is not None
+    assert np.array_equal(got == 0.0, exp == 0.0)               # rank decision
+    rel = np.abs(got - exp) / np.maximum(np.abs(exp), 1e-12)
+    assert np.all(rel <= REL), (rel, got, exp)
+    return float(np.max(rel))
+
+
+@pytest.mark.parametrize("path", REFIT, ids=_ids(REFIT))
+def test_host_gram_refit_within_frozen_pin_on_ill_conditioned_systems(path):
+    import ctypes as C
+
+    from pygcransac import _native as N
+
+    d = _load(path)
+    fs, fo = d["scale_features"], d["orientation_features"]
+    i0 = np.ascontiguousarray(d["i0"], dtype=np.uint32)
+    i1 = np.ascontiguousarray(d["i1"], dtype=np.uint32)
+    assert int(d["rows"]) >= 32768                              # the Gram path
+    m = N.RectModel()
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    u32 = C.POINTER(C.c_uint32)
+    rc = N.lib.gcr_host_fit_nonminimal(N.SOLVER_SIFT22, dp(fs), len(fs), dp(fo), len(fo), i0.ctypes.data_as(u32),
+                                       len(i0), i1.ctypes.data_as(u32), len(i1), C.byref(m))
+    assert rc == 1
+    got = np.array([m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi])
+    # measured worst 1.5e-11 (vp_far)
+    _refit_check(got, d)
+    # the oracle's own blocked-order restatement of the Gram solve, bitwise
+    exp = O.fit_nonminimal(O.KIND_SIFT22, fs, fo, d["i0"], d["i1"], math_mode=O.MATH_TWIN)
+    assert np.array_equal(got.view(np.uint64), exp.view(np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", REFIT, ids=_ids(REFIT))
+def test_gpu_gram_refit_within_frozen_pin_on_ill_conditioned_systems(path):
+    import ctypes as C
+
+    from gcr_testutil import Problem
+    from pygcransac import _native as N
+
+    d = _load(path)
+    fs, fo = d["scale_features"], d["orientation_features"]
+    i0 = np.ascontiguousarray(d["i0"], dtype=np.uint32)
+    i1 = np.ascontiguousarray(d["i1"], dtype=np.uint32)
+    prob = Problem(N.SOLVER_SIFT22, fs, fo)
+    u32 = C.POINTER(C.c_uint32)
+    m = N.RectModel()
+    rc = N.lib.gcr_debug_fit_nonminimal(prob.h, i0.ctypes.data_as(u32), len(i0), i1.ctypes.data_as(u32), len(i1),
+                                        1, C.byref(m))
+    assert rc == 1
+    _refit_check(np.array([m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi]), d)

@@ -13,13 +13,14 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
-from gcr_testutil import Problem, bits, boundary_thresholds, finish_score
+from gcr_testutil import Problem, best_minimal_model, bits, boundary_thresholds, finish_score, first_member_model
 from pygcransac import _native as N
 from pygcransac import synthetic as S
 
 pytestmark = pytest.mark.gpu
 
 KW = dict(min_it=0, max_it=100_000, lo=50, seed=7, confidence=0.99)
+KWB = dict(min_it=300, max_it=300, lo=0, seed=7, confidence=0.99)   # fixed budget, no LO trials
 STATS = ("iteration_number", "local_optimization_number", "graph_cut_number", "slots", "hypotheses")
 
 
@@ -31,19 +32,19 @@ def _problem(kind, seed):
     return f, None, thr, 0.0
 
 
-def _oracle(kind, f0, f1, t0, t1, mode):
+def _oracle(kind, f0, f1, t0, t1, mode, kw=KW):
     if kind == N.SOLVER_SIFT22:
-        r = O.rect_sift(f0, f1, t0, t1, math_mode=mode, **KW)
+        r = O.rect_sift(f0, f1, t0, t1, math_mode=mode, **kw)
         return r, [r["scale_mask"], r["orientation_mask"]]
-    r = O.rect_scale_only(f0, t0, original=kind == N.SOLVER_SCALE3_ORIGINAL, math_mode=mode, **KW)
+    r = O.rect_scale_only(f0, t0, original=kind == N.SOLVER_SCALE3_ORIGINAL, math_mode=mode, **kw)
     return r, [r["mask"]]
 
 
-def _gpu(kind, f0, f1, t0, t1):
+def _gpu(kind, f0, f1, t0, t1, kw=KW):
     import pygcransac
 
-    pos = (0.0, KW["min_it"], KW["max_it"], KW["lo"])
-    extra = dict(seed=KW["seed"], confidence=KW["confidence"], return_stats=True)
+    pos = (0.0, kw["min_it"], kw["max_it"], kw["lo"])
+    extra = dict(seed=kw["seed"], confidence=kw["confidence"], return_stats=True)
     if kind == N.SOLVER_SIFT22:
         H, sm, om, model, st = pygcransac.findRectifyingHomographySIFT(f0, f1, t0, t1, *pos, **extra)
         return H, [sm, om], model, st
@@ -55,8 +56,7 @@ def _gpu(kind, f0, f1, t0, t1):
 
 def _model7(model, kind):
     keys = ("x0", "y0", "s", "h7", "h8", "alpha", "phi")
-    v = [getattr(model, k) for k in keys]
-    return np.array(v if kind == N.SOLVER_SIFT22 else v[:6])
+    return np.array([getattr(model, k) for k in (keys if kind == N.SOLVER_SIFT22 else keys[:6])])
 
 
 @pytest.mark.parametrize("kind", [N.SOLVER_SCALE3, N.SOLVER_SCALE3_ORIGINAL, N.SOLVER_SIFT22])
@@ -89,20 +89,38 @@ def test_gpu_single_model_boundary_decisions(kind, monkeypatch):
 CASES = [(N.SOLVER_SCALE3, 5), (N.SOLVER_SCALE3_ORIGINAL, 6), (N.SOLVER_SIFT22, 5), (N.SOLVER_SIFT22, 9)]
 
 
+def _cases(kind, seed, anchor):
+    """Boundary thresholds and the call's parameters: from the glibc run's
+    final model ("final"), from the first chain member's generated model
+    ("member": a decision every run takes sits at the boundary), or from the
+    best generated hypothesis of a fixed-budget run without LO trials ("best":
+    its MSAC lists are the refit's input)."""
+    f0, f1, thr0, thr1 = _problem(kind, seed)
+    kw = KWB if anchor == "best" else KW
+    if anchor == "final":
+        r, _ = _oracle(kind, f0, f1, thr0, thr1, O.MATH_GLIBC)
+        m = O.model7(r["model"])
+    elif anchor == "member":
+        m = first_member_model(O, kind, f0, f1, thr0, thr1, KW["seed"])
+    else:
+        m = best_minimal_model(O, kind, f0, f1, thr0, thr1, KWB["seed"], KWB["max_it"])
+    return (f0, f1), kw, boundary_thresholds(O, kind, f0, f1, thr0, thr1, m, per_class=4, window=1.0)
+
+
+@pytest.mark.parametrize("anchor", ["final", "member", "best"])
 @pytest.mark.parametrize("kind,seed", CASES)
-def test_gpu_full_runs_at_boundary_thresholds(kind, seed, monkeypatch):
+def test_gpu_full_runs_at_boundary_thresholds(kind, seed, anchor, monkeypatch):
     """Whole pygcransac calls at the constructed thresholds: the reference's
     masks, statistics and model bits (GLIBC mode), and TWIN mode's score bits;
-    the per-slot replay agrees."""
-    f0, f1, thr0, thr1 = _problem(kind, seed)
-    r, _ = _oracle(kind, f0, f1, thr0, thr1, O.MATH_GLIBC)
-    cases = boundary_thresholds(O, kind, f0, f1, thr0, thr1, O.model7(r["model"]), per_class=5)
+    the per-slot replay agrees.  With a hypothesis of the run as anchor the
+    host has decided some pair with glibc."""
+    (f0, f1), kw, cases = _cases(kind, seed, anchor)
     assert cases
     pairs = 0
     for cls, i, t0, t1 in cases:
-        g, gm = _oracle(kind, f0, f1, t0, t1, O.MATH_GLIBC)
-        p, _ = _oracle(kind, f0, f1, t0, t1, O.MATH_TWIN)
-        H, masks, model, st = _gpu(kind, f0, f1, t0, t1)
+        g, gm = _oracle(kind, f0, f1, t0, t1, O.MATH_GLIBC, kw)
+        p, _ = _oracle(kind, f0, f1, t0, t1, O.MATH_TWIN, kw)
+        H, masks, model, st = _gpu(kind, f0, f1, t0, t1, kw)
         for a, b in zip(masks, gm):
             assert np.array_equal(a, b)
         assert [st[k] for k in STATS] == [g["stats"][k] for k in STATS]
@@ -110,34 +128,35 @@ def test_gpu_full_runs_at_boundary_thresholds(kind, seed, monkeypatch):
         assert bits(st["score"]) == bits(p["stats"]["score"])
         pairs += st["exact_pairs"]
         monkeypatch.setenv("GCR_REPLAY", "slots")
-        H2, masks2, model2, st2 = _gpu(kind, f0, f1, t0, t1)
+        H2, masks2, model2, st2 = _gpu(kind, f0, f1, t0, t1, kw)
         monkeypatch.delenv("GCR_REPLAY")
         for a, b in zip(masks2, gm):
             assert np.array_equal(a, b)
         assert np.array_equal(_model7(model2, kind), _model7(model, kind))
-    assert pairs > 0                     # some decisions were taken in glibc on the host
+        assert [st2[k] for k in STATS] == [st[k] for k in STATS]
+    if anchor != "final":
+        assert pairs > 0                 # some decisions were taken in glibc on the host
 
 
-def test_gpu_twin_decisions_differ_somewhere(monkeypatch):
-    """GCR_EXACT=0 keeps the twins' decisions: over the M2 boundary cases some
-    run then differs from the reference's, which the default path matches."""
-    differ = 0
-    flips = 0
-    for seed in (5, 9):
-        f0, f1, thr0, thr1 = _problem(N.SOLVER_SIFT22, seed)
-        r, _ = _oracle(N.SOLVER_SIFT22, f0, f1, thr0, thr1, O.MATH_GLIBC)
-        for cls, i, t0, t1 in boundary_thresholds(O, N.SOLVER_SIFT22, f0, f1, thr0, thr1, O.model7(r["model"]),
-                                                  per_class=5):
-            g, gm = _oracle(N.SOLVER_SIFT22, f0, f1, t0, t1, O.MATH_GLIBC)
-            _, _, _, st = _gpu(N.SOLVER_SIFT22, f0, f1, t0, t1)
-            flips += st["exact_flips"]
-            monkeypatch.setenv("GCR_EXACT", "0")
-            _, masks, model, _ = _gpu(N.SOLVER_SIFT22, f0, f1, t0, t1)
-            monkeypatch.delenv("GCR_EXACT")
-            same = all(np.array_equal(a, b) for a, b in zip(masks, gm)) and \
-                np.array_equal(_model7(model, N.SOLVER_SIFT22), O.model7(g["model"]))
-            differ += not same
-    assert differ >= 1 and flips >= 1
+@pytest.mark.parametrize("kind,seed", CASES)
+def test_gpu_twin_decisions_differ_at_best_boundaries(kind, seed, monkeypatch):
+    """GCR_EXACT=0 keeps the twins' decisions: at the best hypothesis's
+    boundary thresholds most runs then differ from the reference's (which the
+    default path matches, test above), and the default path flipped
+    decisions on the host."""
+    (f0, f1), kw, cases = _cases(kind, seed, "best")
+    differ = flips = 0
+    for cls, i, t0, t1 in cases:
+        g, gm = _oracle(kind, f0, f1, t0, t1, O.MATH_GLIBC, kw)
+        _, _, _, st = _gpu(kind, f0, f1, t0, t1, kw)
+        flips += st["exact_flips"]
+        monkeypatch.setenv("GCR_EXACT", "0")
+        _, masks, model, st0 = _gpu(kind, f0, f1, t0, t1, kw)
+        monkeypatch.delenv("GCR_EXACT")
+        same = all(np.array_equal(a, b) for a, b in zip(masks, gm)) and \
+            np.array_equal(_model7(model, kind), O.model7(g["model"])[:len(_model7(model, kind))])
+        differ += not same
+    assert flips >= 1 and 2 * differ >= len(cases)
 
 
 def test_gpu_models_outside_the_bound_decided_on_the_host():

@@ -87,10 +87,11 @@ def main(root, slots=None, traffic_json=None, stats_csv=None):
                    "source": os.path.normpath(root), "kernel_build_id": bid}
             if k in avg:
                 ent["rocprof_avg_ms"] = avg[k]
-            # VALU view (bench.py "valu"): instructions issued and active VALU
-            # quad-cycles per launch, when that pass was collected
-            for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"):
-                if c in vals[k]:
+            # VALU view (bench.py "valu", "roofline.valu_issue"): instructions
+            # issued per class, active VALU quad-cycles, waits -- every SQ_
+            # counter collected for this kernel (mean per launch)
+            for c in sorted(vals[k]):
+                if c.startswith("SQ_"):
                     ent[c] = sum(vals[k][c]) / len(vals[k][c])
             table[f"{k}@{slots}"] = ent
         with open(traffic_json, "w") as f:
