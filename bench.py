@@ -51,6 +51,31 @@ CLOCK_GHZ = 2.4                # MI355X peak engine clock (spec)
 # VALU issue ceiling: one wave64 VALU instruction per SIMD every 4 cycles (16
 # lanes per cycle; full-rate fp64 on CDNA4), in G wave-instructions/s
 VALU_ISSUE_PEAK = N_SIMD * CLOCK_GHZ / 4.0
+# Issue cost of one wave64 VALU instruction on its SIMD, in cycles, per
+# SQ_INSTS_VALU_* class (MI355X_MICROARCH.md constants table 'vector-instruction
+# ISSUE cost': f32 add / fma 4, f32 transcendentals 8; the rest measured by
+# tools/micro/valu_issue.hip, profiles/r4_valu_issue.log).  Instructions in no
+# class (moves, selects, compares, bit ops, DPP, readlane) cost OTHER.
+VALU_CLASS_COST = {
+    "SQ_INSTS_VALU_ADD_F32": 4.0, "SQ_INSTS_VALU_MUL_F32": 4.0, "SQ_INSTS_VALU_FMA_F32": 4.0,
+    "SQ_INSTS_VALU_TRANS_F32": 8.0,
+    "SQ_INSTS_VALU_ADD_F64": 4.0, "SQ_INSTS_VALU_MUL_F64": 4.0, "SQ_INSTS_VALU_FMA_F64": 4.0,
+    "SQ_INSTS_VALU_TRANS_F64": 16.0,
+    "SQ_INSTS_VALU_INT32": 4.0, "SQ_INSTS_VALU_INT64": 4.0, "SQ_INSTS_VALU_CVT": 4.0,
+}
+VALU_OTHER_COST = 4.0
+
+
+def weighted_issue_cycles(pmc):
+    """Issue cycles of one launch's VALU instructions on their SIMDs, summed
+    over the SIMDs: per-class counts x VALU_CLASS_COST (the rest at
+    VALU_OTHER_COST); None unless every class counter was collected."""
+    if not pmc or not pmc.get("SQ_INSTS_VALU") or any(k not in pmc for k in VALU_CLASS_COST):
+        return None
+    classed = sum(pmc[k] for k in VALU_CLASS_COST)
+    other = max(0.0, pmc["SQ_INSTS_VALU"] - classed)
+    cycles = sum(pmc[k] * c for k, c in VALU_CLASS_COST.items()) + other * VALU_OTHER_COST
+    return cycles, {k.replace("SQ_INSTS_VALU_", ""): pmc[k] for k in VALU_CLASS_COST}, other
 
 
 def score_kernel_name(kind, slots):
@@ -462,13 +487,23 @@ def main():
     # instruction per 4 cycles) during the live average launch
     valu_issue = None
     if pmc and pmc.get("SQ_INSTS_VALU") and avg_kernel_s > 0:
-        floor_s = pmc["SQ_INSTS_VALU"] * 4.0 / (N_SIMD * CLOCK_GHZ * 1e9)
-        valu_issue = {"insts_per_launch": pmc["SQ_INSTS_VALU"], "issue_floor_ms": floor_s * 1e3,
-                      "frac": floor_s / avg_kernel_s, "clock_ghz": CLOCK_GHZ,
+        floor4_s = pmc["SQ_INSTS_VALU"] * 4.0 / (N_SIMD * CLOCK_GHZ * 1e9)
+        valu_issue = {"insts_per_launch": pmc["SQ_INSTS_VALU"], "clock_ghz": CLOCK_GHZ,
+                      # every instruction at 4 cycles (round 3's figure)
+                      "uniform4_floor_ms": floor4_s * 1e3, "frac_uniform4": floor4_s / avg_kernel_s,
                       "wait_frac": (pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
                                     if pmc.get("SQ_WAVE_CYCLES") and pmc.get("SQ_WAIT_ANY") else None),
                       "rocprof_avg_ms": pmc.get("rocprof_avg_ms"),
                       "source": f"profiles/pmc_traffic.json ({pmc.get('source')}, kernel build {build_id})"}
+        w = weighted_issue_cycles(pmc)
+        if w is not None:
+            cycles, per_class, other = w
+            floor_s = cycles / (N_SIMD * CLOCK_GHZ * 1e9)
+            valu_issue.update({"per_class_insts": per_class, "other_insts": other,
+                               "class_cost_cycles": {k.replace("SQ_INSTS_VALU_", ""): c
+                                                     for k, c in VALU_CLASS_COST.items()},
+                               "other_cost_cycles": VALU_OTHER_COST,
+                               "weighted_floor_ms": floor_s * 1e3, "frac": floor_s / avg_kernel_s})
 
     # wall time to 0.99 confidence: full estimator call (incl. upload, LO, refit)
     latency = None
@@ -542,11 +577,14 @@ def main():
                 # the measured limiter: the features are L2-resident (traffic is
                 # <1 % of the algorithmic bytes), so the ceiling that bounds the
                 # dominant kernel is fp64 VALU issue, not HBM
-                "bound": "valu",
-                "achieved": (valu_issue["insts_per_launch"] / avg_kernel_s / 1e9) if valu_issue else None,
-                "peak": VALU_ISSUE_PEAK,
-                "unit": "G wave-instructions/s",
-                "frac": valu_issue["frac"] if valu_issue else None,
+                # null when no PMC pass of this kernel build exists
+                "bound": "valu" if valu_issue and "frac" in valu_issue else None,
+                # issue cycles (per-class weighted) / s, against 1024 SIMDs x 2.4 GHz
+                "achieved": (weighted_issue_cycles(pmc)[0] / avg_kernel_s / 1e9
+                             if valu_issue and "frac" in valu_issue else None),
+                "peak": N_SIMD * CLOCK_GHZ,
+                "unit": "G VALU issue cycles/s",
+                "frac": valu_issue.get("frac") if valu_issue else None,
                 "traffic": traffic_per_launch(pmc),
                 "valu_issue": valu_issue,
                 "kernel": kernel_name,
@@ -568,10 +606,13 @@ def main():
                              "the kernel's live average duration. NOT a roofline fraction: the features stay "
                              "L2/LDS-resident, so the ratio can exceed 1; real HBM bytes are `traffic`"),
                 },
-                "note": ("achieved/frac: SQ_INSTS_VALU of the dominant kernel (rocprofv3 --pmc pass of this "
-                         "same kernel build, profiles/pmc_traffic.json) / its live average duration, against "
-                         "the issue ceiling of 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction. null "
-                         "when no PMC pass exists for this kernel build; the rest of the time is latency "
+                "note": ("achieved/frac: the dominant kernel's VALU instructions per class "
+                         "(SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_{F32,F64}, INT32, INT64, CVT; rocprofv3 --pmc passes of "
+                         "this same kernel build, profiles/pmc_traffic.json) x their issue cycles on one SIMD "
+                         "(valu_issue.class_cost_cycles: the guide's constants table and "
+                         "tools/micro/valu_issue.hip) / its live average duration, against 1024 SIMDs x 2.4 GHz "
+                         "of issue cycles; valu_issue.frac_uniform4 prices every instruction at 4 cycles (round "
+                         "3). null when no PMC pass exists for this kernel build; the rest of the time is latency "
                          "(valu_issue.wait_frac)"),
             },
             "valu": valu,
@@ -605,12 +646,18 @@ def bench_strong(args, rank, world, dist, device, coll_dev, backend):
     f0, f1, thr0, thr1, solver, workload = workload_problem(args.workload, seed)
     budget = args.steps * args.slots
     coll = coll_dev if backend == "nccl" else None
+    # RCCL: the engine's own communicator (ncclAllGather of the device block
+    # summaries, no Python in the exchange); gloo: the callback exchange
+    # (GCR_COMM=0: the callback on RCCL too)
+    comm = None
+    if backend == "nccl" and os.environ.get("GCR_COMM", "1") != "0":
+        comm = D.Comm(dist, rank, world, device=device)
 
     def run(iters):
         prm = dict(scale_residual_thresh=thr0, orientation_residual_thresh=thr1, seed=seed,
                    min_iteration_number=iters, max_iteration_number=iters, batch_slots=args.slots)
         return D.run_problem_sharded(solver, f0, f1, prm, rank=rank, world=world, dist=dist, device=device,
-                                     coll_device=coll)
+                                     coll_device=coll, comm=comm)
 
     def barrier():
         N.check(N.lib.gcr_synchronize(N.context(device)))
@@ -648,8 +695,10 @@ def bench_strong(args, rank, world, dist, device, coll_dev, backend):
             "data": "synthetic (seeded generators, pygcransac/synthetic.py)",
             "config": {"workload": f"{workload}: one problem, fixed budget of {budget} outer iterations "
                                    f"({args.steps} chunks of {args.slots} slots), hypothesis-sharded",
-                       "parallelism": f"hypothesis-sharded x{world} (gcr_problem_run_sharded)",
-                       "collective_backend": backend if world > 1 else None,
+                       "parallelism": f"hypothesis-sharded x{world} "
+                                      f"({'gcr_problem_run_comm' if comm else 'gcr_problem_run_sharded'})",
+                       "collective_backend": (("rccl-engine" if comm else backend) if world > 1 else
+                                              ("rccl-engine" if comm else None)),
                        "iterations": st["iteration_number"], "hypotheses": st["hypotheses"],
                        "inliers": int(sum(int(m.sum()) for m in masks)),
                        "ms_breakdown": {k: st[k] for k in ("ms_setup", "ms_generate", "ms_score", "ms_replay",
@@ -658,6 +707,8 @@ def bench_strong(args, rank, world, dist, device, coll_dev, backend):
             "roofline": None,
             "cpu_baseline": None,
         }))
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -43,6 +43,8 @@
 #include <array>
 #include <condition_variable>
 
+#include <rccl/rccl.h>
+
 #include "gcr.h"
 #include "host_fit.h"
 #include "kernels.h"
@@ -301,6 +303,7 @@ struct Workspace {
     DevBuf<uint8_t> sum_scr[2];
     DevBuf<BlockSummary> dsum[2];
     PinBuf<BlockSummary> hsum[2];       // [0] this rank's, then the all-gathered ones
+    DevBuf<BlockSummary> dall[2];       // gcr_comm: the all-gathered summaries on the device
     DevBuf<double> cs_vals[2];
     DevBuf<uint64_t> cs_bits[2];
     PinBuf<uint64_t> h_cbits[2];        // small-scored chunks: every slot's LO list bits (ListBits)
@@ -343,6 +346,15 @@ struct gcr_ctx {
     // cost milliseconds)
     std::mutex ws_mu;
     std::vector<std::unique_ptr<Workspace>> ws_free;
+};
+
+// A communicator rank for the hypothesis-sharded run (RCCL, one process per
+// GPU): the block summaries are exchanged by ncclAllGather on the context's
+// side stream (RunnerT::exchange).
+struct gcr_comm {
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+    gcr_ctx* ctx = nullptr;
 };
 
 struct gcr_problem {
@@ -812,11 +824,15 @@ void exact_mask(const gcr_problem* P, int cls, const RectModel& md, int rule, do
                 bool all, ExactCount& ec) {
     const size_t N = P->hc[cls].n;
     if (!all) {
-        for (size_t i = 0; i < N; ++i) {
-            if (!(mk[i] & 2)) {
-                mk[i] &= 1;
-                continue;
-            }
+        // flags are rare: find them eight bytes at a time
+        size_t i0 = 0;
+        for (; i0 + 8 <= N; i0 += 8) {
+            uint64_t w;
+            std::memcpy(&w, mk + i0, 8);
+            if (w & 0x0202020202020202ull) break;
+        }
+        for (size_t i = i0; i < N; ++i) {
+            if (!(mk[i] & 2)) continue;
             const uint8_t d = mask_rule(host_r2<GlibcMath>(P, cls, i, md), rule, T, lambda) ? 1 : 0;
             ++ec.pairs;
             ec.flips += (mk[i] & 1) != d ? 1u : 0u;
@@ -1359,6 +1375,16 @@ public:
         std::memset(&st_, 0, sizeof(st_));
     }
 
+    // Shard every chunk over the communicator's ranks, the exchange by
+    // ncclAllGather on the device (summary replay only)
+    gcr_comm* comm_ = nullptr;
+    void set_comm(gcr_comm* c) {
+        rank_ = c->rank;
+        world_ = c->world;
+        comm_ = c;
+        compact_ = false;
+    }
+
     // Shard every fetched chunk over `world` ranks.
     void set_sharding(int rank, int world, gcr_allgather_fn fn, void* user) {
         rank_ = rank;
@@ -1542,6 +1568,10 @@ public:
         w->dsum[set].ensure(1);
         const uint32_t n = rank_nslots(c, rank_);
         if (n == 0) {                                     // an empty block (more ranks than slots)
+            if (comm_) {                                  // it still takes part in the exchange
+                HIPC(hipMemsetAsync(w->dsum[set].p, 0, sizeof(BlockSummary), s));
+                exchange(set, s);
+            }
             HIPC(hipEventRecord(w->sum_done[set], s));
             return;
         }
@@ -1585,13 +1615,29 @@ public:
             }
         }
         HIPC(hipEventRecord(w->sum_k1[set], s));
-        const bool zc = zerocopy_on();
+        const bool zc = zerocopy_on() && !comm_;          // the exchange reads the device summary
         HIPC(launch_summary(c, c.bar, 0, ~0ull, false, zc ? dev_view(w->hsum[set].p) : w->dsum[set].p, s));
-        if (!zc)
+        if (comm_)
+            exchange(set, s);
+        else if (!zc)
             HIPC(hipMemcpyAsync(w->hsum[set].p, w->dsum[set].p, sizeof(BlockSummary), hipMemcpyDeviceToHost, s));
         HIPC(hipEventRecord(w->sum_done[set], s));
         st_.launches += 5;
         st_.hypotheses_computed += np;
+    }
+
+    // gcr_comm: every rank's device summary of set `set` gathered into
+    // dall[set] by ncclAllGather on stream s (the same order of collectives
+    // on every rank: the replay is identical everywhere), then one copy of the
+    // world records into hsum[set][1 ..]
+    void exchange(int set, hipStream_t s) {
+        Workspace* w = P_->w;
+        w->dall[set].ensure((size_t)world_);
+        const ncclResult_t r = ncclAllGather(w->dsum[set].p, w->dall[set].p, sizeof(BlockSummary), ncclUint8,
+                                             comm_->comm, s);
+        if (r != ncclSuccess) throw std::runtime_error(std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        HIPC(hipMemcpyAsync(w->hsum[set].p + 1, w->dall[set].p, (size_t)world_ * sizeof(BlockSummary),
+                            hipMemcpyDeviceToHost, s));
     }
 
     // every rank's summary of its block (this rank's: `mine`, the others':
@@ -1620,10 +1666,14 @@ public:
         st_.ms_score += ms_since(t0);
         BlockSummary mine = empty_summary();
         if (rank_nslots(c, rank_) > 0) {
-            mine = w->hsum[c.set].p[0];
+            if (!comm_) mine = w->hsum[c.set].p[0];
             float kms = 0;
             HIPC(hipEventElapsedTime(&kms, w->sum_k0[c.set], w->sum_k1[c.set]));
             st_.ms_score_kernel += kms;
+        }
+        if (comm_) {                                      // gathered on the device behind the summary
+            for (int r = 0; r < world_; ++r) all[r] = w->hsum[c.set].p[1 + r];
+            return;
         }
         gather_summaries(mine, all);
     }
@@ -1634,6 +1684,28 @@ public:
     void resummarise(const Chunk& c, int owner, uint32_t from_pos, double bar, const uint64_t* target,
                      BlockSummary* all) {
         Workspace* w = P_->w;
+        if (comm_) {
+            // the summary (or an empty record) on the replay stream, the
+            // exchange on the side stream behind it: every collective of the
+            // communicator on one stream, in the same order on every rank
+            if (rank_nslots(c, rank_) > 0 && (target != nullptr || owner == rank_)) {
+                HIPC(launch_summary(c, bar, target ? 0u : from_pos, target ? target[rank_] : ~0ull, target != nullptr,
+                                    w->dsum[c.set].p, s_));
+                st_.launches += 2;
+            } else {
+                HIPC(hipMemsetAsync(w->dsum[c.set].p, 0, sizeof(BlockSummary), s_));
+            }
+            hipStream_t side = P_->ctx->side;
+            HIPC(hipEventRecord(P_->ctx->ev0, s_));
+            HIPC(hipStreamWaitEvent(side, P_->ctx->ev0, 0));
+            const auto t0 = Clock::now();
+            exchange(c.set, side);
+            HIPC(hipEventRecord(P_->ctx->ev1, side));
+            HIPC(hipEventSynchronize(P_->ctx->ev1));
+            st_.ms_score += ms_since(t0);
+            for (int r = 0; r < world_; ++r) all[r] = w->hsum[c.set].p[1 + r];
+            return;
+        }
         BlockSummary mine = empty_summary();
         if (rank_nslots(c, rank_) > 0 && (target != nullptr || owner == rank_)) {
             const bool zc = zerocopy_on();
@@ -1872,6 +1944,8 @@ public:
     int run(uint8_t* mask0, uint8_t* mask1, double* H, gcr_rect_model* model_out) {
         const auto t_all = Clock::now();
         await_spec(P_->w);                // either replay path reuses set 0 / 1's buffers
+        if (comm_ && !summary_replay_on())
+            throw std::runtime_error("GCR_REPLAY=slots exchanges per-hypothesis records: use the callback exchange");
         if (summary_replay_on()) replay_summaries();
         else replay_slots();
 
@@ -3067,6 +3141,61 @@ int gcr_problem_run_sharded(gcr_problem* prob, const gcr_params* params, int ran
         HIPC(hipSetDevice(prob->ctx->device));
         auto go = [&](auto&& r) {
             if (world > 1) r.set_sharding(rank, world, allgather, user);
+            const int total = r.run(mask0_out, mask1_out, H_out, model_out);
+            fill_stats(stats_out, r.stats());
+            return total;
+        };
+        if (prob->solver == GCR_SOLVER_FUNDAMENTAL7) return go(FundRunner(prob, *params));
+        if (prob->solver == GCR_SOLVER_HOMOGRAPHY4) return go(GeoRunner(prob, *params));
+        return go(Runner(prob, *params));
+    });
+}
+
+int gcr_comm_unique_id(uint8_t id_out[GCR_COMM_ID_BYTES]) {
+    if (!id_out) return set_err(GCR_EINVAL, "null id buffer");
+    static_assert(sizeof(ncclUniqueId) == GCR_COMM_ID_BYTES, "nccl unique id size");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return set_err(GCR_EHIP, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    std::memcpy(id_out, &id, sizeof(id));
+    return GCR_OK;
+}
+
+int gcr_comm_create(gcr_ctx* ctx, int rank, int world, const uint8_t id[GCR_COMM_ID_BYTES], gcr_comm** out) {
+    if (!ctx || !id || !out) return set_err(GCR_EINVAL, "null argument");
+    if (world < 1 || rank < 0 || rank >= world) return set_err(GCR_EINVAL, "bad rank/world");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(ctx->device));
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, sizeof(uid));
+        auto c = std::make_unique<gcr_comm>();
+        const ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
+        if (r != ncclSuccess) return set_err(GCR_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        c->rank = rank;
+        c->world = world;
+        c->ctx = ctx;
+        *out = c.release();
+        return GCR_OK;
+    });
+}
+
+void gcr_comm_destroy(gcr_comm* comm) {
+    if (!comm) return;
+    (void)hipSetDevice(comm->ctx->device);
+    if (comm->comm) (void)ncclCommDestroy(comm->comm);
+    delete comm;
+}
+
+int gcr_problem_run_comm(gcr_problem* prob, const gcr_params* params, gcr_comm* comm, uint8_t* mask0_out,
+                         uint8_t* mask1_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out) {
+    if (!prob || !comm) return set_err(GCR_EINVAL, "null problem or communicator");
+    if (comm->ctx != prob->ctx) return set_err(GCR_EINVAL, "communicator and problem on different contexts");
+    if (int e = check_params(params, prob->solver)) return e;
+    if (!mask0_out || !H_out || (prob->K == 2 && !mask1_out)) return set_err(GCR_EINVAL, "null output buffer");
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        auto go = [&](auto&& r) {
+            r.set_comm(comm);
             const int total = r.run(mask0_out, mask1_out, H_out, model_out);
             fill_stats(stats_out, r.stats());
             return total;

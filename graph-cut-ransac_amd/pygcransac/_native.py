@@ -138,6 +138,12 @@ def _load():
     L.gcr_problem_run.argtypes = [vp, C.POINTER(Params), u8p, u8p, dp, C.POINTER(RectModel), C.POINTER(Stats)]
     L.gcr_problem_run_sharded.argtypes = [vp, C.POINTER(Params), C.c_int, C.c_int, ALLGATHER_FN, vp, u8p, u8p, dp,
                                           C.POINTER(RectModel), C.POINTER(Stats)]
+    L.gcr_comm_unique_id.argtypes = [u8p]
+    L.gcr_comm_create.argtypes = [vp, C.c_int, C.c_int, u8p, C.POINTER(vp)]
+    L.gcr_comm_destroy.argtypes = [vp]
+    L.gcr_comm_destroy.restype = None
+    L.gcr_problem_run_comm.argtypes = [vp, C.POINTER(Params), vp, u8p, u8p, dp, C.POINTER(RectModel),
+                                       C.POINTER(Stats)]
     L.gcr_solve_batch.argtypes = [C.c_int, C.POINTER(BatchItem), C.c_size_t, C.c_int]
     L.gcr_problem_verify_batch.argtypes = [vp, C.POINTER(Params), C.c_uint64, C.c_uint32, C.POINTER(BatchResult),
                                            C.POINTER(Stats)]

@@ -199,14 +199,50 @@ def make_allgather(dist, world: int, device=None):
     return N.ALLGATHER_FN(fn)
 
 
+class Comm:
+    """An engine communicator rank (gcr_comm: RCCL over xGMI, one process per
+    GPU) for gcr_problem_run_comm: the block summaries are all-gathered on the
+    device by ncclAllGather, behind the summary kernel, with no Python in the
+    exchange.  Rank 0 draws the RCCL unique id; `dist` (torch.distributed,
+    any backend) broadcasts it once.  Collective: every rank constructs it."""
+
+    def __init__(self, dist, rank: int, world: int, device: Optional[int] = None):
+        import ctypes as C
+
+        from . import _native as N
+
+        self._N = N
+        ident = (C.c_uint8 * 128)()
+        if rank == 0:
+            N.check(N.lib.gcr_comm_unique_id(ident))
+        obj = [bytes(ident)]
+        if dist is not None and world > 1:
+            dist.broadcast_object_list(obj, src=0)
+        buf = (C.c_uint8 * 128).from_buffer_copy(obj[0])
+        h = C.c_void_p()
+        N.check(N.lib.gcr_comm_create(N.context(device), rank, world, buf, C.byref(h)))
+        self.h = h.value
+        self.rank, self.world = rank, world
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._N.lib.gcr_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
 def run_problem_sharded(solver: int, f0, f1=None, params: Optional[dict] = None, rank: int = 0, world: int = 1,
-                        dist=None, device: Optional[int] = None, coll_device=None):
+                        dist=None, device: Optional[int] = None, coll_device=None, comm: Optional[Comm] = None):
     """One estimator problem over `world` ranks.
 
     Every rank calls this with the same inputs; each verifies its block of
     every chunk of slots on its own GPU and the chunks are all-gathered, so
     every rank returns the single-rank result bit for bit.  `params` holds
-    gcr_params fields (scale_residual_thresh, confidence, seed, ...).
+    gcr_params fields (scale_residual_thresh, confidence, seed, ...).  With
+    `comm` (a Comm) the exchange runs inside the engine (ncclAllGather on the
+    device); otherwise through `dist` in a Python callback (gloo or RCCL).
     Returns (H (3, 3) or None, masks tuple, stats dict, rect model record)."""
     import ctypes as C
 
@@ -228,11 +264,16 @@ def run_problem_sharded(solver: int, f0, f1=None, params: Optional[dict] = None,
         H = np.zeros(9)
         model = N.RectModel()
         st = N.Stats()
-        cb = make_allgather(dist, world, coll_device) if world > 1 else N.ALLGATHER_FN(0)
         u8 = C.POINTER(C.c_uint8)
-        rc = N.lib.gcr_problem_run_sharded(h, C.byref(p), rank, world, cb, None, m0.ctypes.data_as(u8),
-                                           m1.ctypes.data_as(u8) if f1 is not None else None, dp(H), C.byref(model),
-                                           C.byref(st))
+        if comm is not None:
+            rc = N.lib.gcr_problem_run_comm(h, C.byref(p), comm.h, m0.ctypes.data_as(u8),
+                                            m1.ctypes.data_as(u8) if f1 is not None else None, dp(H),
+                                            C.byref(model), C.byref(st))
+        else:
+            cb = make_allgather(dist, world, coll_device) if world > 1 else N.ALLGATHER_FN(0)
+            rc = N.lib.gcr_problem_run_sharded(h, C.byref(p), rank, world, cb, None, m0.ctypes.data_as(u8),
+                                               m1.ctypes.data_as(u8) if f1 is not None else None, dp(H),
+                                               C.byref(model), C.byref(st))
         n = N.check(rc)
     finally:
         N.lib.gcr_problem_destroy(h)

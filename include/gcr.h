@@ -200,6 +200,21 @@ int gcr_problem_run_sharded(gcr_problem* prob, const gcr_params* params, int ran
                             gcr_allgather_fn allgather, void* user, uint8_t* mask0_out, uint8_t* mask1_out,
                             double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
 
+/* The same run with the exchange inside the engine: a communicator rank
+ * (RCCL over xGMI, one process per GPU) all-gathers the device-resident block
+ * summaries with ncclAllGather on the context's side stream, behind the
+ * summary kernel -- no host callback, no host staging of the send side, one
+ * copy of the gathered records into pinned memory.  gcr_comm_unique_id on one
+ * rank, the id handed to every rank (e.g. a torch.distributed broadcast),
+ * then gcr_comm_create on every rank (collective). */
+#define GCR_COMM_ID_BYTES 128
+typedef struct gcr_comm gcr_comm;
+int gcr_comm_unique_id(uint8_t id_out[GCR_COMM_ID_BYTES]);
+int gcr_comm_create(gcr_ctx* ctx, int rank, int world, const uint8_t id[GCR_COMM_ID_BYTES], gcr_comm** out);
+void gcr_comm_destroy(gcr_comm* comm);
+int gcr_problem_run_comm(gcr_problem* prob, const gcr_params* params, gcr_comm* comm, uint8_t* mask0_out,
+                         uint8_t* mask1_out, double* H_out, gcr_rect_model* model_out, gcr_stats* stats_out);
+
 /* One pass of the hot path over one batch: draw and solve `nslots`
  * outer-iteration slots starting at `slot0`, MSAC-score every resulting model
  * against all features on the GPU, and return the best-scoring slot (first

@@ -65,3 +65,59 @@ def test_rccl_world1_allgather_callback_and_bench_collectives():
     env = dict(os.environ, GCR_PKG=PKG, GCR_PORT=str(_free_port()), MASTER_ADDR="127.0.0.1")
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0 and "RCCL OK" in out.stdout, out.stdout[-2000:] + out.stderr[-3000:]
+
+
+# ---------------------------------------------------- engine communicator ----
+# gcr_comm (RCCL inside libgcr): the hypothesis-sharded run's block summaries
+# all-gathered by ncclAllGather on the device, behind the summary kernel (no
+# Python callback, no host staging of the send side).  One GPU: a world of 1
+# through that path, against the plain single-rank run, bit for bit -- with a
+# one-member summary cap every chunk overflows, so the device continuation and
+# the stop-slot locate go through the exchange too.
+def _sharded_vs_single(kind, budget, monkeypatch, env):
+    import numpy as np
+
+    from gcr_testutil import bits
+    from pygcransac import distributed as D
+    from pygcransac import synthetic as S
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if kind == N.SOLVER_SIFT22:
+        fs, fo, _, _, t0, t1 = S.problem_m2(1500, 1300, seed=61)
+        f0, f1 = fs, fo
+    elif kind == N.SOLVER_FUNDAMENTAL7:
+        f0, _, _, t0 = S.problem_f(2500, 0.6, seed=63)
+        f1, t1 = None, 0.0
+    else:
+        f0, _, t0 = S.problem_m1(2500, seed=64)
+        f1, t1 = None, 0.0
+    params = dict(scale_residual_thresh=t0, orientation_residual_thresh=t1, seed=11)
+    if budget == "fixed":
+        params.update(min_iteration_number=300_000, max_iteration_number=300_000)
+    else:
+        params.update(min_iteration_number=0, max_iteration_number=10**7, confidence=0.99)
+    ref = D.run_problem_sharded(kind, f0, f1, params, 0, 1, device=0)
+    comm = D.Comm(None, 0, 1, device=0)
+    try:
+        got = D.run_problem_sharded(kind, f0, f1, params, 0, 1, device=0, comm=comm)
+    finally:
+        comm.close()
+    for k in env:
+        monkeypatch.delenv(k)
+    (Hr, mr, sr, rr), (Hg, mg, sg, rg) = ref, got
+    assert all(np.array_equal(a, b) for a, b in zip(mr, mg))
+    assert (Hr is None and Hg is None) or np.array_equal(bits(Hr), bits(Hg))
+    for k in ("iteration_number", "hypotheses", "slots", "local_optimization_number", "graph_cut_number"):
+        assert sr[k] == sg[k], k
+    assert bits(sr["score"]) == bits(sg["score"])
+    assert np.array_equal(bits(np.array(rr)), bits(np.array(rg)))
+
+
+@pytest.mark.parametrize("kind", [N.SOLVER_SCALE3, N.SOLVER_SIFT22, N.SOLVER_FUNDAMENTAL7])
+@pytest.mark.parametrize("budget", ["fixed", "adaptive"])
+def test_engine_comm_world1_equals_single_rank(kind, budget, monkeypatch):
+    if N.lib.gcr_device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    _sharded_vs_single(kind, budget, monkeypatch, {})
+    _sharded_vs_single(kind, budget, monkeypatch, {"GCR_SUMMARY_CAP": "1"})
