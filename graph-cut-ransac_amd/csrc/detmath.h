@@ -4,25 +4,35 @@
 // inside every residual (solver_rectifying_homography_three_sift.hpp:293-317,
 // ..._two_sift.hpp:621-665, model.h:156-165, 194-204).  gfx950 has no fp64
 // transcendental instructions and ocml's expansions are not glibc's, so the GPU
-// engine evaluates these three functions with the code below, compiled
+// engine evaluates its residual VALUES with the code below, compiled
 // identically for the host (engine, LO/refit) and for gfx950 (kernels).  All
 // other arithmetic is IEEE +,-,*,/,sqrt, which both sides round identically.
+// Decisions are the reference's own (glibc), see exact.h.
 //
-//   dm_log      fdlibm e_log.c reduction and minimax polynomial (< 1 ulp),
-//               FMA Horner form, the two fdlibm tail formulas selected
-//               without branches, special operands out of line.
-//   dm_pow_m3   t^-3 via a double-double t^3 and one Newton correction of the
-//               IEEE reciprocal (nearly correctly rounded).
+//   dm_log      table-driven (128 subintervals of [0.686, 1.371), logtab.h):
+//               log x = k ln2 + log c + log1p(z / c - 1), the quotient as one
+//               FMA against the tabulated 1 / c (no division), log1p by its
+//               degree-7 Taylor polynomial (|r| <= 2^-8); the subinterval
+//               around 1 has c = 1 (log 1 = 0, relative accuracy near 1);
+//               < 1.8 ulp (measured max 1.72 ulp on 6M points against long
+//               double, glibc 0.52).
+//   dm_log_fd   fdlibm e_log.c reduction and minimax polynomial (< 1 ulp),
+//               FMA Horner form (round 3's twin; the oracle's PURE_TWIN mode).
+//   dm_pow_m3   t^-3 as 1 / ((t t) t) (< 2 ulp).
 //   dm_atan2    fdlibm s_atan.c polynomial behind a branch-free two-step
 //               reduction (octant swap, then pi/4 shift) with a single IEEE
 //               division; special operands out of line (fdlibm e_atan2.c).
+//   dm_sincos   sin and cos of a model angle: Cody-Waite reduction by pi/2
+//               (fdlibm's 33-bit split) and fdlibm's k_sin / k_cos
+//               polynomials (< 1.5 ulp for |x| <= 16).
 //
-// The accuracy against glibc/mpmath is pinned by tests/test_detmath.py; the
-// oracle's "twin" mode uses these same three functions so GPU-vs-oracle
-// comparisons are bitwise, and its "glibc" mode is cross-checked against twin.
+// The accuracy against glibc is pinned by tests/test_exact.py and
+// tests/test_oracle_modes.py; the oracle's TWIN mode uses these same functions
+// so GPU-vs-oracle comparisons are bitwise.
 #pragma once
 
 #include "gcr_hd.h"
+#include "logtab.h"
 
 namespace gcr {
 namespace dm {
@@ -82,14 +92,65 @@ GCR_COLD GCR_HD double log_special(double x) {
 }
 
 // log(x): fdlibm e_log.c algorithm (< 1 ulp), polynomial in FMA Horner form.
-GCR_HD double dm_log(double x) {
+GCR_HD double dm_log_fd(double x) {
     if (!(x >= 0x1p-1022 && x < HUGE_VAL)) return log_special(x);
     return log_core(as_u64(x), 0);
 }
 
+// The table of dm_log: (1 / c_i, -log(1 / c_i)) pairs, the same doubles on
+// both sides (tools/gen_logtab.py).
+#if defined(__HIP_DEVICE_COMPILE__)
+static __constant__ double kLogTab[256] = {GCR_LOGTAB_ENTRIES};
+#else
+static const double kLogTab[256] = {GCR_LOGTAB_ENTRIES};
+#endif
+
+// k ln2 with ln2's high part ending in 11 zero bits: exact for |k| <= 1075
+constexpr double kLn2HiT = cf(0x3fe62e42fefa3800ull);
+constexpr double kLn2LoT = cf(0x3d2ef35793c76730ull);
+
+// table log of a normal, finite, positive x, x = 2^k z, z in [OFF, 2 OFF),
+// OFF = 0x1.5fp-1 (1.0 in the middle of subinterval 80)
+GCR_HD double log_tab_core(uint64_t ix, int32_t kadj) {
+    constexpr uint64_t kOff = 0x3fe5f00000000000ull;
+    const uint64_t tmp = ix - kOff;
+    const uint32_t i = (uint32_t)(tmp >> 45) & 127u;
+    const int32_t k = (int32_t)((int64_t)tmp >> 52) + kadj;
+    const double z = as_f64(ix - (tmp & 0xfff0000000000000ull));
+    const double invc = kLogTab[2 * i], logc = kLogTab[2 * i + 1];
+    const double r = fma_rn(z, invc, -1.0);                 // z / c - 1, one rounding
+    const double kd = (double)k;
+    const double w = fma_rn(kd, kLn2HiT, logc);              // k ln2hi exact
+    const double hi = w + r;
+    const double lo = fma_rn(kd, kLn2LoT, (w - hi) + r);
+    // log1p(r) - r = -r^2/2 + r^3/3 - r^4/4 + r^5/5 - r^6/6 + r^7/7 (+ O(r^8) < 1e-20)
+    constexpr double A1 = cf(0x3fd5555555555555ull), A2 = -0.25, A3 = cf(0x3fc999999999999aull),
+                     A4 = cf(0xbfc5555555555555ull), A5 = cf(0x3fc2492492492492ull);
+    const double r2 = r * r;
+    const double p = fma_rn(r2, fma_rn(r2, A5, fma_rn(r, A4, A3)), fma_rn(r, A2, A1));
+    return fma_rn(r * r2, p, fma_rn(r2, -0.5, lo)) + hi;
+}
+
+GCR_COLD GCR_HD double log_tab_special(double x) {
+    const uint64_t u = as_u64(x);
+    const int32_t hx = (int32_t)(u >> 32);
+    const uint32_t lx = (uint32_t)u;
+    if (((hx & 0x7fffffff) | (int32_t)lx) == 0) return -HUGE_VAL;   // log(+-0)
+    if (hx < 0) return __builtin_nan("");                           // log(<0), log(-inf)
+    if (hx >= 0x7ff00000) return x + x;                               // +inf, NaN
+    return log_tab_core(as_u64(x * cf(0x4350000000000000ull)), -54); // subnormal: x * 2^54
+}
+
+// log(x), table-driven, no division (the residuals' log)
+GCR_HD double dm_log(double x) {
+    if (!(x >= 0x1p-1022 && x < HUGE_VAL)) return log_tab_special(x);
+    return log_tab_core(as_u64(x), 0);
+}
+
 // --------------------------------------------------------------- t^-3 -----
 // t^-3 = 1 / ((t*t)*t): two roundings in the cube and one in the IEEE
-// division (< 2 ulp), valid while t^3 is normal.
+// division (< 2 ulp), valid while t^3 is normal (round 3's scale residual;
+// the oracle's PURE_TWIN mode).
 GCR_HD double pm3_core(double t) { return 1.0 / ((t * t) * t); }
 
 GCR_COLD GCR_HD double pm3_special(double t) {
@@ -136,6 +197,15 @@ constexpr double kPiF = cf(0x400921fb54442d18ull);
 constexpr double kPiLo = cf(0x3ca1a62633145c07ull);     // pi - kPiF
 constexpr double kPiO4Lo = cf(0x3c81a62633145c07ull);   // pi/4 - kPiO4
 constexpr double kPiO2Lo = cf(0x3c91a62633145c07ull);   // pi/2 - kPiO2
+constexpr double kTanPiO8 = cf(0x3fda827999fcef32ull);   // tan(pi/8)
+
+// atan(n / d) for 0 <= n <= d, d > 0: the same reduction as dm_atan2's first
+// octant (one division), without quadrant restoration
+GCR_HD double atan_ratio(double n, double d) {
+    const bool red = n > kTanPiO8 * d;
+    const double xr = (red ? n - d : n) / (red ? n + d : d);
+    return atan_poly(xr, red ? kPiO4 : 0.0, red ? kPiO4Lo : 0.0);
+}
 
 // IEEE special operands (NaN, zeros, infinities) as fdlibm e_atan2.c.
 GCR_COLD GCR_HD double atan2_special(double y, double x) {
@@ -174,7 +244,6 @@ GCR_COLD GCR_HD double atan2_special(double y, double x) {
 GCR_HD double dm_atan2(double y, double x) {
     const double ay = __builtin_fabs(y), ax = __builtin_fabs(x);
     if (!(ay > 0.0 && ay < HUGE_VAL && ax > 0.0 && ax < HUGE_VAL)) return atan2_special(y, x);
-    constexpr double kTanPiO8 = cf(0x3fda827999fcef32ull);
     const bool swap = ay > ax;
     const double n = swap ? ax : ay;
     const double d = swap ? ay : ax;
@@ -184,6 +253,43 @@ GCR_HD double dm_atan2(double y, double x) {
     if (swap) a = (kPiO2 - a) + kPiO2Lo;
     if (x > 0.0) return (y > 0.0) ? a : -a;
     return (y > 0.0) ? kPiF - (a - kPiLo) : (a - kPiLo) - kPiF;
+}
+
+// ------------------------------------------------------------ sin / cos ---
+// fdlibm k_sin.c / k_cos.c polynomials on |r| <= pi/4 (tail y = 0)
+GCR_HD double ksin(double x) {
+    constexpr double S1 = cf(0xbfc5555555555549ull), S2 = cf(0x3f8111111110f8a6ull), S3 = cf(0xbf2a01a019c161d5ull),
+                     S4 = cf(0x3ec71de357b1fe7dull), S5 = cf(0xbe5ae5e68a2b9cebull), S6 = cf(0x3de5d93a5acfd57cull);
+    const double z = x * x;
+    const double v = z * x;
+    const double r = fma_rn(z, fma_rn(z, fma_rn(z, fma_rn(z, S6, S5), S4), S3), S2);
+    return fma_rn(v, fma_rn(z, r, S1), x);
+}
+GCR_HD double kcos(double x) {
+    constexpr double C1 = cf(0x3fa555555555554cull), C2 = cf(0xbf56c16c16c15177ull), C3 = cf(0x3efa01a019cb1590ull),
+                     C4 = cf(0xbe927e4f809c52adull), C5 = cf(0x3e21ee9ebdb4b1c4ull), C6 = cf(0xbda8fae9be8838d4ull);
+    const double z = x * x;
+    const double r = z * fma_rn(z, fma_rn(z, fma_rn(z, fma_rn(z, fma_rn(z, C6, C5), C4), C3), C2), C1);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + z * r);
+}
+
+// sin and cos of x, |x| <= 16: x = n pi/2 + r with fdlibm's
+// 33 + 53-bit split of pi/2 (n pio2_1 exact for |n| < 2^20, the subtraction
+// exact by Sterbenz), quadrant n mod 4; < 1.5 ulp.  Larger |x| loses accuracy (callers
+// keep to the range); NaN / inf give NaN.
+GCR_HD void dm_sincos(double x, double& s, double& c) {
+    constexpr double kInvPiO2 = cf(0x3fe45f306dc9c883ull);
+    constexpr double kPio2_1 = cf(0x3ff921fb54400000ull);
+    constexpr double kPio2_1t = cf(0x3dd0b4611a626331ull);
+    const double n = __builtin_rint(x * kInvPiO2);
+    const double r = (x - n * kPio2_1) - n * kPio2_1t;
+    const double sr = ksin(r), cr = kcos(r);
+    const int q = (int)((n == n && __builtin_fabs(n) < 0x1p30) ? n : 0.0) & 3;   // NaN / huge: any quadrant
+    const double ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
 }
 
 // -------------------------------------------------------- angle clipping ---

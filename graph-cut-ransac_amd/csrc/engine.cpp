@@ -376,8 +376,8 @@ namespace {
 // host routines take those decisions (and every decision of a model the bound
 // does not cover, scale_unsafe) in the reference's arithmetic.
 
-// one pair's squared residual under model m with the twins (TwinMath: the
-// values the kernels fold) or glibc (GlibcMath: the reference's decision)
+// one pair's squared residual under model m in the reference's formula with
+// glibc (GlibcMath: the reference's decision)
 template <class M>
 double host_r2(const gcr_problem* P, int cls, size_t i, const RectModel& m) {
     const HostClass& h = P->hc[cls];
@@ -387,6 +387,16 @@ double host_r2(const gcr_problem* P, int cls, size_t i, const RectModel& m) {
                               : scale_sq_residual<false, false, M>(h.x[i], h.y[i], h.a[i], m, ac);
     }
     return orient_sq_residual<false, M>(h.x[i], h.y[i], h.c0[i], h.c1[i], m, orient_const(m));
+}
+
+// ... and its value (rect.h scale_sq_value / orient_sq_value: what the
+// kernels fold), vc = value_const of m
+double host_value(const gcr_problem* P, int cls, size_t i, const RectModel& m, const ValueConst& vc) {
+    const HostClass& h = P->hc[cls];
+    if (cls == 0)
+        return P->solver == 1 ? scale_sq_value<true, false>(h.x[i], h.y[i], h.a[i], m, vc.ac, vc.cut)
+                              : scale_sq_value<false, false>(h.x[i], h.y[i], h.a[i], m, vc.ac, vc.cut);
+    return orient_sq_value<false>(h.x[i], h.y[i], h.c0[i], h.c1[i], m, vc.c, vc.s, vc.cphi, vc.cphi2);
 }
 
 struct ExactCount {
@@ -793,10 +803,11 @@ void exact_accumulate(const gcr_problem* P, const RectModel& mv, const RectModel
         double* const vp = val.data();
         uint8_t* const dp = dec.data();
         std::atomic<uint64_t> flips{0};
+        const ValueConst vc = value_const(mv, P->solver == 1, c == 1);
         auto body = [&](size_t lo, size_t hi) {
             uint64_t f = 0;
             for (size_t i = lo; i < hi; ++i) {
-                const double rv = host_r2<TwinMath>(P, c, i, mv);
+                const double rv = host_value(P, c, i, mv, vc);
                 const bool d = host_r2<GlibcMath>(P, c, i, md) <= T[c];
                 vp[i] = rv;
                 dp[i] = d ? 1 : 0;
@@ -3593,6 +3604,22 @@ void gcr_host_homography(const gcr_rect_model* m, double* H_out) {
 double gcr_host_log(double x) { return dm::dm_log(x); }
 double gcr_host_pow_m3(double t) { return dm::dm_pow_m3(t); }
 double gcr_host_atan2(double y, double x) { return dm::dm_atan2(y, x); }
+double gcr_host_math(int op, double a, double b) {
+    double sn, cs;
+    switch (op) {
+        case 0: return dm::dm_log(a);
+        case 1: return dm::dm_pow_m3(a);
+        case 2: return dm::dm_atan2(a, b);
+        case 3: return a / b;
+        case 5: return dm::clip_angle_small(a);
+        case 6: return dm::clip_angle(a);
+        case 8: return dm::dm_log_fd(a);
+        case 9: dm::dm_sincos(a, sn, cs); return sn;
+        case 10: dm::dm_sincos(a, sn, cs); return cs;
+        case 11: return dm::atan_ratio(a, b);
+        default: return sqrt(a);
+    }
+}
 
 int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls, uint64_t n,
                     uint32_t m, uint32_t* out) {
@@ -3602,7 +3629,8 @@ int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream
 }
 
 int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out) {
-    if (!ctx || !a || !out || ((op == 2 || op == 3) && b == nullptr)) return set_err(GCR_EINVAL, "null argument");
+    if (!ctx || !a || !out || ((op == 2 || op == 3 || op == 11) && b == nullptr))
+        return set_err(GCR_EINVAL, "null argument");
     return guard([&]() -> int {
         HIPC(hipSetDevice(ctx->device));
         double *da = nullptr, *db = nullptr, *dout = nullptr;

@@ -9,27 +9,32 @@
 // (GCRANSAC.h:789-870) and the final masks.  The kernels evaluate the detmath
 // twins (detmath.h), whose results can differ from glibc's in the last bits.
 //
-// The twins' deviation from glibc is bounded.  For the residual r (r^2 the
-// squared residual) of one (feature, model) pair,
-//   scale:        |r_twin - r_glibc| <= 9.2e-16 + 2.9e-16 r
-//     (dm_pow_m3 < 1.5 ulp and glibc pow < 0.52 ulp: rs within 2.1 ulp, the
-//     two products round alike -> arg within 4.2 ulp = 9.2e-16 relative ->
-//     log(arg) within 9.2e-16 absolute; dm_log <= 0.77 ulp and glibc log
-//     <= 0.52 ulp of r -> 1.3 ulp(r) <= 2.9e-16 r), valid while rs, arg and
-//     t^-3 are normal numbers and rs is not at the 1e-9 cut (scale_unsafe);
-//   orientation:  |r_twin - r_glibc| <= 8e-15
-//     (dm_atan2 <= 1.8 ulp and glibc atan2 <= 1 ulp of |a| <= pi: 1.25e-15;
-//     the model's phi, when it is a minimal model's twin phi against the glibc
-//     one, as much again plus the phi + pi/2 rounding; th, c0, c1 and the two
-//     minAngleDiff steps add at most 4 roundings of ulp(2 pi) / 2 on each side:
-//     3.6e-15).
-// tests/test_exact.py measures the deviations on random pairs (max 8.9e-16
-// scale, 1.3e-15 orientation) far inside these bounds.
+// The kernels evaluate the residual VALUES of rect.h ("values": the same
+// residuals in a division-light form over the detmath twins), whose deviation
+// from the reference's glibc residuals is bounded.  For the residual r (r^2
+// the squared residual) of one (feature, model) pair,
+//   scale:        |r_value - r_glibc| <= 1.0e-15 + 5.2e-16 r
+//     (the value's argument (ac ps) / ((t t) t) carries 4 roundings, the
+//     reference's ac (ps pow(t, -3)) glibc pow's 0.52 ulp and 2 roundings:
+//     the two arguments agree within 7 ulp = 1.0e-15 relative, i.e. their
+//     logs within 1.0e-15 absolute; dm_log <= 1.8 ulp and glibc log <= 0.52
+//     ulp of r: 2.3 ulp(r) <= 5.2e-16 r), valid while ps ac, t^3 and the
+//     argument are normal numbers and the argument is not at the cut
+//     (scale_unsafe);
+//   orientation:  |r_value - r_glibc| <= 5e-15
+//     (value: the rotation by the model's twin cos / sin (< 1.5 ulp each) moves
+//     the direction by < 6e-16 rad, the division and dm's atan polynomial add
+//     < 3.1e-16; a minimal model's twin phi against its glibc one 1.3e-15;
+//     reference: glibc atan2 <= 1 ulp of |a| <= pi and the clipping's roundings
+//     of ulp(2 pi) / 2, <= 2.2e-15; the rare reference-formula fallback of the
+//     value keeps round 3's bound 3.6e-15).
+// tests/test_exact.py measures the deviations on random pairs far inside
+// these bounds.
 //
 // The kernels therefore flag every pair whose twin r^2 lies within the band
 // [lo, hi] = [((sqrt(T) - D)(1 - 1e-12))^2, ((sqrt(T) + D)(1 + 1e-12))^2]
 // around a decision threshold T, with D = kDevScale / kDevOrient (the bounds
-// above with a 4-5x margin; the 1e-12 relative margin covers the relative
+// above with a 4-8x margin; the 1e-12 relative margin covers the relative
 // term, sqrt's and the squares' roundings).  Outside the band the twin and the
 // glibc residual fall on the same side of T (and of fl(r^2 / T) < 1, which
 // only differs from r^2 < T within 2^-53 T).  Inside it the host recomputes
@@ -37,7 +42,7 @@
 // prefilters of the batch scorers keep every flagged pair: their slack is
 // >= 1e-9 absolute in log scale and tan(1.5 thr) 1e-6 + 1e-12 in angle.
 //
-// Values: the MSAC running sums add the twin r^2 of the pairs the glibc
+// Values: the MSAC running sums add the value r^2 of the pairs the glibc
 // decision makes inliers (a definition, restated by the oracle's TWIN mode);
 // a pair whose decision the recheck flips makes the host re-fold that model's
 // sums in that definition.  A flip moves the finished score by
@@ -50,7 +55,7 @@
 
 namespace gcr {
 
-constexpr double kDevScale = 4e-15;      // bound on |r_twin - r_glibc|, scale class (absolute part)
+constexpr double kDevScale = 4e-15;      // bound on |r_value - r_glibc|, scale class (absolute part)
 constexpr double kDevScaleRel = 1e-12;   // ... its relative part (and the band's rounding margin)
 constexpr double kDevOrient = 4e-14;     // orientation class (radians)
 
@@ -104,11 +109,11 @@ inline FlagBand flag_band(const double T[2]) {
 // sqrt(T) >= 60 (arguments of log near the ends of the normal range),
 // alpha^3 outside [2^-200, 2^200], a problem with a positive finite scale
 // outside [2^-200, 2^200] (`scales_ok` false) -- with both in range, log's
-// argument within [e^-60, e^60] keeps t^-3 and rs normal, so the error
-// analysis holds; other features give inf / NaN on both sides -- or the
-// rectified-scale cut rs < 1e-9 (scale_sq_residual) inside the inlier band
-// (|log(alpha^3 1e-9)| close to sqrt(T): the twin and glibc rs can fall on
-// either side of the cut).  The engine decides every pair of such a model on
+// argument within [e^-60, e^60] keeps ac ps, t^3, t^-3 and rs normal, so the
+// error analysis holds; other features give inf / NaN on both sides -- or the
+// rectified-scale cut rs < 1e-9 (the value's arg < ac 1e-9, scale_sq_value)
+// inside the inlier band (|log(alpha^3 1e-9)| close to sqrt(T): the value's
+// and glibc's sides of the cut can differ).  The engine decides every pair of such a model on
 // the host.  `solver`: 0, 1 (original: arg = rs / alpha^3) or 2.
 inline bool scale_unsafe(int solver, double alpha, double T0, bool scales_ok) {
     const double rT = sqrt(T0);

@@ -316,11 +316,11 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, 
     }
     const RectModel m = models[h];
     const DevClass c0 = p.cls[0];
-    const double ac = alpha_cube(m);
+    const ValueConst vc = value_const(m, KIND == 1, KIND == 2);
     uint32_t cnt0 = 0, nfl = 0;
     double acc0 = 0.0;
     for (uint32_t i = 0; i < c0.n; ++i) {
-        const double r2 = scale_sq_residual<KIND == 1, kIdentity>(c0.x[i], c0.y[i], c0.a[i], m, ac);
+        const double r2 = scale_sq_value<KIND == 1, kIdentity>(c0.x[i], c0.y[i], c0.a[i], m, vc.ac, vc.cut);
         nfl += in_flag_band(r2, fb.mid[0], fb.half[0]) ? 1u : 0u;
         if (r2 <= T0) {
             cnt0 += 1;
@@ -331,9 +331,9 @@ __global__ __launch_bounds__(kScoreBlock) void k_score(DevProblem p, double T0, 
     double acc1 = 0.0, tot = acc0;
     if constexpr (KIND == 2) {
         const DevClass c1 = p.cls[1];
-        const OrientConst oc = orient_const(m);
         for (uint32_t i = 0; i < c1.n; ++i) {
-            const double r2 = orient_sq_residual<kIdentity>(c1.x[i], c1.y[i], c1.c0[i], c1.c1[i], m, oc);
+            const double r2 =
+                orient_sq_value<kIdentity>(c1.x[i], c1.y[i], c1.c0[i], c1.c1[i], m, vc.c, vc.s, vc.cphi, vc.cphi2);
             nfl += in_flag_band(r2, fb.mid[1], fb.half[1]) ? 1u : 0u;
             if (r2 <= T1) {
                 cnt1 += 1;
@@ -381,8 +381,8 @@ struct alignas(16) HypConst {   // per-hypothesis constants of the exact and ban
             // band constants first, in 16-byte pairs (ds_read_b128)
             double h7, h8;      // model
             double lo, hi;      // scale band on s / t^3 (ac-adjusted)
-            double cf, sf;      // orientation: cos(phi), sin(phi) (band test only)
-            double ac;          // scale: alpha^3
+            double cf, sf;      // orientation: twin cos(phi), sin(phi) (band and value; NaN: reference formula)
+            double ac, cut;     // scale: alpha^3, the value's cut (rect.h ValueConst)
             double cphi, cphi2; // orientation: clipped phi, clip(clip(phi + pi/2))
         };
         double g[9];            // homography (KIND 3), row-major
@@ -442,7 +442,31 @@ __device__ __forceinline__ bool orient_band(double x, double y, double ct, doubl
     const double denom = (x * st - y * ct) * q.h8 + ct;
     const double u = __builtin_fabs(denom * q.cf + numer * q.sf);
     const double v = __builtin_fabs(numer * q.cf - denom * q.sf);
-    return !(__builtin_fmin(u, v) > tan_tau * __builtin_fmax(u, v));
+    const double mx = __builtin_fmax(u, v);
+    // a direction of magnitude < 2^-900 (rounding no longer relative) is never rejected
+    return !(__builtin_fmin(u, v) > tan_tau * mx) | !(mx >= 0x1p-900);
+}
+
+template <int KIND>
+__device__ __forceinline__ HypConst make_hyp(const typename ModelOf<KIND>::type& m, double band0) {
+    HypConst q;
+    if constexpr (KIND >= 3) {
+        for (int j = 0; j < 9; ++j) q.g[j] = m.h[j];
+    } else {
+        const ValueConst vc = value_const(m, KIND == 1, KIND == 2);
+        q.h7 = m.h7;
+        q.h8 = m.h8;
+        q.ac = vc.ac;
+        q.cut = vc.cut;
+        // s / t^3 must lie in [exp(-tau), exp(tau)] / ac (new) or * ac (original)
+        q.lo = (KIND == 1 ? q.ac : 1.0 / q.ac) * (1.0 / band0) * (1.0 - 1e-9);
+        q.hi = (KIND == 1 ? q.ac : 1.0 / q.ac) * band0 * (1.0 + 1e-9);
+        q.cf = vc.c;
+        q.sf = vc.s;
+        q.cphi = vc.cphi;
+        q.cphi2 = vc.cphi2;
+    }
+    return q;
 }
 
 // in-kernel generation + per-workgroup selection (kGen), see kernels.h
@@ -613,22 +637,10 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
     } else if (t < H) {
         const bool v = valid_h;
         RectModel m = default_model();
-        if constexpr (KIND < 3) m = v ? (kGen ? gen_m[h] : models[hg]) : default_model();
-        HypConst q;
-        q.h7 = m.h7;
-        q.h8 = m.h8;
-        q.ac = alpha_cube(m);
-        // s / t^3 must lie in [exp(-tau), exp(tau)] / ac (new) or * ac (original)
-        q.lo = (KIND == 1 ? q.ac : 1.0 / q.ac) * (1.0 / band0) * (1.0 - 1e-9);
-        q.hi = (KIND == 1 ? q.ac : 1.0 / q.ac) * band0 * (1.0 + 1e-9);
-        q.cphi = 0.0; q.cphi2 = 0.0; q.cf = 1.0; q.sf = 0.0;
-        if constexpr (KIND == 2) {
-            const OrientConst oc = orient_const(m);
-            q.cphi = oc.cphi;
-            q.cphi2 = oc.cphi2;
-            sincos(m.phi, &q.sf, &q.cf);
+        if constexpr (KIND < 3) {
+            m = v ? (kGen ? gen_m[h] : models[hg]) : default_model();
+            hyp[h] = make_hyp<KIND>(m, band0);
         }
-        hyp[h] = q;
     }
     if (t < 2 * H) cnt_sh[t / H][t % H] = 0;
     if (t < H) fl_sh[t] = 0;
@@ -736,11 +748,11 @@ __global__ __launch_bounds__(kSplitThreads) void k_score_split(DevProblem p, dou
                         r2 = h_sq_residual(fb[0][il], fb[1][il], fb[2][il], fb[3][il], q.g);
                         inl = r2 <= T0;
                     } else if (cls == 0) {
-                        r2 = scale_sq_residual<KIND == 1, true>(fb[0][il], fb[1][il], fb[2][il], m, q.ac);
+                        r2 = scale_sq_value<KIND == 1, true>(fb[0][il], fb[1][il], fb[2][il], m, q.ac, q.cut);
                         inl = r2 <= T0;
                     } else {
-                        const OrientConst oc{q.cphi, q.cphi2};
-                        r2 = orient_sq_residual<true>(fb[0][il], fb[1][il], fb[2][il], fb[3][il], m, oc);
+                        r2 = orient_sq_value<true>(fb[0][il], fb[1][il], fb[2][il], fb[3][il], m, q.cf, q.sf, q.cphi,
+                                                   q.cphi2);
                         inl = r2 <= T1;
                     }
                     if (inl) {
@@ -958,28 +970,6 @@ __device__ __forceinline__ void fm_publish(uint32_t* f, uint32_t v) {
     __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int KIND>
-__device__ __forceinline__ HypConst make_hyp(const typename ModelOf<KIND>::type& m, double band0) {
-    HypConst q;
-    if constexpr (KIND >= 3) {
-        for (int j = 0; j < 9; ++j) q.g[j] = m.h[j];
-    } else {
-        q.h7 = m.h7;
-        q.h8 = m.h8;
-        q.ac = alpha_cube(m);
-        // s / t^3 must lie in [exp(-tau), exp(tau)] / ac (new) or * ac (original)
-        q.lo = (KIND == 1 ? q.ac : 1.0 / q.ac) * (1.0 / band0) * (1.0 - 1e-9);
-        q.hi = (KIND == 1 ? q.ac : 1.0 / q.ac) * band0 * (1.0 + 1e-9);
-        q.cphi = 0.0; q.cphi2 = 0.0; q.cf = 1.0; q.sf = 0.0;
-        if constexpr (KIND == 2) {
-            const OrientConst oc = orient_const(m);
-            q.cphi = oc.cphi;
-            q.cphi2 = oc.cphi2;
-            sincos(m.phi, &q.sf, &q.cf);
-        }
-    }
-    return q;
-}
 
 // Correspondence instantiations (KIND >= 3) keep the survivor regions and
 // queues in dynamic LDS and are held to 64 VGPRs (8 waves per SIMD's worth):
@@ -1563,11 +1553,10 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                         m.h7 = hq.h7;
                         m.h8 = hq.h8;
                         if (cls == 0) {
-                            r2 = scale_sq_residual<KIND == 1, true>(cur.x, cur.y, cur.a2, m, hq.ac);
+                            r2 = scale_sq_value<KIND == 1, true>(cur.x, cur.y, cur.a2, m, hq.ac, hq.cut);
                             inl = r2 <= T0;
                         } else {
-                            const OrientConst oc{hq.cphi, hq.cphi2};
-                            r2 = orient_sq_residual<true>(cur.x, cur.y, cur.a2, cur.a3, m, oc);
+                            r2 = orient_sq_value<true>(cur.x, cur.y, cur.a2, cur.a3, m, hq.cf, hq.sf, hq.cphi, hq.cphi2);
                             inl = r2 <= T1;
                         }
                     }
@@ -1747,15 +1736,22 @@ __global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename 
     const DevClass& c = p.cls[cls];
     const auto m = models[mi];
     const bool live = inc == nullptr || inc[mi] <= 101;   // a slot without a model scores zeros
+    // the model's value constants (a twin sincos for KIND 2): once per block
+    __shared__ ValueConst vc_sh;
+    if constexpr (KIND <= 2) {
+        if (threadIdx.x == 0) vc_sh = value_const(m, KIND == 1, KIND == 2);
+        __syncthreads();
+    }
     double r2 = 0.0;
     bool inl = false;
     if (live && j < ntot && i < c.n) {
         if constexpr (KIND >= 3) {
             r2 = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
         } else if (cls == 0) {
-            r2 = scale_sq_residual<KIND == 1, true>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
+            r2 = scale_sq_value<KIND == 1, true>(c.x[i], c.y[i], c.a[i], m, vc_sh.ac, vc_sh.cut);
         } else {
-            r2 = orient_sq_residual<true>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
+            r2 = orient_sq_value<true>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, vc_sh.c, vc_sh.s, vc_sh.cphi,
+                                       vc_sh.cphi2);
         }
         inl = r2 <= (cls == 0 ? T0 : T1);
     }
@@ -3130,8 +3126,11 @@ __global__ __launch_bounds__(kMaskBlock) void k_mask(DevClass c, int cls, typena
     if (i >= c.n) return;
     double r2;
     if constexpr (KIND >= 3) r2 = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
-    else if (cls == 0) r2 = scale_sq_residual<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, alpha_cube(m));
-    else r2 = orient_sq_residual<false>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, orient_const(m));
+    else {
+        const ValueConst vc = value_const(m, KIND == 1, cls == 1);
+        if (cls == 0) r2 = scale_sq_value<KIND == 1, false>(c.x[i], c.y[i], c.a[i], m, vc.ac, vc.cut);
+        else r2 = orient_sq_value<false>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, vc.c, vc.s, vc.cphi, vc.cphi2);
+    }
     // rule 2: labeling(), BK max-flow with no pairwise edges (empty grid
     // graph, gcransac_python.cpp:63-68) -> SINK iff terminal capacity < 0;
     // bit 1: a decision within the twin-glibc bound (exact.h), rechecked by
@@ -3153,6 +3152,10 @@ __global__ void k_math(int op, const double* __restrict__ a, const double* __res
         case 3: r = a[i] / b[i]; break;
         case 5: r = dm::clip_angle_small(a[i]); break;
         case 6: r = dm::clip_angle(a[i]); break;
+        case 8: r = dm::dm_log_fd(a[i]); break;
+        case 9: { double sn, cs; dm::dm_sincos(a[i], sn, cs); r = sn; } break;
+        case 10: { double sn, cs; dm::dm_sincos(a[i], sn, cs); r = cs; } break;
+        case 11: r = dm::atan_ratio(a[i], b[i]); break;
         default: r = sqrt(a[i]); break;
     }
     out[i] = r;

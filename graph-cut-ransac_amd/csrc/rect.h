@@ -13,6 +13,8 @@
 //   scale_sq_residual         estimators/solver_rectifying_homography_three_sift.hpp:293-317,
 //                             ..._three_sift_original.hpp:316, ..._two_sift.hpp:621-645
 //   orient_sq_residual        ..._two_sift.hpp:647-665, model.h:156-165, math_utils.hpp:78-102
+//   scale_sq_value,           the same residuals in the product's value form
+//   orient_sq_value           (what the kernels evaluate, see "values")
 //   are_collinear             math_utils.hpp:138-155
 //   gauss3                    math_utils.hpp:164-221
 //   convex hull / inside      math_utils.hpp:223-321
@@ -134,6 +136,97 @@ GCR_HD double orient_sq_residual(double x, double y, double ct, double st, const
     const double l2 = __builtin_fmin(min_angle_diff_c(oc.cphi2, c0), min_angle_diff_c(oc.cphi2, c1));
     const double r = __builtin_fmin(l1, l2);
     return r * r;
+}
+
+// ------------------------------------------------------------- values ----
+// The product's residual VALUES: what the kernels evaluate, fold into the
+// MSAC sums and test against the thresholds (the oracle's TWIN mode restates
+// them).  Equal in real arithmetic to the reference's residuals above and
+// within exact.h's bound of the glibc ones, with fewer operations:
+//   scale:   r = |log((ac ps) / t^3)|, |log(ps / (ac t^3))| for the original
+//            solver: one division and the table log (dm_log, no division),
+//            the reference's cut rs < 1e-9 becomes arg < ac 1e-9 (1e-9 / ac),
+//            a per-model constant;
+//   orient:  the distance of the rectified direction's angle to the model's
+//            line family {phi + k pi/2} (the reference's min over phi,
+//            phi + pi/2 and both line directions, two_sift.hpp:647-665) is
+//            the angle of the direction rotated by -phi to its nearest axis,
+//            atan(min(|u|, |v|) / max(|u|, |v|)) of (u, v) = R(-phi) (denom,
+//            numer): one division, no quadrant or clipping logic, with the
+//            model's twin cos / sin (dm_sincos).  Directions whose magnitude
+//            leaves [2^-900, 2^1000] (subnormal or overflowing rotations,
+//            inf / NaN) and models with |phi| > 16 take the reference formula
+//            with the twin atan2 (orient_sq_residual).
+struct ValueConst {
+    double ac;             // alpha^3
+    double cut;            // scale: arg below it <-> the reference's rs < 1e-9
+    double c, s;           // orientation: twin cos / sin of phi (NaN: reference formula)
+    double cphi, cphi2;    // orientation: orient_const (the reference formula's)
+};
+
+GCR_HD ValueConst value_const(const RectModel& m, bool original, bool orient) {
+    ValueConst v;
+    v.ac = alpha_cube(m);
+    v.cut = original ? kEps9 / v.ac : v.ac * kEps9;
+    v.c = 1.0;
+    v.s = 0.0;
+    v.cphi = v.cphi2 = 0.0;
+    if (orient) {
+        const OrientConst oc = orient_const(m);
+        v.cphi = oc.cphi;
+        v.cphi2 = oc.cphi2;
+        if (__builtin_fabs(m.phi) <= 16.0) {
+            dm::dm_sincos(m.phi, v.s, v.c);
+        } else {
+            v.c = v.s = __builtin_nan("");
+        }
+    }
+    return v;
+}
+
+template <bool kOriginal, bool kIdentity>
+GCR_HD double scale_sq_value(double x, double y, double sc, const RectModel& m, double ac, double cut) {
+    double px = x, py = y, ps = sc;
+    if (!kIdentity) {
+        px = m.s * (x - m.x0 * 1.0);
+        py = m.s * (y - m.y0 * 1.0);
+        ps = sc * m.s;
+    }
+    const double t = (-m.h7 * px - m.h8 * py) + 1.0;
+    const double u = (t * t) * t;
+    const double arg = kOriginal ? ps / (ac * u) : (ac * ps) / u;
+    if (!(arg >= cut)) return DBL_MAX * DBL_MAX;          // the cut, negative, NaN: outlier
+    const double r = __builtin_fabs(dm::dm_log(arg));
+    return r * r;
+}
+
+// the reference formula with the twin atan2, out of line (rare)
+GCR_COLD GCR_HD double orient_sq_slow(double px, double py, double ct, double st, double h7, double h8, double cphi,
+                                      double cphi2) {
+    RectModel m = default_model();
+    m.h7 = h7;
+    m.h8 = h8;
+    return orient_sq_residual<true, TwinMath>(px, py, ct, st, m, OrientConst{cphi, cphi2});
+}
+
+template <bool kIdentity>
+GCR_HD double orient_sq_value(double x, double y, double ct, double st, const RectModel& m, double c, double s,
+                              double cphi, double cphi2) {
+    double px = x, py = y;
+    if (!kIdentity) {
+        px = m.s * (x - m.x0 * 1.0);
+        py = m.s * (y - m.y0 * 1.0);
+    }
+    const double numer = (-px * st + py * ct) * m.h7 + st;
+    const double denom = (px * st - py * ct) * m.h8 + ct;
+    const double an = __builtin_fabs(numer), ad = __builtin_fabs(denom);
+    if (an < 0x1p1000 && ad < 0x1p1000 && __builtin_fmax(an, ad) >= 0x1p-900 && c == c) {
+        const double u = __builtin_fabs(denom * c + numer * s);
+        const double w = __builtin_fabs(numer * c - denom * s);
+        const double r = dm::atan_ratio(__builtin_fmin(u, w), __builtin_fmax(u, w));
+        return r * r;
+    }
+    return orient_sq_slow(px, py, ct, st, m.h7, m.h8, cphi, cphi2);
 }
 
 // ---------------------------------------------------------- geometry -------

@@ -158,6 +158,8 @@ def _load():
     L.gcr_host_pow_m3.restype = C.c_double
     L.gcr_host_atan2.argtypes = [C.c_double, C.c_double]
     L.gcr_host_atan2.restype = C.c_double
+    L.gcr_host_math.argtypes = [C.c_int, C.c_double, C.c_double]
+    L.gcr_host_math.restype = C.c_double
     L.gcr_host_sample.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
                                   C.c_uint32, u32p]
     L.gcr_debug_math.argtypes = [vp, C.c_int, dp, dp, C.c_size_t, dp]

@@ -300,11 +300,16 @@ double gcr_host_weighted_mode(const double* angles, const double* weights, size_
 double gcr_host_log(double x);
 double gcr_host_pow_m3(double t);
 double gcr_host_atan2(double y, double x);
+/* host-only: the op of gcr_debug_math below on one operand pair (ops 0-6,
+ * 8-11; the host twin of each device primitive) */
+double gcr_host_math(int op, double a, double b);
 int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream, uint32_t cls, uint64_t n,
                     uint32_t m, uint32_t* out);
 /* device evaluation of the same primitives over arrays (GPU parity tests):
  * op 0 log(a), 1 pow_m3(a), 2 atan2(a, b), 3 a / b, 4 sqrt(a),
- * 5 clip_angle_small(a), 6 clip_angle(a);
+ * 5 clip_angle_small(a), 6 clip_angle(a), 8 round 3's log (dm_log_fd),
+ * 9 / 10 sin / cos of a (dm_sincos), 11 atan(a / b) for 0 <= a <= b
+ * (atan_ratio, the orientation value's);
  * op 7 (n >= 2): out[0] = the wave-parallel exact in-order sum of a[0, n)
  * (k_lo_chain's fold), out[1] = the same sum by a sequential loop */
 int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out);

@@ -25,15 +25,18 @@
 //              reference's (glibc): inlier tests r^2 <= T and the labeling
 //              rule, LO / refit / final lists, the minimal solver's phi, the
 //              fits' rectified angles.  The MSAC running sums add the
-//              residuals of the product's detmath.h twins instead (the GPU
-//              evaluates the twins and rechecks on the host every decision
-//              whose twin residual lies within the proven twin-glibc bound of
-//              the threshold: csrc/exact.h); a minimal 2-SIFT model's sums use
-//              its twin phi (phi_val, the value the generator kernel holds).
+//              product's residual VALUES instead (csrc/rect.h "values": the
+//              same residuals in a division-light form over detmath.h; the GPU
+//              evaluates them and rechecks on the host every decision whose
+//              value lies within the proven value-glibc bound of the
+//              threshold: csrc/exact.h); a minimal 2-SIFT model's sums use its
+//              twin phi (phi_val, the value the generator kernel holds).
 //              Masks, counts and models therefore equal GLIBC mode; the score
 //              values differ from GLIBC's in the last bits only.
-//   PURE_TWIN (2): the round-3 definition, detmath for the three functions
-//              everywhere (decisions included); kept to show what TWIN fixes.
+//   PURE_TWIN (2): the round-3 definition, the reference's formulas with the
+//              round-3 twins (dm_log_fd, dm_pow_m3, dm_atan2) everywhere,
+//              decisions included; kept to show what TWIN fixes and to
+//              reproduce round 3's frozen fixtures.
 // =============================================================================
 #include <algorithm>
 #include <array>
@@ -57,9 +60,10 @@ namespace oracle {
 // ----------------------------------------------------------------- math ----
 enum MathMode { MATH_GLIBC = 0, MATH_TWIN = 1, MATH_PURE_TWIN = 2 };
 static thread_local int g_math = MATH_GLIBC;
-// which implementation m_log / m_pow_m3 / m_atan2 call right now: 0 glibc,
-// 1 the detmath twins (TWIN mode switches to 1 only for the MSAC sums' values
-// and the minimal model's value phi)
+// which arithmetic the residuals use right now: 0 the reference's formulas with
+// glibc, 1 the same formulas with the round-3 detmath twins (PURE_TWIN; TWIN
+// mode's value phi of a minimal model), 2 the product's value formulas
+// (csrc/rect.h "values": TWIN mode's MSAC sums and residual values)
 static thread_local int g_fn = 0;
 static inline void set_mode(int mode) {
     g_math = mode;
@@ -71,7 +75,7 @@ struct FnScope {                       // the twins for one evaluation (TWIN mod
     ~FnScope() { g_fn = saved; }
 };
 
-static inline double m_log(double x) { return g_fn ? gcr::dm::dm_log(x) : std::log(x); }
+static inline double m_log(double x) { return g_fn ? gcr::dm::dm_log_fd(x) : std::log(x); }
 static inline double m_pow_m3(double t) { return g_fn ? gcr::dm::dm_pow_m3(t) : std::pow(t, -3.0); }
 static inline double m_atan2(double y, double x) { return g_fn ? gcr::dm::dm_atan2(y, x) : std::atan2(y, x); }
 
@@ -631,7 +635,46 @@ struct Solver {
         if constexpr (K == 2) return {2, 2}; else return {3};
     }
 
+    // TWIN-mode values (g_fn 2): the product's value formulas (csrc/rect.h
+    // scale_sq_value / orient_sq_value) restated over detmath's primitives:
+    // |log((ac ps) / t^3)| with the cut as arg < ac 1e-9 (original solver:
+    // |log(ps / (ac t^3))|, arg < 1e-9 / ac), and the angle of the rectified
+    // direction rotated by -phi to its nearest axis (the reference formula with
+    // the twin atan2 outside [2^-900, 2^1000] or for |phi| > 16)
+    static double scaleValue(double x, double y, double s, const Model& m) {
+        V3 p{{x, y, 1.0}};
+        double ps = s;
+        m.normalize(p[0], p[1], p[2]);
+        m.normalizeScale(ps);
+        const double t = -m.h7 * p[0] - m.h8 * p[1] + 1.0;
+        const double u = (t * t) * t;
+        const double ac = cube(m.alpha);
+        const double arg = KIND == 1 ? ps / (ac * u) : (ac * ps) / u;
+        const double cut = KIND == 1 ? 1e-9 / ac : ac * 1e-9;
+        if (!(arg >= cut)) return DBL_MAX;
+        return std::fabs(gcr::dm::dm_log(arg));
+    }
+    static double orientationValue(double x, double y, double t, const Model& m) {
+        V3 p{{x, y, 1.0}};
+        m.normalize(p[0], p[1], p[2]);
+        double st, ct;
+        sincos_ref(t, &st, &ct);
+        const double numer = (-p[0] * st + p[1] * ct) * m.h7 + st;
+        const double denom = (p[0] * st - p[1] * ct) * m.h8 + ct;
+        const double an = std::fabs(numer), ad = std::fabs(denom);
+        double c = std::numeric_limits<double>::quiet_NaN(), sn = c;
+        if (std::fabs(m.phi) <= 16.0) gcr::dm::dm_sincos(m.phi, sn, c);
+        if (an < 0x1p1000 && ad < 0x1p1000 && std::fmax(an, ad) >= 0x1p-900 && c == c) {
+            const double u = std::fabs(denom * c + numer * sn);
+            const double w = std::fabs(numer * c - denom * sn);
+            return gcr::dm::atan_ratio(std::fmin(u, w), std::fmax(u, w));
+        }
+        FnScope tw(1);
+        return orientationResidual(x, y, t, m);
+    }
+
     static double scaleResidual(double x, double y, double s, const Model& m) {
+        if (g_fn == 2) return scaleValue(x, y, s, m);
         V3 p{{x, y, 1.0}};
         double scale = s;
         m.normalize(p[0], p[1], p[2]);
@@ -643,6 +686,7 @@ struct Solver {
         else return std::fabs(m_log(ac * rs));
     }
     static double orientationResidual(double x, double y, double t, const Model& m) {
+        if (g_fn == 2) return orientationValue(x, y, t, m);
         V3 p{{x, y, 1.0}};
         m.normalize(p[0], p[1], p[2]);
         const double ro = m.rectifiedAngle(p[0], p[1], t);
@@ -1401,7 +1445,7 @@ static Score<S::K> getScore(const S& solver, const Data<S::K>& data, const typen
             if (r2 <= T[c]) {
                 double v2 = r2;
                 if (twin_values) {
-                    FnScope tw(1);
+                    FnScope tw(2);
                     v2 = solver.squaredResidual(c, f, i, mv);
                 }
                 inliers[c].emplace_back(i);
@@ -2412,7 +2456,7 @@ int oracle_score(int kind, const double* f0, size_t n0, const double* f1, size_t
 // per-feature squared residuals of one model
 int oracle_residuals(int kind, int cls, const double* f, size_t n, const double* model7, int math_mode, double* r2) {
     set_mode(math_mode);
-    if (math_mode == MATH_TWIN) g_fn = 1;          // the values the product's kernels compute
+    if (math_mode == MATH_TWIN) g_fn = 2;          // the values the product's kernels compute
     Features a = make_features(f, n);
     Model m = read_model(model7);
     for (size_t i = 0; i < n; ++i) {

@@ -168,16 +168,18 @@ def thr_between(a, b):
     return None
 
 
-def boundary_thresholds(O, kind, f0, f1, thr0, thr1, model, per_class=4, window=0.3):
+def boundary_thresholds(O, kind, f0, f1, thr0, thr1, model, per_class=4, window=0.3, vs=None):
     """(cls, feature, thr0, thr1) cases: for up to `per_class` features of each
-    class whose glibc and twin r^2 under `model` differ and lie within
+    class whose glibc and `vs` r^2 under `model` differ and lie within
     `window` T of the class threshold, the thresholds with that class's moved
-    between the two residuals."""
+    between the two residuals.  `vs`: MATH_TWIN (default: the product's
+    values, what the kernels evaluate) or MATH_PURE_TWIN (round 3's twins)."""
+    vs = O.MATH_TWIN if vs is None else vs
     out = []
     classes = [(0, f0)] + ([(1, f1)] if kind == N.SOLVER_SIFT22 else [])
     for cls, f in classes:
         g = O.residuals(kind, cls, f, model, math_mode=O.MATH_GLIBC)
-        t = O.residuals(kind, cls, f, model, math_mode=O.MATH_TWIN)
+        t = O.residuals(kind, cls, f, model, math_mode=vs)
         T = msac_T(thr0 if cls == 0 else thr1)
         idx = np.where((g != t) & np.isfinite(g) & (np.abs(g - T) < window * T))[0]
         for i in idx[:per_class]:

@@ -1,11 +1,13 @@
 """Inlier decisions in the reference's arithmetic (csrc/exact.h), CPU side.
 
-The kernels evaluate log / pow(t, -3) / atan2 with the detmath twins; the
-reference uses glibc.  The product takes every decision in glibc: pairs whose
-twin r^2 lies within the proven twin-glibc bound of a threshold are flagged by
-the kernels and decided again on the host.  The oracle's TWIN mode restates
-that product definition (glibc decisions and models, twin values in the MSAC
-sums); its PURE_TWIN mode is the round-3 behaviour (twin decisions).
+The kernels evaluate the residuals in the product's value form (csrc/rect.h
+"values": a division-light restatement over the detmath twins); the reference
+uses glibc.  The product takes every decision in glibc: pairs whose value r^2
+lies within the proven value-glibc bound of a threshold are flagged by the
+kernels and decided again on the host.  The oracle's TWIN mode restates that
+product definition (glibc decisions and models, values in the MSAC sums); its
+PURE_TWIN mode is the round-3 behaviour (the reference's formulas with the
+round-3 twins, decisions included).
 
 Checked here, with thresholds placed between a pair's glibc and twin r^2
 (the construction of VERDICT round 3's probe):
@@ -73,27 +75,35 @@ KW = dict(min_it=0, max_it=100_000, lo=50, seed=7, confidence=0.99)
 
 
 @pytest.mark.parametrize("kind", [N.SOLVER_SCALE3, N.SOLVER_SCALE3_ORIGINAL, N.SOLVER_SIFT22])
-def test_single_model_boundary_decisions_are_glibcs(kind):
+@pytest.mark.parametrize("vs", ["value", "pure"])
+def test_single_model_boundary_decisions_are_glibcs(kind, vs):
+    """Thresholds between a pair's glibc r^2 and its product value r^2
+    ("value": the kernels' arithmetic decides that pair differently, the
+    flag band must catch it) or its round-3 twin r^2 ("pure"): the product's
+    masks and counts (TWIN) are glibc's either way."""
     f0, f1, thr0, thr1 = _problem(kind, 5)
     model = _glibc_model(kind, f0, f1, thr0, thr1, KW)
-    cases = boundary_thresholds(O, kind, f0, f1, thr0, thr1, model, per_class=12, window=1.0)
+    mode = O.MATH_TWIN if vs == "value" else O.MATH_PURE_TWIN
+    cases = boundary_thresholds(O, kind, f0, f1, thr0, thr1, model, per_class=12, window=1.0, vs=mode)
     assert len(cases) >= 4
-    pure_differs = 0
     for cls, i, t0, t1 in cases:
         g = O.score(kind, f0, f1, model, t0, t1, math_mode=O.MATH_GLIBC, want_masks=True)
         p = O.score(kind, f0, f1, model, t0, t1, math_mode=O.MATH_TWIN, want_masks=True)
-        u = O.score(kind, f0, f1, model, t0, t1, math_mode=O.MATH_PURE_TWIN, want_masks=True)
         assert np.array_equal(g["counts"], p["counts"])
         for a, b in zip(g["masks"], p["masks"]):
             assert (a is None and b is None) or np.array_equal(a, b)
-        # the constructed pair decides differently in the twins' arithmetic
-        assert not np.array_equal(u["masks"][cls], g["masks"][cls])
-        assert u["masks"][cls][i] != g["masks"][cls][i]
-        pure_differs += 1
-        # values: twin residuals over the glibc decisions (within the flip's
-        # |1 - r^2 / T| of glibc's score)
+        # the constructed pair decides differently in the `vs` arithmetic
+        T = (2.25 * (t0 if cls == 0 else t1)) * (t0 if cls == 0 else t1)
+        f = f0 if cls == 0 else f1
+        rg = O.residuals(kind, cls, f, model, math_mode=O.MATH_GLIBC)[i]
+        rv = O.residuals(kind, cls, f, model, math_mode=mode)[i]
+        assert (rg <= T) != (rv <= T)
+        if vs == "pure":
+            u = O.score(kind, f0, f1, model, t0, t1, math_mode=O.MATH_PURE_TWIN, want_masks=True)
+            assert u["masks"][cls][i] != g["masks"][cls][i]
+        # values: product residuals over the glibc decisions (within the
+        # flip's |1 - r^2 / T| of glibc's score)
         assert abs(p["value"] - g["value"]) <= 1e-9 * max(1.0, abs(g["value"]))
-    assert pure_differs == len(cases)
 
 
 def _run(kind, f0, f1, t0, t1, mode):
@@ -140,10 +150,12 @@ def test_best_model_boundaries_decide_the_refit(kind, seed):
     returns a different model or masks in most cases (measured 23 of 24)."""
     f0, f1, thr0, thr1 = _problem(kind, seed)
     best = best_minimal_model(O, kind, f0, f1, thr0, thr1, KWB["seed"], KWB["max_it"])
-    cases = boundary_thresholds(O, kind, f0, f1, thr0, thr1, best, per_class=4, window=1.0)
+    cases = boundary_thresholds(O, kind, f0, f1, thr0, thr1, best, per_class=4, window=1.0, vs=O.MATH_PURE_TWIN)
     assert len(cases) >= 4
+    # ... and between glibc and the product's values (the kernels' side)
+    vcases = boundary_thresholds(O, kind, f0, f1, thr0, thr1, best, per_class=2, window=1.0)
     differ = 0
-    for cls, i, t0, t1 in cases:
+    for n, (cls, i, t0, t1) in enumerate(cases + vcases):
         out = {}
         for mode in (O.MATH_GLIBC, O.MATH_TWIN, O.MATH_PURE_TWIN):
             if kind == N.SOLVER_SIFT22:
@@ -156,6 +168,7 @@ def test_best_model_boundaries_decide_the_refit(kind, seed):
         assert all(np.array_equal(a, b) for a, b in zip(gm, pm))
         assert [g["stats"][k] for k in STATS] == [p["stats"][k] for k in STATS]
         assert np.array_equal(O.model7(g["model"]), O.model7(p["model"]))
-        differ += not (all(np.array_equal(a, b) for a, b in zip(gm, um)) and
-                       np.array_equal(O.model7(g["model"]), O.model7(u["model"])))
+        if n < len(cases):
+            differ += not (all(np.array_equal(a, b) for a, b in zip(gm, um)) and
+                           np.array_equal(O.model7(g["model"]), O.model7(u["model"])))
     assert 2 * differ >= len(cases)

@@ -65,6 +65,15 @@ def test_device_math_matches_host_bitwise():
     got = _dev_math(2, y, xx)
     exp = np.array([N.lib.gcr_host_atan2(a, b) for a, b in zip(y, xx)])
     assert np.array_equal(bits(got), bits(exp))
+    # the value primitives (round 4): round 3's log, the model angle's sin /
+    # cos, the first-octant atan of the orientation value
+    for op, a, b in ((8, x, None), (9, np.concatenate([rng.uniform(-20, 20, 20000), [np.nan, np.inf, 0.0]]), None),
+                     (10, np.concatenate([rng.uniform(-20, 20, 20000), [np.nan, np.inf, 0.0]]), None),
+                     (11, np.abs(y[:20000]) * rng.uniform(0, 1, 20000), np.abs(y[:20000]) + 1e-300)):
+        got = _dev_math(op, a, b)
+        exp = np.array([N.lib.gcr_host_math(op, float(u), 0.0 if b is None else float(b[k]))
+                        for k, u in enumerate(a)])
+        assert np.array_equal(bits(got), bits(exp)), op
 
 
 def test_clip_angle_small_equals_clip_angle():
