@@ -252,8 +252,6 @@ struct Workspace {
     DevBuf<uint8_t> mask_all;           // inlier_lists: both classes, one copy back
     DevBuf<double> r2;                  // graph-cut labeling: squared residuals of the LO model
     PinBuf<double> h_r2;
-    DevBuf<double> sm_vals;             // launch_score_small: pair values
-    DevBuf<uint64_t> sm_bits;           // launch_score_small: inlier bitmasks
     PinBuf<RectModel> h_lorect;         // score_models: small batches' models, read in place
     PinBuf<GeoModel> h_logeo;
     PinBuf<uint64_t> h_mbits;           // launch_score_small: MSAC inlier ballots (ListBits.mbits)
@@ -304,8 +302,6 @@ struct Workspace {
     DevBuf<BlockSummary> dsum[2];
     PinBuf<BlockSummary> hsum[2];       // [0] this rank's, then the all-gathered ones
     DevBuf<BlockSummary> dall[2];       // gcr_comm: the all-gathered summaries on the device
-    DevBuf<double> cs_vals[2];
-    DevBuf<uint64_t> cs_bits[2];
     PinBuf<uint64_t> h_cbits[2];        // small-scored chunks: every slot's LO list bits (ListBits)
     hipEvent_t sum_done[2] = {nullptr, nullptr}, sum_k0[2] = {nullptr, nullptr}, sum_k1[2] = {nullptr, nullptr};
     bool spec_pending[2] = {false, false};   // a speculative chunk of this set may still run
@@ -665,6 +661,7 @@ public:
     explicit HostPool(unsigned n) {
         for (unsigned t = 1; t < n; ++t) workers_.emplace_back([this] { loop(); });
     }
+    size_t threads() const { return workers_.size() + 1; }
     ~HostPool() {
         {
             std::lock_guard<std::mutex> lk(mu_);
@@ -1603,8 +1600,6 @@ public:
         } else {
             if (np <= kSmallScore && small_score_on()) {
                 const size_t pairs = small_score_pairs(P_->dp);
-                w->cs_vals[set].ensure(pairs * np);
-                w->cs_bits[set].ensure(3 * pairs * np / 64);   // ballots + two flag planes
                 // every slot's LO lists (Tlo, LO rule) into pinned memory: an LO
                 // triggered by one of these models starts without its own mask
                 // launch and synchronisation
@@ -1618,7 +1613,7 @@ public:
                 }
                 chunk_lists_[set] = cl;
                 HIPC(launch_score_small(P_->dp, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np,
-                                        set_sb(set).dev(), w->cs_vals[set].p, w->cs_bits[set].p, s, cl ? &lb : nullptr));
+                                        set_sb(set).dev(), s, cl ? &lb : nullptr));
             } else {
                 chunk_lists_[set] = false;
                 HIPC(Tr::score(P_, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np, true, set_sb(set).dev(),
@@ -2284,6 +2279,7 @@ private:
                 const HostClass& c = P_->hc[0];
                 const double* cols[4] = {c.x.data(), c.y.data(), c.a.data(), c.c0.data()};
                 grid_edges(cols, 4, c.n, prm_.cell_size, prm_.cell_number, edges_, false);
+                gc_schedule(edges_, host_pool().threads());
                 graph_state_ = edges_.cells() > 0 ? 1 : 0;
             }
         }
@@ -2437,11 +2433,8 @@ private:
         if (kP == 1 && nh <= kSmallScore && small_score_on()) {
             // the few slots a short run needs: all pairs in parallel, one
             // wave per model (the batch scorers' chain would dominate)
-            const size_t pairs = small_score_pairs(P_->dp);
-            P_->w->sm_vals.ensure(pairs * nh);
-            P_->w->sm_bits.ensure(3 * pairs * nh / 64);
             HIPC(launch_score_small(P_->dp, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, P_->w->sb.dev(),
-                                    P_->w->sm_vals.p, P_->w->sm_bits.p, s_));
+                                    s_));
         } else {
             HIPC(Tr::score_live(P_, Tm_, Tr::dmodels(P_->w).p, P_->w->inc.p, (uint32_t)nh, (uint32_t)live,
                                 P_->w->sb.dev(), s_));
@@ -2690,8 +2683,6 @@ private:
             // a few models: all pairs in parallel, then one wave per model
             // adds its inliers in order (no ~90 us batch-scorer chain)
             const size_t pairs = small_score_pairs(P_->dp);
-            P_->w->sm_vals.ensure(pairs * n);
-            P_->w->sm_bits.ensure(3 * pairs * n / 64);
             // the graph-cut labeling with pairwise terms needs the residuals
             lists = req != nullptr && !(req->rule == 2 && use_graph());
             ListBits lb{{0.0, 0.0}, 0, prm_.spatial_coherence_weight, nullptr, nullptr};
@@ -2714,8 +2705,7 @@ private:
                 }
             }
             HIPC(launch_score_small(P_->dp, Tm_, dmodels, nullptr, n,
-                                    zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev(), P_->w->sm_vals.p,
-                                    P_->w->sm_bits.p, s_, lists ? &lb : nullptr));
+                                    zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev(), s_, lists ? &lb : nullptr));
         } else {
             HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
         }
@@ -2789,21 +2779,26 @@ private:
             }
             HIPC(hipStreamSynchronize(s_));
             st_.launches += 1;
-            lists[0].clear();
             lists[1].clear();
-            // the cells are independent components: cut them on the host pool
-            graphcut_labeling(P_->w->h_r2.p, n, T[0], prm_.spatial_coherence_weight, edges_, gc_q_, gc_seg_,
-                              [](size_t ncells, const auto& fn) {
-                                  const size_t parts = ncells < 64 ? 1 : 64;
-                                  const size_t step = (ncells + parts - 1) / parts;
-                                  host_pool().parallel_for(parts, [&](size_t p) {
-                                      thread_local CellScratch cs;
-                                      const size_t c0 = std::min(ncells, p * step);
-                                      fn(c0, std::min(ncells, c0 + step), cs);
-                                  });
-                              });
-            for (size_t i = 0; i < n; ++i)
-                if (gc_seg_[i]) lists[0].push_back((uint32_t)i);
+            // the cells are independent components: cut them on the host
+            // pool, in the cost-balanced jobs of gc_schedule
+            gc_q_.resize(n);
+            gc_seg_.resize(n);
+            graphcut_labeling_jobs(P_->w->h_r2.p, T[0], prm_.spatial_coherence_weight, edges_, gc_q_.data(),
+                                   gc_seg_.data(), [](size_t njobs, const auto& fn) {
+                                       host_pool().parallel_for(njobs, [&](size_t j) {
+                                           thread_local CellScratch cs;
+                                           fn(j, cs);
+                                       });
+                                   });
+            lists[0].resize(n);
+            uint32_t* lp = lists[0].data();
+            size_t m = 0;
+            for (size_t i = 0; i < n; ++i) {
+                lp[m] = (uint32_t)i;
+                m += gc_seg_[i];
+            }
+            lists[0].resize(m);
             return;
         }
         const size_t tot = N_[0] + (K_ == 2 ? N_[1] : 0);
@@ -3398,11 +3393,7 @@ int gcr_debug_score_h(gcr_problem* prob, const gcr_params* params, const double*
         HIPC(hipMemcpyAsync(prob->w->lo_gmodels.p, H, nmodels * sizeof(GeoModel), hipMemcpyHostToDevice, s));
         if (debug_small_scorer(nmodels)) {
             const double Tt[2] = {T, 0.0};
-            const size_t pairs = small_score_pairs(prob->dp);
-            prob->w->sm_vals.ensure(pairs * nmodels);
-            prob->w->sm_bits.ensure(3 * pairs * nmodels / 64);
-            HIPC(launch_score_small(prob->dp, Tt, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(),
-                                    prob->w->sm_vals.p, prob->w->sm_bits.p, s));
+            HIPC(launch_score_small(prob->dp, Tt, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(), s));
         } else {
             HIPC(launch_score_geo(prob->dp, T, prob->w->lo_gmodels.p, nullptr, nmodels, prob->w->lo_sb.dev(), s));
         }
@@ -3493,11 +3484,7 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
         prob->w->lo_sb.ensure(nmodels);
         HIPC(hipMemcpyAsync(prob->w->lo_models.p, hm.data(), nmodels * sizeof(RectModel), hipMemcpyHostToDevice, s));
         if (identity && debug_small_scorer(nmodels)) {
-            const size_t pairs = small_score_pairs(prob->dp);
-            prob->w->sm_vals.ensure(pairs * nmodels);
-            prob->w->sm_bits.ensure(3 * pairs * nmodels / 64);
-            HIPC(launch_score_small(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, prob->w->lo_sb.dev(),
-                                    prob->w->sm_vals.p, prob->w->sm_bits.p, s));
+            HIPC(launch_score_small(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, prob->w->lo_sb.dev(), s));
         } else {
             HIPC(launch_score(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, identity, prob->w->lo_sb.dev(), s));
         }

@@ -259,18 +259,20 @@ hipError_t launch_truncate(uint8_t* inc, uint32_t n, uint64_t budget, hipStream_
 hipError_t launch_sqres_geo(const DevProblem& p, const GeoModel& model, double* r2, hipStream_t stream);
 hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_t* count, hipStream_t stream);
 
-// Low-latency scoring of a few models (LO trials, refits): every pair in
-// parallel into vals / bits (small_score_pairs(p) doubles and 3 x /64 words
-// per model: the inlier ballots, then the MSAC and the list predicate's flag
-// ballots, exact.h), then one wave per model adds the inlier values in
-// feature order and counts the flags (out.fl, out.lfl).
-// Same raw accumulators as launch_score / launch_score_geo.  `models` points
-// to RectModel (solvers 0-2) or GeoModel (3, 4), identity normalisation only;
-// models with inc > 101 (inc may be null) score zeros.
+// Low-latency scoring of a few models (LO trials, refits): one 1024-thread
+// workgroup per model evaluates every (model, feature) pair, compacts the
+// inlier values in feature order into LDS and one wave adds them
+// (k_lo_chain), counting the decisions within the value-glibc bound of the
+// thresholds (out.fl, out.lfl; exact.h).  Same raw accumulators as
+// launch_score / launch_score_geo.  `models` points to RectModel (solvers
+// 0-2) or GeoModel (3, 4), identity normalisation only; models with inc > 101
+// (inc may be null) score zeros.  Bit arrays: per model small_score_pairs(p)
+// / 64 words (class 0 at [0, pad0), class 1 after it, pad_c = n_c rounded up
+// to 64).
 size_t small_score_pairs(const DevProblem& p);
 // Optional second per-pair predicate of the same launch (LO inlier lists):
 // rule 0: r^2 <= T[cls]; rule 2: the 1-class labeling of k_mask with T[0] and
-// lambda.  Bits in the layout of `bits`.
+// lambda, into `bits` (pinned host memory mapped for the device).
 struct ListBits {
     double T[2];
     int rule;
@@ -279,8 +281,7 @@ struct ListBits {
     uint64_t* mbits;         // optional: the MSAC inlier ballots too (r^2 <= the scoring threshold)
 };
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
-                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream,
-                              const ListBits* lists = nullptr);
+                              uint32_t nm, const ScoreOut& out, hipStream_t stream, const ListBits* lists = nullptr);
 
 // Per-feature inlier mask of one model for class `cls`: bit 0 the decision,
 // bit 1 set when the pair's twin r^2 lies in the flag band of T (exact.h:

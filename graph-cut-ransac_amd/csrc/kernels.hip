@@ -1722,62 +1722,6 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
 // pad_c = n_c rounded up to 64 (unused pairs: value 0, bit 0).
 // mask rule of k_mask / launch_mask on a residual: mask_rule, exact.h
 
-template <int KIND>
-__global__ __launch_bounds__(256) void k_lo_values(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
-                                                  const uint8_t* __restrict__ inc, double T0, double T1,
-                                                  uint32_t pad0, uint32_t ntot, double* __restrict__ vals,
-                                                  uint64_t* __restrict__ bits, ListBits lb, FlagBand fbm,
-                                                  FlagBand fbl) {
-    const uint32_t mi = blockIdx.y;
-    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x * 256 >= ntot) return;                // whole block (ntot is a multiple of 64)
-    const int cls = j < pad0 ? 0 : 1;
-    const uint32_t i = cls == 0 ? j : j - pad0;
-    const DevClass& c = p.cls[cls];
-    const auto m = models[mi];
-    const bool live = inc == nullptr || inc[mi] <= 101;   // a slot without a model scores zeros
-    // the model's value constants (a twin sincos for KIND 2): once per block
-    __shared__ ValueConst vc_sh;
-    if constexpr (KIND <= 2) {
-        if (threadIdx.x == 0) vc_sh = value_const(m, KIND == 1, KIND == 2);
-        __syncthreads();
-    }
-    double r2 = 0.0;
-    bool inl = false;
-    if (live && j < ntot && i < c.n) {
-        if constexpr (KIND >= 3) {
-            r2 = geo_sq_residual<KIND>(c.x[i], c.y[i], c.a[i], c.c0[i], m.h);
-        } else if (cls == 0) {
-            r2 = scale_sq_value<KIND == 1, true>(c.x[i], c.y[i], c.a[i], m, vc_sh.ac, vc_sh.cut);
-        } else {
-            r2 = orient_sq_value<true>(c.x[i], c.y[i], c.c0[i], c.c1[i], m, vc_sh.c, vc_sh.s, vc_sh.cphi,
-                                       vc_sh.cphi2);
-        }
-        inl = r2 <= (cls == 0 ? T0 : T1);
-    }
-    const uint64_t b = __ballot(inl);
-    // the LO list predicate of the same residual (launch_mask's rule)
-    const bool lin = lb.bits != nullptr && live && j < ntot && i < c.n &&
-                     mask_rule(r2, lb.rule, cls == 0 ? lb.T[0] : lb.T[1], lb.lambda);
-    const uint64_t lbw = __ballot(lin);
-    // decisions within the twin-glibc bound of their threshold (exact.h): the
-    // MSAC test's and the list predicate's, counted by k_lo_chain
-    const bool ev = live && j < ntot && i < c.n && KIND <= 2;
-    const uint64_t fw = __ballot(ev && in_flag_band(r2, fbm.mid[cls], fbm.half[cls]));
-    const uint64_t lfw = __ballot(ev && lb.bits != nullptr && in_flag_band(r2, fbl.mid[cls], fbl.half[cls]));
-    if (j < ntot) {
-        vals[(size_t)mi * ntot + j] = inl ? -r2 : 0.0;
-        if ((threadIdx.x & 63) == 0) {
-            const size_t wi = ((size_t)mi * ntot + j) / 64, plane = (size_t)gridDim.y * ntot / 64;
-            bits[wi] = b;
-            bits[plane + wi] = fw;
-            bits[2 * plane + wi] = lfw;
-            if (lb.bits != nullptr) lb.bits[wi] = lbw;
-            if (lb.mbits != nullptr) lb.mbits[wi] = b;
-        }
-    }
-}
-
 // k_lo_chain: one 1024-thread workgroup per model, blocks of kLoBlock
 // features.  All 16 waves load the block's values and ballot words at once
 // (one memory round trip; a single wave walking 1024-feature spans spent
@@ -1854,7 +1798,7 @@ __device__ __forceinline__ double fold_seq_lane(const double* __restrict__ cb, u
 }
 
 // fold_seq_lane with batches of 8 (fewer registers; for the short flagged
-// segments of fold_exact_seg)
+// segments of fold_exact_split)
 __device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, uint32_t k, const uint32_t e,
                                                  double run) {
     for (; k + 8 <= e; k += 8) {
@@ -1868,116 +1812,172 @@ __device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, 
     return run;
 }
 
-// fold_exact_seg: the same in-order sum (bit-identical to the sequential
-// loop) by segments.  Lane l takes the l-th of 64 contiguous segments.
+// fold_exact_split: the same in-order sum (bit-identical to the sequential
+// loop) by segments.  Lane 0 takes the first kSplitL0 values (usually folded
+// value by value from the chain's start), lane l > 0 the l-th of 63 equal
+// contiguous segments after them (odd length: the 64 lanes' LDS reads hit
+// distinct banks).
 //  1. Approximate segment sums and a DPP scan give every segment an
-//     approximate start value and so its binade E (ulp U); a segment whose
-//     approximate end lies in another binade, or that starts at a zero /
-//     positive / tiny sum, is flagged.
-//  2. Each lane adds rint(v / U) over its segment (four independent integer
-//     accumulators: integer sums below 2^53 are exact in any order) and flags
-//     ties (a fraction of exactly .5), positive and too large values.
-//  3. Lane 0 walks the segments in order: an unflagged segment whose exact
-//     start s lies in its binade E and whose end s / U + I stays in it is one
-//     exact fp64 addition (s + U I: both multiples of U, the result in the
-//     binade); any other segment is folded value by value (fold_seq_lane).
-// While s stays in one binade, fl(s + v) = s + U rint(v / U) except at ties,
-// so the result equals the sequential sum.  Only the segments where the sum
-// crosses a binade (about one per doubling of the sum) and the first ones
-// (values as large as the sum: ties) are folded value by value.  All lanes
-// call it; returns the sum on every lane.  GCR_LO_FOLD=wide selects it in k_lo_chain (A/B).
-__device__ __forceinline__ double fold_exact_seg(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
-                                                 double run, const int lane, uint32_t* stats = nullptr) {
+//     approximate start g and so its binade E (ulp U); a segment that starts
+//     at a zero / positive / tiny sum, or whose approximate end lies more
+//     than two binades further, is flagged.
+//  2. Each lane adds rint(v / U) over its segment (integer sums below 2^53
+//     are exact in any order).  While the running sum s stays in one binade,
+//     fl(s + v) = s + U rint(v / U) -- except for a tie (v / U ending in
+//     exactly .5: round-to-even then depends on s) and for the value whose
+//     addition leaves the binade (predicted from g).  Up to two such special
+//     values split the segment into parts; after a crossing the part's
+//     increments are taken at 2U.  A third special ends the segment's fast
+//     path there (the tail).  Positive, NaN or too large values flag it.
+//  3. The walk (all lanes alike, records by readlane): for each part, when the
+//     exact running sum lies in the part's binade, one exact addition s + U I
+//     (both multiples of U; the check S > -2^53 keeps every partial sum in the
+//     binade, the sums being monotone), then the special value by an ordinary
+//     addition; any failed check, and the tail, fold the rest of the segment
+//     value by value (fold_seq_lane8).
+// tests/test_fold.py restates it in numpy (segment for segment);
+// tests/test_gpu_fold.py runs it against the sequential sum.
+constexpr uint32_t kSplitL0 = 16;
+
+__device__ __forceinline__ void split_bounds(uint32_t k, uint32_t n, uint32_t L, int lane, uint32_t& b, uint32_t& e) {
+    if (lane == 0) {
+        b = k;
+        e = k + min(n, kSplitL0);
+    } else {
+        const uint32_t o = min(n, kSplitL0 + (uint32_t)(lane - 1) * L);
+        b = k + o;
+        e = k + min(n, o + L);
+    }
+}
+
+__device__ __forceinline__ double fold_exact_split(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
+                                                   double run, const int lane, uint32_t* stats = nullptr) {
     const uint32_t n = e - k;
     if (n < 512) return fold_seq_lane8(cb, k, e, run);   // short: every lane alike
-    // an odd segment length: the 64 lanes' LDS reads (stride 2L dwords) hit
-    // distinct banks
     const uint64_t tp0 = stats ? __builtin_readcyclecounter() : 0;
-    const uint32_t L = ((n + 63) / 64) | 1u;
-    const uint32_t b = min(e, k + (uint32_t)lane * L), ee = min(e, b + L);
-    // 1. approximate sums, approximate starts
+    const uint32_t L = ((n - kSplitL0 + 62) / 63) | 1u;
+    uint32_t b, ee;
+    split_bounds(k, n, L, lane, b, ee);
+    // 1. approximate sums (8 reads in flight per batch), approximate starts
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     uint32_t i = b;
-    for (; i + 4 <= ee; i += 4) {
-        a0 += cb[i];
-        a1 += cb[i + 1];
-        a2 += cb[i + 2];
-        a3 += cb[i + 3];
+    for (; i + 8 <= ee; i += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = cb[i + u];
+        a0 += t[0] + t[4];
+        a1 += t[1] + t[5];
+        a2 += t[2] + t[6];
+        a3 += t[3] + t[7];
     }
     for (; i < ee; ++i) a0 += cb[i];
     const double a = (a0 + a1) + (a2 + a3);
     const double X = wave_incl_scan_f64(a);
     const double g = run + (X - a);                       // approximate start
     const int be = (int)((as_u64(g) >> 52) & 0x7ffu);
-    const int be2 = (int)((as_u64(g + a) >> 52) & 0x7ffu);
-    bool flag = !(g < 0.0) || be < 53 || be == 0x7ff || be2 != be;
+    const int bend = (int)((as_u64(g + a) >> 52) & 0x7ffu);
+    const bool flag = !(g < 0.0) || be < 53 || be >= 0x7fd || bend > be + 2;
     const int bs = flag ? 1075 : be;                      // a harmless scale for flagged segments
-    const double iU = as_f64((uint64_t)(2098 - bs) << 52);
-    // 2. integer increments
-    double i0 = 0.0, i1 = 0.0, i2 = 0.0, i3 = 0.0;
+    // 2. integer increments in up to three parts
+    double u = as_f64((uint64_t)(2098 - bs) << 52);       // 1 / U
+    double P = g * u;                                     // approximate running sum in units of U
+    double acc = 0.0, A0 = 0.0, A1 = 0.0, V0 = 0.0, V1 = 0.0;
+    int c0 = -1, c1 = -1, tail = -1, nsp = 0, xm = 0;
     bool bad = false;
     i = b;
-    for (; i + 4 <= ee; i += 4) {
-        const double v0 = cb[i], v1 = cb[i + 1], v2 = cb[i + 2], v3 = cb[i + 3];
-        const double t0 = v0 * iU, t1 = v1 * iU, t2 = v2 * iU, t3 = v3 * iU;
-        const double n0 = __builtin_rint(t0), n1 = __builtin_rint(t1), n2 = __builtin_rint(t2), n3 = __builtin_rint(t3);
-        bad |= (v0 > 0.0) | (v1 > 0.0) | (v2 > 0.0) | (v3 > 0.0);
-        bad |= !(__builtin_fabs(t0) < 0x1p53) | !(__builtin_fabs(t1) < 0x1p53) | !(__builtin_fabs(t2) < 0x1p53) |
-               !(__builtin_fabs(t3) < 0x1p53);
-        bad |= (__builtin_fabs(t0 - n0) == 0.5) | (__builtin_fabs(t1 - n1) == 0.5) | (__builtin_fabs(t2 - n2) == 0.5) |
-               (__builtin_fabs(t3 - n3) == 0.5);
-        i0 += n0;
-        i1 += n1;
-        i2 += n2;
-        i3 += n3;
-    }
-    for (; i < ee; ++i) {
-        const double v0 = cb[i], t0 = v0 * iU, n0 = __builtin_rint(t0);
-        bad |= (v0 > 0.0) | !(__builtin_fabs(t0) < 0x1p53) | (__builtin_fabs(t0 - n0) == 0.5);
-        i0 += n0;
-    }
-    flag = flag || bad;
-    const double I = flag ? 0.0 : (i0 + i1) + (i2 + i3);
-    const int E = flag ? 0 : be;
-    // 3. the in-order walk over the segments, by every lane alike (the
-    //    segments' records by readlane: cross-lane reads stay in uniform
-    //    control flow, and the result is the same on every lane)
-    double s = run;
-    const uint64_t tp1 = stats ? __builtin_readcyclecounter() : 0;
-    {
-        uint32_t folded = 0;
-        for (int l = 0; l < 64; ++l) {
-            const uint32_t sb = min(e, k + (uint32_t)l * L), se = min(e, sb + L);
-            if (sb >= se) break;
-            const int el = __builtin_amdgcn_readlane(E, l);
-            const int es = (int)((as_u64(s) >> 52) & 0x7ffu);
-            if (el != 0 && es == el && s < 0.0) {
-                const double Ul = as_f64((uint64_t)(el - 52) << 52), iUl = as_f64((uint64_t)(2098 - el) << 52);
-                const double S = s * iUl + readlane_f64(I, l);      // exact when it stays below 2^53
-                if (S > -0x1p53 && S <= -0x1p52) {
-                    s = S * Ul;
+    while (i < ee && tail < 0) {
+        double t8[8];
+        const uint32_t m = min(8u, ee - i);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t8[q] = cb[i + ((uint32_t)q < m ? (uint32_t)q : 0u)];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if ((uint32_t)q >= m || tail >= 0) continue;
+            const double x = t8[q];
+            const double t = x * u;
+            const double r = __builtin_rint(t);
+            bad |= !(x <= 0.0) | !(__builtin_fabs(t) < 0x1p53);
+            const double Pn = P + r;
+            const bool tie = __builtin_fabs(t - r) == 0.5;
+            const bool cross = Pn <= -0x1p53;
+            if (tie || cross) {                           // rare, divergent
+                const int pos = (int)(i + q - b);
+                if (nsp == 2) {
+                    tail = pos;
                     continue;
                 }
+                if (nsp == 0) { A0 = acc; V0 = x; c0 = pos; }
+                else { A1 = acc; V1 = x; c1 = pos; }
+                acc = 0.0;
+                if (cross) {
+                    xm |= 1 << nsp;
+                    u *= 0.5;
+                    P = Pn * 0.5;
+                } else {
+                    P = Pn;
+                }
+                ++nsp;
+                continue;
             }
-            const uint64_t tf0 = stats ? __builtin_readcyclecounter() : 0;
-            s = fold_seq_lane8(cb, sb, se, s);
-            ++folded;
-            if (stats) stats[4] += (uint32_t)(__builtin_readcyclecounter() - tf0);
+            P = Pn;
+            acc += r;
         }
-        if (stats) {
-            stats[0] += 64;
-            stats[1] += folded;
-            stats[2] += (uint32_t)(tp1 - tp0);
-            stats[3] += (uint32_t)(__builtin_readcyclecounter() - tp1);
+        i += m;
+    }
+    const int E = (flag || bad) ? 0 : be;
+    // 3. the in-order walk over the segments
+    double s = run;
+    const uint64_t tp1 = stats ? __builtin_readcyclecounter() : 0;
+    uint32_t folded = 0;
+    for (int l = 0; l < 64; ++l) {
+        uint32_t sb, se;
+        split_bounds(k, n, L, l, sb, se);
+        if (sb >= se) break;
+        int el = __builtin_amdgcn_readlane(E, l);
+        uint32_t pos = sb;                                // first value not yet added
+        if (el != 0) {
+            const int np = __builtin_amdgcn_readlane(nsp, l);
+            const int xl = __builtin_amdgcn_readlane(xm, l);
+            bool done = false;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                if (q > np) break;
+                if (!((int)((as_u64(s) >> 52) & 0x7ffu) == el && s < 0.0)) break;
+                const double Ap = q == 0 ? (np == 0 ? readlane_f64(acc, l) : readlane_f64(A0, l))
+                                         : (q == 1 ? (np == 1 ? readlane_f64(acc, l) : readlane_f64(A1, l))
+                                                   : readlane_f64(acc, l));
+                const double S = s * as_f64((uint64_t)(2098 - el) << 52) + Ap;
+                if (!(S > -0x1p53)) break;
+                s = S * as_f64((uint64_t)(el - 52) << 52);
+                if (q == np) {
+                    const int tl = __builtin_amdgcn_readlane(tail, l);
+                    pos = tl < 0 ? se : sb + (uint32_t)tl;
+                    done = true;
+                    break;
+                }
+                s = s + readlane_f64(q == 0 ? V0 : V1, l);
+                pos = sb + (uint32_t)__builtin_amdgcn_readlane(q == 0 ? c0 : c1, l) + 1u;
+                if ((xl >> q) & 1) ++el;
+            }
+            if (done && pos == se) continue;
         }
+        s = fold_seq_lane8(cb, pos, se, s);
+        ++folded;
+    }
+    if (stats) {
+        stats[0] += 64;
+        stats[1] += folded;
+        stats[2] += (uint32_t)(tp1 - tp0);
+        stats[3] += (uint32_t)(__builtin_readcyclecounter() - tp1);
     }
     return s;
 }
 
 template <int KIND, bool kWide>
-__global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t ntot,
-                                                        const double* __restrict__ vals,
-                                                        const uint64_t* __restrict__ bits, ScoreOut out) {
+__global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
+                                                        const uint8_t* __restrict__ inc, double T0, double T1,
+                                                        uint32_t pad0, uint32_t ntot, ListBits lb, FlagBand fbm,
+                                                        FlagBand fbl, ScoreOut out) {
     __shared__ double cbuf[2][kLoBlock];
     __shared__ uint32_t ccnt[2][kLoChunks];                // inliers per chunk
     __shared__ uint32_t coff[2][kLoChunks + 1];            // exclusive prefix; [kLoChunks] = block total
@@ -1985,44 +1985,73 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint64_t below = (1ull << lane) - 1ull;
     constexpr int kChains = KIND == 2 ? 2 : 1;
-    const double* mv = vals + (size_t)mi * ntot;
-    const uint64_t* mb = bits + (size_t)mi * ntot / 64;
     const uint32_t nchunks = ntot / 64;
     const uint32_t cb0 = pad0 / 64;                        // first class-1 chunk (nchunks: none)
     const uint32_t nblk = (nchunks + kLoChunks - 1) / kLoChunks;
     double run = 0.0, hold = 0.0;
     uint32_t cnt0 = 0, cntall = 0;
-    // flagged decisions (k_lo_values' flag planes: MSAC, list predicate),
-    // counted before the fold (the block loop's barriers order them)
+    const auto m = models[mi];
+    const bool live = inc == nullptr || inc[mi] <= 101;   // a slot without a model scores zeros
+    // flagged decisions (the MSAC test's and the list predicate's, exact.h),
+    // counted during the block loop (its barriers order them); the model's
+    // value constants (a twin sincos for KIND 2) once per workgroup
     __shared__ uint32_t fcnt[2];
+    __shared__ ValueConst vc_sh;
     if (t < 2) fcnt[t] = 0;
+    if constexpr (KIND <= 2)
+        if (t == 0) vc_sh = value_const(m, KIND == 1, KIND == 2);
     __syncthreads();
-    {
-        const size_t plane = (size_t)gridDim.x * ntot / 64;
-        const uint64_t* fw = bits + plane + (size_t)mi * ntot / 64;
-        uint32_t a = 0, l = 0;
-        for (uint32_t c = (uint32_t)t; c < nchunks; c += kLoThreads) {
-            a += (uint32_t)__builtin_popcountll(fw[c]);
-            l += (uint32_t)__builtin_popcountll(fw[plane + c]);
-        }
-        if (a) atomicAdd(&fcnt[0], a);
-        if (l) atomicAdd(&fcnt[1], l);
-    }
     for (uint32_t b = 0; b < nblk; ++b) {
         const uint32_t ch0 = b * kLoChunks;
         const uint32_t nch = min(kLoChunks, nchunks - ch0);
         double* cb = cbuf[b & 1];
         uint32_t* cc = ccnt[b & 1];
         uint32_t* co = coff[b & 1];
-        // 1) this wave's chunks j = wave + 16 i: values and ballot words
+        // 1) this wave's chunks j = wave + 16 i: every (model, feature) pair's
+        //    residual, -r^2 or +0.0, its MSAC ballot word, the LO list
+        //    predicate's ballot (launch_mask's rule) into pinned memory, and
+        //    the decisions within the value-glibc bound of their thresholds
         double v[kLoPer];
         uint64_t w[kLoPer];
+        uint32_t nfm = 0, nfl = 0;
 #pragma unroll
         for (int i = 0; i < kLoPer; ++i) {
             const uint32_t j = (uint32_t)wave + 16u * i;
-            const uint32_t q = j < nch ? j : 0u;
-            v[i] = mv[(size_t)(ch0 + q) * 64 + lane];
-            w[i] = mb[ch0 + q];
+            const uint32_t jj = (ch0 + (j < nch ? j : 0u)) * 64u + (uint32_t)lane;   // pair index
+            const int cls = jj < pad0 ? 0 : 1;                // chunk-uniform (pad0 % 64 == 0)
+            const uint32_t fi = cls == 0 ? jj : jj - pad0;
+            const DevClass& c = p.cls[cls];
+            const bool ev = live && j < nch && fi < c.n;
+            double r2 = 0.0;
+            if (ev) {
+                if constexpr (KIND >= 3) {
+                    r2 = geo_sq_residual<KIND>(c.x[fi], c.y[fi], c.a[fi], c.c0[fi], m.h);
+                } else if (cls == 0) {
+                    r2 = scale_sq_value<KIND == 1, true>(c.x[fi], c.y[fi], c.a[fi], m, vc_sh.ac, vc_sh.cut);
+                } else {
+                    r2 = orient_sq_value<true>(c.x[fi], c.y[fi], c.c0[fi], c.c1[fi], m, vc_sh.c, vc_sh.s, vc_sh.cphi,
+                                               vc_sh.cphi2);
+                }
+            }
+            const bool inl = ev && r2 <= (cls == 0 ? T0 : T1);
+            v[i] = inl ? -r2 : 0.0;
+            w[i] = __ballot(inl);
+            const bool lin = lb.bits != nullptr && ev && mask_rule(r2, lb.rule, cls == 0 ? lb.T[0] : lb.T[1], lb.lambda);
+            const uint64_t lbw = __ballot(lin);
+            if (j < nch && lane == 0) {
+                const size_t wi = (size_t)mi * nchunks + ch0 + j;
+                if (lb.bits != nullptr) lb.bits[wi] = lbw;
+                if (lb.mbits != nullptr) lb.mbits[wi] = w[i];
+            }
+            if constexpr (KIND <= 2) {
+                nfm += (uint32_t)__builtin_popcountll(__ballot(ev && in_flag_band(r2, fbm.mid[cls], fbm.half[cls])));
+                nfl += (uint32_t)__builtin_popcountll(
+                    __ballot(ev && lb.bits != nullptr && in_flag_band(r2, fbl.mid[cls], fbl.half[cls])));
+            }
+        }
+        if (KIND <= 2 && lane == 0) {
+            if (nfm) atomicAdd(&fcnt[0], nfm);
+            if (nfl) atomicAdd(&fcnt[1], nfl);
         }
 #pragma unroll
         for (int i = 0; i < kLoPer; ++i) {
@@ -2081,7 +2110,7 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(uint32_t pad0, uint32_t
                     cc = 0.0;
                 }
                 const uint32_t kb = ps < 2 ? 0u : bpos, ke = ps < 2 ? bpos : total;
-                const double r = fold_exact_seg(cb, kb, ke, (ps & 1) ? tt : cc, lane);
+                const double r = fold_exact_split(cb, kb, ke, (ps & 1) ? tt : cc, lane);
                 if (ps & 1) tt = r; else cc = r;
             }
             run = (KIND == 2 && lane == 1) ? tt : cc;
@@ -3533,25 +3562,22 @@ size_t small_score_pairs(const DevProblem& p) {
 }
 
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
-                              uint32_t nm, const ScoreOut& out, double* vals, uint64_t* bits, hipStream_t stream,
-                              const ListBits* lists) {
+                              uint32_t nm, const ScoreOut& out, hipStream_t stream, const ListBits* lists) {
     const ListBits lb = lists ? *lists : ListBits{{0.0, 0.0}, 0, 0.0, nullptr, nullptr};
     if (nm == 0) return hipSuccess;
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t ntot = (uint32_t)small_score_pairs(p);
     if (ntot == 0) return hipErrorInvalidValue;
-    const dim3 ga((ntot + 255) / 256, nm), ba(256);
     auto go = [&](auto ktag) {
         constexpr int KIND = decltype(ktag)::value;
         using M = typename ModelOf<KIND>::type;
-        hipLaunchKernelGGL(k_lo_values<KIND>, ga, ba, 0, stream, p, static_cast<const M*>(models), inc, T[0], T[1],
-                           pad0, ntot, vals, bits, lb, flag_band(T), flag_band(lb.T));
+        const M* mp = static_cast<const M*>(models);
         if (lo_fold_wide())
-            hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals, bits,
-                               out);
+            hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1],
+                               pad0, ntot, lb, flag_band(T), flag_band(lb.T), out);
         else
-            hipLaunchKernelGGL((k_lo_chain<KIND, false>), dim3(nm), dim3(kLoThreads), 0, stream, pad0, ntot, vals,
-                               bits, out);
+            hipLaunchKernelGGL((k_lo_chain<KIND, false>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0],
+                               T[1], pad0, ntot, lb, flag_band(T), flag_band(lb.T), out);
     };
     switch (p.solver) {
         case 0: go(std::integral_constant<int, 0>{}); break;
@@ -3578,7 +3604,7 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
     return hipGetLastError();
 }
 
-// op 7 of gcr_debug_math: out[0] = fold_exact_seg over a[0, n) from +0.0,
+// op 7 of gcr_debug_math: out[0] = fold_exact_split over a[0, n) from +0.0,
 // out[1] = the same sum by one lane's sequential loop (one wave).  For
 // n <= kLoBlock both run over an LDS copy (as in k_lo_chain) and out[2..5] =
 // cycles of the segment fold, cycles of the one-lane fold, segments, segments
@@ -3594,7 +3620,7 @@ __global__ __launch_bounds__(64) void k_fold_test(const double* __restrict__ a, 
     const double* v = lds ? buf : a;
     uint32_t st[5] = {0, 0, 0, 0, 0};
     const uint64_t t0 = __builtin_readcyclecounter();
-    const double w = fold_exact_seg(v, 0, n, 0.0, lane, st);
+    const double w = fold_exact_split(v, 0, n, 0.0, lane, st);
     const uint64_t t1 = __builtin_readcyclecounter();
     double s = 0.0;
     if (lane == 0) s = lds ? fold_seq_lane(buf, 0, n, 0.0) : 0.0;

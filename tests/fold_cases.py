@@ -1,5 +1,5 @@
 """Value sequences for the exact wave-parallel fold tests (k_lo_chain's
-fold_exact_wave): the reference adds MSAC terms one by one in fp64
+fold_exact_split): the reference adds MSAC terms one by one in fp64
 (MSAC_scoring_function.hpp:53-107), so every case is checked against the
 sequential left-to-right sum (np.add.accumulate)."""
 import numpy as np

@@ -1,4 +1,4 @@
-"""Device check of k_lo_chain's wave-parallel exact fold (fold_exact_wave,
+"""Device check of k_lo_chain's wave-parallel exact fold (fold_exact_split,
 gcr_debug_math op 7) against the sequential fp64 sum on adversarial sequences
 (ties at every scale, binade crossings, zeros, subnormals, huge values, inf,
 NaN, lengths around the 64-lane batch), and the small-batch scorer with the
