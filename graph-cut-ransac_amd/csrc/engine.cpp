@@ -1414,6 +1414,10 @@ public:
         const char* e = getenv("GCR_LO_REUSE");            // read per run
         return !(e && e[0] == '0');
     }
+    static bool lo_cache_check_on() {
+        const char* e = getenv("GCR_LO_CACHE_CHECK");      // read per run
+        return e && e[0] == '1';
+    }
 
     // GCR_SPEC_TRIM=0: speculate even when the chunk's best member already
     // ends the run inside it
@@ -1991,6 +1995,17 @@ public:
                 lists[1] = lo_cache_.lists[1];
                 have_lists = true;
                 bufs_[off_] = Buffer{true, best_model_, {lo_cache_.raw[0], lo_cache_.raw[1]}};
+                if (lo_cache_check_on()) {
+                    // the rescore the cache replaces, compared bit for bit
+                    HScore s;
+                    uint32_t rn[2];
+                    std::vector<uint32_t> rl[2];
+                    const bool bits = score_models(&best_val_, 1, &s, rn, &msac, &best_model_) && !sm_lbad_[0];
+                    if (bits) list_of(0, rl);
+                    const bool same = std::memcmp(&s, &best_, sizeof(HScore)) == 0 && rn[0] == lo_cache_.raw[0] &&
+                                      rn[1] == lo_cache_.raw[1] && (!bits || (rl[0] == lists[0] && rl[1] == lists[1]));
+                    if (!same) throw std::runtime_error("LO cache differs from the refit's rescore (GCR_LO_CACHE_CHECK)");
+                }
             } else if (diff) {
                 HScore s;
                 uint32_t rn[2];
@@ -2169,9 +2184,12 @@ private:
     Buffer bufs_[2];
     int off_ = 0;
     uint64_t lo_number_ = 0, gc_number_ = 0;
-    // the last adopted LO winner: its score, raw counts and the inlier lists
-    // of its scoring launch (LO rule 0 with Tlo, two-class problems), so the
-    // final refit need not rescore it when Tlo equals the MSAC threshold
+    // the last adopted LO winner: its score, raw counts and MSAC inlier lists
+    // (threshold Tm) from its own small-scorer launch, which scored it with Tm
+    // and mirrored its MSAC ballots (ListReq::msac) -- any estimator, whenever
+    // that launch returned bits and none of the model's MSAC decisions was
+    // flagged (lo_lists_from_bits_); the final refit then need not rescore it.
+    // GCR_LO_CACHE_CHECK=1 rescores anyway and requires bit-identical results.
     struct LoCache {
         bool valid = false;
         Model model{};

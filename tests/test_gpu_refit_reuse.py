@@ -1,9 +1,11 @@
-"""Reuse of scoring launches.  The final refit reuses the adopted LO winner's score, raw counts and
-inlier lists from its own scoring launch when the LO lists used the MSAC
-threshold itself (two-class problems: Tlo = (1.5 thr)^2 and Tm = (2.25 thr)
-thr rounding alike, rule 0), instead of rescoring it (GCRANSAC.h:628-675).
-Runs must be identical with and without the reuse (GCR_LO_REUSE=0), and
-equal to the oracle (covered by the golden and end-to-end tests)."""
+"""Reuse of scoring launches.  The final refit reuses the adopted LO winner's
+score, raw counts and MSAC inlier lists from its own small-scorer launch
+(which scored it with the MSAC threshold and mirrored its MSAC ballots),
+instead of rescoring it (GCRANSAC.h:628-675) -- for every estimator, unless
+one of the winner's MSAC decisions was flagged for the glibc recheck.  Runs
+must be identical with and without the reuse (GCR_LO_REUSE=0), the check mode
+(GCR_LO_CACHE_CHECK=1) rescores and requires bit-identical score, counts and
+lists, and runs equal the oracle (the golden and end-to-end tests)."""
 import numpy as np
 import pytest
 
@@ -30,6 +32,25 @@ def test_refit_reuse_equals_rescore(n, seed, conf, monkeypatch):
     b = _run(fs, fo, ts, to, seed, conf)
     assert a == b
     assert a[0] is not None and a[4] > 0
+    monkeypatch.setenv("GCR_LO_REUSE", "1")
+    monkeypatch.setenv("GCR_LO_CACHE_CHECK", "1")
+    assert _run(fs, fo, ts, to, seed, conf) == a
+
+
+@pytest.mark.parametrize("kind", ["m1", "h", "f"])
+def test_refit_reuse_check_mode_other_estimators(kind, monkeypatch):
+    # the cache is used by every estimator: the check mode's rescore agrees
+    monkeypatch.setenv("GCR_LO_CACHE_CHECK", "1")
+    if kind == "m1":
+        f, _, thr = S.problem_m1(4000, seed=21)
+        out = pygcransac.findRectifyingHomographyScaleOnly(f, thr, 0.0, 0, 10**6, 50, seed=3, confidence=0.99)
+    elif kind == "h":
+        c, _, _, thr = S.problem_h(3000, 0.5, seed=22)
+        out = pygcransac.findHomography(c, 960, 1280, 960, 1280, threshold=thr, conf=0.99, seed=3)
+    else:
+        c, _, _, thr = S.problem_f(3000, 0.6, seed=23)
+        out = pygcransac.findFundamentalMatrix(c, 960, 1280, 960, 1280, threshold=thr, conf=0.99, seed=3)
+    assert out[0] is not None
 
 
 @pytest.mark.parametrize("budget", ["fixed", "adaptive", "tiny", "floor"])

@@ -286,6 +286,23 @@ def test_two_point_cells_closed_form_equals_bk(tmp_path):
     assert "mismatches 0" in out.stdout
 
 
+def test_scheduled_labeling_equals_serial(tmp_path):
+    # the engine's path: gc_schedule's cost-balanced jobs (largest cells
+    # first, q written per cell) in schedule order, reversed, shuffled and on
+    # 4 threads give the serial driver's labeling bit for bit (random
+    # clustered 4-D grids, ties at the truncated threshold, 5 pool sizes)
+    import os
+    import subprocess
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = str(tmp_path / "gc_jobs")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-pthread",
+                           os.path.join(here, "cpp", "gc_jobs.cpp"), "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches 0" in out.stdout
+
+
 def test_frozen_tie_fixtures():
     # tests/golden/graphcut_ties.json (tools/gen_gc_ties.py, written once, never
     # regenerated): labeling() calls whose energies tie on purpose (residuals
