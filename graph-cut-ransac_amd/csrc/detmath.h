@@ -115,7 +115,7 @@ GCR_HD double log_tab_core(uint64_t ix, int32_t kadj) {
     constexpr uint64_t kOff = 0x3fe5f00000000000ull;
     const uint64_t tmp = ix - kOff;
     const uint32_t i = (uint32_t)(tmp >> 45) & 127u;
-    const int32_t k = (int32_t)((int64_t)tmp >> 52) + kadj;
+    const int32_t k = ((int32_t)(uint32_t)(tmp >> 32) >> 20) + kadj;   // the exponent of x / OFF (32-bit ops)
     const double z = as_f64(ix - (tmp & 0xfff0000000000000ull));
     const double invc = kLogTab[2 * i], logc = kLogTab[2 * i + 1];
     const double r = fma_rn(z, invc, -1.0);                 // z / c - 1, one rounding
