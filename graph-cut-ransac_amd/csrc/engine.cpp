@@ -3609,6 +3609,23 @@ void gcr_host_homography(const gcr_rect_model* m, double* H_out) {
 double gcr_host_log(double x) { return dm::dm_log(x); }
 double gcr_host_pow_m3(double t) { return dm::dm_pow_m3(t); }
 double gcr_host_atan2(double y, double x) { return dm::dm_atan2(y, x); }
+int gcr_host_residuals(int solver, int cls, const double* features, size_t n, const gcr_rect_model* model, int arith,
+                       double* r2_out) {
+    if (solver < 0 || solver > 2 || cls < 0 || cls > (solver == 2 ? 1 : 0) || !model || (n && (!features || !r2_out)))
+        return set_err(GCR_EINVAL, "bad residual request");
+    return guard([&]() -> int {
+        gcr_problem P;
+        P.solver = solver;
+        P.K = solver == 2 ? 2 : 1;
+        // the features as class `cls` (fill_host_classes: glibc pow / sincos)
+        fill_host_classes(solver, features, cls == 0 ? n : 0, features, cls == 1 ? n : 0, P.hc);
+        const RectModel m{model->x0, model->y0, model->s, model->h7, model->h8, model->alpha, model->phi};
+        const ValueConst vc = value_const(m, solver == 1, cls == 1);
+        for (size_t i = 0; i < n; ++i)
+            r2_out[i] = arith == 0 ? host_value(&P, cls, i, m, vc) : host_r2<GlibcMath>(&P, cls, i, m);
+        return GCR_OK;
+    });
+}
 double gcr_host_math(int op, double a, double b) {
     double sn, cs;
     switch (op) {

@@ -184,6 +184,8 @@ def _load():
     L.gcr_host_weighted_mode.restype = C.c_double
     L.gcr_host_homography.argtypes = [C.POINTER(RectModel), dp]
     L.gcr_host_homography.restype = None
+    L.gcr_host_residuals.argtypes = [C.c_int, C.c_int, dp, C.c_size_t, C.POINTER(RectModel), C.c_int, dp]
+    L.gcr_host_residuals.restype = C.c_int
     return L
 
 

@@ -278,6 +278,13 @@ int gcr_host_fit_h(const double* correspondences, size_t n, const uint32_t* idx,
 int gcr_host_fit_f(const double* correspondences, size_t n, const uint32_t* idx, size_t k, double* F_out);
 /* host-only: RectifyingHomography::getHomography (model.h:211-226), row-major */
 void gcr_host_homography(const gcr_rect_model* model, double* H_out);
+/* host-only: squared residuals of one rectification model over n features of
+ * class `cls` (0 scale, 1 orientation; solver 0-2), rows as the entry points
+ * take them (x, y, scale | angle).  arith 0: the product's values (rect.h
+ * scale_sq_value / orient_sq_value, what the kernels evaluate and fold);
+ * 1: the reference's formulas in glibc (the decisions, exact.h). */
+int gcr_host_residuals(int solver, int cls, const double* features, size_t n, const gcr_rect_model* model, int arith,
+                       double* r2_out);
 /* host-only (no GPU): the graph-cut labeling's pieces (graphcut.h).
  * grid_edges: the neighbourhood grid's edges over n points of `dims` (<= 4)
  * row-major coordinates in labeling()'s order (GCRANSAC.h:821-857,
