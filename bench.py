@@ -51,19 +51,23 @@ CLOCK_GHZ = 2.4                # MI355X peak engine clock (spec)
 # VALU issue ceiling: one wave64 VALU instruction per SIMD every 4 cycles (16
 # lanes per cycle; full-rate fp64 on CDNA4), in G wave-instructions/s
 VALU_ISSUE_PEAK = N_SIMD * CLOCK_GHZ / 4.0
-# Issue cost of one wave64 VALU instruction on its SIMD, in cycles, per
-# SQ_INSTS_VALU_* class (MI355X_MICROARCH.md constants table 'vector-instruction
-# ISSUE cost': f32 add / fma 4, f32 transcendentals 8; the rest measured by
-# tools/micro/valu_issue.hip, profiles/r4_valu_issue.log).  Instructions in no
-# class (moves, selects, compares, bit ops, DPP, readlane) cost OTHER.
+# Issue cycles per wave64 VALU instruction on one SIMD (SQ_INSTS_VALU_* class)
+# at the scorers' occupancy (4 waves per SIMD; one wave alone issues every
+# ~6.4 cycles, the guide's constants table quotes 4 for f32), measured by tools/micro/valu_issue.hip on
+# MI355X (profiles/r4_valu_issue.log: 16 independent chains per wave, per-SIMD
+# cycles at 4 waves): f64 add / mul / fma 3.03, v_rcp_f64 / v_sqrt_f64 10.5,
+# f32 add 2.02, f32 fma / pk_fma 2.97-3.03, f32 transcendentals 5.48, u32 add
+# 2.13, cvt_f64_i32 3.20.  MUL_F32 is taken as ADD_F32 and INT64 (64-bit
+# shifts / adds) as the f64 ALU rate (not measured); the other VALU
+# instructions (moves, compares, selects, bit ops) at the 32-bit rate.
 VALU_CLASS_COST = {
-    "SQ_INSTS_VALU_ADD_F32": 4.0, "SQ_INSTS_VALU_MUL_F32": 4.0, "SQ_INSTS_VALU_FMA_F32": 4.0,
-    "SQ_INSTS_VALU_TRANS_F32": 8.0,
-    "SQ_INSTS_VALU_ADD_F64": 4.0, "SQ_INSTS_VALU_MUL_F64": 4.0, "SQ_INSTS_VALU_FMA_F64": 4.0,
-    "SQ_INSTS_VALU_TRANS_F64": 16.0,
-    "SQ_INSTS_VALU_INT32": 4.0, "SQ_INSTS_VALU_INT64": 4.0, "SQ_INSTS_VALU_CVT": 4.0,
+    "SQ_INSTS_VALU_ADD_F32": 2.02, "SQ_INSTS_VALU_MUL_F32": 2.02, "SQ_INSTS_VALU_FMA_F32": 2.97,
+    "SQ_INSTS_VALU_TRANS_F32": 5.48,
+    "SQ_INSTS_VALU_ADD_F64": 3.03, "SQ_INSTS_VALU_MUL_F64": 3.03, "SQ_INSTS_VALU_FMA_F64": 3.03,
+    "SQ_INSTS_VALU_TRANS_F64": 10.53,
+    "SQ_INSTS_VALU_INT32": 2.13, "SQ_INSTS_VALU_INT64": 3.03, "SQ_INSTS_VALU_CVT": 3.20,
 }
-VALU_OTHER_COST = 4.0
+VALU_OTHER_COST = 2.13
 
 
 def weighted_issue_cycles(pmc):

@@ -1797,8 +1797,7 @@ __device__ __forceinline__ double fold_seq_lane(const double* __restrict__ cb, u
     return run;
 }
 
-// fold_seq_lane with batches of 8 (fewer registers; for the short flagged
-// segments of fold_exact_split)
+// fold_seq_lane with batches of 8 (fewer registers: short ranges)
 __device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, uint32_t k, const uint32_t e,
                                                  double run) {
     for (; k + 8 <= e; k += 8) {
@@ -1812,165 +1811,176 @@ __device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, 
     return run;
 }
 
-// fold_exact_split: the same in-order sum (bit-identical to the sequential
-// loop) by segments.  Lane 0 takes the first kSplitL0 values (usually folded
-// value by value from the chain's start), lane l > 0 the l-th of 63 equal
-// contiguous segments after them (odd length: the 64 lanes' LDS reads hit
-// distinct banks).
-//  1. Approximate segment sums and a DPP scan give every segment an
-//     approximate start g and so its binade E (ulp U); a segment that starts
-//     at a zero / positive / tiny sum, or whose approximate end lies more
-//     than two binades further, is flagged.
-//  2. Each lane adds rint(v / U) over its segment (integer sums below 2^53
-//     are exact in any order).  While the running sum s stays in one binade,
-//     fl(s + v) = s + U rint(v / U) -- except for a tie (v / U ending in
-//     exactly .5: round-to-even then depends on s) and for the value whose
-//     addition leaves the binade (predicted from g).  Up to two such special
-//     values split the segment into parts; after a crossing the part's
-//     increments are taken at 2U.  A third special ends the segment's fast
-//     path there (the tail).  Positive, NaN or too large values flag it.
-//  3. The walk (all lanes alike, records by readlane): for each part, when the
-//     exact running sum lies in the part's binade, one exact addition s + U I
-//     (both multiples of U; the check S > -2^53 keeps every partial sum in the
-//     binade, the sums being monotone), then the special value by an ordinary
-//     addition; any failed check, and the tail, fold the rest of the segment
-//     value by value (fold_seq_lane8).
-// tests/test_fold.py restates it in numpy (segment for segment);
-// tests/test_gpu_fold.py runs it against the sequential sum.
-constexpr uint32_t kSplitL0 = 16;
+// fold_exact_block: the same in-order sum by all kLoThreads threads of the
+// workgroup (every thread calls it, in uniform control flow; it holds
+// barriers).  The first kBlkHead values are added one by one (the sum is still
+// small there); thread t takes the t-th of kLoThreads contiguous chunks of the
+// rest.  A block scan of approximate chunk sums gives every chunk an
+// approximate start; walking its chunk with an approximate running sum, a
+// thread adds the integer increments rint(v / U) (U the ulp of the binade the
+// running sum is predicted to be in) and marks as special every value whose
+// addition is predicted to leave the binade, and every tie (v / U ending in
+// exactly .5).  Specials are numbered in sequence order (a block scan of the
+// per-thread counts); the parts between consecutive specials are runs: run
+// r's increments are summed over all threads with LDS atomics (exact:
+// integers of one sign, below 2^53 whenever the run is valid), its binade
+// recorded.  Wave 0 then walks the runs: s + U A_r as one exact addition when
+// the exact running sum lies in run r's binade and the result stays in it,
+// then special r by an ordinary addition; the first failed check folds the
+// rest value by value.  A positive / NaN / too large value, a run whose parts
+// disagree on the binade, more than two specials in a chunk or more than
+// kBlkSpecials in all fold the whole range value by value.  Returns the sum on
+// every thread.  tests/test_fold.py restates it in numpy (fold_exact_block).
+constexpr uint32_t kBlkHead = 16;
+constexpr int kBlkSpecials = 63;
 
-__device__ __forceinline__ void split_bounds(uint32_t k, uint32_t n, uint32_t L, int lane, uint32_t& b, uint32_t& e) {
-    if (lane == 0) {
-        b = k;
-        e = k + min(n, kSplitL0);
-    } else {
-        const uint32_t o = min(n, kSplitL0 + (uint32_t)(lane - 1) * L);
-        b = k + o;
-        e = k + min(n, o + L);
-    }
-}
+struct BlkFoldScratch {
+    double wsum[kLoThreads / 64];           // wave totals (approximate chunk sums)
+    uint32_t wcnt[kLoThreads / 64];         // wave totals of the special counts
+    double runA[kBlkSpecials + 1];
+    int runEmin[kBlkSpecials + 1], runEmax[kBlkSpecials + 1];
+    double specV[kBlkSpecials];
+    uint32_t specPos[kBlkSpecials];
+    uint32_t bad, nspec;
+    double head, result;
+};
 
-__device__ __forceinline__ double fold_exact_split(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
-                                                   double run, const int lane, uint32_t* stats = nullptr) {
+__device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
+                                                   const double run, BlkFoldScratch& sc) {
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t n = e - k;
-    if (n < 512) return fold_seq_lane8(cb, k, e, run);   // short: every lane alike
-    const uint64_t tp0 = stats ? __builtin_readcyclecounter() : 0;
-    const uint32_t L = ((n - kSplitL0 + 62) / 63) | 1u;
-    uint32_t b, ee;
-    split_bounds(k, n, L, lane, b, ee);
-    // 1. approximate sums (8 reads in flight per batch), approximate starts
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    uint32_t i = b;
-    for (; i + 8 <= ee; i += 8) {
-        double t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = cb[i + u];
-        a0 += t[0] + t[4];
-        a1 += t[1] + t[5];
-        a2 += t[2] + t[6];
-        a3 += t[3] + t[7];
+    if (n < kBlkHead + kLoThreads / 4) {                  // short: one lane's fold, broadcast
+        if (t == 0) sc.result = fold_seq_lane8(cb, k, e, run);
+        __syncthreads();
+        const double r = sc.result;
+        __syncthreads();
+        return r;
     }
-    for (; i < ee; ++i) a0 += cb[i];
-    const double a = (a0 + a1) + (a2 + a3);
-    const double X = wave_incl_scan_f64(a);
-    const double g = run + (X - a);                       // approximate start
-    const int be = (int)((as_u64(g) >> 52) & 0x7ffu);
-    const int bend = (int)((as_u64(g + a) >> 52) & 0x7ffu);
-    const bool flag = !(g < 0.0) || be < 53 || be >= 0x7fd || bend > be + 2;
-    const int bs = flag ? 1075 : be;                      // a harmless scale for flagged segments
-    // 2. integer increments in up to three parts
-    double u = as_f64((uint64_t)(2098 - bs) << 52);       // 1 / U
-    double P = g * u;                                     // approximate running sum in units of U
+    if (t <= kBlkSpecials) {
+        sc.runA[t] = 0.0;
+        sc.runEmin[t] = 0x7fffffff;
+        sc.runEmax[t] = -1;
+    }
+    if (t == 0) {
+        sc.bad = 0;
+        sc.head = fold_seq_lane8(cb, k, k + kBlkHead, run);   // exact; also the approximate start
+    }
+    // 1. approximate chunk sums, block exclusive scan
+    const uint32_t rest = n - kBlkHead;
+    const uint32_t m = (rest + kLoThreads - 1) / kLoThreads;
+    const uint32_t b = k + kBlkHead + min(rest, (uint32_t)t * m), ee = k + kBlkHead + min(rest, (uint32_t)t * m + m);
+    double a = 0.0;
+    for (uint32_t i = b; i < ee; ++i) a += cb[i];
+    const double xin = wave_incl_scan_f64(a);
+    if (lane == 63) sc.wsum[wave] = xin;
+    __syncthreads();
+    double wpre = 0.0;
+    for (int w = 0; w < wave; ++w) wpre += sc.wsum[w];
+    double P = sc.head + (wpre + (xin - a));              // approximate start of the chunk
+    // 2. integer increments in up to three parts (two specials)
     double acc = 0.0, A0 = 0.0, A1 = 0.0, V0 = 0.0, V1 = 0.0;
-    int c0 = -1, c1 = -1, tail = -1, nsp = 0, xm = 0;
+    int E0 = 0, E1 = 0, nsp = 0;
+    uint32_t p0 = 0, p1 = 0;
     bool bad = false;
-    i = b;
-    while (i < ee && tail < 0) {
-        double t8[8];
-        const uint32_t m = min(8u, ee - i);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) t8[q] = cb[i + ((uint32_t)q < m ? (uint32_t)q : 0u)];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if ((uint32_t)q >= m || tail >= 0) continue;
-            const double x = t8[q];
-            const double t = x * u;
-            const double r = __builtin_rint(t);
-            bad |= !(x <= 0.0) | !(__builtin_fabs(t) < 0x1p53);
-            const double Pn = P + r;
-            const bool tie = __builtin_fabs(t - r) == 0.5;
-            const bool cross = Pn <= -0x1p53;
-            if (tie || cross) {                           // rare, divergent
-                const int pos = (int)(i + q - b);
-                if (nsp == 2) {
-                    tail = pos;
-                    continue;
-                }
-                if (nsp == 0) { A0 = acc; V0 = x; c0 = pos; }
-                else { A1 = acc; V1 = x; c1 = pos; }
-                acc = 0.0;
-                if (cross) {
-                    xm |= 1 << nsp;
-                    u *= 0.5;
-                    P = Pn * 0.5;
-                } else {
-                    P = Pn;
-                }
-                ++nsp;
-                continue;
-            }
-            P = Pn;
+    int be = (int)((as_u64(P) >> 52) & 0x7ffu);
+    for (uint32_t i = b; i < ee && !bad; ++i) {
+        const double x = cb[i];
+        be = (int)((as_u64(P) >> 52) & 0x7ffu);
+        if (!(P < 0.0) || be < 53 || be >= 0x7fe) { bad = true; break; }
+        const double tt = x * as_f64((uint64_t)(2098 - be) << 52);
+        const double r = __builtin_rint(tt);
+        if (!(x <= 0.0) || !(__builtin_fabs(tt) < 0x1p53)) { bad = true; break; }
+        const double Pn = P + x;
+        if (__builtin_fabs(tt - r) == 0.5 || (int)((as_u64(Pn) >> 52) & 0x7ffu) != be) {
+            if (nsp == 2) { bad = true; break; }
+            if (nsp == 0) { A0 = acc; E0 = be; V0 = x; p0 = i; }
+            else { A1 = acc; E1 = be; V1 = x; p1 = i; }
+            acc = 0.0;
+            ++nsp;
+        } else {
             acc += r;
         }
-        i += m;
+        P = Pn;
     }
-    const int E = (flag || bad) ? 0 : be;
-    // 3. the in-order walk over the segments
-    double s = run;
-    const uint64_t tp1 = stats ? __builtin_readcyclecounter() : 0;
-    uint32_t folded = 0;
-    for (int l = 0; l < 64; ++l) {
-        uint32_t sb, se;
-        split_bounds(k, n, L, l, sb, se);
-        if (sb >= se) break;
-        int el = __builtin_amdgcn_readlane(E, l);
-        uint32_t pos = sb;                                // first value not yet added
-        if (el != 0) {
-            const int np = __builtin_amdgcn_readlane(nsp, l);
-            const int xl = __builtin_amdgcn_readlane(xm, l);
-            bool done = false;
+    const int Elast = nsp > 0 ? (int)((as_u64(P) >> 52) & 0x7ffu) : be;
+    // 3. number the specials: block exclusive scan of the per-thread counts
+    uint32_t ci = (uint32_t)nsp;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                if (q > np) break;
-                if (!((int)((as_u64(s) >> 52) & 0x7ffu) == el && s < 0.0)) break;
-                const double Ap = q == 0 ? (np == 0 ? readlane_f64(acc, l) : readlane_f64(A0, l))
-                                         : (q == 1 ? (np == 1 ? readlane_f64(acc, l) : readlane_f64(A1, l))
-                                                   : readlane_f64(acc, l));
-                const double S = s * as_f64((uint64_t)(2098 - el) << 52) + Ap;
-                if (!(S > -0x1p53)) break;
-                s = S * as_f64((uint64_t)(el - 52) << 52);
-                if (q == np) {
-                    const int tl = __builtin_amdgcn_readlane(tail, l);
-                    pos = tl < 0 ? se : sb + (uint32_t)tl;
-                    done = true;
-                    break;
-                }
-                s = s + readlane_f64(q == 0 ? V0 : V1, l);
-                pos = sb + (uint32_t)__builtin_amdgcn_readlane(q == 0 ? c0 : c1, l) + 1u;
-                if ((xl >> q) & 1) ++el;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(ci, d);
+        if (lane >= d) ci += o;
+    }
+    if (lane == 63) sc.wcnt[wave] = ci;
+    if (bad) atomicOr(&sc.bad, 1u);
+    __syncthreads();
+    uint32_t base = ci - (uint32_t)nsp;
+    for (int w = 0; w < wave; ++w) base += sc.wcnt[w];
+    if (t == kLoThreads - 1) sc.nspec = base + (uint32_t)nsp;
+    const bool fits = base + (uint32_t)nsp <= (uint32_t)kBlkSpecials;
+    if (fits && !bad) {
+        // parts: run base (before special 1), base + 1, base + 2
+        auto part = [&](uint32_t r, double A, int E) {
+            if (A != 0.0) atomicAdd(&sc.runA[r], A);
+            atomicMin(&sc.runEmin[r], E);
+            atomicMax(&sc.runEmax[r], E);
+        };
+        if (nsp == 0) {
+            part(base, acc, Elast);
+        } else {
+            part(base, A0, E0);
+            sc.specV[base] = V0;
+            sc.specPos[base] = p0;
+            if (nsp == 1) {
+                part(base + 1, acc, Elast);
+            } else {
+                part(base + 1, A1, E1);
+                sc.specV[base + 1] = V1;
+                sc.specPos[base + 1] = p1;
+                part(base + 2, acc, Elast);
             }
-            if (done && pos == se) continue;
         }
-        s = fold_seq_lane8(cb, pos, se, s);
-        ++folded;
     }
-    if (stats) {
-        stats[0] += 64;
-        stats[1] += folded;
-        stats[2] += (uint32_t)(tp1 - tp0);
-        stats[3] += (uint32_t)(__builtin_readcyclecounter() - tp1);
+    __syncthreads();
+    // 4. the walk (wave 0; the running sum wave-uniform, decisions on its
+    //    high word in a scalar register)
+    if (wave == 0) {
+        auto hi_s = [](double v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(as_u64(v) >> 32)); };
+        double s = sc.head;
+        uint32_t pos = k + kBlkHead;
+        const uint32_t nspec = sc.nspec;
+        const bool all_ok = sc.bad == 0 && nspec <= (uint32_t)kBlkSpecials;
+        if (all_ok) {
+            const uint32_t nr = nspec + 1;
+            // run r's record in lane r
+            const int rl = lane < (int)nr ? lane : 0;
+            const double rA = sc.runA[rl];
+            const int rE = sc.runEmin[rl] == sc.runEmax[rl] ? sc.runEmin[rl] : 0;
+            const double rV = lane < (int)nspec ? sc.specV[lane] : 0.0;
+            const uint32_t rP = lane < (int)nspec ? sc.specPos[lane] : 0u;
+            uint32_t r = 0;
+            for (; r < nr; ++r) {
+                const uint32_t el = (uint32_t)__builtin_amdgcn_readlane(rE, (int)r);
+                if (el == 0u || (hi_s(s) >> 20) != (0x800u | el)) break;   // s < 0 in binade el
+                const double S = s * as_f64((uint64_t)(2098 - el) << 52) + readlane_f64(rA, (int)r);
+                if ((hi_s(S) >> 20) != 0xc33u) break;                       // S in (-2^53, -2^52]
+                s = S * as_f64((uint64_t)(el - 52) << 52);
+                if (r + 1 < nr) {
+                    s = s + readlane_f64(rV, (int)r);
+                    pos = (uint32_t)__builtin_amdgcn_readlane((int)rP, (int)r) + 1u;
+                }
+            }
+            if (r == nr) pos = e;
+        } else {
+            s = run;
+            pos = k;
+        }
+        if (pos < e) s = fold_seq_lane(cb, pos, e, s);
+        if (lane == 0) sc.result = s;
     }
-    return s;
+    __syncthreads();
+    const double res = sc.result;
+    __syncthreads();                                      // the scratch is reused by the next call
+    return res;
 }
 
 template <int KIND, bool kWide>
@@ -1990,6 +2000,8 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
     const uint32_t nblk = (nchunks + kLoChunks - 1) / kLoChunks;
     double run = 0.0, hold = 0.0;
     uint32_t cnt0 = 0, cntall = 0;
+    double wcc = 0.0, wtt = 0.0, whold = 0.0;             // kWide: the chains, uniform in every thread
+    __shared__ BlkFoldScratch bsc;
     const auto m = models[mi];
     const bool live = inc == nullptr || inc[mi] <= 101;   // a slot without a model scores zeros
     // flagged decisions (the MSAC test's and the list predicate's, exact.h),
@@ -2082,39 +2094,44 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             if (j < nch && ((w[i] >> lane) & 1ull)) cb[co[j] + (uint32_t)__builtin_popcountll(w[i] & below)] = v[i];
         }
         __syncthreads();
-        // 4) wave 0 folds the block; the other waves go on to the next
-        //    block's loads (the other buffer set: this one is rewritten only
-        //    after the next block's barriers, which wave 0 reaches once this
-        //    fold is done).  KIND 2: lane 0 restarts at the first class-1 value.
-        if (wave != 0) continue;
+        // 4) the block's fold.  kWide: every wave takes part in the
+        //    block-parallel exact fold (fold_exact_block, barriers inside).
+        //    Otherwise wave 0 folds the block one value per step while the
+        //    other waves go on to the next block's loads (the other buffer
+        //    set: this one is rewritten only after the next block's barriers,
+        //    which wave 0 reaches once this fold is done).  KIND 2: the class
+        //    chain restarts at the first class-1 value.
         const uint32_t total = co[kLoChunks];
         const bool has_b = cb0 >= ch0 && cb0 < ch0 + nch;
         const uint32_t bpos = cb0 < ch0 ? 0u : (has_b ? co[cb0 - ch0] : total);   // values before class 1
-        cnt0 += bpos;
-        cntall += total;
         if constexpr (kWide) {
-            // whole-wave exact folds, one call site (register pressure): the
-            // class sum (lane 0's chain) and, for KIND 2, the running total
-            // (lane 1's), which before the class boundary is the same sum
-            double cc = __shfl(run, 0), tt = __shfl(run, 1);
-            const bool same = as_u64(cc) == as_u64(tt);
+            // the class sum and, for KIND 2, the running total, which before
+            // the class boundary is the same sum (uniform in every thread)
+            cnt0 += bpos;
+            cntall += total;
+            const bool same = as_u64(wcc) == as_u64(wtt);
 #pragma unroll 1
             for (int ps = 0; ps < 4; ++ps) {
                 // 0: class-0 part of the class chain; 1: of the total (KIND 2,
                 // when it differs); 2: class-1 part of the class chain (after
                 // the boundary's restart); 3: of the total (KIND 2)
                 if ((ps == 1 || ps == 3) && KIND != 2) continue;
-                if (ps == 1 && same) { tt = cc; continue; }
+                if (ps == 1 && same) { wtt = wcc; continue; }
                 if (ps == 2 && KIND == 2 && has_b) {
-                    hold = cc;                       // lane 0 keeps it (uniform value)
-                    cc = 0.0;
+                    whold = wcc;
+                    wcc = 0.0;
                 }
                 const uint32_t kb = ps < 2 ? 0u : bpos, ke = ps < 2 ? bpos : total;
-                const double r = fold_exact_split(cb, kb, ke, (ps & 1) ? tt : cc, lane);
-                if (ps & 1) tt = r; else cc = r;
+                if (kb == ke) continue;
+                const double r = fold_exact_block(cb, kb, ke, (ps & 1) ? wtt : wcc, bsc);
+                if (ps & 1) wtt = r; else wcc = r;
             }
-            run = (KIND == 2 && lane == 1) ? tt : cc;
-        } else {
+            continue;
+        }
+        if (wave != 0) continue;
+        cnt0 += bpos;
+        cntall += total;
+        {
             // one-lane folds: lane 0 the class sum, lane 1 (KIND 2) the total
             auto fold = [&](uint32_t k, uint32_t e) {
                 if (lane >= kChains) return;
@@ -2159,6 +2176,10 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             }
             fold(bpos, total);
         }
+    }
+    if constexpr (kWide) {
+        run = (KIND == 2 && lane == 1) ? wtt : wcc;
+        hold = whold;
     }
     if (wave == 0) {
         const double tot = KIND == 2 ? __shfl(run, 1) : run;
@@ -3604,40 +3625,38 @@ hipError_t launch_mask(const DevProblem& p, int cls, const RectModel& model, int
     return hipGetLastError();
 }
 
-// op 7 of gcr_debug_math: out[0] = fold_exact_split over a[0, n) from +0.0,
-// out[1] = the same sum by one lane's sequential loop (one wave).  For
-// n <= kLoBlock both run over an LDS copy (as in k_lo_chain) and out[2..5] =
-// cycles of the segment fold, cycles of the one-lane fold, segments, segments
-// folded value by value, cycles of the parallel part, of the walk, of the
-// walk's value-by-value folds (n >= 9).
-__global__ __launch_bounds__(64) void k_fold_test(const double* __restrict__ a, uint32_t n, double* out) {
+// op 7 of gcr_debug_math: out[0] = fold_exact_block over a[0, n) from +0.0
+// (one kLoThreads workgroup), out[1] = the same sum by one lane's sequential
+// loop.  For n <= kLoBlock both run over an LDS copy (as in k_lo_chain) and
+// out[2..5] = cycles of the block fold, cycles of the one-lane fold, the
+// number of special values, whether any fallback occurred (n >= 6).
+__global__ __launch_bounds__(kLoThreads) void k_fold_test(const double* __restrict__ a, uint32_t n, double* out) {
     __shared__ double buf[kLoBlock];
-    const int lane = threadIdx.x;
+    __shared__ BlkFoldScratch bsc;
+    const int t = threadIdx.x;
     const bool lds = n <= kLoBlock;
     if (lds)
-        for (uint32_t i = lane; i < n; i += 64) buf[i] = a[i];
+        for (uint32_t i = t; i < n; i += kLoThreads) buf[i] = a[i];
     __syncthreads();
     const double* v = lds ? buf : a;
-    uint32_t st[5] = {0, 0, 0, 0, 0};
     const uint64_t t0 = __builtin_readcyclecounter();
-    const double w = fold_exact_split(v, 0, n, 0.0, lane, st);
+    const double w = fold_exact_block(v, 0, n, 0.0, bsc);
     const uint64_t t1 = __builtin_readcyclecounter();
     double s = 0.0;
-    if (lane == 0) s = lds ? fold_seq_lane(buf, 0, n, 0.0) : 0.0;
-    if (lane == 0 && !lds)
-        for (uint32_t k = 0; k < n; ++k) s = s + v[k];
+    if (t == 0) {
+        if (lds) s = fold_seq_lane(buf, 0, n, 0.0);
+        else
+            for (uint32_t k = 0; k < n; ++k) s = s + v[k];
+    }
     const uint64_t t2 = __builtin_readcyclecounter();
-    if (lane == 0) {
+    if (t == 0) {
         out[0] = w;
         out[1] = s;
-        if (lds && n >= 9) {                  // out holds n doubles
+        if (lds && n >= 6) {                  // out holds n doubles
             out[2] = (double)(t1 - t0);
             out[3] = (double)(t2 - t1);
-            out[4] = st[0];
-            out[5] = st[1];
-            out[6] = st[2];
-            out[7] = st[3];
-            out[8] = st[4];
+            out[4] = (double)bsc.nspec;
+            out[5] = (double)bsc.bad;
         }
     }
 }
@@ -3646,7 +3665,7 @@ hipError_t launch_math(int op, const double* a, const double* b, size_t n, doubl
     if (n == 0) return hipSuccess;
     if (op == 7) {
         if (n < 2 || n > 0xffffffffull) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_fold_test, dim3(1), dim3(64), 0, stream, a, (uint32_t)n, out);
+        hipLaunchKernelGGL(k_fold_test, dim3(1), dim3(kLoThreads), 0, stream, a, (uint32_t)n, out);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_math, dim3(blocks_for(n, 256)), dim3(256), 0, stream, op, a, b, n, out);

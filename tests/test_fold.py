@@ -1,39 +1,19 @@
-"""The segment-parallel exact fold (kernels.hip fold_exact_split, used by
-k_lo_chain under GCR_LO_FOLD=wide) restated in numpy, segment for segment:
-a 16-value first segment and 63 equal ones; approximate segment sums and a
-DPP-order scan give each segment a binade; each segment adds rint(v / ulp)
-as exact integers in parts separated by up to two special values (binade
-crossings, ties); an in-order walk adds each part in one exact fp64 addition
-and each special value on its own, and folds value by value wherever a check
-fails.  Checked against the sequential fp64 sum the reference computes
-(MSAC_scoring_function.hpp:53-107) on adversarial sequences; the device
-kernel itself is checked against the same sequences in
-tests/test_gpu_fold.py."""
+"""The block-parallel exact fold (kernels.hip fold_exact_block, used by
+k_lo_chain under GCR_LO_FOLD=wide) restated in numpy, chunk for chunk: a
+16-value head added one by one, 1024 chunks whose integer increments
+rint(v / ulp) are summed exactly per run of one binade, runs separated by the
+special values (predicted binade crossings, ties) that the walk adds on their
+own; the walk folds value by value wherever a check fails.  Checked against
+the sequential fp64 sum the reference computes (MSAC_scoring_function.hpp:
+53-107) on adversarial sequences; the device kernel itself is checked against
+the same sequences in tests/test_gpu_fold.py.  (Round 3's segment fold and
+round 4's first split fold were replaced by this one; git history.)"""
 import math
 
 import numpy as np
 import pytest
 
 from fold_cases import cases, sequential
-
-
-def _scan(x):
-    """wave_incl_scan_f64's DPP order: row shifts 1, 2, 4, 8, then the row
-    broadcasts of lanes 15 (into rows 1, 3) and 31 (into rows 2, 3)."""
-    x = np.asarray(x, dtype=np.float64).copy()
-    lanes = np.arange(64)
-    for n in (1, 2, 4, 8):
-        moved = np.zeros(64)
-        ok = (lanes % 16) >= n
-        moved[ok] = x[lanes[ok] - n]
-        x = x + moved
-    moved = np.zeros(64)
-    moved[16:32] = x[15]
-    moved[48:64] = x[47]
-    x = x + moved
-    moved = np.zeros(64)
-    moved[32:64] = x[31]
-    return x + moved
 
 
 def _fold_seq(v, s):
@@ -46,169 +26,152 @@ def _exp(x):
     return (int(np.float64(x).view(np.uint64)) >> 52) & 0x7ff
 
 
-# ------------------------------------------------------------------ round 4 --
-# fold_exact_split (kernels.hip): the segment fold with up to two "special"
-# values per segment handled exactly -- a binade crossing (predicted from the
-# approximate start) or a tie (a value whose increment ends in exactly .5 ulp,
-# where round-to-even depends on the running sum's parity).  A short first
-# segment (16 values, usually folded value by value from the chain's start),
-# 63 segments after it.  Phase 2 adds the integer increments at the
-# segment's ulp U in parts separated by the specials (2U after a crossing);
-# the walk applies each part in one exact addition and each special by an
-# ordinary addition, each verified against the exact running sum; a failed
-# check, or a third special, folds the rest of the segment value by value.
-L0_SPLIT = 16
-MAX_SPECIAL = 2
+# --------------------------------------------------------- round 4: block ----
+# fold_exact_block (kernels.hip): the in-order sum by all 1024 threads of a
+# workgroup.  The first BLK_HEAD values are added one by one (the sum is still
+# small there); thread t then takes the t-th of 1024 contiguous chunks of the
+# rest.  A block scan of approximate chunk sums gives every chunk an
+# approximate start; walking its chunk with an approximate running sum, a
+# thread adds the integer increments rint(v / U) (U the ulp of the binade the
+# running sum is predicted to be in) and marks as special every value whose
+# addition is predicted to leave the binade, and every tie.  Specials are
+# numbered in sequence order (a block scan of the per-thread counts); the
+# parts between consecutive specials are runs: run r's integer increments are
+# summed over all threads (exact: integers of one sign below 2^53), its binade
+# recorded.  One wave then walks the runs: s + U * A_r in one exact addition
+# when the exact running sum lies in run r's binade and the result stays in it,
+# then special r by an ordinary addition; the first failed check folds the rest
+# value by value.  Any positive, NaN or too large value, a run whose parts
+# disagree on the binade, more than BLK_SPECIALS specials or more than two in
+# one chunk fold the whole sequence value by value.
+BLK_THREADS = 1024
+BLK_HEAD = 16
+BLK_SPECIALS = 64
 
 
-def _seg_bounds(n, lane):
-    L = ((n - L0_SPLIT + 62) // 63) | 1
-    if lane == 0:
-        return 0, min(n, L0_SPLIT)
-    b = min(n, L0_SPLIT + (lane - 1) * L)
-    return b, min(n, b + L)
+def _ulp_scale(be):
+    return math.ldexp(1.0, 1075 - be)
 
 
-def _ldexp(e):
-    return math.ldexp(1.0, e)
-
-
-def _phase2(seg, g, be, flag):
-    """One lane's records: parts A[0..k], specials (index, value, crossing?),
-    tail index (-1: none), validity."""
-    bs = 1075 if flag else be
-    iU = _ldexp(1075 - bs)
-    P = g * iU
-    mode = 0
-    acc = 0.0
-    A, SPI, SPV, SPX = [], [], [], []
-    tail = -1
-    bad = False
-    for j, x in enumerate(seg):
-        x = float(x)
-        t = x * (iU * 0.5 ** mode)
-        r = float(np.rint(t))
-        if not (x <= 0.0) or not (abs(t) < 2.0 ** 53):
-            bad = True
-        tie = abs(t - r) == 0.5
-        cross = P + r <= -2.0 ** 53
-        if tie or cross:
-            if len(SPI) == MAX_SPECIAL:
-                tail = j
-                break
-            A.append(acc)
-            acc = 0.0
-            SPI.append(j)
-            SPV.append(x)
-            SPX.append(cross)
-            if cross:
-                mode += 1
-                P = (P + r) * 0.5
-            else:
-                P = P + r
-            continue
-        P = P + r
-        acc = acc + r
-    A.append(acc)
-    return A, SPI, SPV, SPX, tail, not (flag or bad)
-
-
-def fold_exact_split(v, run=0.0, stats=None):
-    """kernels.hip fold_exact_split, segment for segment (stats: counts of
-    the walk's paths: "fast" whole segments, "slow" value by value from the
-    segment start, "tail" value by value from a later point)."""
-    st = {"fast": 0, "tail": 0, "slow": 0, "specials": 0}
+def fold_exact_block(v, run=0.0, stats=None):
     v = np.asarray(v, dtype=np.float64)
     n = v.size
-    if n < 512:
+    st = {"runs": 0, "specials": 0, "fallback": None}
+    if n < BLK_HEAD + BLK_THREADS // 4:
         return _fold_seq(v, run)
-    a = np.zeros(64)
-    rec = []
+    head = _fold_seq(v[:BLK_HEAD], run)                   # exact (thread 0)
+    ahead = _fold_seq(v[:BLK_HEAD], run)                  # the approximate start is the same value here
+    rest = n - BLK_HEAD
+    m = (rest + BLK_THREADS - 1) // BLK_THREADS
+    bounds = [(BLK_HEAD + min(rest, t * m), BLK_HEAD + min(rest, t * m + m)) for t in range(BLK_THREADS)]
     with np.errstate(over="ignore", invalid="ignore"):
-        for lane in range(64):
-            b, e = _seg_bounds(n, lane)
-            seg = v[b:e]
-            acc = np.zeros(4)
-            m = seg.size - seg.size % 4
-            for q in range(0, m, 4):
-                acc = acc + seg[q:q + 4]
-            acc[0] = _fold_seq(seg[m:], acc[0])
-            a[lane] = (acc[0] + acc[1]) + (acc[2] + acc[3])
-        X = _scan(a)
-        for lane in range(64):
-            b, e = _seg_bounds(n, lane)
-            g = run + (X[lane] - a[lane])
-            be, bend = _exp(g), _exp(g + a[lane])
-            flag = not (g < 0.0) or be < 53 or be >= 0x7fd or bend > be + MAX_SPECIAL
-            rec.append((be,) + _phase2(v[b:e], g, be, flag))
-    s = run
-    for lane in range(64):
-        b, e = _seg_bounds(n, lane)
-        if b >= e:
-            break
-        be, A, SPI, SPV, SPX, tail, ok = rec[lane]
+        a = np.array([_fold_seq(v[b:e], 0.0) for b, e in bounds])
+        X = np.concatenate([[0.0], np.cumsum(a)[:-1]])    # exclusive scan (any order: approximate)
+        parts, specials, bad = [], [], False
+        for t, (b, e) in enumerate(bounds):
+            P = ahead + X[t]
+            acc = 0.0
+            loc = []
+            be = _exp(P)
+            for j in range(b, e):
+                x = float(v[j])
+                be = _exp(P)
+                if not (P < 0.0) or be < 53 or be >= 0x7fe:
+                    bad = True
+                    break
+                t_ = x * _ulp_scale(be)
+                r = float(np.rint(t_))
+                if not (x <= 0.0) or not (abs(t_) < 2.0 ** 53):
+                    bad = True
+                    break
+                Pn = P + x
+                if abs(t_ - r) == 0.5 or _exp(Pn) != be:
+                    loc.append((acc, be, j, x))
+                    acc = 0.0
+                else:
+                    acc = acc + r
+                P = Pn
+            if bad:
+                break
+            if len(loc) > 2:
+                bad = True
+                break
+            # parts: before special 1, between, after the last (binade of each)
+            pb = [(p[0], p[1]) for p in loc] + [(acc, _exp(P) if loc else be)]
+            parts.append(pb)
+            specials.extend((j, x) for (_, _, j, x) in loc)
+        if bad or len(specials) > BLK_SPECIALS:
+            st["fallback"] = "all"
+            if stats is not None:
+                stats.update(st)
+            return _fold_seq(v, run)
+        nr = len(specials) + 1
+        runA = [0.0] * nr
+        runE = [set() for _ in range(nr)]
+        rid = 0
+        for pb in parts:
+            for q, (A, e) in enumerate(pb):
+                runA[rid] += A
+                if not (A == 0.0 and q == len(pb) - 1 and False):
+                    runE[rid].add(e)
+                if q < len(pb) - 1:
+                    rid += 1
+    s = head
+    pos = BLK_HEAD
+    for r in range(nr):
+        E = runE[r]
+        ok = len(E) == 1
+        if ok:
+            el = next(iter(E))
+            ok = _exp(s) == el and s < 0.0
+        if ok:
+            S = s * _ulp_scale(el) + runA[r]
+            ok = S > -2.0 ** 53
         if not ok:
-            s = _fold_seq(v[b:e], s)
-            st["slow"] += 1
-            continue
-        el = be
-        pos = b                       # first value not yet added
-        done = False
-        for q in range(len(A)):
-            if not (_exp(s) == el and s < 0.0):
-                break
-            S = s * _ldexp(1075 - el) + A[q]
-            if not (S > -2.0 ** 53):
-                break
-            s = S * _ldexp(el - 1075)
-            if q == len(SPI):
-                pos = e if tail < 0 else b + tail
-                done = True
-                break
-            s = s + SPV[q]
+            st["fallback"] = r
+            s = _fold_seq(v[pos:], s)
+            break
+        s = S * math.ldexp(1.0, el - 1075)
+        st["runs"] += 1
+        if r < nr - 1:
+            j, x = specials[r]
+            s = s + x
             st["specials"] += 1
-            pos = b + SPI[q] + 1
-            if SPX[q]:
-                el = el + 1
-        if done and pos == e:
-            st["fast"] += 1
-            continue
-        st["slow" if pos == b else "tail"] += 1
-        s = _fold_seq(v[pos:e], s)
+            pos = j + 1
     if stats is not None:
         stats.update(st)
     return s
 
 
 @pytest.mark.parametrize("name", sorted(cases()))
-def test_split_fold_restatement_equals_sequential_sum(name):
+def test_block_fold_restatement_equals_sequential_sum(name):
     v = cases()[name]
     for run in (0.0, -3.0, float(sequential(v[: len(v) // 3]))):
-        got = fold_exact_split(v, run)
+        got = fold_exact_block(v, run)
         ref = _fold_seq(v, run)
         assert np.float64(got).tobytes() == np.float64(ref).tobytes() or (ref != ref and got != got), (got, ref)
 
 
-def test_split_fold_restatement_random_prefixes():
-    rng = np.random.default_rng(12)
-    for _ in range(120):
-        n = int(rng.integers(1, 3000))
+def test_block_fold_restatement_random():
+    rng = np.random.default_rng(14)
+    for _ in range(60):
+        n = int(rng.integers(1, 9000))
         scale = 10.0 ** rng.uniform(-8, 8)
         v = -rng.uniform(0, scale, n)
-        if rng.random() < 0.5:                       # quantised values: frequent ties
+        if rng.random() < 0.5:
             v = np.round(v / scale * 64) * scale / 64
         run = 0.0 if rng.random() < 0.5 else -float(rng.uniform(0, scale * n))
-        assert np.float64(fold_exact_split(v, run)).tobytes() == np.float64(_fold_seq(v, run)).tobytes()
+        assert np.float64(fold_exact_block(v, run)).tobytes() == np.float64(_fold_seq(v, run)).tobytes()
 
 
-def test_split_fold_fast_paths_dominate_msac_sums():
-    """On MSAC-like sums (the LO trial scores, 2500-5000 inliers) every
-    segment but the first takes an exact fast path, the ones crossing a
-    binade or holding a tie included (those values added on their own)."""
-    rng = np.random.default_rng(13)
-    for n, run in ((5000, 0.0), (2500, 0.0), (2500, -1400.0)):
+def test_block_fold_fast_on_msac_sums():
+    """MSAC-like sums (LO trial scores): no fallback, one run per binade the
+    sum passes through plus the tie-free crossings."""
+    rng = np.random.default_rng(15)
+    for n, run in ((5000, 0.0), (2500, 0.0), (2500, -1400.0), (8000, 0.0)):
         v = -rng.uniform(0, 2.25, n)
         st = {}
-        got = fold_exact_split(v, run, st)
+        got = fold_exact_block(v, run, st)
         assert np.float64(got).tobytes() == np.float64(_fold_seq(v, run)).tobytes()
-        assert st["slow"] <= 1 and st["tail"] <= 1 and st["specials"] >= 1, st
+        assert st["fallback"] is None, st
+        assert st["runs"] <= 24, st

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Cycle counts of k_lo_chain's two in-order folds over an LDS copy of one
-value sequence (gcr_debug_math op 7): the segment-parallel exact fold and the
-one-lane batched fold, on MSAC-like sequences (-r^2 of inliers)."""
+value sequence (gcr_debug_math op 7): the block-parallel exact fold
+(fold_exact_block, one 1024-thread workgroup) and the one-lane batched fold,
+on MSAC-like sequences (-r^2 of inliers)."""
 import ctypes as C
 import os
 import sys
@@ -17,7 +18,7 @@ def run(v):
     out = np.zeros(max(16, v.size))
     dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
     N.check(N.lib.gcr_debug_math(N.context(0), 7, dp(v), None, v.size, dp(out)))
-    return out[:9]
+    return out[:6]
 
 
 rng = np.random.default_rng(1)
@@ -32,6 +33,5 @@ for name, v in cases.items():
     for _ in range(2):
         o = run(v)
     same = o[0].tobytes() == o[1].tobytes()
-    print(f"{name:22s} n={v.size:5d} wide {o[2]:9.0f} cyc  seq {o[3]:9.0f} cyc  ratio {o[3] / o[2]:5.2f}  "
-          f"segments {o[4]:4.0f}  folded one by one {o[5]:4.0f}  parallel {o[6]:7.0f} cyc  walk {o[7]:7.0f} cyc (folds {o[8]:7.0f})  "
-          f"equal {same}")
+    print(f"{name:22s} n={v.size:5d} block {o[2]:9.0f} cyc  seq {o[3]:9.0f} cyc  ratio {o[3] / o[2]:5.2f}  "
+          f"specials {o[4]:4.0f}  fallback {o[5]:1.0f}  equal {same}")

@@ -22,7 +22,8 @@ import bench  # noqa: E402
 import pygcransac  # noqa: E402
 from pygcransac import _native as N  # noqa: E402
 
-KEYS = ("ms_setup", "ms_score", "ms_replay", "ms_lo", "ms_lo_lists", "ms_lo_fit", "ms_lo_score", "ms_refit_fit",
+KEYS = ("ms_setup", "ms_score", "ms_replay", "ms_lo", "ms_lo_lists", "ms_lo_fit", "ms_lo_score", "ms_refit_fit", "ms_exact",
+        "exact_models", "exact_pairs",
         "ms_refit", "ms_total")
 
 
@@ -78,7 +79,7 @@ def main():
         summary[name] = {"median_ms": statistics.median(ms), "mean_ms": statistics.fmean(ms), "n": len(ms),
                          "breakdown_median": bd}
         print(f"{a.workload} {name:>10}: median {statistics.median(ms):.3f} ms  mean {statistics.fmean(ms):.3f}  " +
-              " ".join(f"{k[3:]}={v:.3f}" for k, v in bd.items()), flush=True)
+              " ".join(f"{k[3:] if k.startswith('ms_') else k}={v:.3f}" for k, v in bd.items()), flush=True)
     if a.json:
         with open(a.json, "w") as f:
             json.dump({"workload": text, "settings": dict(sets), "summary": summary,
