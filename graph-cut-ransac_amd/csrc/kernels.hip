@@ -1747,6 +1747,37 @@ __device__ __forceinline__ double wave_incl_scan_f64(double x) {
     x = x + dpp_f64<0x143, 0xc>(x);     // row_bcast:31 into rows 2, 3
     return x;
 }
+// the same DPP pattern for 32-bit integers
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
+    x += dpp_u32<0x111, 0xf>(x);
+    x += dpp_u32<0x112, 0xf>(x);
+    x += dpp_u32<0x114, 0xf>(x);
+    x += dpp_u32<0x118, 0xf>(x);
+    x += dpp_u32<0x142, 0xa>(x);
+    x += dpp_u32<0x143, 0xc>(x);
+    return x;
+}
+// segmented inclusive scan: lanes with equal key (non-decreasing over the
+// wave) form the segments; each lane gets the sum over its segment up to it
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double seg_step(double x, uint32_t key) {
+    const double y = dpp_f64<CTRL, ROWS>(x);
+    const uint32_t k = dpp_u32<CTRL, ROWS>(key);
+    return k == key ? x + y : x;
+}
+__device__ __forceinline__ double wave_seg_scan_f64(double x, uint32_t key) {
+    x = seg_step<0x111, 0xf>(x, key);
+    x = seg_step<0x112, 0xf>(x, key);
+    x = seg_step<0x114, 0xf>(x, key);
+    x = seg_step<0x118, 0xf>(x, key);
+    x = seg_step<0x142, 0xa>(x, key);
+    x = seg_step<0x143, 0xc>(x, key);
+    return x;
+}
 __device__ __forceinline__ double readlane_f64(double x, int l) {
     const uint64_t u = as_u64(x);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
@@ -1764,7 +1795,7 @@ constexpr int kLoPer = kLoChunks / (kLoThreads / 64); // chunks per wave per blo
 // (sched_barrier keeps the scheduler from sinking the reads back next to
 // their adds).
 __device__ __forceinline__ double fold_seq_lane(const double* __restrict__ cb, uint32_t k, const uint32_t e,
-                                                double run) {
+                                                double run, const uint32_t cap = kLoBlock) {
     if (k + 32 <= e) {
         double ta[16], tb[16];
 #pragma unroll
@@ -1777,9 +1808,9 @@ __device__ __forceinline__ double fold_seq_lane(const double* __restrict__ cb, u
 #pragma unroll
             for (int u = 0; u < 16; ++u) run += ta[u];
             __builtin_amdgcn_sched_barrier(0);
-            // the batch after next (clamped inside the buffer: a clamped
-            // batch lies past e and is never added)
-            const uint32_t nx = min(k + 32, kLoBlock - 16);
+            // the batch after next (clamped inside the buffer of cap >= e
+            // values: a clamped batch lies past e and is never added)
+            const uint32_t nx = min(k + 32, cap - 16);
 #pragma unroll
             for (int u = 0; u < 16; ++u) ta[u] = cb[nx + u];
             __builtin_amdgcn_sched_barrier(0);
@@ -1833,6 +1864,7 @@ __device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, 
 // every thread.  tests/test_fold.py restates it in numpy (fold_exact_block).
 constexpr uint32_t kBlkHead = 16;
 constexpr int kBlkSpecials = 63;
+constexpr uint32_t kBlkMaxM = 16;                       // values per chunk, held in registers
 
 struct BlkFoldScratch {
     double wsum[kLoThreads / 64];           // wave totals (approximate chunk sums)
@@ -1846,10 +1878,11 @@ struct BlkFoldScratch {
 };
 
 __device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
-                                                   const double run, BlkFoldScratch& sc) {
+                                                   const double run, BlkFoldScratch& sc, const uint32_t cap) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t n = e - k;
-    if (n < kBlkHead + kLoThreads / 4) {                  // short: one lane's fold, broadcast
+    // short (one lane's fold, broadcast), or chunks too long for the registers
+    if (n < kBlkHead + kLoThreads / 4 || n - kBlkHead > kBlkMaxM * (uint32_t)kLoThreads) {
         if (t == 0) sc.result = fold_seq_lane8(cb, k, e, run);
         __syncthreads();
         const double r = sc.result;
@@ -1869,13 +1902,20 @@ __device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb
     const uint32_t rest = n - kBlkHead;
     const uint32_t m = (rest + kLoThreads - 1) / kLoThreads;
     const uint32_t b = k + kBlkHead + min(rest, (uint32_t)t * m), ee = k + kBlkHead + min(rest, (uint32_t)t * m + m);
+    // the chunk's values in registers (all reads in flight together)
+    double xv[kBlkMaxM];
+#pragma unroll
+    for (uint32_t q = 0; q < kBlkMaxM; ++q) xv[q] = b + q < ee ? cb[b + q] : 0.0;
     double a = 0.0;
-    for (uint32_t i = b; i < ee; ++i) a += cb[i];
+#pragma unroll
+    for (uint32_t q = 0; q < kBlkMaxM; ++q)
+        if (b + q < ee) a += xv[q];
     const double xin = wave_incl_scan_f64(a);
     if (lane == 63) sc.wsum[wave] = xin;
     __syncthreads();
-    double wpre = 0.0;
-    for (int w = 0; w < wave; ++w) wpre += sc.wsum[w];
+    // the earlier waves' totals: one read per lane, a row scan, one readlane
+    const double wps = wave_incl_scan_f64(sc.wsum[lane & 15]);
+    const double wpre = wave > 0 ? readlane_f64(wps, wave - 1) : 0.0;
     double P = sc.head + (wpre + (xin - a));              // approximate start of the chunk
     // 2. integer increments in up to three parts (two specials)
     double acc = 0.0, A0 = 0.0, A1 = 0.0, V0 = 0.0, V1 = 0.0;
@@ -1883,8 +1923,11 @@ __device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb
     uint32_t p0 = 0, p1 = 0;
     bool bad = false;
     int be = (int)((as_u64(P) >> 52) & 0x7ffu);
-    for (uint32_t i = b; i < ee && !bad; ++i) {
-        const double x = cb[i];
+#pragma unroll
+    for (uint32_t q = 0; q < kBlkMaxM; ++q) {
+        const uint32_t i = b + q;
+        if (i >= ee || bad) break;
+        const double x = xv[q];
         be = (int)((as_u64(P) >> 52) & 0x7ffu);
         if (!(P < 0.0) || be < 53 || be >= 0x7fe) { bad = true; break; }
         const double tt = x * as_f64((uint64_t)(2098 - be) << 52);
@@ -1904,40 +1947,45 @@ __device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb
     }
     const int Elast = nsp > 0 ? (int)((as_u64(P) >> 52) & 0x7ffu) : be;
     // 3. number the specials: block exclusive scan of the per-thread counts
-    uint32_t ci = (uint32_t)nsp;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(ci, d);
-        if (lane >= d) ci += o;
-    }
+    const uint32_t ci = wave_incl_scan_u32((uint32_t)nsp);
     if (lane == 63) sc.wcnt[wave] = ci;
     if (bad) atomicOr(&sc.bad, 1u);
     __syncthreads();
-    uint32_t base = ci - (uint32_t)nsp;
-    for (int w = 0; w < wave; ++w) base += sc.wcnt[w];
+    const uint32_t wcs = wave_incl_scan_u32(sc.wcnt[lane & 15]);
+    uint32_t base = ci - (uint32_t)nsp + (wave > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wcs, wave - 1) : 0u);
     if (t == kLoThreads - 1) sc.nspec = base + (uint32_t)nsp;
     const bool fits = base + (uint32_t)nsp <= (uint32_t)kBlkSpecials;
+    // the runs' increments.  Every thread's last part belongs to run
+    // R = base + nsp; those of consecutive lanes with equal R are summed by a
+    // segmented wave scan and added by the segment's last lane (one LDS atomic
+    // per run and wave, not per thread); the binade is reported by the
+    // segment's first and last lanes and by every lane whose binade differs
+    // from its left neighbour's (a run whose parts disagree then shows
+    // min != max).  The rare parts before a special are added one by one.
+    const uint32_t R = fits ? base + (uint32_t)nsp : 0xffffffffu;
+    const double seg = wave_seg_scan_f64(acc, R);
+    const uint32_t Rl = (uint32_t)__shfl_up((int)R, 1), Rr = (uint32_t)__shfl_down((int)R, 1);
+    const int El = __shfl_up(Elast, 1);
+    const bool first = lane == 0 || Rl != R, last = lane == 63 || Rr != R;
     if (fits && !bad) {
-        // parts: run base (before special 1), base + 1, base + 2
-        auto part = [&](uint32_t r, double A, int E) {
-            if (A != 0.0) atomicAdd(&sc.runA[r], A);
-            atomicMin(&sc.runEmin[r], E);
-            atomicMax(&sc.runEmax[r], E);
-        };
-        if (nsp == 0) {
-            part(base, acc, Elast);
-        } else {
-            part(base, A0, E0);
+        if (last && seg != 0.0) atomicAdd(&sc.runA[R], seg);
+        if (first || last || El != Elast) {
+            atomicMin(&sc.runEmin[R], Elast);
+            atomicMax(&sc.runEmax[R], Elast);
+        }
+        if (nsp > 0) {
+            if (A0 != 0.0) atomicAdd(&sc.runA[base], A0);
+            atomicMin(&sc.runEmin[base], E0);
+            atomicMax(&sc.runEmax[base], E0);
             sc.specV[base] = V0;
             sc.specPos[base] = p0;
-            if (nsp == 1) {
-                part(base + 1, acc, Elast);
-            } else {
-                part(base + 1, A1, E1);
-                sc.specV[base + 1] = V1;
-                sc.specPos[base + 1] = p1;
-                part(base + 2, acc, Elast);
-            }
+        }
+        if (nsp > 1) {
+            if (A1 != 0.0) atomicAdd(&sc.runA[base + 1], A1);
+            atomicMin(&sc.runEmin[base + 1], E1);
+            atomicMax(&sc.runEmax[base + 1], E1);
+            sc.specV[base + 1] = V1;
+            sc.specPos[base + 1] = p1;
         }
     }
     __syncthreads();
@@ -1974,7 +2022,7 @@ __device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb
             s = run;
             pos = k;
         }
-        if (pos < e) s = fold_seq_lane(cb, pos, e, s);
+        if (pos < e) s = fold_seq_lane(cb, pos, e, s, cap);
         if (lane == 0) sc.result = s;
     }
     __syncthreads();
@@ -1987,7 +2035,7 @@ template <int KIND, bool kWide>
 __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
                                                         const uint8_t* __restrict__ inc, double T0, double T1,
                                                         uint32_t pad0, uint32_t ntot, ListBits lb, FlagBand fbm,
-                                                        FlagBand fbl, ScoreOut out) {
+                                                        FlagBand fbl, ScoreOut out, uint32_t probe) {
     __shared__ double cbuf[2][kLoBlock];
     __shared__ uint32_t ccnt[2][kLoChunks];                // inliers per chunk
     __shared__ uint32_t coff[2][kLoChunks + 1];            // exclusive prefix; [kLoChunks] = block total
@@ -2009,14 +2057,22 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
     // value constants (a twin sincos for KIND 2) once per workgroup
     __shared__ uint32_t fcnt[2];
     __shared__ ValueConst vc_sh;
+    GCR_STAMP(0, 14u);
     if (t < 2) fcnt[t] = 0;
     if constexpr (KIND <= 2)
         if (t == 0) vc_sh = value_const(m, KIND == 1, KIND == 2);
     __syncthreads();
+    GCR_STAMP(1, 14u);
+    // kWide with at most 2 kLoBlock pairs (every inlier fits both buffers
+    // together): the blocks' inliers are appended to one LDS array and folded
+    // once at the end by the whole workgroup
+    const bool single = kWide && ntot <= 2u * kLoBlock;
+    double* const cball = &cbuf[0][0];
+    uint32_t boff = 0;                                     // single: inliers of the previous blocks
     for (uint32_t b = 0; b < nblk; ++b) {
         const uint32_t ch0 = b * kLoChunks;
         const uint32_t nch = min(kLoChunks, nchunks - ch0);
-        double* cb = cbuf[b & 1];
+        double* cb = single ? cball + boff : cbuf[b & 1];
         uint32_t* cc = ccnt[b & 1];
         uint32_t* co = coff[b & 1];
         // 1) this wave's chunks j = wave + 16 i: every (model, feature) pair's
@@ -2026,8 +2082,26 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
         double v[kLoPer];
         uint64_t w[kLoPer];
         uint32_t nfm = 0, nfl = 0;
+        // the features of chunk i + 1 are requested before chunk i is
+        // evaluated (branch-free loads, index clamped inside the class), so the
+        // L2 latency of one chunk hides behind the previous one's arithmetic
+        auto fetch = [&](int i, double (&f)[4]) {
+            const uint32_t j = (uint32_t)wave + 16u * i;
+            const uint32_t jj = (ch0 + (j < nch ? j : 0u)) * 64u + (uint32_t)lane;
+            const int cls = jj < pad0 ? 0 : 1;
+            const DevClass& c = p.cls[cls];
+            const uint32_t fi = cls == 0 ? jj : jj - pad0;
+            const uint32_t ic = fi < c.n ? fi : 0u;
+            f[0] = c.x[ic];
+            f[1] = c.y[ic];
+            f[2] = (KIND < 3 && cls == 1) ? c.c0[ic] : c.a[ic];
+            f[3] = KIND >= 3 ? c.c0[ic] : (cls == 1 ? c.c1[ic] : 0.0);
+        };
+        double fc[4], fn[4];
+        fetch(0, fc);
 #pragma unroll
         for (int i = 0; i < kLoPer; ++i) {
+            if (i + 1 < kLoPer) fetch(i + 1, fn);
             const uint32_t j = (uint32_t)wave + 16u * i;
             const uint32_t jj = (ch0 + (j < nch ? j : 0u)) * 64u + (uint32_t)lane;   // pair index
             const int cls = jj < pad0 ? 0 : 1;                // chunk-uniform (pad0 % 64 == 0)
@@ -2035,16 +2109,20 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             const DevClass& c = p.cls[cls];
             const bool ev = live && j < nch && fi < c.n;
             double r2 = 0.0;
-            if (ev) {
+            if (probe & 512u) {
+                r2 = ev ? 1e-3 * (double)(fi & 1023u) : 0.0;   // timing probe: no residual evaluation
+            } else if (ev) {
                 if constexpr (KIND >= 3) {
-                    r2 = geo_sq_residual<KIND>(c.x[fi], c.y[fi], c.a[fi], c.c0[fi], m.h);
+                    r2 = geo_sq_residual<KIND>(fc[0], fc[1], fc[2], fc[3], m.h);
                 } else if (cls == 0) {
-                    r2 = scale_sq_value<KIND == 1, true>(c.x[fi], c.y[fi], c.a[fi], m, vc_sh.ac, vc_sh.cut);
+                    r2 = scale_sq_value<KIND == 1, true>(fc[0], fc[1], fc[2], m, vc_sh.ac, vc_sh.cut);
                 } else {
-                    r2 = orient_sq_value<true>(c.x[fi], c.y[fi], c.c0[fi], c.c1[fi], m, vc_sh.c, vc_sh.s, vc_sh.cphi,
+                    r2 = orient_sq_value<true>(fc[0], fc[1], fc[2], fc[3], m, vc_sh.c, vc_sh.s, vc_sh.cphi,
                                                vc_sh.cphi2);
                 }
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fc[q] = fn[q];
             const bool inl = ev && r2 <= (cls == 0 ? T0 : T1);
             v[i] = inl ? -r2 : 0.0;
             w[i] = __ballot(inl);
@@ -2065,6 +2143,7 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             if (nfm) atomicAdd(&fcnt[0], nfm);
             if (nfl) atomicAdd(&fcnt[1], nfl);
         }
+        GCR_STAMP(0, b);
 #pragma unroll
         for (int i = 0; i < kLoPer; ++i) {
             const uint32_t j = (uint32_t)wave + 16u * i;
@@ -2087,6 +2166,7 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             if (lane == 63) co[kLoChunks] = inc;
         }
         __syncthreads();
+        GCR_STAMP(1, b);
         // 3) in-order compaction of the inlier values
 #pragma unroll
         for (int i = 0; i < kLoPer; ++i) {
@@ -2104,28 +2184,11 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
         const uint32_t total = co[kLoChunks];
         const bool has_b = cb0 >= ch0 && cb0 < ch0 + nch;
         const uint32_t bpos = cb0 < ch0 ? 0u : (has_b ? co[cb0 - ch0] : total);   // values before class 1
-        if constexpr (kWide) {
-            // the class sum and, for KIND 2, the running total, which before
-            // the class boundary is the same sum (uniform in every thread)
+        GCR_STAMP(2, b);
+        if (single) {
             cnt0 += bpos;
             cntall += total;
-            const bool same = as_u64(wcc) == as_u64(wtt);
-#pragma unroll 1
-            for (int ps = 0; ps < 4; ++ps) {
-                // 0: class-0 part of the class chain; 1: of the total (KIND 2,
-                // when it differs); 2: class-1 part of the class chain (after
-                // the boundary's restart); 3: of the total (KIND 2)
-                if ((ps == 1 || ps == 3) && KIND != 2) continue;
-                if (ps == 1 && same) { wtt = wcc; continue; }
-                if (ps == 2 && KIND == 2 && has_b) {
-                    whold = wcc;
-                    wcc = 0.0;
-                }
-                const uint32_t kb = ps < 2 ? 0u : bpos, ke = ps < 2 ? bpos : total;
-                if (kb == ke) continue;
-                const double r = fold_exact_block(cb, kb, ke, (ps & 1) ? wtt : wcc, bsc);
-                if (ps & 1) wtt = r; else wcc = r;
-            }
+            boff += total;
             continue;
         }
         if (wave != 0) continue;
@@ -2177,7 +2240,21 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             fold(bpos, total);
         }
     }
-    if constexpr (kWide) {
+    if (single && !(probe & 256u)) {
+        // the class sum and, for KIND 2, the running total: class 0 from +0,
+        // class 1 from +0 (the class chain's restart) and from the class-0 sum
+        GCR_STAMP(2, 14u);
+        const double c0 = fold_exact_block(cball, 0, cnt0, 0.0, bsc, 2 * kLoBlock);
+        GCR_STAMP(3, 14u);
+        if constexpr (KIND == 2) {
+            whold = c0;
+            wcc = fold_exact_block(cball, cnt0, cntall, 0.0, bsc, 2 * kLoBlock);
+            GCR_STAMP(4, 14u);
+            wtt = fold_exact_block(cball, cnt0, cntall, c0, bsc, 2 * kLoBlock);
+            GCR_STAMP(5, 14u);
+        } else {
+            wcc = c0;
+        }
         run = (KIND == 2 && lane == 1) ? wtt : wcc;
         hold = whold;
     }
@@ -3568,12 +3645,12 @@ hipError_t launch_select_batches(const WgBest* wg, size_t wg_stride, const RectM
 }
 
 
-// GCR_LO_FOLD=wide: k_lo_chain folds with the wave-parallel exact fold
-// instead of one lane per chain (read per launch; measured no faster, see
-// DESIGN.md)
+// k_lo_chain's fold: the block-parallel exact fold (default, round 4:
+// M2 latency 0.865 -> 0.836 ms on one box, profiles/r4_s7_lat.log) or, with
+// GCR_LO_FOLD=seq, one lane per chain (read per launch)
 bool lo_fold_wide() {
     const char* e = getenv("GCR_LO_FOLD");
-    return e && e[0] == 'w';
+    return !(e && e[0] == 's');
 }
 
 size_t small_score_pairs(const DevProblem& p) {
@@ -3593,12 +3670,13 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         constexpr int KIND = decltype(ktag)::value;
         using M = typename ModelOf<KIND>::type;
         const M* mp = static_cast<const M*>(models);
+        const uint32_t probe = probe_bits();               // GCR_PROBE bits 8 / 9: timing probes (results invalid)
         if (lo_fold_wide())
             hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1],
-                               pad0, ntot, lb, flag_band(T), flag_band(lb.T), out);
+                               pad0, ntot, lb, flag_band(T), flag_band(lb.T), out, probe);
         else
             hipLaunchKernelGGL((k_lo_chain<KIND, false>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0],
-                               T[1], pad0, ntot, lb, flag_band(T), flag_band(lb.T), out);
+                               T[1], pad0, ntot, lb, flag_band(T), flag_band(lb.T), out, probe);
     };
     switch (p.solver) {
         case 0: go(std::integral_constant<int, 0>{}); break;
@@ -3640,7 +3718,7 @@ __global__ __launch_bounds__(kLoThreads) void k_fold_test(const double* __restri
     __syncthreads();
     const double* v = lds ? buf : a;
     const uint64_t t0 = __builtin_readcyclecounter();
-    const double w = fold_exact_block(v, 0, n, 0.0, bsc);
+    const double w = fold_exact_block(v, 0, n, 0.0, bsc, lds ? kLoBlock : n);
     const uint64_t t1 = __builtin_readcyclecounter();
     double s = 0.0;
     if (t == 0) {

@@ -1,5 +1,5 @@
 """The block-parallel exact fold (kernels.hip fold_exact_block, used by
-k_lo_chain under GCR_LO_FOLD=wide) restated in numpy, chunk for chunk: a
+k_lo_chain by default) restated in numpy, chunk for chunk: a
 16-value head added one by one, 1024 chunks whose integer increments
 rint(v / ulp) are summed exactly per run of one binade, runs separated by the
 special values (predicted binade crossings, ties) that the walk adds on their
@@ -46,7 +46,8 @@ def _exp(x):
 # one chunk fold the whole sequence value by value.
 BLK_THREADS = 1024
 BLK_HEAD = 16
-BLK_SPECIALS = 64
+BLK_SPECIALS = 63
+BLK_MAXM = 16          # values per chunk held in registers (longer ranges: one by one)
 
 
 def _ulp_scale(be):
@@ -57,7 +58,7 @@ def fold_exact_block(v, run=0.0, stats=None):
     v = np.asarray(v, dtype=np.float64)
     n = v.size
     st = {"runs": 0, "specials": 0, "fallback": None}
-    if n < BLK_HEAD + BLK_THREADS // 4:
+    if n < BLK_HEAD + BLK_THREADS // 4 or n - BLK_HEAD > BLK_MAXM * BLK_THREADS:
         return _fold_seq(v, run)
     head = _fold_seq(v[:BLK_HEAD], run)                   # exact (thread 0)
     ahead = _fold_seq(v[:BLK_HEAD], run)                  # the approximate start is the same value here
@@ -168,7 +169,7 @@ def test_block_fold_fast_on_msac_sums():
     """MSAC-like sums (LO trial scores): no fallback, one run per binade the
     sum passes through plus the tie-free crossings."""
     rng = np.random.default_rng(15)
-    for n, run in ((5000, 0.0), (2500, 0.0), (2500, -1400.0), (8000, 0.0)):
+    for n, run in ((5000, 0.0), (2500, 0.0), (2500, -1400.0), (8000, 0.0), (16000, 0.0)):
         v = -rng.uniform(0, 2.25, n)
         st = {}
         got = fold_exact_block(v, run, st)

@@ -1,8 +1,9 @@
-"""Device check of k_lo_chain's wave-parallel exact fold (fold_exact_split,
+"""Device check of k_lo_chain's block-parallel exact fold (fold_exact_block,
 gcr_debug_math op 7) against the sequential fp64 sum on adversarial sequences
 (ties at every scale, binade crossings, zeros, subnormals, huge values, inf,
 NaN, lengths around the 64-lane batch), and the small-batch scorer with the
-wide fold (GCR_LO_FOLD=wide) against the default one-lane fold on every estimator."""
+default block fold against the one-lane fold (GCR_LO_FOLD=seq) on every
+estimator."""
 import ctypes as C
 
 import numpy as np
@@ -86,6 +87,20 @@ def _small_scores(kind, fold, monkeypatch):
 @pytest.mark.parametrize("kind", [N.SOLVER_SCALE3, N.SOLVER_SCALE3_ORIGINAL, N.SOLVER_SIFT22,
                                   N.SOLVER_HOMOGRAPHY4, N.SOLVER_FUNDAMENTAL7])
 def test_small_scorer_wide_fold_equals_one_lane_fold(kind, monkeypatch):
-    a = _small_scores(kind, "wide", monkeypatch)
-    b = _small_scores(kind, None, monkeypatch)
+    a = _small_scores(kind, None, monkeypatch)           # default: the block fold
+    b = _small_scores(kind, "seq", monkeypatch)
+    assert a == b
+
+
+def test_small_scorer_large_problem_keeps_per_block_folds(monkeypatch):
+    # more than 2 kLoBlock pairs: the default path folds block by block one
+    # value per step (the inliers no longer fit one LDS array)
+    monkeypatch.setenv("GCR_DEBUG_SCORER", "small")
+    fs, _, t0 = S.problem_m1(20000, seed=35)
+    prob = Problem(N.SOLVER_SCALE3, fs, None)
+    inc, models = prob.generate(29, 0, 128)
+    uniq = models[inc <= 101][:20]
+    a = b"".join(np.asarray(x).tobytes() for x in prob.score_raw(uniq, t0, 0.0))
+    monkeypatch.setenv("GCR_LO_FOLD", "seq")
+    b = b"".join(np.asarray(x).tobytes() for x in prob.score_raw(uniq, t0, 0.0))
     assert a == b

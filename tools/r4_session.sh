@@ -21,8 +21,8 @@ for s in $STEPS; do
     micro) run micro 120 ./tools/micro/valu_issue.bin ;;
     smoke) run smoke 300 python __graft_entry__.py ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
-    latm2) run latm2 300 python -u tools/lat_ab.py --workload m2 --reps 5 base: wide:GCR_LO_FOLD=wide ;;
-    latf)  run latf 300 python -u tools/lat_ab.py --workload f --reps 3 base: wide:GCR_LO_FOLD=wide ;;
+    latm2) run latm2 300 python -u tools/lat_ab.py --workload m2 --reps 5 base: seq:GCR_LO_FOLD=seq ;;
+    latf)  run latf 300 python -u tools/lat_ab.py --workload f --reps 3 base: seq:GCR_LO_FOLD=seq ;;
     bench) run bench 600 python -u bench.py ${BENCH_ARGS:-} ;;
     prof)  export TMPDIR=/tmp
            run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --no-latency ${BENCH_ARGS:-} ;;
