@@ -254,6 +254,8 @@ struct Workspace {
     PinBuf<double> h_r2;
     PinBuf<RectModel> h_lorect;         // score_models: small batches' models, read in place
     PinBuf<GeoModel> h_logeo;
+    DevBuf<double> lo_vals;             // launch_score_small's split scorer (DevProblem::lo)
+    DevBuf<uint32_t> lo_meta;
     PinBuf<uint64_t> h_mbits;           // launch_score_small: MSAC inlier ballots (ListBits.mbits)
     PinBuf<uint64_t> h_lbits;           // launch_score_small: LO list bits (ListBits), written by
                                         // the kernel straight into this mapped pinned buffer
@@ -1070,6 +1072,14 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
             *dst[q] = P->w->feat.p + off;
             off += np[c];
         }
+    }
+    // the split small-batch scorer's scratch (launch_score_small)
+    P->dp.lo = SmallScratch{};
+    const size_t spairs = small_score_pairs(P->dp);
+    if (spairs > 0 && spairs <= kSplitMaxPairs) {
+        P->w->lo_vals.ensure(spairs * kSplitModels);
+        P->w->lo_meta.ensure(spairs / 64 * kSplitModels);
+        P->dp.lo = SmallScratch{P->w->lo_vals.p, P->w->lo_meta.p, kSplitModels};
     }
     HIPC(hipMemcpyAsync(P->w->feat.p, hst, total * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
@@ -3651,7 +3661,7 @@ int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream
 }
 
 int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out) {
-    if (!ctx || !a || !out || ((op == 2 || op == 3 || op == 11) && b == nullptr))
+    if (!ctx || !a || !out || ((op == 2 || op == 3 || op == 11 || op == 12) && b == nullptr))
         return set_err(GCR_EINVAL, "null argument");
     return guard([&]() -> int {
         HIPC(hipSetDevice(ctx->device));

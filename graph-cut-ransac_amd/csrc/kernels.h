@@ -47,9 +47,21 @@ struct ModelOf<4> {                 // fundamental matrix: same 9-double POD
 
 // solver 3 (homography): class 0 holds correspondences, x = x1, y = y1,
 // a = x2, c0 = y2
+// Scratch of the split small-batch scorer (launch_score_small): per model
+// small_score_pairs(p) doubles (each 64-pair chunk's inlier values, compacted
+// to the chunk's start) and small_score_pairs(p) / 64 chunk counts.
+constexpr uint32_t kSplitModels = 64;          // models per split launch
+constexpr size_t kSplitMaxPairs = 16384;       // pairs (every inlier value fits k_lo_fold's LDS)
+struct SmallScratch {
+    double* vals = nullptr;
+    uint32_t* meta = nullptr;
+    uint32_t cap_models = 0;
+};
+
 struct DevProblem {
     int solver;     // GCR_SOLVER_*
     DevClass cls[2];
+    SmallScratch lo;
 };
 
 // Raw MSAC accumulators per hypothesis (host finishes the score exactly as
@@ -259,11 +271,15 @@ hipError_t launch_truncate(uint8_t* inc, uint32_t n, uint64_t budget, hipStream_
 hipError_t launch_sqres_geo(const DevProblem& p, const GeoModel& model, double* r2, hipStream_t stream);
 hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_t* count, hipStream_t stream);
 
-// Low-latency scoring of a few models (LO trials, refits): one 1024-thread
-// workgroup per model evaluates every (model, feature) pair, compacts the
-// inlier values in feature order into LDS and one wave adds them
-// (k_lo_chain), counting the decisions within the value-glibc bound of the
-// thresholds (out.fl, out.lfl; exact.h).  Same raw accumulators as
+// Low-latency scoring of a few models (LO trials, refits).  Split scorer
+// (at most kSplitModels models, at most kSplitMaxPairs pairs, p.lo set):
+// k_lo_resid evaluates one (model, feature) pair per thread over as many
+// workgroups as the pairs need and compacts each 64-pair chunk's inlier
+// values into p.lo; k_lo_fold (one 1024-thread workgroup per model) gathers
+// them in feature order into LDS and folds them (fold_exact_chains).
+// Otherwise one 1024-thread workgroup per model does both (k_lo_chain).
+// Both count the decisions within the value-glibc bound of the thresholds
+// (out.fl, out.lfl; exact.h).  Same raw accumulators as
 // launch_score / launch_score_geo.  `models` points to RectModel (solvers
 // 0-2) or GeoModel (3, 4), identity normalisation only; models with inc > 101
 // (inc may be null) score zeros.  Bit arrays: per model small_score_pairs(p)

@@ -1842,26 +1842,6 @@ __device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, 
     return run;
 }
 
-// fold_exact_block: the same in-order sum by all kLoThreads threads of the
-// workgroup (every thread calls it, in uniform control flow; it holds
-// barriers).  The first kBlkHead values are added one by one (the sum is still
-// small there); thread t takes the t-th of kLoThreads contiguous chunks of the
-// rest.  A block scan of approximate chunk sums gives every chunk an
-// approximate start; walking its chunk with an approximate running sum, a
-// thread adds the integer increments rint(v / U) (U the ulp of the binade the
-// running sum is predicted to be in) and marks as special every value whose
-// addition is predicted to leave the binade, and every tie (v / U ending in
-// exactly .5).  Specials are numbered in sequence order (a block scan of the
-// per-thread counts); the parts between consecutive specials are runs: run
-// r's increments are summed over all threads with LDS atomics (exact:
-// integers of one sign, below 2^53 whenever the run is valid), its binade
-// recorded.  Wave 0 then walks the runs: s + U A_r as one exact addition when
-// the exact running sum lies in run r's binade and the result stays in it,
-// then special r by an ordinary addition; the first failed check folds the
-// rest value by value.  A positive / NaN / too large value, a run whose parts
-// disagree on the binade, more than two specials in a chunk or more than
-// kBlkSpecials in all fold the whole range value by value.  Returns the sum on
-// every thread.  tests/test_fold.py restates it in numpy (fold_exact_block).
 constexpr uint32_t kBlkHead = 16;
 constexpr int kBlkSpecials = 63;
 constexpr uint32_t kBlkMaxM = 16;                       // values per chunk, held in registers
@@ -1877,84 +1857,210 @@ struct BlkFoldScratch {
     double head, result;
 };
 
-__device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
-                                                   const double run, BlkFoldScratch& sc, const uint32_t cap) {
-    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    const uint32_t n = e - k;
-    // short (one lane's fold, broadcast), or chunks too long for the registers
-    if (n < kBlkHead + kLoThreads / 4 || n - kBlkHead > kBlkMaxM * (uint32_t)kLoThreads) {
-        if (t == 0) sc.result = fold_seq_lane8(cb, k, e, run);
-        __syncthreads();
-        const double r = sc.result;
-        __syncthreads();
-        return r;
+// One in-order sum of fold_exact_chains: the values cb[k, e) added to a
+// start that is either given (from < 0) or the exact result of chain `from`
+// (an earlier chain, walked first by the same wave).
+struct BlkChain {
+    uint32_t k, e;
+    double start;
+    int from;
+};
+
+// the walk of one chain's runs by one wave (wave-uniform; decisions on the
+// running sum's high word in a scalar register): exact running sum s at
+// position pos (after the head).  s + U A_r is one exact addition when s lies
+// in run r's binade and the result stays in it; then special r by an ordinary
+// addition.  A bad chain, too many specials or the first failed check fold
+// the rest value by value.
+__device__ __forceinline__ double blk_walk(const double* __restrict__ cb, uint32_t pos, const uint32_t e, double s,
+                                           const BlkFoldScratch& sc, const uint32_t cap) {
+    const int lane = threadIdx.x & 63;
+    auto hi_s = [](double v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(as_u64(v) >> 32)); };
+    const uint32_t nspec = sc.nspec;
+    if (sc.bad == 0 && nspec <= (uint32_t)kBlkSpecials) {
+        const uint32_t nr = nspec + 1;
+        // run r's record in lane r
+        const int rl = lane < (int)nr ? lane : 0;
+        const double rA = sc.runA[rl];
+        const int rE = sc.runEmin[rl] == sc.runEmax[rl] ? sc.runEmin[rl] : 0;
+        const double rV = lane < (int)nspec ? sc.specV[lane] : 0.0;
+        const uint32_t rP = lane < (int)nspec ? sc.specPos[lane] : 0u;
+        uint32_t r = 0;
+        for (; r < nr; ++r) {
+            const uint32_t el = (uint32_t)__builtin_amdgcn_readlane(rE, (int)r);
+            if (el == 0u || (hi_s(s) >> 20) != (0x800u | el)) break;   // s < 0 in binade el
+            const double S = s * as_f64((uint64_t)(2098 - el) << 52) + readlane_f64(rA, (int)r);
+            if ((hi_s(S) >> 20) != 0xc33u) break;                       // S in (-2^53, -2^52]
+            s = S * as_f64((uint64_t)(el - 52) << 52);
+            if (r + 1 < nr) {
+                s = s + readlane_f64(rV, (int)r);
+                pos = (uint32_t)__builtin_amdgcn_readlane((int)rP, (int)r) + 1u;
+            }
+        }
+        if (r == nr) pos = e;
     }
-    if (t <= kBlkSpecials) {
-        sc.runA[t] = 0.0;
-        sc.runEmin[t] = 0x7fffffff;
-        sc.runEmax[t] = -1;
-    }
-    if (t == 0) {
-        sc.bad = 0;
-        sc.head = fold_seq_lane8(cb, k, k + kBlkHead, run);   // exact; also the approximate start
-    }
-    // 1. approximate chunk sums, block exclusive scan
-    const uint32_t rest = n - kBlkHead;
-    const uint32_t m = (rest + kLoThreads - 1) / kLoThreads;
-    const uint32_t b = k + kBlkHead + min(rest, (uint32_t)t * m), ee = k + kBlkHead + min(rest, (uint32_t)t * m + m);
-    // the chunk's values in registers (all reads in flight together)
-    double xv[kBlkMaxM];
+    if (pos < e) s = fold_seq_lane(cb, pos, e, s, cap);
+    return s;
+}
+
+// a chunk of at most M values: its approximate sum (all reads in flight together)
+template <uint32_t M>
+__device__ __forceinline__ double blk_chunk_sum(const double* __restrict__ cb, const uint32_t b, const uint32_t ee) {
+    double xv[M];
 #pragma unroll
-    for (uint32_t q = 0; q < kBlkMaxM; ++q) xv[q] = b + q < ee ? cb[b + q] : 0.0;
+    for (uint32_t q = 0; q < M; ++q) xv[q] = b + q < ee ? cb[b + q] : 0.0;
     double a = 0.0;
 #pragma unroll
-    for (uint32_t q = 0; q < kBlkMaxM; ++q)
+    for (uint32_t q = 0; q < M; ++q)
         if (b + q < ee) a += xv[q];
-    const double xin = wave_incl_scan_f64(a);
-    if (lane == 63) sc.wsum[wave] = xin;
-    __syncthreads();
-    // the earlier waves' totals: one read per lane, a row scan, one readlane
-    const double wps = wave_incl_scan_f64(sc.wsum[lane & 15]);
-    const double wpre = wave > 0 ? readlane_f64(wps, wave - 1) : 0.0;
-    double P = sc.head + (wpre + (xin - a));              // approximate start of the chunk
-    // 2. integer increments in up to three parts (two specials)
-    double acc = 0.0, A0 = 0.0, A1 = 0.0, V0 = 0.0, V1 = 0.0;
-    int E0 = 0, E1 = 0, nsp = 0;
-    uint32_t p0 = 0, p1 = 0;
-    bool bad = false;
-    int be = (int)((as_u64(P) >> 52) & 0x7ffu);
+    return a;
+}
+
+// a chunk's integer increments in up to three parts (two specials) from the
+// approximate start P (fold_exact_chains, phase 2)
+struct BlkParts {
+    double acc, a0, a1, v0, v1;
+    int e0, e1, el, ns;
+    uint32_t q0, q1;
+    bool bad;
+};
+
+template <uint32_t M>
+__device__ __forceinline__ void blk_parts(const double* __restrict__ cb, const uint32_t b, const uint32_t ee, double P,
+                                          BlkParts& o) {
+    double xv[M];
 #pragma unroll
-    for (uint32_t q = 0; q < kBlkMaxM; ++q) {
-        const uint32_t i = b + q;
-        if (i >= ee || bad) break;
-        const double x = xv[q];
-        be = (int)((as_u64(P) >> 52) & 0x7ffu);
-        if (!(P < 0.0) || be < 53 || be >= 0x7fe) { bad = true; break; }
-        const double tt = x * as_f64((uint64_t)(2098 - be) << 52);
-        const double r = __builtin_rint(tt);
-        if (!(x <= 0.0) || !(__builtin_fabs(tt) < 0x1p53)) { bad = true; break; }
-        const double Pn = P + x;
-        if (__builtin_fabs(tt - r) == 0.5 || (int)((as_u64(Pn) >> 52) & 0x7ffu) != be) {
-            if (nsp == 2) { bad = true; break; }
-            if (nsp == 0) { A0 = acc; E0 = be; V0 = x; p0 = i; }
-            else { A1 = acc; E1 = be; V1 = x; p1 = i; }
-            acc = 0.0;
-            ++nsp;
-        } else {
-            acc += r;
+    for (uint32_t q = 0; q < M; ++q) xv[q] = b + q < ee ? cb[b + q] : 0.0;
+    bool bd = false;
+    int be = (int)((as_u64(P) >> 52) & 0x7ffu);
+    double ac = 0.0, a0 = 0.0, a1 = 0.0, v0 = 0.0, v1 = 0.0;
+    int e0 = 0, e1 = 0, ns = 0;
+    uint32_t q0 = 0, q1 = 0;
+    const uint32_t len = ee - b;
+#pragma unroll
+    for (uint32_t q = 0; q < M; ++q) {
+        if (q < len && !bd) {
+            const double x = xv[q];
+            be = (int)((as_u64(P) >> 52) & 0x7ffu);
+            const double tt = x * as_f64((uint64_t)(2098 - be) << 52);
+            const double r = __builtin_rint(tt);
+            const double Pn = P + x;
+            const bool sp = __builtin_fabs(tt - r) == 0.5 || (int)((as_u64(Pn) >> 52) & 0x7ffu) != be;
+            bd = !(P < 0.0) || be < 53 || be >= 0x7fe || !(x <= 0.0) || !(__builtin_fabs(tt) < 0x1p53) ||
+                 (sp && ns == 2);
+            if (sp) {
+                if (ns == 0) { a0 = ac; e0 = be; v0 = x; q0 = b + q; }
+                else { a1 = ac; e1 = be; v1 = x; q1 = b + q; }
+                ac = 0.0;
+                ++ns;
+            } else {
+                ac += r;
+            }
+            P = Pn;
         }
-        P = Pn;
     }
-    const int Elast = nsp > 0 ? (int)((as_u64(P) >> 52) & 0x7ffu) : be;
-    // 3. number the specials: block exclusive scan of the per-thread counts
-    const uint32_t ci = wave_incl_scan_u32((uint32_t)nsp);
-    if (lane == 63) sc.wcnt[wave] = ci;
-    if (bad) atomicOr(&sc.bad, 1u);
+    o.acc = ac; o.a0 = a0; o.a1 = a1; o.v0 = v0; o.v1 = v1;
+    o.e0 = e0; o.e1 = e1; o.ns = ns; o.q0 = q0; o.q1 = q1;
+    o.bad = bd;
+    o.el = ns > 0 ? (int)((as_u64(P) >> 52) & 0x7ffu) : be;
+}
+
+// fold_exact_chains: NC in-order sums by all kLoThreads threads of the
+// workgroup at once, sharing the barriers (every thread calls it, in uniform
+// control flow).  Per chain the first kBlkHead values are added one by one
+// (the sum is still small there); thread t takes the t-th of kLoThreads
+// contiguous chunks of the rest.  A block scan of approximate chunk sums
+// gives every chunk an approximate start (a continuing chain starts at the
+// approximate total of the chain it continues); walking its chunk with an
+// approximate running sum, a thread adds the integer increments rint(v / U)
+// (U the ulp of the binade the running sum is predicted to be in) and marks
+// as special every value whose addition is predicted to leave the binade, and
+// every tie (v / U ending in exactly .5).  Specials are numbered in sequence
+// order (a block scan of the per-thread counts); the parts between
+// consecutive specials are runs: run r's increments are summed exactly
+// (integers of one sign, below 2^53 whenever the run is valid) by a
+// segmented wave scan and one LDS atomic per run and wave, its binade
+// recorded.  Then wave c walks chain c (blk_walk) and, right after it, the
+// chains continuing it.  A positive / NaN / too large value, a run whose
+// parts disagree on the binade, more than two specials in a chunk or more
+// than kBlkSpecials in all fold the chain value by value, as do chains too
+// short or too long for the chunks.  res[c] = chain c's sum on every thread.
+// tests/test_fold.py restates one chain in numpy (fold_exact_block).
+template <int NC>
+__device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb, const BlkChain (&ch)[NC],
+                                                  BlkFoldScratch (&sc)[NC], const uint32_t cap, double (&res)[NC]) {
+    static_assert(NC <= kLoThreads / 64, "one wave per chain");
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    bool seq[NC];
+    uint32_t b[NC], ee[NC], m[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t n = ch[c].e - ch[c].k;
+        seq[c] = n < kBlkHead + kLoThreads / 4 || n - kBlkHead > kBlkMaxM * (uint32_t)kLoThreads;
+        const uint32_t rest = seq[c] ? 0u : n - kBlkHead;
+        // values per chunk (uniform: the loops below are unrolled for 4, 8 or 16)
+        m[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)((rest + kLoThreads - 1) / kLoThreads));
+        b[c] = ch[c].k + kBlkHead + min(rest, (uint32_t)t * m[c]);
+        ee[c] = ch[c].k + kBlkHead + min(rest, (uint32_t)t * m[c] + m[c]);
+        if (t <= kBlkSpecials) {
+            sc[c].runA[t] = 0.0;
+            sc[c].runEmin[t] = 0x7fffffff;
+            sc[c].runEmax[t] = -1;
+        }
+        // the head: exact for a chain with a given start, approximate (from
+        // +0) for a continuing one (its walk adds it to the exact start)
+        if (t == 64 * c) {
+            sc[c].bad = 0;
+            if (!seq[c]) sc[c].head = fold_seq_lane8(cb, ch[c].k, ch[c].k + kBlkHead, ch[c].from < 0 ? ch[c].start : 0.0);
+        }
+    }
+    // 1. approximate chunk sums, block scans
+    double xin[NC], a[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        a[c] = m[c] <= 4 ? blk_chunk_sum<4>(cb, b[c], ee[c])
+                         : (m[c] <= 8 ? blk_chunk_sum<8>(cb, b[c], ee[c]) : blk_chunk_sum<kBlkMaxM>(cb, b[c], ee[c]));
+        xin[c] = wave_incl_scan_f64(a[c]);
+        if (lane == 63) sc[c].wsum[wave] = xin[c];
+    }
     __syncthreads();
-    const uint32_t wcs = wave_incl_scan_u32(sc.wcnt[lane & 15]);
-    uint32_t base = ci - (uint32_t)nsp + (wave > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wcs, wave - 1) : 0u);
-    if (t == kLoThreads - 1) sc.nspec = base + (uint32_t)nsp;
-    const bool fits = base + (uint32_t)nsp <= (uint32_t)kBlkSpecials;
+    // 2. integer increments in up to three parts (two specials) per chunk
+    BlkParts pt[NC];
+    double total[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        // the earlier waves' totals: one read per lane, a row scan, readlanes
+        const double wps = wave_incl_scan_f64(sc[c].wsum[lane & 15]);
+        const double wpre = wave > 0 ? readlane_f64(wps, wave - 1) : 0.0;
+        total[c] = sc[c].head + readlane_f64(wps, 15);
+        double base = sc[c].head;
+#pragma unroll
+        for (int d = 0; d < c; ++d)
+            if (ch[c].from == d) base += total[d];
+        const double P = base + (wpre + (xin[c] - a[c]));  // approximate start of the chunk
+        if (m[c] <= 4) blk_parts<4>(cb, b[c], ee[c], P, pt[c]);
+        else if (m[c] <= 8) blk_parts<8>(cb, b[c], ee[c], P, pt[c]);
+        else blk_parts<kBlkMaxM>(cb, b[c], ee[c], P, pt[c]);
+    }
+    double acc[NC], A0[NC], A1[NC], V0[NC], V1[NC];
+    int E0[NC], E1[NC], El[NC], nsp[NC];
+    uint32_t p0[NC], p1[NC];
+    bool bad[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        acc[c] = pt[c].acc; A0[c] = pt[c].a0; A1[c] = pt[c].a1; V0[c] = pt[c].v0; V1[c] = pt[c].v1;
+        E0[c] = pt[c].e0; E1[c] = pt[c].e1; El[c] = pt[c].el; nsp[c] = pt[c].ns; p0[c] = pt[c].q0; p1[c] = pt[c].q1;
+        bad[c] = pt[c].bad;
+    }
+    // 3. number the specials: block scans of the per-thread counts
+    uint32_t ci[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        ci[c] = wave_incl_scan_u32((uint32_t)nsp[c]);
+        if (lane == 63) sc[c].wcnt[wave] = ci[c];
+        if (bad[c]) atomicOr(&sc[c].bad, 1u);
+    }
+    __syncthreads();
     // the runs' increments.  Every thread's last part belongs to run
     // R = base + nsp; those of consecutive lanes with equal R are summed by a
     // segmented wave scan and added by the segment's last lane (one LDS atomic
@@ -1962,73 +2068,74 @@ __device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb
     // segment's first and last lanes and by every lane whose binade differs
     // from its left neighbour's (a run whose parts disagree then shows
     // min != max).  The rare parts before a special are added one by one.
-    const uint32_t R = fits ? base + (uint32_t)nsp : 0xffffffffu;
-    const double seg = wave_seg_scan_f64(acc, R);
-    const uint32_t Rl = (uint32_t)__shfl_up((int)R, 1), Rr = (uint32_t)__shfl_down((int)R, 1);
-    const int El = __shfl_up(Elast, 1);
-    const bool first = lane == 0 || Rl != R, last = lane == 63 || Rr != R;
-    if (fits && !bad) {
-        if (last && seg != 0.0) atomicAdd(&sc.runA[R], seg);
-        if (first || last || El != Elast) {
-            atomicMin(&sc.runEmin[R], Elast);
-            atomicMax(&sc.runEmax[R], Elast);
-        }
-        if (nsp > 0) {
-            if (A0 != 0.0) atomicAdd(&sc.runA[base], A0);
-            atomicMin(&sc.runEmin[base], E0);
-            atomicMax(&sc.runEmax[base], E0);
-            sc.specV[base] = V0;
-            sc.specPos[base] = p0;
-        }
-        if (nsp > 1) {
-            if (A1 != 0.0) atomicAdd(&sc.runA[base + 1], A1);
-            atomicMin(&sc.runEmin[base + 1], E1);
-            atomicMax(&sc.runEmax[base + 1], E1);
-            sc.specV[base + 1] = V1;
-            sc.specPos[base + 1] = p1;
-        }
-    }
-    __syncthreads();
-    // 4. the walk (wave 0; the running sum wave-uniform, decisions on its
-    //    high word in a scalar register)
-    if (wave == 0) {
-        auto hi_s = [](double v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(as_u64(v) >> 32)); };
-        double s = sc.head;
-        uint32_t pos = k + kBlkHead;
-        const uint32_t nspec = sc.nspec;
-        const bool all_ok = sc.bad == 0 && nspec <= (uint32_t)kBlkSpecials;
-        if (all_ok) {
-            const uint32_t nr = nspec + 1;
-            // run r's record in lane r
-            const int rl = lane < (int)nr ? lane : 0;
-            const double rA = sc.runA[rl];
-            const int rE = sc.runEmin[rl] == sc.runEmax[rl] ? sc.runEmin[rl] : 0;
-            const double rV = lane < (int)nspec ? sc.specV[lane] : 0.0;
-            const uint32_t rP = lane < (int)nspec ? sc.specPos[lane] : 0u;
-            uint32_t r = 0;
-            for (; r < nr; ++r) {
-                const uint32_t el = (uint32_t)__builtin_amdgcn_readlane(rE, (int)r);
-                if (el == 0u || (hi_s(s) >> 20) != (0x800u | el)) break;   // s < 0 in binade el
-                const double S = s * as_f64((uint64_t)(2098 - el) << 52) + readlane_f64(rA, (int)r);
-                if ((hi_s(S) >> 20) != 0xc33u) break;                       // S in (-2^53, -2^52]
-                s = S * as_f64((uint64_t)(el - 52) << 52);
-                if (r + 1 < nr) {
-                    s = s + readlane_f64(rV, (int)r);
-                    pos = (uint32_t)__builtin_amdgcn_readlane((int)rP, (int)r) + 1u;
-                }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t wcs = wave_incl_scan_u32(sc[c].wcnt[lane & 15]);
+        const uint32_t base =
+            ci[c] - (uint32_t)nsp[c] + (wave > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wcs, wave - 1) : 0u);
+        if (t == kLoThreads - 1) sc[c].nspec = base + (uint32_t)nsp[c];
+        const bool fits = base + (uint32_t)nsp[c] <= (uint32_t)kBlkSpecials;
+        const uint32_t R = fits ? base + (uint32_t)nsp[c] : 0xffffffffu;
+        const double seg = wave_seg_scan_f64(acc[c], R);
+        const uint32_t Rl = (uint32_t)__shfl_up((int)R, 1), Rr = (uint32_t)__shfl_down((int)R, 1);
+        const int Ell = __shfl_up(El[c], 1);
+        const bool first = lane == 0 || Rl != R, last = lane == 63 || Rr != R;
+        if (fits && !bad[c]) {
+            if (last && seg != 0.0) atomicAdd(&sc[c].runA[R], seg);
+            if (first || last || Ell != El[c]) {
+                atomicMin(&sc[c].runEmin[R], El[c]);
+                atomicMax(&sc[c].runEmax[R], El[c]);
             }
-            if (r == nr) pos = e;
-        } else {
-            s = run;
-            pos = k;
+            if (nsp[c] > 0) {
+                if (A0[c] != 0.0) atomicAdd(&sc[c].runA[base], A0[c]);
+                atomicMin(&sc[c].runEmin[base], E0[c]);
+                atomicMax(&sc[c].runEmax[base], E0[c]);
+                sc[c].specV[base] = V0[c];
+                sc[c].specPos[base] = p0[c];
+            }
+            if (nsp[c] > 1) {
+                if (A1[c] != 0.0) atomicAdd(&sc[c].runA[base + 1], A1[c]);
+                atomicMin(&sc[c].runEmin[base + 1], E1[c]);
+                atomicMax(&sc[c].runEmax[base + 1], E1[c]);
+                sc[c].specV[base + 1] = V1[c];
+                sc[c].specPos[base + 1] = p1[c];
+            }
         }
-        if (pos < e) s = fold_seq_lane(cb, pos, e, s, cap);
-        if (lane == 0) sc.result = s;
     }
     __syncthreads();
-    const double res = sc.result;
+    // 4. the walks: chain c on wave c, the chains continuing it right after
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (ch[c].from >= 0 || wave != c) continue;
+        double s = seq[c] ? fold_seq_lane(cb, ch[c].k, ch[c].e, ch[c].start, cap)
+                          : blk_walk(cb, ch[c].k + kBlkHead, ch[c].e, sc[c].head, sc[c], cap);
+        if (lane == 0) sc[c].result = s;
+#pragma unroll
+        for (int d = c + 1; d < NC; ++d) {
+            if (ch[d].from != c) continue;
+            double u;
+            if (seq[d]) {
+                u = fold_seq_lane(cb, ch[d].k, ch[d].e, s, cap);
+            } else {
+                u = fold_seq_lane8(cb, ch[d].k, ch[d].k + kBlkHead, s);      // its head, from the exact start
+                u = blk_walk(cb, ch[d].k + kBlkHead, ch[d].e, u, sc[d], cap);
+            }
+            if (lane == 0) sc[d].result = u;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NC; ++c) res[c] = sc[c].result;
     __syncthreads();                                      // the scratch is reused by the next call
-    return res;
+}
+
+// one chain from a given start (k_fold_test)
+__device__ __forceinline__ double fold_exact_block(const double* __restrict__ cb, const uint32_t k, const uint32_t e,
+                                                   const double run, BlkFoldScratch& sc, const uint32_t cap) {
+    const BlkChain ch[1] = {{k, e, run, -1}};
+    double res[1];
+    fold_exact_chains<1>(cb, ch, *reinterpret_cast<BlkFoldScratch (*)[1]>(&sc), cap, res);
+    return res[0];
 }
 
 template <int KIND, bool kWide>
@@ -2049,7 +2156,7 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
     double run = 0.0, hold = 0.0;
     uint32_t cnt0 = 0, cntall = 0;
     double wcc = 0.0, wtt = 0.0, whold = 0.0;             // kWide: the chains, uniform in every thread
-    __shared__ BlkFoldScratch bsc;
+    __shared__ BlkFoldScratch bsc[3];
     const auto m = models[mi];
     const bool live = inc == nullptr || inc[mi] <= 101;   // a slot without a model scores zeros
     // flagged decisions (the MSAC test's and the list predicate's, exact.h),
@@ -2244,17 +2351,20 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
         // the class sum and, for KIND 2, the running total: class 0 from +0,
         // class 1 from +0 (the class chain's restart) and from the class-0 sum
         GCR_STAMP(2, 14u);
-        const double c0 = fold_exact_block(cball, 0, cnt0, 0.0, bsc, 2 * kLoBlock);
-        GCR_STAMP(3, 14u);
         if constexpr (KIND == 2) {
-            whold = c0;
-            wcc = fold_exact_block(cball, cnt0, cntall, 0.0, bsc, 2 * kLoBlock);
-            GCR_STAMP(4, 14u);
-            wtt = fold_exact_block(cball, cnt0, cntall, c0, bsc, 2 * kLoBlock);
-            GCR_STAMP(5, 14u);
+            const BlkChain chs[3] = {{0u, cnt0, 0.0, -1}, {cnt0, cntall, 0.0, -1}, {cnt0, cntall, 0.0, 0}};
+            double r3[3];
+            fold_exact_chains<3>(cball, chs, bsc, 2 * kLoBlock, r3);
+            whold = r3[0];
+            wcc = r3[1];
+            wtt = r3[2];
         } else {
-            wcc = c0;
+            const BlkChain chs[1] = {{0u, cnt0, 0.0, -1}};
+            double r1[1];
+            fold_exact_chains<1>(cball, chs, *reinterpret_cast<BlkFoldScratch (*)[1]>(&bsc[0]), 2 * kLoBlock, r1);
+            wcc = r1[0];
         }
+        GCR_STAMP(3, 14u);
         run = (KIND == 2 && lane == 1) ? wtt : wcc;
         hold = whold;
     }
@@ -2269,6 +2379,146 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             if (out.fl) out.fl[mi] = fcnt[0];
             if (out.lfl) out.lfl[mi] = fcnt[1];
         }
+    }
+}
+
+// ------------------------------------------- split small-batch scorer ----
+// The small scorer for a few models (LO trials, refits) in two launches, so
+// the per-pair arithmetic spreads over the chip instead of one workgroup per
+// model: k_lo_resid evaluates one pair per thread (one 64-pair chunk per
+// wave, any number of workgroups per model) and writes its chunk's inlier
+// values compacted to the chunk's start in p.lo.vals, the chunk's counts in
+// p.lo.meta and the list / MSAC ballots; k_lo_fold (one workgroup per model)
+// gathers the chunks in order into LDS and folds them (fold_exact_chains).
+// Same results as k_lo_chain<KIND, true> bit for bit.
+constexpr int kLrThreads = 256;
+static_assert(kSplitMaxPairs == 2 * kLoBlock, "k_lo_fold holds every inlier value in LDS");
+
+template <int KIND>
+__global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
+                                                        const uint8_t* __restrict__ inc, double T0, double T1,
+                                                        uint32_t pad0, uint32_t nchunks, ListBits lb, FlagBand fbm,
+                                                        FlagBand fbl) {
+    const uint32_t mi = blockIdx.y;
+    const uint32_t j = blockIdx.x * (kLrThreads / 64) + (threadIdx.x >> 6);      // chunk
+    const int lane = threadIdx.x & 63;
+    const auto m = models[mi];
+    __shared__ ValueConst vc_sh;
+    if constexpr (KIND <= 2) {
+        if (threadIdx.x == 0) vc_sh = value_const(m, KIND == 1, KIND == 2);
+        __syncthreads();
+    }
+    if (j >= nchunks) return;                                // wave-uniform, after the barrier
+    const bool live = inc == nullptr || inc[mi] <= 101;
+    const uint32_t jj = j * 64u + (uint32_t)lane;            // pair index
+    const int cls = jj < pad0 ? 0 : 1;                        // chunk-uniform (pad0 % 64 == 0)
+    const uint32_t fi = cls == 0 ? jj : jj - pad0;
+    const DevClass& c = p.cls[cls];
+    const bool ev = live && fi < c.n;
+    double r2 = 0.0;
+    if (ev) {
+        const double x = c.x[fi], y = c.y[fi];
+        const double f2 = (KIND < 3 && cls == 1) ? c.c0[fi] : c.a[fi];
+        const double f3 = KIND >= 3 ? c.c0[fi] : (cls == 1 ? c.c1[fi] : 0.0);
+        if constexpr (KIND >= 3) {
+            r2 = geo_sq_residual<KIND>(x, y, f2, f3, m.h);
+        } else if (cls == 0) {
+            r2 = scale_sq_value<KIND == 1, true>(x, y, f2, m, vc_sh.ac, vc_sh.cut);
+        } else {
+            r2 = orient_sq_value<true>(x, y, f2, f3, m, vc_sh.c, vc_sh.s, vc_sh.cphi, vc_sh.cphi2);
+        }
+    }
+    const bool inl = ev && r2 <= (cls == 0 ? T0 : T1);
+    const uint64_t w = __ballot(inl);
+    const size_t wi = (size_t)mi * nchunks + j;
+    if (inl) p.lo.vals[wi * 64u + (uint32_t)__builtin_popcountll(w & ((1ull << lane) - 1ull))] = -r2;
+    const bool lin = lb.bits != nullptr && ev && mask_rule(r2, lb.rule, cls == 0 ? lb.T[0] : lb.T[1], lb.lambda);
+    const uint64_t lbw = __ballot(lin);
+    uint32_t nfm = 0, nfl = 0;
+    if constexpr (KIND <= 2) {
+        nfm = (uint32_t)__builtin_popcountll(__ballot(ev && in_flag_band(r2, fbm.mid[cls], fbm.half[cls])));
+        nfl = (uint32_t)__builtin_popcountll(__ballot(ev && lb.bits != nullptr && in_flag_band(r2, fbl.mid[cls], fbl.half[cls])));
+    }
+    if (lane == 0) {
+        if (lb.bits != nullptr) lb.bits[wi] = lbw;
+        if (lb.mbits != nullptr) lb.mbits[wi] = w;
+        p.lo.meta[wi] = (uint32_t)__builtin_popcountll(w) | nfm << 8 | nfl << 16;
+    }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kLoThreads) void k_lo_fold(DevProblem p, const uint8_t* __restrict__ inc, uint32_t pad0,
+                                                       uint32_t nchunks, ScoreOut out) {
+    __shared__ double cball[2 * kLoBlock];
+    __shared__ uint32_t coff[2 * kLoChunks + 1];
+    __shared__ uint32_t wtot[kLoThreads / 64];
+    __shared__ uint32_t fsum[2];
+    __shared__ BlkFoldScratch bsc[3];
+    const uint32_t mi = blockIdx.x;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    (void)inc;                                               // a dead slot's chunks hold no inliers
+    if (t < 2) fsum[t] = 0;
+    // the chunk counts (one chunk per thread: nchunks <= 2 kLoChunks), block scan
+    const uint32_t mt = (uint32_t)t < nchunks ? p.lo.meta[(size_t)mi * nchunks + t] : 0u;
+    const uint32_t cnt = mt & 0xffu;
+    const uint32_t ci = wave_incl_scan_u32(cnt);
+    if (lane == 63) wtot[wave] = ci;
+    uint32_t nfm = mt >> 8 & 0xffu, nfl = mt >> 16 & 0xffu;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        nfm += (uint32_t)__shfl_xor((int)nfm, d);
+        nfl += (uint32_t)__shfl_xor((int)nfl, d);
+    }
+    __syncthreads();
+    if (lane == 0 && (nfm | nfl)) {
+        atomicAdd(&fsum[0], nfm);
+        atomicAdd(&fsum[1], nfl);
+    }
+    const uint32_t wcs = wave_incl_scan_u32(wtot[lane & 15]);
+    const uint32_t excl = ci - cnt + (wave > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)wcs, wave - 1) : 0u);
+    if ((uint32_t)t < nchunks) coff[t] = excl;
+    if ((uint32_t)t == nchunks - 1) coff[nchunks] = excl + cnt;
+    __syncthreads();
+    // gather: wave w copies chunks w, w + 16, ... (all reads in flight together)
+    {
+        constexpr int kPer = 2 * kLoChunks / (kLoThreads / 64);
+        const double* src = p.lo.vals + (size_t)mi * nchunks * 64u;
+        double g[kPer];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const uint32_t j = (uint32_t)wave + 16u * i;
+            g[i] = (j < nchunks && (uint32_t)lane < coff[j + 1] - coff[j]) ? src[j * 64u + lane] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const uint32_t j = (uint32_t)wave + 16u * i;
+            if (j < nchunks && (uint32_t)lane < coff[j + 1] - coff[j]) cball[coff[j] + lane] = g[i];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt0 = coff[min(pad0 / 64u, nchunks)], cntall = coff[nchunks];
+    double whold = 0.0, wcc, wtt;
+    if constexpr (KIND == 2) {
+        const BlkChain chs[3] = {{0u, cnt0, 0.0, -1}, {cnt0, cntall, 0.0, -1}, {cnt0, cntall, 0.0, 0}};
+        double r3[3];
+        fold_exact_chains<3>(cball, chs, bsc, 2 * kLoBlock, r3);
+        whold = r3[0];
+        wcc = r3[1];
+        wtt = r3[2];
+    } else {
+        const BlkChain chs[1] = {{0u, cnt0, 0.0, -1}};
+        double r1[1];
+        fold_exact_chains<1>(cball, chs, *reinterpret_cast<BlkFoldScratch (*)[1]>(&bsc[0]), 2 * kLoBlock, r1);
+        wcc = wtt = r1[0];
+    }
+    if (t == 0) {
+        out.n0[mi] = cnt0;
+        out.n1[mi] = cntall - cnt0;
+        out.v0[mi] = KIND == 2 ? whold : wcc;
+        out.v1[mi] = KIND == 2 ? wcc : 0.0;
+        out.tot[mi] = wtt;
+        if (out.fl) out.fl[mi] = fsum[0];
+        if (out.lfl) out.lfl[mi] = fsum[1];
     }
 }
 
@@ -3653,6 +3903,14 @@ bool lo_fold_wide() {
     return !(e && e[0] == 's');
 }
 
+// launch_score_small: the split scorer (k_lo_resid + k_lo_fold) when the
+// problem has its scratch and the launch fits it; GCR_LO_SPLIT=0 keeps one
+// k_lo_chain workgroup per model (read per launch)
+bool lo_split() {
+    const char* e = getenv("GCR_LO_SPLIT");
+    return !(e && e[0] == '0');
+}
+
 size_t small_score_pairs(const DevProblem& p) {
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t pad1 = (p.solver == 2) ? ((p.cls[1].n + 63u) & ~63u) : 0u;
@@ -3671,7 +3929,14 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         using M = typename ModelOf<KIND>::type;
         const M* mp = static_cast<const M*>(models);
         const uint32_t probe = probe_bits();               // GCR_PROBE bits 8 / 9: timing probes (results invalid)
-        if (lo_fold_wide())
+        const uint32_t nchunks = ntot / 64;
+        if (lo_split() && lo_fold_wide() && probe == 0 && ntot <= 2 * kLoBlock && nm <= p.lo.cap_models &&
+            p.lo.vals != nullptr && p.lo.meta != nullptr) {
+            const dim3 grid((nchunks + kLrThreads / 64 - 1) / (kLrThreads / 64), nm);
+            hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, mp, inc, T[0], T[1], pad0,
+                               nchunks, lb, flag_band(T), flag_band(lb.T));
+            hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, p, inc, pad0, nchunks, out);
+        } else if (lo_fold_wide())
             hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1],
                                pad0, ntot, lb, flag_band(T), flag_band(lb.T), out, probe);
         else
@@ -3739,8 +4004,48 @@ __global__ __launch_bounds__(kLoThreads) void k_fold_test(const double* __restri
     }
 }
 
+// op 12 of gcr_debug_math: the three chains of k_lo_chain's KIND-2 fold over
+// an LDS copy of a[0, n), split at h = b[0]: out[0] = a[0, h) from +0,
+// out[1] = a[h, n) from +0, out[2] = a[h, n) from out[0] (fold_exact_chains);
+// out[3..5] = the same sums by one lane's sequential loop, out[6] = cycles of
+// the chains (n >= 7).
+__global__ __launch_bounds__(kLoThreads) void k_fold3_test(const double* __restrict__ a, uint32_t n,
+                                                          const double* __restrict__ hb, double* out) {
+    __shared__ double buf[kLoBlock];
+    __shared__ BlkFoldScratch bsc[3];
+    const int t = threadIdx.x;
+    const double hd = hb[0];
+    const uint32_t h = hd >= 0.0 && hd <= (double)n ? (uint32_t)hd : 0u;
+    for (uint32_t i = t; i < n; i += kLoThreads) buf[i] = a[i];
+    __syncthreads();
+    const BlkChain ch[3] = {{0u, h, 0.0, -1}, {h, n, 0.0, -1}, {h, n, 0.0, 0}};
+    double r[3];
+    const uint64_t t0 = __builtin_readcyclecounter();
+    fold_exact_chains<3>(buf, ch, bsc, kLoBlock, r);
+    const uint64_t t1 = __builtin_readcyclecounter();
+    if (t == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (uint32_t k = 0; k < h; ++k) s0 = s0 + buf[k];
+        for (uint32_t k = h; k < n; ++k) s1 = s1 + buf[k];
+        double s2 = s0;
+        for (uint32_t k = h; k < n; ++k) s2 = s2 + buf[k];
+        out[0] = r[0];
+        out[1] = r[1];
+        out[2] = r[2];
+        out[3] = s0;
+        out[4] = s1;
+        out[5] = s2;
+        out[6] = (double)(t1 - t0);
+    }
+}
+
 hipError_t launch_math(int op, const double* a, const double* b, size_t n, double* out, hipStream_t stream) {
     if (n == 0) return hipSuccess;
+    if (op == 12) {
+        if (n < 7 || n > kLoBlock) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_fold3_test, dim3(1), dim3(kLoThreads), 0, stream, a, (uint32_t)n, b, out);
+        return hipGetLastError();
+    }
     if (op == 7) {
         if (n < 2 || n > 0xffffffffull) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_fold_test, dim3(1), dim3(kLoThreads), 0, stream, a, (uint32_t)n, out);

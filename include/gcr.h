@@ -317,8 +317,11 @@ int gcr_host_sample(uint64_t seed, uint64_t index, uint32_t sub, uint32_t stream
  * 5 clip_angle_small(a), 6 clip_angle(a), 8 round 3's log (dm_log_fd),
  * 9 / 10 sin / cos of a (dm_sincos), 11 atan(a / b) for 0 <= a <= b
  * (atan_ratio, the orientation value's);
- * op 7 (n >= 2): out[0] = the wave-parallel exact in-order sum of a[0, n)
- * (k_lo_chain's fold), out[1] = the same sum by a sequential loop */
+ * op 7 (n >= 2): out[0] = the block-parallel exact in-order sum of a[0, n)
+ * (k_lo_chain's fold), out[1] = the same sum by a sequential loop;
+ * op 12 (7 <= n <= 8192, split h = b[0]): out[0..2] = the three chains of
+ * k_lo_chain's two-class fold (a[0, h) from +0, a[h, n) from +0, a[h, n)
+ * from out[0]), out[3..5] = the same by sequential loops, out[6] = cycles */
 int gcr_debug_math(gcr_ctx* ctx, int op, const double* a, const double* b, size_t n, double* out);
 /* perspective_warp's resampling (examples/utils.py:92-123, cv2.warpPerspective
  * with INTER_LINEAR): dst pixel (x, y) <- bilinear sample of src at

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Cycle counts of k_lo_chain's two in-order folds over an LDS copy of one
+"""Cycle counts of the small scorer's in-order folds over an LDS copy of one
 value sequence (gcr_debug_math op 7): the block-parallel exact fold
 (fold_exact_block, one 1024-thread workgroup) and the one-lane batched fold,
 on MSAC-like sequences (-r^2 of inliers)."""
@@ -35,3 +35,25 @@ for name, v in cases.items():
     same = o[0].tobytes() == o[1].tobytes()
     print(f"{name:22s} n={v.size:5d} block {o[2]:9.0f} cyc  seq {o[3]:9.0f} cyc  ratio {o[3] / o[2]:5.2f}  "
           f"specials {o[4]:4.0f}  fallback {o[5]:1.0f}  equal {same}")
+
+
+def run3(v, h):
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    out = np.zeros(max(16, v.size))
+    hb = np.full(v.size, float(h))
+    dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+    N.check(N.lib.gcr_debug_math(N.context(0), 12, dp(v), dp(hb), v.size, dp(out)))
+    return out[:7]
+
+
+# the three chains of the two-class fold (gcr_debug_math op 12: class 0 from
+# +0, class 1 from +0 and from the class-0 sum) in one fold_exact_chains call
+for name, v, h in (("M2-like 2 x 2500", np.concatenate([cases["scale r^2, thr 0.05"][:2500],
+                                                         cases["orient r^2, 1 deg"][:2500]]), 2500),
+                   ("M2-like 2 x 4000", np.concatenate([cases["scale r^2, thr 0.05"][:4000],
+                                                         cases["orient r^2, 1 deg"][:4000]]), 4000),
+                   ("one class 5000", cases["scale r^2, thr 0.05"], 5000)):
+    for _ in range(2):
+        o = run3(v, h)
+    ok = all(o[i].tobytes() == o[i + 3].tobytes() for i in range(3))
+    print(f"3 chains {name:18s} n={v.size:5d} h={h:5d} {o[6]:9.0f} cyc  equal {ok}")

@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.join(REPO, "graph-cut-ransac_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 os.environ.setdefault("GCR_LIB", "libgcr_stamps.so")
 os.environ["GCR_DEBUG_SCORER"] = "small"
+os.environ["GCR_LO_SPLIT"] = "0"                    # k_lo_chain (the split scorer has no stamps)
 
 import ctypes as C  # noqa: E402
 
@@ -58,8 +59,8 @@ def main():
             print(f"  block {blk}: residuals done (w0 / min / max over waves) {res[0]} / {min(res)} / {max(res)}, "
                   f"prefix done {b[wg, 0, blk, 1] - t0_}, compaction done {b[wg, 0, blk, 2] - t0_}")
         s = b[wg, 0, 14]
-        print(f"  folds: start {s[2] - t0_}, class 0 {s[3] - s[2]}, class 1 {s[4] - s[3]}, total {s[5] - s[4]} cyc;"
-              f" end {s[5] - t0_} cyc")
+        print(f"  folds (all chains, one fold_exact_chains call): start {s[2] - t0_}, {s[3] - s[2]} cyc;"
+              f" end {s[3] - t0_} cyc")
 
 
 if __name__ == "__main__":
