@@ -1988,9 +1988,15 @@ __device__ __forceinline__ void blk_parts(const double* __restrict__ cb, const u
 // tests/test_fold.py restates one chain in numpy (fold_exact_block).
 template <int NC>
 __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb, const BlkChain (&ch)[NC],
-                                                  BlkFoldScratch (&sc)[NC], const uint32_t cap, double (&res)[NC]) {
+                                                  BlkFoldScratch (&sc)[NC], const uint32_t cap, double (&res)[NC],
+                                                  double* dbg = nullptr) {
     static_assert(NC <= kLoThreads / 64, "one wave per chain");
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    // cycle stamps after each barrier (k_fold3_test only)
+    auto stamp = [&](int i) {
+        if (dbg != nullptr && t == 0) dbg[i] = (double)__builtin_readcyclecounter();
+    };
+    stamp(0);
     bool seq[NC];
     uint32_t b[NC], ee[NC], m[NC];
 #pragma unroll
@@ -2024,6 +2030,7 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
         if (lane == 63) sc[c].wsum[wave] = xin[c];
     }
     __syncthreads();
+    stamp(1);
     // 2. integer increments in up to three parts (two specials) per chunk
     BlkParts pt[NC];
     double total[NC];
@@ -2061,6 +2068,7 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
         if (bad[c]) atomicOr(&sc[c].bad, 1u);
     }
     __syncthreads();
+    stamp(2);
     // the runs' increments.  Every thread's last part belongs to run
     // R = base + nsp; those of consecutive lanes with equal R are summed by a
     // segmented wave scan and added by the segment's last lane (one LDS atomic
@@ -2103,6 +2111,7 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
         }
     }
     __syncthreads();
+    stamp(3);
     // 4. the walks: chain c on wave c, the chains continuing it right after
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -2124,6 +2133,7 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
         }
     }
     __syncthreads();
+    stamp(4);
 #pragma unroll
     for (int c = 0; c < NC; ++c) res[c] = sc[c].result;
     __syncthreads();                                      // the scratch is reused by the next call
@@ -2402,24 +2412,30 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
     const uint32_t mi = blockIdx.y;
     const uint32_t j = blockIdx.x * (kLrThreads / 64) + (threadIdx.x >> 6);      // chunk
     const int lane = threadIdx.x & 63;
-    const auto m = models[mi];
-    __shared__ ValueConst vc_sh;
-    if constexpr (KIND <= 2) {
-        if (threadIdx.x == 0) vc_sh = value_const(m, KIND == 1, KIND == 2);
-        __syncthreads();
-    }
-    if (j >= nchunks) return;                                // wave-uniform, after the barrier
-    const bool live = inc == nullptr || inc[mi] <= 101;
-    const uint32_t jj = j * 64u + (uint32_t)lane;            // pair index
+    const bool jin = j < nchunks;                             // the last workgroup's tail
+    const uint32_t jj = (jin ? j : 0u) * 64u + (uint32_t)lane;   // pair index
     const int cls = jj < pad0 ? 0 : 1;                        // chunk-uniform (pad0 % 64 == 0)
     const uint32_t fi = cls == 0 ? jj : jj - pad0;
     const DevClass& c = p.cls[cls];
+    // the pair's features first: their latency overlaps the model's read
+    // (pinned host memory for small batches) and its value constants
+    const uint32_t ic = fi < c.n ? fi : 0u;                  // a class with chunks has features
+    const double x = c.x[ic], y = c.y[ic];
+    const double f2 = (KIND < 3 && cls == 1) ? c.c0[ic] : c.a[ic];
+    const double f3 = KIND >= 3 ? c.c0[ic] : (cls == 1 ? c.c1[ic] : 0.0);
+    __shared__ typename ModelOf<KIND>::type m_sh;
+    __shared__ ValueConst vc_sh;
+    if (threadIdx.x == 0) {
+        m_sh = models[mi];
+        if constexpr (KIND <= 2) vc_sh = value_const(m_sh, KIND == 1, KIND == 2);
+    }
+    __syncthreads();
+    if (!jin) return;                                        // wave-uniform, after the barrier
+    const auto m = m_sh;
+    const bool live = inc == nullptr || inc[mi] <= 101;
     const bool ev = live && fi < c.n;
     double r2 = 0.0;
     if (ev) {
-        const double x = c.x[fi], y = c.y[fi];
-        const double f2 = (KIND < 3 && cls == 1) ? c.c0[fi] : c.a[fi];
-        const double f3 = KIND >= 3 ? c.c0[fi] : (cls == 1 ? c.c1[fi] : 0.0);
         if constexpr (KIND >= 3) {
             r2 = geo_sq_residual<KIND>(x, y, f2, f3, m.h);
         } else if (cls == 0) {
@@ -3930,7 +3946,10 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         const M* mp = static_cast<const M*>(models);
         const uint32_t probe = probe_bits();               // GCR_PROBE bits 8 / 9: timing probes (results invalid)
         const uint32_t nchunks = ntot / 64;
-        if (lo_split() && lo_fold_wide() && probe == 0 && ntot <= 2 * kLoBlock && nm <= p.lo.cap_models &&
+        // the split pays where the per-pair arithmetic is heavy (the value
+        // formulas); the correspondence estimators' residuals are cheap and
+        // their one-kernel launch was faster (F latency A/B, round 4)
+        if (KIND <= 2 && lo_split() && lo_fold_wide() && probe == 0 && ntot <= 2 * kLoBlock && nm <= p.lo.cap_models &&
             p.lo.vals != nullptr && p.lo.meta != nullptr) {
             const dim3 grid((nchunks + kLrThreads / 64 - 1) / (kLrThreads / 64), nm);
             hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, mp, inc, T[0], T[1], pad0,
@@ -4008,7 +4027,8 @@ __global__ __launch_bounds__(kLoThreads) void k_fold_test(const double* __restri
 // an LDS copy of a[0, n), split at h = b[0]: out[0] = a[0, h) from +0,
 // out[1] = a[h, n) from +0, out[2] = a[h, n) from out[0] (fold_exact_chains);
 // out[3..5] = the same sums by one lane's sequential loop, out[6] = cycles of
-// the chains (n >= 7).
+// the chains (n >= 7); out[8..12] = cycle stamps after the fold's barriers
+// (n >= 13).
 __global__ __launch_bounds__(kLoThreads) void k_fold3_test(const double* __restrict__ a, uint32_t n,
                                                           const double* __restrict__ hb, double* out) {
     __shared__ double buf[kLoBlock];
@@ -4021,7 +4041,7 @@ __global__ __launch_bounds__(kLoThreads) void k_fold3_test(const double* __restr
     const BlkChain ch[3] = {{0u, h, 0.0, -1}, {h, n, 0.0, -1}, {h, n, 0.0, 0}};
     double r[3];
     const uint64_t t0 = __builtin_readcyclecounter();
-    fold_exact_chains<3>(buf, ch, bsc, kLoBlock, r);
+    fold_exact_chains<3>(buf, ch, bsc, kLoBlock, r, n >= 13 ? out + 8 : nullptr);
     const uint64_t t1 = __builtin_readcyclecounter();
     if (t == 0) {
         double s0 = 0.0, s1 = 0.0;
