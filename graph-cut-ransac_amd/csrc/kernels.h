@@ -50,7 +50,7 @@ struct ModelOf<4> {                 // fundamental matrix: same 9-double POD
 // Scratch of the split small-batch scorer (launch_score_small): per model
 // small_score_pairs(p) doubles (each 64-pair chunk's inlier values, compacted
 // to the chunk's start) and small_score_pairs(p) / 64 chunk counts.
-constexpr uint32_t kSplitModels = 64;          // models per split launch
+constexpr uint32_t kSplitModels = 256;         // models per split launch (kSmallScore)
 constexpr size_t kSplitMaxPairs = 16384;       // pairs (every inlier value fits k_lo_fold's LDS)
 struct SmallScratch {
     double* vals = nullptr;

@@ -132,12 +132,14 @@ def test_small_scorer_wide_fold_equals_one_lane_fold(kind, monkeypatch):
     assert a == c
 
 
-@pytest.mark.parametrize("kind", [N.SOLVER_SIFT22, N.SOLVER_HOMOGRAPHY4])
-def test_small_scorer_beyond_split_capacity(kind, monkeypatch):
-    # more models than the split scratch holds (kSplitModels = 64): k_lo_chain
-    a = _small_scores(kind, None, monkeypatch, nmodels=90)
-    b = _small_scores(kind, "seq", monkeypatch, nmodels=90)
+@pytest.mark.parametrize("kind", [N.SOLVER_SCALE3, N.SOLVER_SIFT22])
+def test_small_scorer_many_models(kind, monkeypatch):
+    # a replay chunk's worth of models (up to kSplitModels = 256) in one split launch
+    a = _small_scores(kind, None, monkeypatch, nmodels=250)
+    b = _small_scores(kind, "seq", monkeypatch, nmodels=250)
+    c = _small_scores(kind, None, monkeypatch, split=False, nmodels=250)
     assert a == b
+    assert a == c
 
 
 def test_small_scorer_large_problem_keeps_per_block_folds(monkeypatch):
