@@ -1866,38 +1866,46 @@ struct BlkChain {
     int from;
 };
 
-// the walk of one chain's runs by one wave (wave-uniform; decisions on the
-// running sum's high word in a scalar register): exact running sum s at
-// position pos (after the head).  s + U A_r is one exact addition when s lies
-// in run r's binade and the result stays in it; then special r by an ordinary
-// addition.  A bad chain, too many specials or the first failed check fold
+// the walk of one chain's runs by one wave (wave-uniform): exact running sum
+// s at position pos (after the head).  s + U A_r is one exact addition when s
+// lies in run r's binade and the result stays in it; then special r by an
+// ordinary addition.  The loop has no data-dependent branch: each run's
+// checks only clear a sticky `ok` flag, and s / pos stop advancing at the
+// first failed check (the serial dependence per run is one fma, one scaling
+// and one addition).  A bad chain, too many specials or a failed check fold
 // the rest value by value.
 __device__ __forceinline__ double blk_walk(const double* __restrict__ cb, uint32_t pos, const uint32_t e, double s,
-                                           const BlkFoldScratch& sc, const uint32_t cap) {
+                                           const BlkFoldScratch& sc, const uint32_t cap, double* dbg = nullptr) {
     const int lane = threadIdx.x & 63;
-    auto hi_s = [](double v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(as_u64(v) >> 32)); };
     const uint32_t nspec = sc.nspec;
     if (sc.bad == 0 && nspec <= (uint32_t)kBlkSpecials) {
         const uint32_t nr = nspec + 1;
-        // run r's record in lane r
+        // run r's record in lane r: its sum A_r, binade el (0: the parts
+        // disagree), the scalings 2^(1075 - el) / 2^(el - 1075), special r
         const int rl = lane < (int)nr ? lane : 0;
         const double rA = sc.runA[rl];
-        const int rE = sc.runEmin[rl] == sc.runEmax[rl] ? sc.runEmin[rl] : 0;
+        const int emin = sc.runEmin[rl], emax = sc.runEmax[rl];
+        const uint32_t rE = emin == emax && emin >= 53 && emin < 0x7fe ? (uint32_t)emin : 0u;
+        const uint32_t eu = rE != 0u ? rE : 1075u;
+        const double up = as_f64((uint64_t)(2098u - eu) << 52), dn = as_f64((uint64_t)(eu - 52u) << 52);
         const double rV = lane < (int)nspec ? sc.specV[lane] : 0.0;
-        const uint32_t rP = lane < (int)nspec ? sc.specPos[lane] : 0u;
-        uint32_t r = 0;
-        for (; r < nr; ++r) {
-            const uint32_t el = (uint32_t)__builtin_amdgcn_readlane(rE, (int)r);
-            if (el == 0u || (hi_s(s) >> 20) != (0x800u | el)) break;   // s < 0 in binade el
-            const double S = s * as_f64((uint64_t)(2098 - el) << 52) + readlane_f64(rA, (int)r);
-            if ((hi_s(S) >> 20) != 0xc33u) break;                       // S in (-2^53, -2^52]
-            s = S * as_f64((uint64_t)(el - 52) << 52);
-            if (r + 1 < nr) {
-                s = s + readlane_f64(rV, (int)r);
-                pos = (uint32_t)__builtin_amdgcn_readlane((int)rP, (int)r) + 1u;
-            }
+        const uint32_t rP = lane < (int)nspec ? sc.specPos[lane] + 1u : e;
+        bool ok = true;
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)rE, (int)r);
+            const bool in_b = el != 0u && (uint32_t)(as_u64(s) >> 52) == (0x800u | el);   // s < 0 in binade el
+            const double S = __builtin_fma(s, readlane_f64(up, (int)r), readlane_f64(rA, (int)r));
+            const bool fits = (uint32_t)(as_u64(S) >> 52) == 0xc33u;                       // S in (-2^53, -2^52]
+            ok = ok && in_b && fits;
+            // s * 2^(1075 - el) is exact, so the fma rounds what s*U + A did
+            const double sn = S * readlane_f64(dn, (int)r) + readlane_f64(rV, (int)r);
+            s = ok ? sn : s;
+            pos = ok ? (uint32_t)__builtin_amdgcn_readlane((int)rP, (int)r) : pos;
         }
-        if (r == nr) pos = e;
+    }
+    if (dbg != nullptr && (threadIdx.x & 63) == 0) {
+        dbg[0] = (double)pos;
+        dbg[1] = (double)e;
     }
     if (pos < e) s = fold_seq_lane(cb, pos, e, s, cap);
     return s;
@@ -2117,8 +2125,10 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
     for (int c = 0; c < NC; ++c) {
         if (ch[c].from >= 0 || wave != c) continue;
         double s = seq[c] ? fold_seq_lane(cb, ch[c].k, ch[c].e, ch[c].start, cap)
-                          : blk_walk(cb, ch[c].k + kBlkHead, ch[c].e, sc[c].head, sc[c], cap);
+                          : blk_walk(cb, ch[c].k + kBlkHead, ch[c].e, sc[c].head, sc[c], cap,
+                                     dbg != nullptr && c == 0 ? dbg + 8 : nullptr);
         if (lane == 0) sc[c].result = s;
+        if (c == 0) stamp(5);
 #pragma unroll
         for (int d = c + 1; d < NC; ++d) {
             if (ch[d].from != c) continue;
@@ -2127,9 +2137,11 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
                 u = fold_seq_lane(cb, ch[d].k, ch[d].e, s, cap);
             } else {
                 u = fold_seq_lane8(cb, ch[d].k, ch[d].k + kBlkHead, s);      // its head, from the exact start
+                if (c == 0) stamp(6);
                 u = blk_walk(cb, ch[d].k + kBlkHead, ch[d].e, u, sc[d], cap);
             }
             if (lane == 0) sc[d].result = u;
+            if (c == 0) stamp(7);
         }
     }
     __syncthreads();
@@ -4027,8 +4039,9 @@ __global__ __launch_bounds__(kLoThreads) void k_fold_test(const double* __restri
 // an LDS copy of a[0, n), split at h = b[0]: out[0] = a[0, h) from +0,
 // out[1] = a[h, n) from +0, out[2] = a[h, n) from out[0] (fold_exact_chains);
 // out[3..5] = the same sums by one lane's sequential loop, out[6] = cycles of
-// the chains (n >= 7); out[8..12] = cycle stamps after the fold's barriers
-// (n >= 13).
+// the chains (n >= 7); out[8..15] = cycle stamps: after the fold's four
+// barriers, then wave 0's walks (chain 0 done, chain 2's head, chain 2 done)
+// (n >= 16).
 __global__ __launch_bounds__(kLoThreads) void k_fold3_test(const double* __restrict__ a, uint32_t n,
                                                           const double* __restrict__ hb, double* out) {
     __shared__ double buf[kLoBlock];
@@ -4041,7 +4054,7 @@ __global__ __launch_bounds__(kLoThreads) void k_fold3_test(const double* __restr
     const BlkChain ch[3] = {{0u, h, 0.0, -1}, {h, n, 0.0, -1}, {h, n, 0.0, 0}};
     double r[3];
     const uint64_t t0 = __builtin_readcyclecounter();
-    fold_exact_chains<3>(buf, ch, bsc, kLoBlock, r, n >= 13 ? out + 8 : nullptr);
+    fold_exact_chains<3>(buf, ch, bsc, kLoBlock, r, n >= 18 ? out + 8 : nullptr);
     const uint64_t t1 = __builtin_readcyclecounter();
     if (t == 0) {
         double s0 = 0.0, s1 = 0.0;

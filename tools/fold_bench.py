@@ -43,7 +43,7 @@ def run3(v, h):
     hb = np.full(v.size, float(h))
     dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
     N.check(N.lib.gcr_debug_math(N.context(0), 12, dp(v), dp(hb), v.size, dp(out)))
-    return out[:13]
+    return out[:18]
 
 
 # the three chains of the two-class fold (gcr_debug_math op 12: class 0 from
@@ -57,5 +57,7 @@ for name, v, h in (("M2-like 2 x 2500", np.concatenate([cases["scale r^2, thr 0.
         o = run3(v, h)
     ok = all(o[i].tobytes() == o[i + 3].tobytes() for i in range(3))
     ph = np.diff(o[8:13])
+    wk = np.diff(np.concatenate([o[11:12], o[13:16]]))
     print(f"3 chains {name:18s} n={v.size:5d} h={h:5d} {o[6]:9.0f} cyc  equal {ok}  phases (chunk sums, parts, "
-          f"runs, walks) {' / '.join(f'{x:.0f}' for x in ph)}")
+          f"runs, walks) {' / '.join(f'{x:.0f}' for x in ph)}; wave 0: walk 0 {wk[0]:.0f}, head 2 {wk[1]:.0f}, "
+          f"walk 2 {wk[2]:.0f}; walk 0 stopped at {o[16]:.0f} of {o[17]:.0f}")
