@@ -1842,7 +1842,7 @@ __device__ __forceinline__ double fold_seq_lane8(const double* __restrict__ cb, 
     return run;
 }
 
-constexpr uint32_t kBlkHead = 16;
+constexpr uint32_t kBlkHead = 128;                    // a chain from a given start (0 when continuing)
 constexpr int kBlkSpecials = 63;
 constexpr uint32_t kBlkMaxM = 16;                       // values per chunk, held in registers
 
@@ -1854,7 +1854,7 @@ struct BlkFoldScratch {
     double specV[kBlkSpecials];
     uint32_t specPos[kBlkSpecials];
     uint32_t bad, nspec;
-    double head, result;
+    double head, hexact, result;         // head: approximate (any order), hexact: in order
 };
 
 // One in-order sum of fold_exact_chains: the values cb[k, e) added to a
@@ -1975,9 +1975,11 @@ __device__ __forceinline__ void blk_parts(const double* __restrict__ cb, const u
 
 // fold_exact_chains: NC in-order sums by all kLoThreads threads of the
 // workgroup at once, sharing the barriers (every thread calls it, in uniform
-// control flow).  Per chain the first kBlkHead values are added one by one
-// (the sum is still small there); thread t takes the t-th of kLoThreads
-// contiguous chunks of the rest.  A block scan of approximate chunk sums
+// control flow).  A chain from a given start adds its first kBlkHead values
+// one by one (the sum is still small there and would cross a binade every
+// few values; a continuing chain's sum is already large and has no head);
+// thread t takes the t-th of the contiguous chunks of 4, 8 or 16 values of
+// the rest.  A block scan of approximate chunk sums
 // gives every chunk an approximate start (a continuing chain starts at the
 // approximate total of the chain it continues); walking its chunk with an
 // approximate running sum, a thread adds the integer increments rint(v / U)
@@ -2006,27 +2008,40 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
     };
     stamp(0);
     bool seq[NC];
-    uint32_t b[NC], ee[NC], m[NC];
+    uint32_t b[NC], ee[NC], m[NC], hl[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const uint32_t n = ch[c].e - ch[c].k;
-        seq[c] = n < kBlkHead + kLoThreads / 4 || n - kBlkHead > kBlkMaxM * (uint32_t)kLoThreads;
-        const uint32_t rest = seq[c] ? 0u : n - kBlkHead;
+        hl[c] = ch[c].from < 0 ? kBlkHead : 0u;
+        seq[c] = n < hl[c] + kLoThreads / 4 || n - hl[c] > kBlkMaxM * (uint32_t)kLoThreads;
+        const uint32_t rest = seq[c] ? 0u : n - hl[c];
         // values per chunk (uniform: the loops below are unrolled for 4, 8 or 16)
-        m[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)((rest + kLoThreads - 1) / kLoThreads));
-        b[c] = ch[c].k + kBlkHead + min(rest, (uint32_t)t * m[c]);
-        ee[c] = ch[c].k + kBlkHead + min(rest, (uint32_t)t * m[c] + m[c]);
+        // chunks of 4, 8 or 16 values (the fewest threads the length needs:
+        // the VALU work scales with the busy waves)
+        const uint32_t mneed = (uint32_t)__builtin_amdgcn_readfirstlane((int)((rest + kLoThreads - 1) / kLoThreads));
+        m[c] = mneed <= 4u ? 4u : (mneed <= 8u ? 8u : kBlkMaxM);
+        b[c] = ch[c].k + hl[c] + min(rest, (uint32_t)t * m[c]);
+        ee[c] = ch[c].k + hl[c] + min(rest, (uint32_t)t * m[c] + m[c]);
         if (t <= kBlkSpecials) {
             sc[c].runA[t] = 0.0;
             sc[c].runEmin[t] = 0x7fffffff;
             sc[c].runEmax[t] = -1;
         }
-        // the head: exact for a chain with a given start, approximate (from
-        // +0) for a continuing one (its walk adds it to the exact start)
-        if (t == 64 * c) {
-            sc[c].bad = 0;
-            if (!seq[c]) sc[c].head = fold_seq_lane8(cb, ch[c].k, ch[c].k + kBlkHead, ch[c].from < 0 ? ch[c].start : 0.0);
+        if (t == 0) sc[c].bad = 0;
+    }
+    // the heads (chains from a given start) on the last waves, which hold no
+    // chunk unless the chain fills most of the chunks: here their sum in any
+    // order (the chunks' approximate start), in phase 2 their in-order sum
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        if (wave != kLoThreads / 64 - 1 - c) continue;
+        double h = 0.0;
+        if (!seq[c] && ch[c].from < 0) {
+            h = lane == 0 ? ch[c].start : 0.0;
+            for (uint32_t q = (uint32_t)lane; q < hl[c]; q += 64) h += cb[ch[c].k + q];
         }
+        h = wave_incl_scan_f64(h);
+        if (lane == 63) sc[c].head = h;
     }
     // 1. approximate chunk sums, block scans
     double xin[NC], a[NC];
@@ -2039,6 +2054,10 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
     }
     __syncthreads();
     stamp(1);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        if (t == kLoThreads - 64 * (c + 1) && !seq[c] && ch[c].from < 0)
+            sc[c].hexact = fold_seq_lane8(cb, ch[c].k, ch[c].k + hl[c], ch[c].start);
     // 2. integer increments in up to three parts (two specials) per chunk
     BlkParts pt[NC];
     double total[NC];
@@ -2125,7 +2144,7 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
     for (int c = 0; c < NC; ++c) {
         if (ch[c].from >= 0 || wave != c) continue;
         double s = seq[c] ? fold_seq_lane(cb, ch[c].k, ch[c].e, ch[c].start, cap)
-                          : blk_walk(cb, ch[c].k + kBlkHead, ch[c].e, sc[c].head, sc[c], cap,
+                          : blk_walk(cb, ch[c].k + hl[c], ch[c].e, sc[c].hexact, sc[c], cap,
                                      dbg != nullptr && c == 0 ? dbg + 8 : nullptr);
         if (lane == 0) sc[c].result = s;
         if (c == 0) stamp(5);
@@ -2136,9 +2155,8 @@ __device__ __forceinline__ void fold_exact_chains(const double* __restrict__ cb,
             if (seq[d]) {
                 u = fold_seq_lane(cb, ch[d].k, ch[d].e, s, cap);
             } else {
-                u = fold_seq_lane8(cb, ch[d].k, ch[d].k + kBlkHead, s);      // its head, from the exact start
                 if (c == 0) stamp(6);
-                u = blk_walk(cb, ch[d].k + kBlkHead, ch[d].e, u, sc[d], cap);
+                u = blk_walk(cb, ch[d].k, ch[d].e, s, sc[d], cap);        // no head: from the exact start
             }
             if (lane == 0) sc[d].result = u;
             if (c == 0) stamp(7);

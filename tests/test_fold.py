@@ -1,6 +1,7 @@
 """The block-parallel exact fold (kernels.hip fold_exact_block, used by
-k_lo_chain by default) restated in numpy, chunk for chunk: a
-16-value head added one by one, 1024 chunks whose integer increments
+the small scorer) restated in numpy, chunk for chunk: a
+128-value head added one by one (none for a chain that continues another),
+chunks of 4, 8 or 16 values whose integer increments
 rint(v / ulp) are summed exactly per run of one binade, runs separated by the
 special values (predicted binade crossings, ties) that the walk adds on their
 own; the walk folds value by value wherever a check fails.  Checked against
@@ -28,9 +29,9 @@ def _exp(x):
 
 # --------------------------------------------------------- round 4: block ----
 # fold_exact_block (kernels.hip): the in-order sum by all 1024 threads of a
-# workgroup.  The first BLK_HEAD values are added one by one (the sum is still
-# small there); thread t then takes the t-th of 1024 contiguous chunks of the
-# rest.  A block scan of approximate chunk sums gives every chunk an
+# workgroup.  The first `head` values are added one by one (the sum is still
+# small there); thread t then takes the t-th of the contiguous chunks of 4, 8
+# or 16 values (the fewest threads the length needs) of the rest.  A block scan of approximate chunk sums gives every chunk an
 # approximate start; walking its chunk with an approximate running sum, a
 # thread adds the integer increments rint(v / U) (U the ulp of the binade the
 # running sum is predicted to be in) and marks as special every value whose
@@ -45,7 +46,7 @@ def _exp(x):
 # disagree on the binade, more than BLK_SPECIALS specials or more than two in
 # one chunk fold the whole sequence value by value.
 BLK_THREADS = 1024
-BLK_HEAD = 16
+BLK_HEAD = 128
 BLK_SPECIALS = 63
 BLK_MAXM = 16          # values per chunk held in registers (longer ranges: one by one)
 
@@ -54,17 +55,22 @@ def _ulp_scale(be):
     return math.ldexp(1.0, 1075 - be)
 
 
-def fold_exact_block(v, run=0.0, stats=None):
+def fold_exact_block(v, run=0.0, stats=None, head_len=BLK_HEAD):
+    """head_len = 0: a continuing chain (fold_exact_chains from >= 0), whose
+    walk starts at the exact start itself."""
     v = np.asarray(v, dtype=np.float64)
     n = v.size
     st = {"runs": 0, "specials": 0, "fallback": None}
-    if n < BLK_HEAD + BLK_THREADS // 4 or n - BLK_HEAD > BLK_MAXM * BLK_THREADS:
+    if n < head_len + BLK_THREADS // 4 or n - head_len > BLK_MAXM * BLK_THREADS:
         return _fold_seq(v, run)
-    head = _fold_seq(v[:BLK_HEAD], run)                   # exact (thread 0)
-    ahead = _fold_seq(v[:BLK_HEAD], run)                  # the approximate start is the same value here
-    rest = n - BLK_HEAD
-    m = (rest + BLK_THREADS - 1) // BLK_THREADS
-    bounds = [(BLK_HEAD + min(rest, t * m), BLK_HEAD + min(rest, t * m + m)) for t in range(BLK_THREADS)]
+    head = _fold_seq(v[:head_len], run)                   # exact (thread 64 c)
+    # the chunks' approximate start: the device sums the head in any order
+    # (a wave scan); the exact result does not depend on it
+    ahead = float(run + np.sum(v[:head_len]))
+    rest = n - head_len
+    mneed = (rest + BLK_THREADS - 1) // BLK_THREADS
+    m = 4 if mneed <= 4 else (8 if mneed <= 8 else BLK_MAXM)
+    bounds = [(head_len + min(rest, t * m), head_len + min(rest, t * m + m)) for t in range(BLK_THREADS)]
     with np.errstate(over="ignore", invalid="ignore"):
         a = np.array([_fold_seq(v[b:e], 0.0) for b, e in bounds])
         X = np.concatenate([[0.0], np.cumsum(a)[:-1]])    # exclusive scan (any order: approximate)
@@ -118,7 +124,7 @@ def fold_exact_block(v, run=0.0, stats=None):
                 if q < len(pb) - 1:
                     rid += 1
     s = head
-    pos = BLK_HEAD
+    pos = head_len
     for r in range(nr):
         E = runE[r]
         ok = len(E) == 1
@@ -148,9 +154,10 @@ def fold_exact_block(v, run=0.0, stats=None):
 def test_block_fold_restatement_equals_sequential_sum(name):
     v = cases()[name]
     for run in (0.0, -3.0, float(sequential(v[: len(v) // 3]))):
-        got = fold_exact_block(v, run)
-        ref = _fold_seq(v, run)
-        assert np.float64(got).tobytes() == np.float64(ref).tobytes() or (ref != ref and got != got), (got, ref)
+        for head_len in (BLK_HEAD, 0):
+            got = fold_exact_block(v, run, head_len=head_len)
+            ref = _fold_seq(v, run)
+            assert np.float64(got).tobytes() == np.float64(ref).tobytes() or (ref != ref and got != got), (got, ref)
 
 
 def test_block_fold_restatement_random():
