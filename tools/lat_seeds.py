@@ -44,11 +44,16 @@ for rep in range(a.reps):
             st = out[-1]
             res.setdefault((name, seed), []).append((ms, st["iteration_number"], st["slots"],
                                                      st["local_optimization_number"], st["graph_cut_number"],
-                                                     st.get("prefetched_chunks", 0)))
+                                                     st.get("prefetched_chunks", 0),
+                                                     {k: st.get(k, 0.0) for k in ("ms_score", "ms_replay", "ms_lo",
+                                                                                  "ms_lo_fit", "ms_lo_score",
+                                                                                  "ms_refit", "lo_models")}))
 for seed in range(100, 111):
     row = [f"seed {seed}"]
     for name, _ in sets:
         r = res[(name, seed)]
+        ph = " ".join(f"{k[3:] if k.startswith('ms_') else k}={statistics.median(x[6][k] for x in r):.3f}"
+                      for k in r[0][6])
         row.append(f"{name}: {statistics.median(x[0] for x in r):6.3f} ms it {r[0][1]:5d} slots {r[0][2]:6d} "
-                   f"lo {r[0][3]} gc {r[0][4]} pf {r[0][5]}")
+                   f"lo {r[0][3]} gc {r[0][4]} pf {r[0][5]} {ph}")
     print("  |  ".join(row))
