@@ -97,6 +97,19 @@ GCR_HD void gram_add_row(DD acc[kGramN], const double r[4]) {
         for (int b = a; b < 4; ++b, ++k) acc[k] = dd_add(acc[k], dd_two_prod(r[a], r[b]));
 }
 
+// a pair row (r2 == +0.0) with finite r0, r1, r3: its four products with r2
+// are zeros, and adding a zero double-double to a finite accumulator of
+// gram_add_row leaves it bit for bit unchanged (the accumulators are
+// normalised and never hold a -0.0), so only the other six are added
+GCR_HD void gram_add_pair_row(DD acc[kGramN], const double r[4]) {
+    acc[0] = dd_add(acc[0], dd_two_prod(r[0], r[0]));
+    acc[1] = dd_add(acc[1], dd_two_prod(r[0], r[1]));
+    acc[3] = dd_add(acc[3], dd_two_prod(r[0], r[3]));
+    acc[4] = dd_add(acc[4], dd_two_prod(r[1], r[1]));
+    acc[6] = dd_add(acc[6], dd_two_prod(r[1], r[3]));
+    acc[9] = dd_add(acc[9], dd_two_prod(r[3], r[3]));
+}
+
 // pair p (0-based, lexicographic i < j over n) -> (i, j): a floating
 // estimate corrected with exact integer arithmetic
 GCR_HD void pair_of(uint64_t p, uint64_t n, uint64_t& i, uint64_t& j) {

@@ -2779,6 +2779,15 @@ __global__ __launch_bounds__(kGramBlock) void k_sift_gram(DevClass sc, DevClass 
             }
             const uint32_t c = oi[pj];
             sift_pair_row(xi, yi, cosi, sini, oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], row);
+            // row[2] == 0: the same sums as gram_add_row while the row and
+            // the four accumulators its zeros would touch are finite (an
+            // infinite accumulator plus a zero double-double is NaN)
+            if (__builtin_isfinite(row[0]) && __builtin_isfinite(row[1]) && __builtin_isfinite(row[3]) &&
+                __builtin_isfinite(acc[2].hi) && __builtin_isfinite(acc[5].hi) && __builtin_isfinite(acc[7].hi) &&
+                __builtin_isfinite(acc[8].hi)) {
+                gram_add_pair_row(acc, row);
+                continue;
+            }
         }
         gram_add_row(acc, row);
     }

@@ -449,6 +449,32 @@ def test_gpu_refit_matches_host_and_oracle_bitwise(ks, ko, refit, monkeypatch):
         assert np.all(np.abs(out[0] - frz) <= 1e-6 * np.maximum(np.abs(frz), 1e-12))
 
 
+@pytest.mark.parametrize("huge", [1e200, 1e150])
+def test_gpu_gram_refit_with_overflowing_scale_rows(huge):
+    # a scale inlier at huge coordinates overflows its Gram products to inf:
+    # the kernel's shortcut for the pair rows (their four zero products are
+    # skipped while the touched accumulators are finite) must leave the result
+    # bit for bit equal to the host's full accumulation (NaN where it is NaN)
+    fs, fo, ts, to, _, _ = S.problem_m2(3000, 3000, seed=77)
+    rng = np.random.default_rng(78)
+    i0 = np.sort(rng.choice(np.flatnonzero(ts), size=50, replace=False)).astype(np.uint32)
+    i1 = np.sort(rng.choice(np.flatnonzero(to), size=400, replace=False)).astype(np.uint32)
+    fs = np.array(fs, dtype=np.float64, copy=True)
+    fs[i0[7], 0] = huge
+    fs[i0[7], 1] = -huge
+    prob = Problem(N.SOLVER_SIFT22, fs, fo)
+    u32 = C.POINTER(C.c_uint32)
+    out, rcs = [], []
+    for use_gpu in (1, 0):
+        m = N.RectModel()
+        rc = N.lib.gcr_debug_fit_nonminimal(prob.h, i0.ctypes.data_as(u32), len(i0), i1.ctypes.data_as(u32),
+                                            len(i1), use_gpu, C.byref(m))
+        rcs.append(rc)
+        out.append(np.array([m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi]))
+    assert rcs[0] == rcs[1]
+    assert np.array_equal(bits(out[0]), bits(out[1]))
+
+
 # --------------------------------------------- band prefilter, adversarial ----
 def _boundary_problem(kind, rng, anchors, per=160, eps=(-1e-6, -1e-7, 0.0, 1e-7, 1e-6)):
     """Features placed at the inlier boundary (+-1.5 thr relative offsets eps)
