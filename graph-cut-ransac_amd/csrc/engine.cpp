@@ -2733,7 +2733,8 @@ private:
                 }
             }
             HIPC(launch_score_small(P_->dp, Tm_, dmodels, nullptr, n,
-                                    zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev(), s_, lists ? &lb : nullptr));
+                                    zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev(), s_, lists ? &lb : nullptr,
+                                    kRect ? static_cast<const void*>(models) : nullptr));
         } else {
             HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
         }
@@ -3512,7 +3513,8 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
         prob->w->lo_sb.ensure(nmodels);
         HIPC(hipMemcpyAsync(prob->w->lo_models.p, hm.data(), nmodels * sizeof(RectModel), hipMemcpyHostToDevice, s));
         if (identity && debug_small_scorer(nmodels)) {
-            HIPC(launch_score_small(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, prob->w->lo_sb.dev(), s));
+            HIPC(launch_score_small(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, prob->w->lo_sb.dev(), s,
+                                    nullptr, hm.data()));
         } else {
             HIPC(launch_score(prob->dp, T, prob->w->lo_models.p, nullptr, nmodels, identity, prob->w->lo_sb.dev(), s));
         }

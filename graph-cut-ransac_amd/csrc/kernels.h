@@ -296,8 +296,14 @@ struct ListBits {
     uint64_t* bits;
     uint64_t* mbits;         // optional: the MSAC inlier ballots too (r^2 <= the scoring threshold)
 };
+// hmodels (optional, rectification solvers): a host copy of the nm
+// RectModels; with at most kArgModels of them the split scorer takes the
+// models as a kernel argument instead of reading `models` (pinned host memory
+// for small batches: a PCIe round trip at the start of every workgroup).
+constexpr uint32_t kArgModels = 50;
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
-                              uint32_t nm, const ScoreOut& out, hipStream_t stream, const ListBits* lists = nullptr);
+                              uint32_t nm, const ScoreOut& out, hipStream_t stream, const ListBits* lists = nullptr,
+                              const void* hmodels = nullptr);
 
 // Per-feature inlier mask of one model for class `cls`: bit 0 the decision,
 // bit 1 set when the pair's twin r^2 lies in the flag band of T (exact.h:

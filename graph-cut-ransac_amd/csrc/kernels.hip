@@ -19,6 +19,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace gcr {
@@ -2434,11 +2435,18 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
 constexpr int kLrThreads = 256;
 static_assert(kSplitMaxPairs == 2 * kLoBlock, "k_lo_fold holds every inlier value in LDS");
 
+// up to kArgModels rectification models passed by value (the kernel-argument
+// segment), n = 0: read `models`
+struct ArgModels {
+    RectModel m[kArgModels];
+    uint32_t n;
+};
+
 template <int KIND>
 __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
                                                         const uint8_t* __restrict__ inc, double T0, double T1,
                                                         uint32_t pad0, uint32_t nchunks, ListBits lb, FlagBand fbm,
-                                                        FlagBand fbl) {
+                                                        FlagBand fbl, ArgModels am) {
     const uint32_t mi = blockIdx.y;
     const uint32_t j = blockIdx.x * (kLrThreads / 64) + (threadIdx.x >> 6);      // chunk
     const int lane = threadIdx.x & 63;
@@ -2456,8 +2464,12 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
     __shared__ typename ModelOf<KIND>::type m_sh;
     __shared__ ValueConst vc_sh;
     if (threadIdx.x == 0) {
-        m_sh = models[mi];
-        if constexpr (KIND <= 2) vc_sh = value_const(m_sh, KIND == 1, KIND == 2);
+        if constexpr (KIND <= 2) {
+            m_sh = mi < am.n ? am.m[mi] : models[mi];
+            vc_sh = value_const(m_sh, KIND == 1, KIND == 2);
+        } else {
+            m_sh = models[mi];
+        }
     }
     __syncthreads();
     if (!jin) return;                                        // wave-uniform, after the barrier
@@ -3966,6 +3978,13 @@ bool lo_split() {
     return !(e && e[0] == '0');
 }
 
+// GCR_LO_ARGMODELS=0: the split scorer reads its models from `models` even
+// when they fit the kernel arguments (read per launch)
+bool lo_argmodels() {
+    const char* e = getenv("GCR_LO_ARGMODELS");
+    return !(e && e[0] == '0');
+}
+
 size_t small_score_pairs(const DevProblem& p) {
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t pad1 = (p.solver == 2) ? ((p.cls[1].n + 63u) & ~63u) : 0u;
@@ -3973,7 +3992,8 @@ size_t small_score_pairs(const DevProblem& p) {
 }
 
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
-                              uint32_t nm, const ScoreOut& out, hipStream_t stream, const ListBits* lists) {
+                              uint32_t nm, const ScoreOut& out, hipStream_t stream, const ListBits* lists,
+                              const void* hmodels) {
     const ListBits lb = lists ? *lists : ListBits{{0.0, 0.0}, 0, 0.0, nullptr, nullptr};
     if (nm == 0) return hipSuccess;
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
@@ -3991,8 +4011,14 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         if (KIND <= 2 && lo_split() && lo_fold_wide() && probe == 0 && ntot <= 2 * kLoBlock && nm <= p.lo.cap_models &&
             p.lo.vals != nullptr && p.lo.meta != nullptr) {
             const dim3 grid((nchunks + kLrThreads / 64 - 1) / (kLrThreads / 64), nm);
+            ArgModels am;
+            am.n = 0;
+            if (KIND <= 2 && hmodels != nullptr && nm <= kArgModels && lo_argmodels()) {
+                std::memcpy(am.m, hmodels, (size_t)nm * sizeof(RectModel));
+                am.n = nm;
+            }
             hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, mp, inc, T[0], T[1], pad0,
-                               nchunks, lb, flag_band(T), flag_band(lb.T));
+                               nchunks, lb, flag_band(T), flag_band(lb.T), am);
             hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, p, inc, pad0, nchunks, out);
         } else if (lo_fold_wide())
             hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1],

@@ -130,6 +130,14 @@ def test_small_scorer_wide_fold_equals_one_lane_fold(kind, monkeypatch):
     c = _small_scores(kind, None, monkeypatch, split=False)   # k_lo_chain, block fold
     assert a == b
     assert a == c
+    # <= kArgModels (50) rectification models travel as kernel arguments;
+    # GCR_LO_ARGMODELS=0 reads them from memory instead
+    for nm in (1, 50):
+        d = _small_scores(kind, None, monkeypatch, nmodels=nm)
+        monkeypatch.setenv("GCR_LO_ARGMODELS", "0")
+        e = _small_scores(kind, None, monkeypatch, nmodels=nm)
+        monkeypatch.delenv("GCR_LO_ARGMODELS")
+        assert d == e
 
 
 @pytest.mark.parametrize("kind", [N.SOLVER_SCALE3, N.SOLVER_SIFT22])
