@@ -594,10 +594,12 @@ def main():
                 "kernel": kernel_name,
                 "kernel_build_id": build_id,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
-                "avg_kernel_ms_note": ("HIP events on the engine's stream around every 4th launch "
-                                       "(GCR_TIMING_STRIDE), never the launch right after a deferred-selection "
-                                       "flush; the sampled mean is extrapolated to all launches. The whole "
-                                       "queue, selections included, is ms_per_step"),
+                "avg_kernel_ms_note": ("HIP events on the engine's stream: when no deferred selection falls "
+                                       "inside a call's launches 1..K-2 (K <= 64), one event pair brackets those "
+                                       "back-to-back launches and their mean is taken (GCR_TIMING_SPAN); "
+                                       "otherwise pairs around every 4th launch (GCR_TIMING_STRIDE), never the "
+                                       "launch right after a deferred-selection flush. The mean is extrapolated "
+                                       "to all launches. The whole queue, selections included, is ms_per_step"),
                 "hypotheses_per_launch": models_per_launch,
                 "algorithmic_hbm": {
                     "achieved_gbs": achieved,

@@ -938,6 +938,18 @@ uint32_t timing_stride() {
     return v;
 }
 
+// Span timing (the fused, non-pipelined path; default): ONE event pair
+// around the back-to-back scoring launches 1 .. nb-2 of a call when no
+// deferred selection falls between them -- their mean duration without the
+// per-batch pairs' ~6 us queue gaps (a 20-step call: 10 gaps, ~3 % of its
+// time).  The first launch (it generates its own slots: no look-ahead batch
+// before it) and the last (followed by the selection) are left out.
+// GCR_TIMING_SPAN=0 keeps the per-batch pairs.
+bool timing_span() {
+    const char* e = getenv("GCR_TIMING_SPAN");
+    return !(e && e[0] == '0');
+}
+
 // hybrid systems at least this tall are solved on the GPU (the host QR costs
 // ~15 ns/row; the GPU path ~0.3 ms + ~15 synchronisations)
 size_t gpu_refit_rows() {
@@ -2106,6 +2118,7 @@ public:
             P_->w->evs.push_back(ev);
         }
         uint32_t timed = 0;
+        uint32_t span_launches = 0;              // > 0: evs[0..1] bracket that many launches
         if (Tr::kPipe && nb > 1 && pipe_on()) {
             // two-stream pipeline (Tr::verify_gen / verify_score): generation
             // of batch b on the side stream once batch b - 2 (same buffer set)
@@ -2150,13 +2163,25 @@ public:
                 timed += t;
             }
         } else {
+            bool span = nb >= 4 && timing_span();
+            for (uint32_t b = 2; span && b + 2 <= nb; ++b)
+                if (Tr::select_flush_before(b, nslots)) span = false;    // a selection inside the span
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint64_t s0 = slot0 + (uint64_t)b * nslots;
-                const bool t = b % stride == 0 && !Tr::select_flush_before(b, nslots) && timed < ntimed;
-                HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, drecs + b,
-                                t ? P_->w->evs[2 * timed] : nullptr, t ? P_->w->evs[2 * timed + 1] : nullptr, s_,
-                                b, nb));
-                timed += t;
+                hipEvent_t e0 = nullptr, e1 = nullptr;
+                if (span) {
+                    if (b == 1) e0 = P_->w->evs[0];
+                    if (b + 2 == nb) e1 = P_->w->evs[1];
+                } else if (b % stride == 0 && !Tr::select_flush_before(b, nslots) && timed < ntimed) {
+                    e0 = P_->w->evs[2 * timed];
+                    e1 = P_->w->evs[2 * timed + 1];
+                    ++timed;
+                }
+                HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, drecs + b, e0, e1, s_, b, nb));
+            }
+            if (span) {
+                span_launches = nb - 2;
+                timed = 1;
             }
         }
         if (!zc)
@@ -2169,7 +2194,10 @@ public:
             HIPC(hipEventElapsedTime(&kms, P_->w->evs[2 * q], P_->w->evs[2 * q + 1]));
             kms_sum += kms;
         }
-        st_.ms_score_kernel += timed ? kms_sum * (double)nb / (double)timed : 0.0;   // scaled to all batches
+        // scaled to all batches: the sampled launches' mean (span: the span's
+        // time over its launches)
+        const double per = span_launches ? (double)span_launches : (double)timed;
+        st_.ms_score_kernel += timed ? kms_sum * (double)nb / per : 0.0;
         for (uint32_t b = 0; b < nb; ++b) st_.hypotheses += out[b].models;
         st_.launches += 2 * nb;
         st_.hypotheses_computed += (uint64_t)nslots * nb * kP;
