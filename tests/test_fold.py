@@ -55,9 +55,11 @@ def _ulp_scale(be):
     return math.ldexp(1.0, 1075 - be)
 
 
-def fold_exact_block(v, run=0.0, stats=None, head_len=BLK_HEAD):
+def fold_exact_block(v, run=0.0, stats=None, head_len=BLK_HEAD, approx_start=None):
     """head_len = 0: a continuing chain (fold_exact_chains from >= 0), whose
-    walk starts at the exact start itself."""
+    walk starts at the exact start itself.  approx_start: the chunks'
+    approximate start in place of run (a continuing chain's is the chain it
+    continues's approximate total)."""
     v = np.asarray(v, dtype=np.float64)
     n = v.size
     st = {"runs": 0, "specials": 0, "fallback": None}
@@ -66,7 +68,7 @@ def fold_exact_block(v, run=0.0, stats=None, head_len=BLK_HEAD):
     head = _fold_seq(v[:head_len], run)                   # exact (thread 64 c)
     # the chunks' approximate start: the device sums the head in any order
     # (a wave scan); the exact result does not depend on it
-    ahead = float(run + np.sum(v[:head_len]))
+    ahead = float((run if approx_start is None else approx_start) + np.sum(v[:head_len]))
     rest = n - head_len
     mneed = (rest + BLK_THREADS - 1) // BLK_THREADS
     m = 4 if mneed <= 4 else (8 if mneed <= 8 else BLK_MAXM)
@@ -183,3 +185,21 @@ def test_block_fold_fast_on_msac_sums():
         assert np.float64(got).tobytes() == np.float64(_fold_seq(v, run)).tobytes()
         assert st["fallback"] is None, st
         assert st["runs"] <= 24, st
+
+
+def test_continuing_chain_exact_with_approximate_start():
+    """The two-class fold's third chain (class 1 continuing the class-0 sum)
+    starts its chunks from the class-0 chain's APPROXIMATE total: whatever the
+    error of that start, the walk from the exact class-0 sum gives the
+    sequential sum bit for bit (a wrong binade prediction only costs runs)."""
+    rng = np.random.default_rng(16)
+    for _ in range(40):
+        n0, n1 = int(rng.integers(300, 6000)), int(rng.integers(300, 6000))
+        v0 = -rng.uniform(0, 2.25, n0) * 10.0 ** rng.uniform(-6, 1)
+        v1 = -rng.uniform(0, 2.25, n1) * 10.0 ** rng.uniform(-6, 1)
+        a = _fold_seq(v0, 0.0)
+        want = _fold_seq(v1, a)
+        for err in (0.0, 1e-15, 1e-9, 1e-3, 0.5):
+            st = {}
+            got = fold_exact_block(v1, a, st, head_len=0, approx_start=a * (1.0 + err))
+            assert np.float64(got).tobytes() == np.float64(want).tobytes(), (err, got, want)
