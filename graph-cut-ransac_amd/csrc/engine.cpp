@@ -305,6 +305,11 @@ struct Workspace {
     PinBuf<BlockSummary> hsum[2];       // [0] this rank's, then the all-gathered ones
     DevBuf<BlockSummary> dall[2];       // gcr_comm: the all-gathered summaries on the device
     PinBuf<uint64_t> h_cbits[2];        // small-scored chunks: every slot's LO list bits (ListBits)
+    // small-scored chunks: the split scorer's scratch of each chunk set.  Such
+    // a chunk may run on the side stream while the replay stream scores LO
+    // trials / the refit through DevProblem::lo, so they never share one.
+    DevBuf<double> cs_vals[2];
+    DevBuf<uint32_t> cs_meta[2];
     hipEvent_t sum_done[2] = {nullptr, nullptr}, sum_k0[2] = {nullptr, nullptr}, sum_k1[2] = {nullptr, nullptr};
     bool spec_pending[2] = {false, false};   // a speculative chunk of this set may still run
     ~Workspace() {
@@ -402,6 +407,8 @@ struct ExactCount {
     uint64_t pairs = 0;        // pairs decided with glibc
     uint64_t flips = 0;        // ... whose decision differs from the twin's
     double ms = 0.0;
+    uint64_t near_ties = 0;    // score comparisons decided by glibc scores (exact.h ScoreBound)
+    uint64_t near_flips = 0;   // ... whose outcome differs from the value comparison
 };
 
 // GCR_EXACT=0: decisions stay the twins' (no host recheck, no glibc phi):
@@ -422,9 +429,11 @@ bool model_unsafe(const gcr_problem* P, const RectModel& m, double T0) {
 // fold; mv differs from md only in a generated 2-SIFT model's phi.  Sums in
 // feature order, class 0 then 1, the total running across classes.  Pairs in
 // parallel on the host pool, the sums sequential.  `lists`: the MSAC inlier
-// lists too.
+// lists too.  `glibc_sums`: add -(the glibc r^2 under md) instead -- the
+// reference's own score (the near-tie comparisons, exact.h ScoreBound).
 void exact_accumulate(const gcr_problem* P, const RectModel& mv, const RectModel& md, const double T[2],
-                      uint32_t n[2], double v[2], double& tot, std::vector<uint32_t>* lists, ExactCount& ec);
+                      uint32_t n[2], double v[2], double& tot, std::vector<uint32_t>* lists, ExactCount& ec,
+                      bool glibc_sums = false);
 
 // k_mask bytes of one class (bit 0 the twin decision, bit 1 flagged) turned
 // into the reference's decisions under md: flagged pairs -- every pair when
@@ -785,7 +794,8 @@ HostPool& host_pool() {
 
 // ---------------------------------------- decisions in glibc: bodies ----
 void exact_accumulate(const gcr_problem* P, const RectModel& mv, const RectModel& md, const double T[2],
-                      uint32_t n[2], double v[2], double& tot, std::vector<uint32_t>* lists, ExactCount& ec) {
+                      uint32_t n[2], double v[2], double& tot, std::vector<uint32_t>* lists, ExactCount& ec,
+                      bool glibc_sums) {
     const auto t0 = Clock::now();
     thread_local std::vector<double> val;
     thread_local std::vector<uint8_t> dec;
@@ -806,8 +816,9 @@ void exact_accumulate(const gcr_problem* P, const RectModel& mv, const RectModel
         auto body = [&](size_t lo, size_t hi) {
             uint64_t f = 0;
             for (size_t i = lo; i < hi; ++i) {
-                const double rv = host_value(P, c, i, mv, vc);
-                const bool d = host_r2<GlibcMath>(P, c, i, md) <= T[c];
+                const double rg = host_r2<GlibcMath>(P, c, i, md);
+                const bool d = rg <= T[c];
+                const double rv = glibc_sums ? rg : host_value(P, c, i, mv, vc);
                 vp[i] = rv;
                 dp[i] = d ? 1 : 0;
                 f += (rv <= T[c]) != d ? 1u : 0u;
@@ -1403,6 +1414,17 @@ public:
         log_prob_ = std::log(1.0 - prm.confidence);
         do_lo_ = (prm.flags & GCR_FLAG_NO_LO) == 0;
         std::memset(&st_, 0, sizeof(st_));
+        if (kRect && exact_) {
+            sbnd_ = score_bound(Tm_, K_);
+            // any two scores of the problem: counts at most N_c, scores at most N
+            const double nf0 = (double)N_[0], nf1 = (double)N_[1];
+            // the best's glibc score is at least every processed hypothesis's,
+            // so its value score is within 2 B of their running maximum, and a
+            // near tie of it within 4 B: every comparison the reference could
+            // decide differently, and every one the host compares in glibc,
+            // is a chain member
+            if (sbnd_.finite) chain_tol_ = 4.0 * score_dev(sbnd_, nf0, nf1, nf0 + nf1);
+        }
     }
 
     // Shard every chunk over the communicator's ranks, the exchange by
@@ -1505,7 +1527,8 @@ public:
                 if (!b.exact) resolve(b, &cur);         // flagged: the reference's score
                 bufs_[off_] = b;
                 ++st_.hypotheses;
-                if (best_.sum < cur.sum && valid_model(model)) {
+                if (valid_model(model) &&
+                    score_less(best_, [&] { return best_model_; }, cur, [&] { return dec_model(bufs_[off_]); })) {
                     resolve(bufs_[off_]);               // the glibc phi of a generated 2-SIFT model
                     best_model_ = bufs_[off_].model;
                     best_val_ = model;
@@ -1584,7 +1607,7 @@ public:
         if (!chunk_lists_[c.set]) sc.lfl = nullptr;      // list flags exist with the chunk's list bits only
         return launch_block_summary(P_->solver, set_inc(c.set).p, set_models(c.set).p, sc,
                                     kP > 1 ? set_hmap(c.set).p : nullptr, n, (uint32_t)kP, m32, Tm_, bar, from_pos,
-                                    target, w->sum_scr[c.set].p, out, s, parts_ready);
+                                    target, w->sum_scr[c.set].p, out, s, parts_ready, chain_tol_);
     }
 
     // generate + score + summarise this rank's block of chunk c on stream s
@@ -1638,7 +1661,13 @@ public:
                     lb.bits = static_cast<uint64_t*>(dptr);
                 }
                 chunk_lists_[set] = cl;
-                HIPC(launch_score_small(P_->dp, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np,
+                DevProblem dpc = P_->dp;                  // this set's own split-scorer scratch
+                if (dpc.lo.vals) {
+                    w->cs_vals[set].ensure(pairs * kSplitModels);
+                    w->cs_meta[set].ensure(pairs / 64 * kSplitModels);
+                    dpc.lo = SmallScratch{w->cs_vals[set].p, w->cs_meta[set].p, kSplitModels};
+                }
+                HIPC(launch_score_small(dpc, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np,
                                         set_sb(set).dev(), s, cl ? &lb : nullptr));
             } else {
                 chunk_lists_[set] = false;
@@ -1897,7 +1926,8 @@ public:
                     Buffer b = gen_buf(model, gslot, h.inc, rn, h.fl);
                     if (!b.exact) resolve(b, &cur);     // flagged: the reference's score
                     bufs_[off_] = b;
-                    if (best_.sum < cur.sum && valid_model(model)) {
+                    if (valid_model(model) &&
+                        score_less(best_, [&] { return best_model_; }, cur, [&] { return dec_model(bufs_[off_]); })) {
                         resolve(bufs_[off_]);           // the glibc phi of a generated 2-SIFT model
                         best_model_ = bufs_[off_].model;
                         best_val_ = model;
@@ -2051,7 +2081,7 @@ public:
                 const bool rl = score_models(&refit, 1, &s, rn, &msac) && !sm_lbad_[0];
                 const int idx = 1 - off_;
                 bufs_[idx] = Buffer{true, refit, {rn[0], rn[1]}};
-                if (best_.sum < s.sum) {
+                if (score_less(best_, [&] { return best_model_; }, s, [&] { return refit; })) {
                     best_model_ = refit;
                     best_val_ = refit;
                     off_ = idx;
@@ -2075,11 +2105,25 @@ public:
         st_.exact_pairs = ec_.pairs;
         st_.exact_flips = ec_.flips;
         st_.ms_exact = ec_.ms;
+        st_.near_ties = ec_.near_ties;
+        st_.near_tie_flips = ec_.near_flips;
         st_.ms_total = ms_since(t_all);
         return total;
     }
 
     gcr_stats stats() const { return st_; }
+
+    // gcr_debug_score_less: a and b scored by the small scorer, compared as
+    // the run loop compares (bit 0 the decision, 1 a near tie, 2 value order)
+    int debug_less(const Model& a, const Model& b) {
+        const Model ms[2] = {a, b};
+        HScore sc[2];
+        uint32_t raw[4];
+        score_models(ms, 2, sc, raw);
+        const uint64_t nt0 = ec_.near_ties;
+        const bool d = score_less(sc[0], [&] { return a; }, sc[1], [&] { return b; });
+        return (d ? 1 : 0) | (ec_.near_ties > nt0 ? 2 : 0) | (sc[0].sum < sc[1].sum ? 4 : 0);
+    }
 
     // One hot-path batch (bench): generate + score + first strict maximum.
     // `nb` back-to-back batches of `nslots` slots starting at slot0, each
@@ -2305,6 +2349,67 @@ private:
             throw std::logic_error("exact_score: rectification solvers only");
         }
     }
+    // ---- score comparisons in the reference's arithmetic (exact.h ScoreBound)
+    // The reference compares glibc scores (score.hpp:28-36 at GCRANSAC.h:440,
+    // :662, :1036, :1054); the engine holds value scores within a proven
+    // bound of them.  Two value scores further apart than their two bounds
+    // compare the same; a closer pair is compared by its glibc scores, recounted
+    // on the host (exact_accumulate, glibc sums).  The device chains keep every
+    // hypothesis within chain_tol_ of the running maximum as a member, so the
+    // replay sees every possible near tie.
+    ScoreBound sbnd_{{0.0, 0.0}, {0.0, 0.0}, 0.0, false};
+    double chain_tol_ = 0.0;              // 4 x the bound at full counts (constructor)
+    struct GCache {
+        Model m;
+        double g;
+    };
+    std::vector<GCache> gcache_;
+    double dev_of(const HScore& s) const { return score_dev(sbnd_, (double)s.n[0], (double)s.n[1], s.sum); }
+    // the glibc score of decision model md (s: its value score; zero scores
+    // -- a class below its minimal sample -- are zero in both arithmetics)
+    double glibc_score(const HScore& s, const Model& md) {
+        if constexpr (kRect) {
+            if (s.total == 0 && s.sum == 0.0) return 0.0;
+            for (const GCache& e : gcache_)
+                if (std::memcmp(&e.m, &md, sizeof(Model)) == 0) return e.g;
+            uint32_t n[2];
+            double v[2], tot;
+            exact_accumulate(P_, md, md, Tm_, n, v, tot, nullptr, ec_, true);
+            const double g = finish(n, v[0], v[1], tot).sum;
+            if (gcache_.size() >= 16) gcache_.erase(gcache_.begin());
+            gcache_.push_back(GCache{md, g});
+            return g;
+        } else {
+            (void)md;
+            return s.sum;
+        }
+    }
+    // the reference's `a < b` on the scores of decision models dec_a(),
+    // dec_b() (evaluated only for a near tie)
+    template <class FA, class FB>
+    bool score_less(const HScore& a, FA&& dec_a, const HScore& b, FB&& dec_b) {
+        const bool vl = a.sum < b.sum;
+        if constexpr (!kRect) {
+            return vl;
+        } else {
+            if (!exact_ || !sbnd_.finite) return vl;
+            const double tol = dev_of(a) + dev_of(b);
+            if (!(tol > 0.0) || !(std::fabs(b.sum - a.sum) <= tol)) return vl;
+            ++ec_.near_ties;
+            const Model ma = dec_a(), mb = dec_b();
+            bool gl;
+            if (std::memcmp(&ma, &mb, sizeof(Model)) == 0) gl = false;     // one model: equal glibc scores
+            else gl = glibc_score(a, ma) < glibc_score(b, mb);
+            if (gl != vl) ++ec_.near_flips;
+            return gl;
+        }
+    }
+    // the decision model of the hypothesis in an inlier buffer
+    Model dec_model(Buffer b) {
+        resolve(b);
+        return b.model;
+    }
+
     // buffer b with its decisions resolved: a generated model's glibc phi,
     // the reference's counts (*sc: the finished score when recounted)
     void resolve(Buffer& b, HScore* sc = nullptr) {
@@ -2626,8 +2731,9 @@ private:
         for (uint64_t j = 0; j < cnt; ++j) {
             // a flagged slot may be a new best whatever its twin score (exact.h)
             const bool fl = kRect && exact_ && P_->w->sb.hfl.p[j] != 0;
-            if ((run < chunk_sc_[j].sum || fl) && chunk_ok_[j]) {
-                if (!fl) run = chunk_sc_[j].sum;
+            // (or a near tie of the running maximum: compared in glibc)
+            if ((run - chain_tol_ < chunk_sc_[j].sum || fl) && chunk_ok_[j]) {
+                if (!fl && run < chunk_sc_[j].sum) run = chunk_sc_[j].sum;
                 trig = (int64_t)j;
             }
         }
@@ -2987,7 +3093,8 @@ private:
                 st_.ms_lo_score += ms_since(tp);
                 size_t win = 0;
                 for (size_t q = 0; q < trial_models.size(); ++q) {
-                    if (max_score.sum < trial_scores[q].sum) {
+                    if (score_less(max_score, [&] { return lo_model; }, trial_scores[q],
+                                   [&] { return trial_models[q]; })) {
                         updated = true;
                         win = q;
                         max_score = trial_scores[q];
@@ -3009,7 +3116,7 @@ private:
             if (!updated) break;
         }
         st_.ms_lo += ms_since(t0);
-        if (best_.sum < max_score.sum) {
+        if (score_less(best_, [&] { return best_model_; }, max_score, [&] { return lo_model; })) {
             best_ = max_score;
             best_model_ = lo_model;
             best_val_ = lo_model;
@@ -3178,6 +3285,11 @@ void gcr_problem_destroy(gcr_problem* prob) {
         std::lock_guard<std::mutex> lk(prob->ctx->ws_mu);
         if (prob->ctx->ws_free.size() < 4) prob->ctx->ws_free.push_back(std::move(prob->own));
     }
+    // a workspace that is about to be freed may still have a speculative
+    // chunk in flight (a recycled one is awaited by its next user)
+    if (prob->own) {
+        try { await_spec(prob->own.get()); } catch (...) {}
+    }
     delete prob;
 }
 
@@ -3251,6 +3363,10 @@ int gcr_comm_create(gcr_ctx* ctx, int rank, int world, const uint8_t id[GCR_COMM
 void gcr_comm_destroy(gcr_comm* comm) {
     if (!comm) return;
     (void)hipSetDevice(comm->ctx->device);
+    // a run can return with a speculative chunk's ncclAllGather still queued
+    // on the side stream (gcr_problem_run_comm also drains it; this covers a
+    // caller that destroys the communicator first)
+    (void)hipStreamSynchronize(comm->ctx->side);
     if (comm->comm) (void)ncclCommDestroy(comm->comm);
     delete comm;
 }
@@ -3266,6 +3382,10 @@ int gcr_problem_run_comm(gcr_problem* prob, const gcr_params* params, gcr_comm* 
         auto go = [&](auto&& r) {
             r.set_comm(comm);
             const int total = r.run(mask0_out, mask1_out, H_out, model_out);
+            // no collective of this run may outlive it: a speculative chunk
+            // and its all-gather are drained before the caller can tear the
+            // communicator down (every rank issued the same sequence)
+            await_spec(prob->w);
             fill_stats(stats_out, r.stats());
             return total;
         };
@@ -3575,6 +3695,23 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
                 }
         }
         return GCR_OK;
+    });
+}
+
+int gcr_debug_score_less(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* a,
+                         const gcr_rect_model* b) {
+    if (!prob || !a || !b) return set_err(GCR_EINVAL, "null argument");
+    if (prob->solver > 2) return set_err(GCR_EINVAL, "gcr_debug_score_less: rectification solvers only");
+    if (int e = check_params(params, prob->solver)) return e;
+    return guard([&]() -> int {
+        HIPC(hipSetDevice(prob->ctx->device));
+        await_spec(prob->w);
+        Runner r(prob, *params);
+        RectModel ma, mb;
+        static_assert(sizeof(RectModel) == sizeof(gcr_rect_model), "model layout");
+        std::memcpy(&ma, a, sizeof(ma));
+        std::memcpy(&mb, b, sizeof(mb));
+        return r.debug_less(ma, mb);
     });
 }
 

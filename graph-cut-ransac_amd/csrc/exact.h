@@ -105,6 +105,55 @@ inline FlagBand flag_band(const double T[2]) {
     return b;
 }
 
+// Score comparisons in the reference's arithmetic.
+// With the decisions glibc's, a hypothesis's MSAC score in the value
+// definition (what the kernels fold) and in glibc's (what the reference
+// compares, GCRANSAC.h:440, :662, :1036, :1054) differ only through the
+// inliers' r^2 values and the two sums' roundings.  For counts n_c,
+//   |Δv_c|   <= n_c d_c + 2 n_c^2 u T_c            (d_c: |r^2_value - r^2_glibc|
+//   |Δtot|   <= sum_c n_c d_c + 2 n^2 u max T_c      of one inlier, r <= sqrt(T_c) + D_c;
+//                                                   each sequential sum of n terms
+//                                                   of size <= T_c rounds by <= (n-1) u n T_c)
+//   |Δscore| <= |Δtot| + sum_c (1 + 1/T_c) |Δv_c| + 16 u (|tot| + |v| + |v'| + |score|)
+// (the finish's few operations round on both sides), doubled for margin.
+// Two scores further apart than the sum of their bounds compare the same in
+// both arithmetics; closer ones are compared in glibc on the host.
+struct ScoreBound {
+    double a[2];     // per inlier of class c
+    double b[2];     // per (inlier of class c)^2
+    double g;        // per (inlier of both classes)^2
+    bool finite;
+};
+inline ScoreBound score_bound(const double T[2], int K) {
+    const double u = 0x1p-53;
+    ScoreBound sb{{0.0, 0.0}, {0.0, 0.0}, 0.0, true};
+    double tmax = 0.0;
+    for (int c = 0; c < K; ++c) {
+        const double Tc = T[c];
+        if (!(Tc > 0.0) || !(Tc < HUGE_VAL)) {
+            sb.finite = false;
+            continue;
+        }
+        const double R0 = sqrt(Tc) * (1.0 + 1e-9) + 1e-12;
+        const double D = c == 0 ? 4.0 * (1.0e-15 + 5.2e-16 * R0) : kDevOrient;
+        const double d = D * (2.0 * (R0 + D) + D);
+        const double inv = 1.0 + 1.0 / Tc;
+        sb.a[c] = 2.0 * (d * inv + d + 16.0 * u * (2.0 * Tc + 2.0));
+        sb.b[c] = 2.0 * (2.0 * u * Tc * inv);
+        if (Tc > tmax) tmax = Tc;
+    }
+    sb.g = 2.0 * 2.0 * u * tmax;
+    return sb;
+}
+// the bound of one hypothesis (+inf when a threshold is not positive finite
+// and the class has inliers)
+GCR_HD double score_dev(const ScoreBound& sb, double n0, double n1, double score) {
+    if (!sb.finite && (n0 > 0.0 || n1 > 0.0)) return __builtin_huge_val();
+    const double n = n0 + n1;
+    return ((n0 * (sb.a[0] + n0 * sb.b[0]) + n1 * (sb.a[1] + n1 * sb.b[1])) + n * n * sb.g) +
+           32.0 * 0x1p-53 * __builtin_fabs(score);
+}
+
 // A rectification model whose scale residuals the bound above does not cover:
 // sqrt(T) >= 60 (arguments of log near the ends of the normal range),
 // alpha^3 outside [2^-200, 2^200], a problem with a positive finite scale

@@ -331,12 +331,14 @@ hipError_t launch_warp(const void* src, int sh, int sw, int ch, int dtype, const
 // the block's last live hypothesis; otherwise locate the first slot whose
 // iterations-before reach `target` (block-relative) -- parts_ready: the
 // per-part totals of an earlier summary of the same block are reused.
+// tol: hypotheses within tol of the running maximum are members too (near
+// ties of the score comparison, exact.h ScoreBound).
 // scratch: summary_scratch_bytes(nslots * per, per) bytes of device memory.
 size_t summary_scratch_bytes(uint32_t npos, uint32_t per);
 hipError_t launch_block_summary(int solver, const uint8_t* inc, const void* models, const ScoreOut& sc,
                                 const uint32_t* hmap, uint32_t nslots, uint32_t per, const uint32_t m[2],
                                 const double Tm[2], double bar, uint32_t from_pos, uint64_t target, void* scratch,
-                                BlockSummary* out, hipStream_t stream, bool parts_ready = false);
+                                BlockSummary* out, hipStream_t stream, bool parts_ready = false, double tol = 0.0);
 
 // streaming copy of `bytes` (a multiple of 16) for the HBM peak probe
 hipError_t launch_hbm_copy(const void* src, void* dst, size_t bytes, int nontemporal, hipStream_t stream);

@@ -129,6 +129,9 @@ struct SumArgs {
     uint32_t m0, m1;
     double Tm0, Tm1;
     double bar;                         // chain members must beat it
+    double tol;                         // ... or come within tol of the running maximum
+                                        // (a near tie, compared in glibc by the host:
+                                        // exact.h ScoreBound; 0 for the correspondences)
     uint32_t from_pos;                  // positions below are not eligible (continuation)
     uint64_t target;                    // locate: iteration target (block-relative); ~0 = none
     uint32_t cap;                       // members kept per part and per summary (<= kCandCap)
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
         const double im = wave_incl_max(val, lane);
         const double before = prev_lane_f64(run, im);
         const double bar = lane == 0 ? run : (run < before ? before : run);
-        const bool cand = (val >= 0.0 && val > bar) || flagged;
+        const bool cand = (val >= 0.0 && val > bar - a.tol) || flagged;
         const uint64_t bc = __ballot(cand);
         if (cand) {
             const uint32_t r = nc + (uint32_t)__builtin_popcountll(bc & ((1ull << lane) - 1ull));
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(64) void k_sum_chain(SumArgs a) {
                 pc.it_before = coff + cs - c - own;
                 pc.hyps_before = hb;
                 pc.val = flagged ? __builtin_huge_val() : val;
-                pc.rb = flagged ? bar : val;
+                pc.rb = (flagged || !(val > bar)) ? bar : val;      // the running maximum after it
             }
         }
         nflag += (uint32_t)__builtin_popcountll(__ballot(flagged));
@@ -306,8 +309,8 @@ __global__ __launch_bounds__(kSumFinalThreads) void k_sum_final(SumArgs a) {
     // have lost members
     uint32_t g = 0;
     if (mine) {
-        for (uint32_t i = 0; i < sp.ncand; ++i) g += a.pcand[(size_t)t * kPartCap + i].val > mb ? 1u : 0u;
-        if (sp.over && (sp.maxv > mb || sp.nflag > 0)) atomicMin(&s_fail, (uint32_t)t);
+        for (uint32_t i = 0; i < sp.ncand; ++i) g += a.pcand[(size_t)t * kPartCap + i].val > mb - a.tol ? 1u : 0u;
+        if (sp.over && (sp.maxv > mb - a.tol || sp.nflag > 0)) atomicMin(&s_fail, (uint32_t)t);
         if (sp.live > 0) atomicMax(&s_lastpart, t);
     }
     if (locate && mine && (uint64_t)coff < a.target && (uint64_t)coff + sp.contrib >= a.target)
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(kSumFinalThreads) void k_sum_final(SumArgs a) {
             uint32_t r = gbase;
             for (uint32_t i = 0; i < sp.ncand && r < a.cap; ++i) {
                 const PartCand& pc = a.pcand[(size_t)t * kPartCap + i];
-                if (!(pc.val > mb)) continue;
+                if (!(pc.val > mb - a.tol)) continue;
                 fill_hyp<M>(a, pc.pos, pc.it_before, pc.hyps_before, out->cand[r]);
                 if (r + 1 == min(total, a.cap)) {                        // the last member emitted
                     out->resume_pos = pc.pos + 1;
@@ -515,7 +518,7 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
             const double im = wave_incl_max(val, lane);
             const double before = prev_lane_f64(run, im);
             const double bar = lane == 0 ? run : (run < before ? before : run);
-            const bool cand = (val >= 0.0 && val > bar) || flagged;
+            const bool cand = (val >= 0.0 && val > bar - a.tol) || flagged;
             const uint64_t bc = __ballot(cand);
             if (cand) {
                 const uint32_t r = nc + (uint32_t)__builtin_popcountll(bc & ((1ull << lane) - 1ull));
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(64) void k_sum_one(SumArgs a) {
                     fill_hyp<M>(a, p, excl - own, hb, out->cand[r]);
                     if (r + 1 == a.cap) {                      // the last member a full summary holds
                         out->resume_pos = p + 1;
-                        out->resume_bar = flagged ? bar : val;
+                        out->resume_bar = (flagged || !(val > bar)) ? bar : val;
                     }
                 }
             }
@@ -585,7 +588,7 @@ size_t summary_scratch_bytes(uint32_t npos, uint32_t per) {
 hipError_t launch_block_summary(int solver, const uint8_t* inc, const void* models, const ScoreOut& sc,
                                 const uint32_t* hmap, uint32_t nslots, uint32_t per, const uint32_t m[2],
                                 const double Tm[2], double bar, uint32_t from_pos, uint64_t target, void* scratch,
-                                BlockSummary* out, hipStream_t stream, bool parts_ready) {
+                                BlockSummary* out, hipStream_t stream, bool parts_ready, double tol) {
     SumArgs a{};
     a.inc = inc;
     a.models = models;
@@ -601,6 +604,7 @@ hipError_t launch_block_summary(int solver, const uint8_t* inc, const void* mode
     a.Tm0 = Tm[0];
     a.Tm1 = Tm[1];
     a.bar = bar;
+    a.tol = tol >= 0.0 ? tol : 0.0;
     a.from_pos = from_pos;
     a.target = target;
     // GCR_SUMMARY_CAP=n (1 .. kCandCap): fewer members per summary, so that

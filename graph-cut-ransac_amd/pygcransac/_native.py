@@ -72,6 +72,8 @@ class Stats(C.Structure):
         ("exact_pairs", C.c_uint64),
         ("exact_flips", C.c_uint64),
         ("ms_exact", C.c_double),
+        ("near_ties", C.c_uint64),
+        ("near_tie_flips", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -151,6 +153,7 @@ def _load():
                                              C.POINTER(BatchResult), C.POINTER(Stats)]
     L.gcr_debug_generate.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, u8p, C.POINTER(RectModel)]
     L.gcr_debug_score.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_uint32, u32p, u32p, dp, dp, dp]
+    L.gcr_debug_score_less.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.POINTER(RectModel)]
     L.gcr_debug_mask.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_int, C.c_int, u8p]
     L.gcr_host_log.argtypes = [C.c_double]
     L.gcr_host_log.restype = C.c_double

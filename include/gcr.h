@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GCR_ABI_VERSION 3
+#define GCR_ABI_VERSION 4
 
 /* error codes */
 #define GCR_OK 0
@@ -114,6 +114,10 @@ typedef struct gcr_stats {
     uint64_t exact_pairs;         /* (feature, model) decisions taken with glibc    */
     uint64_t exact_flips;         /* ... that differ from the detmath decision      */
     double ms_exact;              /* host time of those recounts                    */
+    /* score comparisons in glibc (exact.h ScoreBound): two value scores closer
+     * than their proven bounds are compared by their glibc scores */
+    uint64_t near_ties;           /* comparisons decided in glibc                   */
+    uint64_t near_tie_flips;      /* ... whose outcome differs from the values'     */
 } gcr_stats;
 
 /* ---- context ---------------------------------------------------------- */
@@ -218,7 +222,15 @@ int gcr_problem_run_comm(gcr_problem* prob, const gcr_params* params, gcr_comm* 
 /* One pass of the hot path over one batch: draw and solve `nslots`
  * outer-iteration slots starting at `slot0`, MSAC-score every resulting model
  * against all features on the GPU, and return the best-scoring slot (first
- * strict maximum, the reference's update rule).  Timings go to stats_out. */
+ * strict maximum of the reference's update rule, `best < score &&
+ * isValidModel`, GCRANSAC.h:440-446).  This is the throughput API of the hot
+ * path: the rectification solvers' scores, inlier decisions and the 2-SIFT
+ * best_model's phi are the kernels' own (the detmath twins, csrc/exact.h),
+ * with no host recheck of flagged decisions or near-tie comparisons, so a
+ * batch whose best is decided within the twin-glibc bounds can differ from
+ * the reference's choice.  gcr_problem_run (and the pygcransac entry points)
+ * take every decision, comparison and model in the reference's arithmetic.
+ * Timings go to stats_out. */
 typedef struct gcr_batch_result {
     uint64_t models;        /* hypotheses scored                        */
     uint64_t iterations;    /* sum of iteration increments of the batch */
@@ -243,6 +255,14 @@ int gcr_debug_generate(gcr_problem* prob, uint64_t seed, uint64_t slot0, uint32_
 /* raw MSAC accumulators for explicit models: counts, per-class sums, total */
 int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* models, uint32_t nmodels,
                     uint32_t* n0, uint32_t* n1, double* v0, double* v1, double* tot);
+/* The run loop's score comparison `score(a) < score(b)` (GCRANSAC.h:440) as
+ * gcr_problem_run takes it: both models scored by the GPU small scorer (value
+ * scores), compared directly when they are further apart than their proven
+ * value-glibc bounds (csrc/exact.h ScoreBound), else by their glibc scores
+ * recounted on the host.  Returns bit 0 the decision, bit 1 a near tie, bit 2
+ * the value scores' own order; < 0 an error. */
+int gcr_debug_score_less(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* a,
+                         const gcr_rect_model* b);
 /* inlier mask of one model: rule 0 = MSAC (2.25 thr^2), 1 = LO threshold
  * ((1.5 thr)^2), 2 = 1-class graph-cut labeling */
 int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* model, int cls, int rule,

@@ -1851,7 +1851,57 @@ struct Settings {
 struct Statistics {
     size_t iteration_number = 0, local_optimization_number = 0, graph_cut_number = 0, slots = 0, hypotheses = 0;
     double score = 0.0, seconds = 0.0;
+    size_t near_ties = 0, near_tie_flips = 0;
 };
+
+// TWIN mode's score comparisons (the product's rule, csrc/exact.h ScoreBound,
+// restated with the same operations): the reference compares glibc scores
+// (score.hpp:28-36 at GCRANSAC.h:440, :662, :1036, :1054); TWIN holds value
+// scores, within a proven bound of the glibc ones.  Value scores further
+// apart than the sum of the two bounds compare as their glibc scores do;
+// closer ones are compared by their glibc scores.  So TWIN takes every
+// decision GLIBC takes.
+struct ScoreBoundR {
+    double a[2], b[2], g;
+    bool finite;
+};
+static ScoreBoundR score_bound_r(const double* T, size_t K) {
+    const double u = 0x1p-53;
+    ScoreBoundR sb{{0.0, 0.0}, {0.0, 0.0}, 0.0, true};
+    double tmax = 0.0;
+    for (size_t c = 0; c < K; ++c) {
+        const double Tc = T[c];
+        if (!(Tc > 0.0) || !(Tc < HUGE_VAL)) {
+            sb.finite = false;
+            continue;
+        }
+        const double R0 = std::sqrt(Tc) * (1.0 + 1e-9) + 1e-12;
+        const double D = c == 0 ? 4.0 * (1.0e-15 + 5.2e-16 * R0) : 4e-14;   // exact.h kDevOrient
+        const double d = D * (2.0 * (R0 + D) + D);
+        const double inv = 1.0 + 1.0 / Tc;
+        sb.a[c] = 2.0 * (d * inv + d + 16.0 * u * (2.0 * Tc + 2.0));
+        sb.b[c] = 2.0 * (2.0 * u * Tc * inv);
+        if (Tc > tmax) tmax = Tc;
+    }
+    sb.g = 2.0 * 2.0 * u * tmax;
+    return sb;
+}
+static double score_dev_r(const ScoreBoundR& sb, double n0, double n1, double score) {
+    if (!sb.finite && (n0 > 0.0 || n1 > 0.0)) return HUGE_VAL;
+    const double n = n0 + n1;
+    return ((n0 * (sb.a[0] + n0 * sb.b[0]) + n1 * (sb.a[1] + n1 * sb.b[1])) + n * n * sb.g) +
+           32.0 * 0x1p-53 * std::fabs(score);
+}
+template <class M>
+static bool same_model7(const M& a, const M& b) {
+    if constexpr (std::is_same<M, Model>::value) {
+        const double x[7] = {a.x0, a.y0, a.s, a.h7, a.h8, a.alpha, a.phi};
+        const double y[7] = {b.x0, b.y0, b.s, b.h7, b.h8, b.alpha, b.phi};
+        return std::memcmp(x, y, sizeof(x)) == 0;
+    } else {
+        return std::memcmp(&a, &b, sizeof(M)) == 0;
+    }
+}
 
 template <class S>
 class GCRANSAC {
@@ -1918,7 +1968,7 @@ public:
             for (auto& model : models) {
                 cur = getScore(solver, data, model, settings.threshold, tmp[off]);
                 ++stats.hypotheses;
-                if (best < cur && solver.isValidModel(model)) {
+                if (solver.isValidModel(model) && score_less(data, solver, best, best_model, cur, model)) {
                     off = 1 - off;
                     best_model = model;
                     best = cur;
@@ -1962,12 +2012,51 @@ public:
             const size_t idx = 1 - off;
             for (auto& s : tmp[idx]) s.clear();
             cur = getScore(solver, data, model, settings.threshold, tmp[idx]);
-            if (best < cur) { best_model = model; off = idx; }
+            if (score_less(data, solver, best, best_model, cur, model)) { best_model = model; off = idx; }
         }
         final_inliers.swap(tmp[off]);
         stats.score = best.value();
         out_model = best_model;
         stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+
+    // `a < b` on the glibc scores of models ma, mb (GLIBC mode: the scores
+    // themselves; TWIN: the rule above)
+    bool score_less(const Data<K>& data, const S& solver, const Score<K>& a, const Model& ma, const Score<K>& b,
+                    const Model& mb) {
+        const bool vl = a < b;
+        if constexpr (!std::is_same<Model, oracle::Model>::value) {
+            return vl;
+        } else {
+            if (g_math != MATH_TWIN) return vl;
+            double T[K];
+            for (size_t c = 0; c < K; ++c) T[c] = (2.25 * settings.threshold[c]) * settings.threshold[c];
+            const ScoreBoundR sb = score_bound_r(T, K);
+            if (!sb.finite) return vl;
+            auto dev = [&](const Score<K>& s) {
+                return score_dev_r(sb, (double)s.n[0], K > 1 ? (double)s.n[K - 1] : 0.0, s.sum);
+            };
+            const double tol = dev(a) + dev(b);
+            if (!(tol > 0.0) || !(std::fabs(b.sum - a.sum) <= tol)) return vl;
+            ++stats.near_ties;
+            bool gl;
+            if (same_model7(ma, mb)) {
+                gl = false;
+            } else {
+                auto glibc = [&](const Score<K>& s, const Model& m) {
+                    if (s.total == 0 && s.sum == 0.0) return 0.0;
+                    const int saved = g_math;
+                    set_mode(MATH_GLIBC);
+                    Inliers<K> tmp{};
+                    const double g = getScore(solver, data, m, settings.threshold, tmp).value();
+                    set_mode(saved);
+                    return g;
+                };
+                gl = glibc(a, ma) < glibc(b, mb);
+            }
+            if (gl != vl) ++stats.near_tie_flips;
+            return gl;
+        }
     }
 
 private:
@@ -2093,7 +2182,7 @@ private:
                 for (auto& model : models) {
                     for (auto& s : tmp_inl) s.clear();
                     Score<K> sc = getScore(solver, data, model, settings.threshold, tmp_inl);
-                    if (max_score < sc) {
+                    if (score_less(data, solver, max_score, best_model, sc, model)) {
                         updated = true;
                         max_score = sc;
                         best_model = model;
@@ -2103,7 +2192,7 @@ private:
             }
             if (!updated) break;
         }
-        if (sfb_score < max_score) {
+        if (score_less(data, solver, sfb_score, sfb_model, max_score, best_model)) {
             sfb_score = max_score;
             sfb_model = best_model;
             sfb_inliers.swap(best_inliers);
@@ -2132,6 +2221,7 @@ struct oracle_params {
 struct oracle_stats {
     uint64_t iteration_number, local_optimization_number, graph_cut_number, slots, hypotheses;
     double score, seconds;
+    uint64_t near_ties, near_tie_flips;
 };
 
 static Features make_features(const double* p, size_t n, size_t cols = 3) {
@@ -2191,6 +2281,8 @@ static int run_generic(const Data<Solver<KIND>::K>& data, const oracle_params* p
         st->hypotheses = g.stats.hypotheses;
         st->score = g.stats.score;
         st->seconds = g.stats.seconds;
+        st->near_ties = g.stats.near_ties;
+        st->near_tie_flips = g.stats.near_tie_flips;
     }
     return (int)total;
 }
@@ -2249,6 +2341,8 @@ int oracle_find_homography(const double* corr, size_t n, const oracle_params* p,
         st->hypotheses = g.stats.hypotheses;
         st->score = g.stats.score;
         st->seconds = g.stats.seconds;
+        st->near_ties = g.stats.near_ties;
+        st->near_tie_flips = g.stats.near_tie_flips;
     }
     return (int)g.final_inliers[0].size();
 }
@@ -2290,6 +2384,8 @@ int oracle_find_fundamental(const double* corr, size_t n, const oracle_params* p
         st->hypotheses = g.stats.hypotheses;
         st->score = g.stats.score;
         st->seconds = g.stats.seconds;
+        st->near_ties = g.stats.near_ties;
+        st->near_tie_flips = g.stats.near_tie_flips;
     }
     return (int)g.final_inliers[0].size();
 }
@@ -2454,6 +2550,32 @@ int oracle_score(int kind, const double* f0, size_t n0, const double* f1, size_t
 }
 
 // per-feature squared residuals of one model
+// The score comparison `score(a) < score(b)` of the run loop (GCRANSAC.h:440)
+// in math_mode: GLIBC compares the glibc scores, TWIN the value scores with
+// the near-tie rule (score_less).  Returns bit 0 the decision, bit 1 a near
+// tie (TWIN compared glibc scores), bit 2 the value scores' own order.
+int oracle_score_less(int kind, const double* f0, size_t n0, const double* f1, size_t n1, const double* ma7,
+                      const double* mb7, double thr0, double thr1, int math_mode) {
+    set_mode(math_mode);
+    Features a = make_features(f0, n0), b = f1 ? make_features(f1, n1) : Features{};
+    const Model ma = read_model(ma7), mb = read_model(mb7);
+    auto go = [&](auto solver, auto data) {
+        using S = decltype(solver);
+        constexpr size_t K = S::K;
+        GCRANSAC<S> g;
+        g.settings.threshold[0] = thr0;
+        g.settings.threshold[1] = thr1;
+        Inliers<K> in{};
+        const auto sa = getScore(solver, data, ma, g.settings.threshold, in);
+        const auto sb = getScore(solver, data, mb, g.settings.threshold, in);
+        const bool d = g.score_less(data, solver, sa, ma, sb, mb);
+        return (d ? 1 : 0) | (g.stats.near_ties ? 2 : 0) | (sa.sum < sb.sum ? 4 : 0);
+    };
+    if (kind == 0) return go(Solver<0>{}, Data<1>{&a});
+    if (kind == 1) return go(Solver<1>{}, Data<1>{&a});
+    return go(Solver<2>{}, Data<2>{&a, &b});
+}
+
 int oracle_residuals(int kind, int cls, const double* f, size_t n, const double* model7, int math_mode, double* r2) {
     set_mode(math_mode);
     if (math_mode == MATH_TWIN) g_fn = 2;          // the values the product's kernels compute

@@ -35,6 +35,7 @@ class OracleStats(C.Structure):
         ("iteration_number", C.c_uint64), ("local_optimization_number", C.c_uint64),
         ("graph_cut_number", C.c_uint64), ("slots", C.c_uint64), ("hypotheses", C.c_uint64),
         ("score", C.c_double), ("seconds", C.c_double),
+        ("near_ties", C.c_uint64), ("near_tie_flips", C.c_uint64),
     ]
 
 
@@ -393,3 +394,18 @@ def grid_edges(points, cell_size, cell_number):
     out = np.zeros((max(m, 1), 2), dtype=np.uint32)
     lib().oracle_grid_edges(_dp(pts), n, d, _dp(cs), int(cell_number), out.ctypes.data_as(C.POINTER(C.c_uint32)), m)
     return out[:m]
+
+
+def score_less(kind, f0, f1, ma, mb, thr0, thr1=0.0, math_mode=MATH_TWIN):
+    """The run loop's `score(ma) < score(mb)` (GCRANSAC.h:440) in math_mode:
+    (decision, near_tie, value_order) -- GLIBC compares glibc scores, TWIN the
+    value scores with the near-tie rule (csrc/exact.h ScoreBound)."""
+    f0 = _f64(f0)
+    f1 = _f64(f1) if f1 is not None else None
+    L = lib()
+    dp = C.POINTER(C.c_double)
+    L.oracle_score_less.restype = C.c_int
+    L.oracle_score_less.argtypes = [C.c_int, dp, C.c_size_t, dp, C.c_size_t, dp, dp, C.c_double, C.c_double, C.c_int]
+    r = L.oracle_score_less(kind, _dp(f0), f0.shape[0], _dp(f1) if f1 is not None else None,
+                            0 if f1 is None else f1.shape[0], _dp(_f64(ma)), _dp(_f64(mb)), thr0, thr1, math_mode)
+    return bool(r & 1), bool(r & 2), bool(r & 4)

@@ -93,3 +93,52 @@ def test_slot_replay_after_speculative_chunks_on_recycled_workspace(monkeypatch)
     for _ in range(3):
         assert _run(kind, "adaptive", monkeypatch, {}) == ref
         assert _run(kind, "adaptive", monkeypatch, {"GCR_REPLAY": "slots"}) == ref
+
+
+def _run_m(kind, seed, outliers, monkeypatch, env):
+    """An adaptive 0.99 run of a larger M1 / M2 problem with LO on (50
+    trials), so several small-scored chunks run on the side stream while the
+    replay stream scores LO trials and refits."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if kind == N.SOLVER_SIFT22:
+        f0, f1, _, _, thr0, thr1 = S.problem_m2(3000, 3000, outliers, seed=seed)
+    else:
+        f0, _, thr0 = S.problem_m1(6000, outliers, seed=seed)
+        f1, thr1 = None, 0.0
+    prob = Problem(kind, f0, f1)
+    p = N.default_params()
+    p.scale_residual_thresh, p.orientation_residual_thresh, p.seed = thr0, thr1, seed
+    p.min_iteration_number, p.max_iteration_number, p.confidence = 0, 10**7, 0.99
+    m0 = np.zeros(f0.shape[0], np.uint8)
+    m1 = np.zeros(0 if f1 is None else f1.shape[0], np.uint8)
+    H = np.zeros(9)
+    model = N.RectModel()
+    st = N.Stats()
+    u8 = C.POINTER(C.c_uint8)
+    n = N.check(N.lib.gcr_problem_run(prob.h, C.byref(p), m0.ctypes.data_as(u8),
+                                      m1.ctypes.data_as(u8) if f1 is not None else None,
+                                      H.ctypes.data_as(C.POINTER(C.c_double)), C.byref(model), C.byref(st)))
+    for k in env:
+        monkeypatch.delenv(k)
+    prob.close()
+    return (n, m0.tobytes(), m1.tobytes(), bits(H).tobytes(), st.iteration_number, st.hypotheses,
+            st.local_optimization_number, st.graph_cut_number, bits(st.score).tobytes(), st.slots)
+
+
+@pytest.mark.parametrize("kind,outliers", [(N.SOLVER_SCALE3, 0.8), (N.SOLVER_SIFT22, 0.75)])
+def test_small_chunks_on_side_stream_do_not_race_lo_scoring(kind, outliers, monkeypatch):
+    """small-scored chunks (<= 256 slots, the split
+    scorer) issued speculatively on the side stream must not share the split
+    scorer's scratch with the LO trials / refit scored on the replay stream
+    (engine.cpp Workspace::cs_vals).  Tiny first chunks keep every chunk of
+    the run small-scored; the result must equal the run without any chunk
+    issued ahead, and the per-slot replay."""
+    for seed in (3, 4, 5):
+        ref = _run_m(kind, seed, outliers, monkeypatch, {"GCR_PREFETCH": "0", "GCR_FIRST_CHUNK": "8"})
+        assert ref[0] > 0 and ref[6] > 0
+        for _ in range(2):
+            assert _run_m(kind, seed, outliers, monkeypatch, {"GCR_FIRST_CHUNK": "8"}) == ref
+        assert _run_m(kind, seed, outliers, monkeypatch, {"GCR_FIRST_CHUNK": "8", "GCR_CHUNK_CAP": "0"})[:5] == \
+            ref[:5]
+        assert _run_m(kind, seed, outliers, monkeypatch, {"GCR_REPLAY": "slots"}) == ref
