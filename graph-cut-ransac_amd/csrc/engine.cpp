@@ -45,6 +45,10 @@
 
 #include <rccl/rccl.h>
 
+#include <csignal>
+#include <execinfo.h>
+#include <unistd.h>
+
 #include "gcr.h"
 #include "host_fit.h"
 #include "kernels.h"
@@ -256,6 +260,7 @@ struct Workspace {
     PinBuf<GeoModel> h_logeo;
     DevBuf<double> lo_vals;             // launch_score_small's split scorer (DevProblem::lo)
     DevBuf<uint32_t> lo_meta;
+    DevBuf<uint32_t> lo_arrive;         // ... k_lo_split's per-model arrival counters (zeroed once)
     PinBuf<uint64_t> h_mbits;           // launch_score_small: MSAC inlier ballots (ListBits.mbits)
     PinBuf<uint64_t> h_lbits;           // launch_score_small: LO list bits (ListBits), written by
                                         // the kernel straight into this mapped pinned buffer
@@ -310,6 +315,7 @@ struct Workspace {
     // trials / the refit through DevProblem::lo, so they never share one.
     DevBuf<double> cs_vals[2];
     DevBuf<uint32_t> cs_meta[2];
+    DevBuf<uint32_t> cs_arrive[2];
     hipEvent_t sum_done[2] = {nullptr, nullptr}, sum_k0[2] = {nullptr, nullptr}, sum_k1[2] = {nullptr, nullptr};
     bool spec_pending[2] = {false, false};   // a speculative chunk of this set may still run
     ~Workspace() {
@@ -321,6 +327,42 @@ struct Workspace {
 };
 
 namespace {
+// GCR_EXCHANGE_LOG=1 (read per run): the summary replay logs every event that
+// is a collective under gcr_comm -- a chunk's issue (the all-gather of its
+// block summaries) and a re-summary (chain continuation or stop locate) --
+// and every chunk collected, on the calling thread (gcr_debug_exchange_log).
+// RCCL needs every rank to issue the same collectives in the same order; the
+// tests compare these logs across ranks (callback path) and between the
+// callback and the gcr_comm paths.  Four words per event: kind (1 issue, 2
+// re-summary, 3 collect), chunk number, set | ahead << 1 (issue) or set |
+// locate << 1 (re-summary), slots (issue) or owner + 1 | from_pos << 16.
+thread_local std::vector<uint64_t> t_xlog;
+
+// GCR_BACKTRACE=1 (read at load): SIGABRT / SIGSEGV print the native stack
+// to stderr before the default action (diagnostics on the GPU box, which has
+// no debugger)
+void gcr_crash_handler(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    const char msg[] = "gcr: fatal signal, native backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+[[maybe_unused]] const bool g_crash_hook = [] {
+    const char* e = getenv("GCR_BACKTRACE");
+    if (e && e[0] == '1') {
+        signal(SIGABRT, gcr_crash_handler);
+        signal(SIGSEGV, gcr_crash_handler);
+    }
+    return true;
+}();
+bool xlog_on() {
+    const char* e = getenv("GCR_EXCHANGE_LOG");
+    return e && e[0] == '1';
+}
+
 // A run can end with a speculative chunk of the summary replay still running
 // on the side stream (RunnerT::replay_summaries leaves it in flight so the
 // run returns sooner).  It writes set 0 / 1's chunk buffers and reads the
@@ -1102,7 +1144,11 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     if (spairs > 0 && spairs <= kSplitMaxPairs) {
         P->w->lo_vals.ensure(spairs * kSplitModels);
         P->w->lo_meta.ensure(spairs / 64 * kSplitModels);
-        P->dp.lo = SmallScratch{P->w->lo_vals.p, P->w->lo_meta.p, kSplitModels};
+        if (!P->w->lo_arrive.p) {
+            P->w->lo_arrive.ensure(kSplitModels);
+            HIPC(hipMemsetAsync(P->w->lo_arrive.p, 0, kSplitModels * sizeof(uint32_t), ctx->stream));
+        }
+        P->dp.lo = SmallScratch{P->w->lo_vals.p, P->w->lo_meta.p, kSplitModels, P->w->lo_arrive.p};
     }
     HIPC(hipMemcpyAsync(P->w->feat.p, hst, total * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
@@ -1585,7 +1631,12 @@ public:
         uint64_t it_lo = 0;       // iterations before the chunk (exact, or a lower bound when issued ahead)
         int set = 0;              // buffer set
         double bar = 0.0;         // the best score when issued (members beat it)
+        uint64_t no = 0;          // chunk number of the run
     };
+    bool xlog_ = false;
+    void xlog(uint64_t kind, uint64_t no, uint64_t a, uint64_t b) {
+        if (xlog_) t_xlog.insert(t_xlog.end(), {kind, no, a, b});
+    }
     uint64_t rank_slot0(const Chunk& c, int r) const { return c.s0 + (uint64_t)r * c.per; }
     uint32_t rank_nslots(const Chunk& c, int r) const {
         const uint64_t b = (uint64_t)r * c.per;
@@ -1665,7 +1716,11 @@ public:
                 if (dpc.lo.vals) {
                     w->cs_vals[set].ensure(pairs * kSplitModels);
                     w->cs_meta[set].ensure(pairs / 64 * kSplitModels);
-                    dpc.lo = SmallScratch{w->cs_vals[set].p, w->cs_meta[set].p, kSplitModels};
+                    if (!w->cs_arrive[set].p) {
+                        w->cs_arrive[set].ensure(kSplitModels);
+                        HIPC(hipMemsetAsync(w->cs_arrive[set].p, 0, kSplitModels * sizeof(uint32_t), s));
+                    }
+                    dpc.lo = SmallScratch{w->cs_vals[set].p, w->cs_meta[set].p, kSplitModels, w->cs_arrive[set].p};
                 }
                 HIPC(launch_score_small(dpc, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np,
                                         set_sb(set).dev(), s, cl ? &lb : nullptr));
@@ -1722,6 +1777,7 @@ public:
     // chunk c's summaries of every rank into `all` (waits for this rank's)
     void collect_chunk(const Chunk& c, BlockSummary* all) {
         Workspace* w = P_->w;
+        xlog(3, c.no, (uint64_t)c.set, 0);
         const auto t0 = Clock::now();
         HIPC(hipEventSynchronize(w->sum_done[c.set]));
         st_.ms_score += ms_since(t0);
@@ -1745,6 +1801,7 @@ public:
     void resummarise(const Chunk& c, int owner, uint32_t from_pos, double bar, const uint64_t* target,
                      BlockSummary* all) {
         Workspace* w = P_->w;
+        xlog(2, c.no, (uint64_t)c.set | (target ? 2u : 0u), (uint64_t)(owner + 1) | ((uint64_t)from_pos << 16));
         if (comm_) {
             // the summary (or an empty record) on the replay stream, the
             // exchange on the side stream behind it: every collective of the
@@ -1803,6 +1860,8 @@ public:
         // speculative chunks a previous run left in flight (their pinned
         // summary buffers are rewritten below)
         await_spec(P_->w);
+        xlog_ = xlog_on();
+        if (xlog_) t_xlog.clear();
         const uint64_t ones[2] = {1, 1};
         uint64_t max_iteration = iteration_number(ones);
         const uint64_t min_it = prm_.min_iteration_number, max_it = prm_.max_iteration_number;
@@ -1822,7 +1881,7 @@ public:
         // plan + issue the chunk after the last issued one; `it_lo`: iterations
         // before it (exact, or a lower bound: every slot adds at least one)
         const bool spec_ok = ahead_ok && speculate_on() && min_it < max_it && prm_.batch_slots == 0;
-        auto issue = [&](uint64_t it_lo) -> bool {
+        auto issue = [&](uint64_t it_lo, bool ahead) -> bool {
             if (it_lo >= L) return false;
             Chunk c;
             c.B = (uint32_t)plan_chunk(chunk_no, last_B, it_lo, L, thr(), next_slot);
@@ -1831,6 +1890,8 @@ public:
             c.it_lo = it_lo;
             c.set = next_set;
             c.bar = best_.sum;
+            c.no = chunk_no;
+            xlog(1, c.no, (uint64_t)c.set | (ahead ? 2u : 0u), c.B);
             issue_chunk(c, P_->ctx->side);
             next_set ^= 1;
             next_slot += c.B;
@@ -1840,12 +1901,12 @@ public:
             return true;
         };
         while (min_it > it_ || it_ < std::min(max_iteration, max_it)) {
-            if (q.empty() && !issue(it_)) break;
+            if (q.empty() && !issue(it_, false)) break;
             const Chunk c = q.front();
             // the chunk after it goes ahead (before this one is replayed) when
             // the loop certainly reaches it: the iteration floor min_it alone
             // keeps the loop going, and every slot adds at least one iteration
-            if (ahead_ok && q.size() == 1 && c.it_lo + c.B < min_it && issue(c.it_lo + c.B)) ++st_.prefetched_chunks;
+            if (ahead_ok && q.size() == 1 && c.it_lo + c.B < min_it && issue(c.it_lo + c.B, true)) ++st_.prefetched_chunks;
             collect_chunk(c, S.data());
             const auto t_rep = Clock::now();
             itb[0] = it_;
@@ -1877,7 +1938,7 @@ public:
                             spec_thr = std::min(spec_thr, std::max(min_it, iteration_number(sc.n)));
                     }
             if (ahead_ok && q.size() == 1 && (itb[world_] < min_it || (spec_ok && itb[world_] < spec_thr)) &&
-                issue(itb[world_]))
+                issue(itb[world_], true))
                 ++st_.prefetched_chunks;
             bool stopped = false;
             // LO runs once per slot, after all of the slot's models (the
@@ -3696,6 +3757,12 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
         }
         return GCR_OK;
     });
+}
+
+size_t gcr_debug_exchange_log(uint64_t* out, size_t cap) {
+    const size_t n = t_xlog.size();
+    if (out) std::memcpy(out, t_xlog.data(), std::min(n, cap) * sizeof(uint64_t));
+    return n;
 }
 
 int gcr_debug_score_less(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* a,

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <memory_resource>
 #include <unordered_map>
 
 namespace gcr {
@@ -30,8 +31,12 @@ double weighted_mode(const std::vector<double>& angles, const std::vector<double
     // only on the sequence in which NEW keys were inserted (lookups of
     // existing keys do not touch the table), so the sums are accumulated in
     // flat arrays and only each bin's first occurrence goes into the map.
+    // small calls (the LO trials' 7 m angles) run out of a stack arena: the
+    // same containers and hash table (so the same iteration order), no heap
+    alignas(16) unsigned char arena[12288];
+    std::pmr::monotonic_buffer_resource mr(arena, sizeof(arena));
     const size_t n = angles.size();
-    std::vector<int> bins(n);
+    std::pmr::vector<int> bins(n, &mr);
     int lo = 0, hi = -1;
     for (size_t i = 0; i < n; i++) {
         bins[i] = static_cast<int>(std::round(angles[i] / bin_width));
@@ -52,9 +57,9 @@ double weighted_mode(const std::vector<double>& angles, const std::vector<double
         return vmap[mode_bin] / wmap[mode_bin];
     }
     const size_t span = (size_t)((int64_t)hi - (int64_t)lo + 1);
-    std::vector<double> w(span, 0.0), v(span, 0.0);
-    std::vector<char> seen(span, 0);
-    std::unordered_map<int, double> order;               // the reference's wmap keys, in its insertion order
+    std::pmr::vector<double> w(span, 0.0, &mr), v(span, 0.0, &mr);
+    std::pmr::vector<char> seen(span, 0, &mr);
+    std::pmr::unordered_map<int, double> order(&mr);     // the reference's wmap keys, in its insertion order
     for (size_t i = 0; i < n; i++) {
         const size_t k = (size_t)(bins[i] - lo);
         if (!seen[k]) {
@@ -299,13 +304,26 @@ bool fit_sift22(const HostClass* cls, const std::vector<uint32_t>* idx, RectMode
         gram_solve3(g, rows, sol);
     } else if (big && rows >= big_rows) {
         big->solve(si, oi, rows, sol);
+    } else if (rows <= 256) {
+        // LO trials (<= 14 + C(14, 2) rows): the system on the stack
+        double A[4 * 256];
+        sift_rows_host(sc, oc, si, oi, rows, A, A + 3 * rows);
+        HostQRStore st{{A, A + rows, A + 2 * rows, A + 3 * rows}};
+        qr3_solve(st, rows, sol);
     } else {
         std::vector<double> A(rows * 3), b(rows);
         sift_rows_host(sc, oc, si, oi, rows, A.data(), b.data());
         colpiv_qr_solve3(A, rows, b, sol);
     }
     if (!finish_model(sol, out)) return false;
-    std::vector<double> ang(no), wts(no);
+    // the calling thread's scratch, bound to references: the angle lambda
+    // below runs on the host pool's threads too, and a thread_local named
+    // inside it would be each worker's own instance
+    thread_local std::vector<double> tl_ang, tl_wts;
+    std::vector<double>& ang = tl_ang;
+    std::vector<double>& wts = tl_wts;
+    ang.resize(no);
+    wts.resize(no);
     double wsum = 0;
     // the rectified angles are independent (a big refit spreads them over
     // the solver's threads); the weights and the mode stay in order

@@ -56,6 +56,7 @@ struct SmallScratch {
     double* vals = nullptr;
     uint32_t* meta = nullptr;
     uint32_t cap_models = 0;
+    uint32_t* arrive = nullptr;     // per model: k_lo_split's arrival counter (zero between launches)
 };
 
 struct DevProblem {

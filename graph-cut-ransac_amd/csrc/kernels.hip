@@ -2442,38 +2442,18 @@ struct ArgModels {
     uint32_t n;
 };
 
+// one (model, feature) pair per lane of chunk j (64 pairs) of model mi:
+// the value formula, the MSAC ballot and the chunk's inlier values compacted
+// to its start in p.lo.vals, its counts in p.lo.meta, the list / MSAC
+// ballots into ListBits (k_lo_resid, k_lo_split)
 template <int KIND>
-__global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
-                                                        const uint8_t* __restrict__ inc, double T0, double T1,
-                                                        uint32_t pad0, uint32_t nchunks, ListBits lb, FlagBand fbm,
-                                                        FlagBand fbl, ArgModels am) {
-    const uint32_t mi = blockIdx.y;
-    const uint32_t j = blockIdx.x * (kLrThreads / 64) + (threadIdx.x >> 6);      // chunk
-    const int lane = threadIdx.x & 63;
-    const bool jin = j < nchunks;                             // the last workgroup's tail
-    const uint32_t jj = (jin ? j : 0u) * 64u + (uint32_t)lane;   // pair index
-    const int cls = jj < pad0 ? 0 : 1;                        // chunk-uniform (pad0 % 64 == 0)
-    const uint32_t fi = cls == 0 ? jj : jj - pad0;
+__device__ __forceinline__ void lo_resid_chunk(const DevProblem& p, const typename ModelOf<KIND>::type& m,
+                                               const ValueConst& vc, const uint8_t* __restrict__ inc, uint32_t mi,
+                                               uint32_t j, int lane, double T0, double T1, uint32_t pad0,
+                                               uint32_t nchunks, const ListBits& lb, const FlagBand& fbm,
+                                               const FlagBand& fbl, double x, double y, double f2, double f3,
+                                               int cls, uint32_t fi) {
     const DevClass& c = p.cls[cls];
-    // the pair's features first: their latency overlaps the model's read
-    // (pinned host memory for small batches) and its value constants
-    const uint32_t ic = fi < c.n ? fi : 0u;                  // a class with chunks has features
-    const double x = c.x[ic], y = c.y[ic];
-    const double f2 = (KIND < 3 && cls == 1) ? c.c0[ic] : c.a[ic];
-    const double f3 = KIND >= 3 ? c.c0[ic] : (cls == 1 ? c.c1[ic] : 0.0);
-    __shared__ typename ModelOf<KIND>::type m_sh;
-    __shared__ ValueConst vc_sh;
-    if (threadIdx.x == 0) {
-        if constexpr (KIND <= 2) {
-            m_sh = mi < am.n ? am.m[mi] : models[mi];
-            vc_sh = value_const(m_sh, KIND == 1, KIND == 2);
-        } else {
-            m_sh = models[mi];
-        }
-    }
-    __syncthreads();
-    if (!jin) return;                                        // wave-uniform, after the barrier
-    const auto m = m_sh;
     const bool live = inc == nullptr || inc[mi] <= 101;
     const bool ev = live && fi < c.n;
     double r2 = 0.0;
@@ -2481,9 +2461,9 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
         if constexpr (KIND >= 3) {
             r2 = geo_sq_residual<KIND>(x, y, f2, f3, m.h);
         } else if (cls == 0) {
-            r2 = scale_sq_value<KIND == 1, true>(x, y, f2, m, vc_sh.ac, vc_sh.cut);
+            r2 = scale_sq_value<KIND == 1, true>(x, y, f2, m, vc.ac, vc.cut);
         } else {
-            r2 = orient_sq_value<true>(x, y, f2, f3, m, vc_sh.c, vc_sh.s, vc_sh.cphi, vc_sh.cphi2);
+            r2 = orient_sq_value<true>(x, y, f2, f3, m, vc.c, vc.s, vc.cphi, vc.cphi2);
         }
     }
     const bool inl = ev && r2 <= (cls == 0 ? T0 : T1);
@@ -2504,17 +2484,65 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
     }
 }
 
+// the pair's features of chunk j (loaded before the model's constants)
 template <int KIND>
-__global__ __launch_bounds__(kLoThreads) void k_lo_fold(DevProblem p, const uint8_t* __restrict__ inc, uint32_t pad0,
-                                                       uint32_t nchunks, ScoreOut out) {
+__device__ __forceinline__ void lo_pair_features(const DevProblem& p, uint32_t j, int lane, uint32_t pad0, int& cls,
+                                                 uint32_t& fi, double& x, double& y, double& f2, double& f3) {
+    const uint32_t jj = j * 64u + (uint32_t)lane;             // pair index
+    cls = jj < pad0 ? 0 : 1;                                  // chunk-uniform (pad0 % 64 == 0)
+    fi = cls == 0 ? jj : jj - pad0;
+    const DevClass& c = p.cls[cls];
+    const uint32_t ic = fi < c.n ? fi : 0u;                   // a class with chunks has features
+    x = c.x[ic];
+    y = c.y[ic];
+    f2 = (KIND < 3 && cls == 1) ? c.c0[ic] : c.a[ic];
+    f3 = KIND >= 3 ? c.c0[ic] : (cls == 1 ? c.c1[ic] : 0.0);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
+                                                        const uint8_t* __restrict__ inc, double T0, double T1,
+                                                        uint32_t pad0, uint32_t nchunks, ListBits lb, FlagBand fbm,
+                                                        FlagBand fbl, ArgModels am) {
+    const uint32_t mi = blockIdx.y;
+    const uint32_t j = blockIdx.x * (kLrThreads / 64) + (threadIdx.x >> 6);      // chunk
+    const int lane = threadIdx.x & 63;
+    const bool jin = j < nchunks;                             // the last workgroup's tail
+    // the pair's features first: their latency overlaps the model's read
+    // (pinned host memory for small batches) and its value constants
+    int cls;
+    uint32_t fi;
+    double x, y, f2, f3;
+    lo_pair_features<KIND>(p, jin ? j : 0u, lane, pad0, cls, fi, x, y, f2, f3);
+    __shared__ typename ModelOf<KIND>::type m_sh;
+    __shared__ ValueConst vc_sh;
+    if (threadIdx.x == 0) {
+        if constexpr (KIND <= 2) {
+            m_sh = mi < am.n ? am.m[mi] : models[mi];
+            vc_sh = value_const(m_sh, KIND == 1, KIND == 2);
+        } else {
+            m_sh = models[mi];
+        }
+    }
+    __syncthreads();
+    if (!jin) return;                                        // wave-uniform, after the barrier
+    lo_resid_chunk<KIND>(p, m_sh, vc_sh, inc, mi, j, lane, T0, T1, pad0, nchunks, lb, fbm, fbl, x, y, f2, f3, cls,
+                         fi);
+}
+
+// The fold of one model's compacted chunks (k_lo_fold, and the last
+// workgroup of a model in k_lo_split): scan the chunk counts, gather the
+// chunks in feature order into LDS (all of a wave's reads in flight
+// together) and fold them (fold_exact_chains).  1024 threads.
+template <int KIND>
+__device__ __forceinline__ void lo_fold_model(const DevProblem& p, uint32_t mi, uint32_t pad0, uint32_t nchunks,
+                                              const ScoreOut& out) {
     __shared__ double cball[2 * kLoBlock];
     __shared__ uint32_t coff[2 * kLoChunks + 1];
     __shared__ uint32_t wtot[kLoThreads / 64];
     __shared__ uint32_t fsum[2];
     __shared__ BlkFoldScratch bsc[3];
-    const uint32_t mi = blockIdx.x;
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-    (void)inc;                                               // a dead slot's chunks hold no inliers
     if (t < 2) fsum[t] = 0;
     // the chunk counts (one chunk per thread: nchunks <= 2 kLoChunks), block scan
     const uint32_t mt = (uint32_t)t < nchunks ? p.lo.meta[(size_t)mi * nchunks + t] : 0u;
@@ -2578,6 +2606,70 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_fold(DevProblem p, const uint
         if (out.fl) out.fl[mi] = fsum[0];
         if (out.lfl) out.lfl[mi] = fsum[1];
     }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kLoThreads) void k_lo_fold(DevProblem p, const uint8_t* __restrict__ inc, uint32_t pad0,
+                                                       uint32_t nchunks, ScoreOut out) {
+    (void)inc;                                               // a dead slot's chunks hold no inliers
+    lo_fold_model<KIND>(p, blockIdx.x, pad0, nchunks, out);
+}
+
+// The split scorer in ONE launch (round 5, the default): 1024-thread
+// workgroups, blockIdx.y the model, each workgroup evaluating per wave
+// `cpw` chunks of the model (k_lo_resid's work), then counting itself done on
+// the model's arrival counter; the model's last workgroup to arrive folds
+// the model's chunks (k_lo_fold's work) and resets the counter for the next
+// launch.  No second launch, and no kernel boundary between the last
+// residual of a model and its fold: the fold of one model overlaps the
+// residuals of the next.
+template <int KIND>
+__global__ __launch_bounds__(kLoThreads) void k_lo_split(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
+                                                        const uint8_t* __restrict__ inc, double T0, double T1,
+                                                        uint32_t pad0, uint32_t nchunks, uint32_t cpw, ListBits lb,
+                                                        FlagBand fbm, FlagBand fbl, ArgModels am, ScoreOut out) {
+    const uint32_t mi = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t j0 = (blockIdx.x * (kLoThreads / 64) + (uint32_t)wave) * cpw;    // this wave's first chunk
+    __shared__ typename ModelOf<KIND>::type m_sh;
+    __shared__ ValueConst vc_sh;
+    __shared__ uint32_t last_sh;
+    // the first chunk's features ahead of the model's constants
+    int cls;
+    uint32_t fi;
+    double x, y, f2, f3;
+    lo_pair_features<KIND>(p, j0 < nchunks ? j0 : 0u, lane, pad0, cls, fi, x, y, f2, f3);
+    if (threadIdx.x == 0) {
+        if constexpr (KIND <= 2) {
+            m_sh = mi < am.n ? am.m[mi] : models[mi];
+            vc_sh = value_const(m_sh, KIND == 1, KIND == 2);
+        } else {
+            m_sh = models[mi];
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < cpw; ++q) {
+        const uint32_t j = j0 + q;
+        if (j >= nchunks) break;                             // wave-uniform
+        if (q > 0) lo_pair_features<KIND>(p, j, lane, pad0, cls, fi, x, y, f2, f3);
+        lo_resid_chunk<KIND>(p, m_sh, vc_sh, inc, mi, j, lane, T0, T1, pad0, nchunks, lb, fbm, fbl, x, y, f2, f3,
+                             cls, fi);
+    }
+    // arrival: this workgroup's chunk values and counts are visible device-
+    // wide before its count (one agent-scope release after the barrier: the
+    // release is an L2 writeback on gfx950, whose XCDs have their own L2s --
+    // once per workgroup, not per thread); the last arrival acquires them
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t prev = atomicAdd(&p.lo.arrive[mi], 1u);
+        last_sh = prev + 1u == gridDim.x ? 1u : 0u;
+        if (last_sh) p.lo.arrive[mi] = 0u;                  // reset for the next launch (no other arrival left)
+    }
+    __syncthreads();
+    if (!last_sh) return;                                    // workgroup-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    lo_fold_model<KIND>(p, mi, pad0, nchunks, out);
 }
 
 // -------------------------------------------------------------- compact ----
@@ -3985,6 +4077,29 @@ bool lo_argmodels() {
     return !(e && e[0] == '0');
 }
 
+// GCR_LO_FUSED=0: the split scorer as two launches (k_lo_resid + k_lo_fold)
+// instead of k_lo_split (read per launch)
+bool lo_fused() {
+    const char* e = getenv("GCR_LO_FUSED");
+    return !(e && e[0] == '0');
+}
+
+// k_lo_split's chunks per wave: every workgroup takes a whole CU (the fold's
+// LDS), so the launch is sized to about one workgroup per CU -- the fewest
+// chunks per wave with nm x workgroups <= 256 (GCR_LO_CPW=n pins it)
+uint32_t lo_cpw(uint32_t nm, uint32_t nchunks) {
+    if (const char* e = getenv("GCR_LO_CPW")) {
+        const long v = atol(e);
+        if (v >= 1 && v <= 64) return (uint32_t)v;
+    }
+    const uint32_t wpw = kLoThreads / 64;
+    for (uint32_t c = 1; c < 64; ++c) {
+        const uint32_t nwg = (nchunks + wpw * c - 1) / (wpw * c);
+        if ((size_t)nwg * nm <= 256) return c;
+    }
+    return 64;
+}
+
 size_t small_score_pairs(const DevProblem& p) {
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t pad1 = (p.solver == 2) ? ((p.cls[1].n + 63u) & ~63u) : 0u;
@@ -4017,9 +4132,18 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
                 std::memcpy(am.m, hmodels, (size_t)nm * sizeof(RectModel));
                 am.n = nm;
             }
-            hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, mp, inc, T[0], T[1], pad0,
-                               nchunks, lb, flag_band(T), flag_band(lb.T), am);
-            hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, p, inc, pad0, nchunks, out);
+            if (lo_fused() && p.lo.arrive != nullptr) {
+                const uint32_t cpw = lo_cpw(nm, nchunks);
+                const uint32_t per = (kLoThreads / 64) * cpw;
+                const dim3 g2((nchunks + per - 1) / per, nm);
+                hipLaunchKernelGGL((k_lo_split<KIND>), g2, dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1], pad0,
+                                   nchunks, cpw, lb, flag_band(T), flag_band(lb.T), am, out);
+            } else {
+                hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, mp, inc, T[0], T[1],
+                                   pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am);
+                hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, p, inc, pad0, nchunks,
+                                   out);
+            }
         } else if (lo_fold_wide())
             hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1],
                                pad0, ntot, lb, flag_band(T), flag_band(lb.T), out, probe);

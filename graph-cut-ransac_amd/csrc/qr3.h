@@ -40,6 +40,25 @@ constexpr size_t kSumSuper = 64 * kSumBlock;     // super-blocks: 64 blocks
 // for short ranges (the LO trials' 105-row systems).
 template <class F>
 inline double block_partial(size_t base, size_t lo, size_t hi, F f) {
+    if (base == 0 && hi <= kSumLanes) {
+        // one row per lane (systems of at most 256 rows, e.g. the LO trials'):
+        // the same lane values and halving tree without the lane loop's
+        // read-modify-write (+0.0 + f, as the lane sum of one row)
+        double acc[kSumLanes];
+        if (hi == 0) return 0.0;
+        for (size_t l = 0; l < lo; ++l) acc[l] = 0.0;
+        for (size_t l = lo; l < hi; ++l) acc[l] = 0.0 + f(l);
+        size_t top = hi;
+        for (size_t h = kSumLanes / 2; h >= 1; h >>= 1) {
+            if (top <= h) continue;
+            double* __restrict d = acc;                 // [0, top - h) and [h, top) do not overlap
+            const double* __restrict u = acc + h;
+            const size_t n2 = top - h;
+            for (size_t l = 0; l < n2; ++l) d[l] = d[l] + u[l];
+            top = h;
+        }
+        return acc[0];
+    }
     double acc[kSumLanes];
     const size_t b0 = std::max(base, lo), b1 = std::min(base + kSumBlock, hi);
     size_t top = b1 > base ? std::min(kSumLanes, b1 - base) : 0;

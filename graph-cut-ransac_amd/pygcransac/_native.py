@@ -154,6 +154,8 @@ def _load():
     L.gcr_debug_generate.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, u8p, C.POINTER(RectModel)]
     L.gcr_debug_score.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_uint32, u32p, u32p, dp, dp, dp]
     L.gcr_debug_score_less.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.POINTER(RectModel)]
+    L.gcr_debug_exchange_log.argtypes = [C.POINTER(C.c_uint64), C.c_size_t]
+    L.gcr_debug_exchange_log.restype = C.c_size_t
     L.gcr_debug_mask.argtypes = [vp, C.POINTER(Params), C.POINTER(RectModel), C.c_int, C.c_int, u8p]
     L.gcr_host_log.argtypes = [C.c_double]
     L.gcr_host_log.restype = C.c_double
@@ -240,3 +242,16 @@ def default_params() -> Params:
     p = Params()
     lib.gcr_default_params(C.byref(p))
     return p
+
+
+def exchange_log():
+    """The collective events of the calling thread's last summary replay
+    (GCR_EXCHANGE_LOG=1; gcr_debug_exchange_log): a list of (kind, chunk,
+    flags, arg) tuples -- kind 1 chunk issue (flags: set | ahead << 1, arg:
+    slots), 2 re-summary (flags: set | locate << 1, arg: owner + 1 | from_pos
+    << 16), 3 chunk collected."""
+    n = lib.gcr_debug_exchange_log(None, 0)
+    buf = (C.c_uint64 * max(n, 1))()
+    lib.gcr_debug_exchange_log(buf, n)
+    w = list(buf)[:n]
+    return [tuple(w[i:i + 4]) for i in range(0, n, 4)]

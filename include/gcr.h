@@ -263,6 +263,12 @@ int gcr_debug_score(gcr_problem* prob, const gcr_params* params, const gcr_rect_
  * the value scores' own order; < 0 an error. */
 int gcr_debug_score_less(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* a,
                          const gcr_rect_model* b);
+/* With GCR_EXCHANGE_LOG=1, the summary replay of the last run on the calling
+ * thread logs every event that is a collective under gcr_comm (chunk issue,
+ * re-summary) and every chunk it collected: 4 words per event (engine.cpp
+ * t_xlog).  Copies min(count, cap) words to out (may be null); returns the
+ * count.  No GPU needed. */
+size_t gcr_debug_exchange_log(uint64_t* out, size_t cap);
 /* inlier mask of one model: rule 0 = MSAC (2.25 thr^2), 1 = LO threshold
  * ((1.5 thr)^2), 2 = 1-class graph-cut labeling */
 int gcr_debug_mask(gcr_problem* prob, const gcr_params* params, const gcr_rect_model* model, int cls, int rule,

@@ -97,12 +97,19 @@ def _sharded_vs_single(kind, budget, monkeypatch, env):
         params.update(min_iteration_number=300_000, max_iteration_number=300_000)
     else:
         params.update(min_iteration_number=0, max_iteration_number=10**7, confidence=0.99)
+    monkeypatch.setenv("GCR_EXCHANGE_LOG", "1")
     ref = D.run_problem_sharded(kind, f0, f1, params, 0, 1, device=0)
+    ref_ev = N.exchange_log()
     comm = D.Comm(None, 0, 1, device=0)
     try:
         got = D.run_problem_sharded(kind, f0, f1, params, 0, 1, device=0, comm=comm)
+        got_ev = N.exchange_log()
     finally:
         comm.close()
+    monkeypatch.delenv("GCR_EXCHANGE_LOG")
+    # the gcr_comm run issues its collectives (chunk issues and re-summaries)
+    # in exactly the callback path's event sequence
+    assert ref_ev and got_ev == ref_ev
     for k in env:
         monkeypatch.delenv(k)
     (Hr, mr, sr, rr), (Hg, mg, sg, rg) = ref, got

@@ -39,10 +39,18 @@ def _digest(res):
                 hyp=st["hypotheses"], score=bits(st["score"]).tolist(), rec=bits(rec).tolist())
 
 
+def _events(log):
+    # the collectives of a gcr_comm run (issue, re-summary) in order, with the
+    # collected chunks: RCCL deadlocks unless every rank issues the same
+    # sequence (engine.cpp t_xlog)
+    return [list(map(int, e)) for e in log]
+
+
 def _worker(rank, world, port, outdir, env=None):
     import torch.distributed as dist
 
     os.environ.update(env or {})
+    os.environ["GCR_EXCHANGE_LOG"] = "1"
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -50,6 +58,7 @@ def _worker(rank, world, port, outdir, env=None):
         for name, solver, f0, f1, prm in _cases():
             out[name] = _digest(D.run_problem_sharded(solver, f0, f1, prm, rank=rank, world=world, dist=dist,
                                                       device=0))
+            out[name + "_events"] = _events(N.exchange_log())
         with open(os.path.join(outdir, f"rank{rank}.json"), "w") as fh:
             json.dump(out, fh)
     finally:
@@ -68,14 +77,39 @@ def _free_port():
     # a two-member summary cap: chains continue on the owner's device, every
     # rank joins each continuation exchange
     (2, {"GCR_SUMMARY_CAP": "2"}),
+    # every summary overflows: every chunk's chain continues by re-summaries
+    (2, {"GCR_SUMMARY_CAP": "1"}),
+    # speculative chunks issued even when the current chunk ends the run:
+    # chunks whose collectives every rank issues and no rank replays
+    (2, {"GCR_SPEC_TRIM": "0"}),
     # three ranks, the per-slot exchange of round 2 (GCR_REPLAY=slots) as reference
     (3, {}),
+    (3, {"GCR_SUMMARY_CAP": "1"}),
 ])
 def test_sharded_problem_equals_single_rank(tmp_path, world, env):
     if N.lib.gcr_device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), env), nprocs=world, join=True)
     outs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    # every rank logged the same collectives in the same order (VERDICT round
+    # 4, item 6): chunk issues -- speculative ones the replay later abandons
+    # included -- and re-summaries (continuations with a small summary cap,
+    # stop locates)
+    for name, *_ in _cases():
+        ev = outs[0][name + "_events"]
+        assert ev and all(o[name + "_events"] == ev for o in outs), name
+        issued = {e[1] for e in ev if e[0] == 1}
+        collected = {e[1] for e in ev if e[0] == 3}
+        assert collected <= issued
+        if env.get("GCR_SUMMARY_CAP") == "1":
+            assert any(e[0] == 2 and not (e[2] & 2) for e in ev), name      # a continuation exchange
+    abandoned = sum(len({e[1] for e in outs[0][n + "_events"] if e[0] == 1} -
+                        {e[1] for e in outs[0][n + "_events"] if e[0] == 3}) for n, *_ in _cases())
+    if env.get("GCR_SPEC_TRIM") == "0":
+        assert abandoned >= 1, "no speculative chunk was abandoned: the case does not cover it"
+    for r in range(world):
+        for name, *_ in _cases():
+            outs[r].pop(name + "_events")
     saved = {k: os.environ.get(k) for k in ("GCR_REPLAY",)}
     try:
         if world == 3:

@@ -22,6 +22,7 @@ for s in $STEPS; do
     benchf) timeout -k 10 600 python -u bench.py --workload f --steps 200 --warmup 20 --cpu-seconds 0 > $O/bench_f.log 2>&1 || fail benchf $? $O/bench_f.log; tail -1 $O/bench_f.log > $O/bench_f.json; python3 -c "import json;d=json.load(open('$O/bench_f.json'));w=d.get('wall_time_to_0.99_confidence',{});print(d['value'],d['ms_per_step'],w.get('ms_median'),max(w.get('ms_all',[0])))" ;;
     stats) (cd /tmp && true); export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python3 bench.py --cpu-seconds 0 ${BENCH_ARGS:-} > $O/stats.log 2>&1 || fail stats $? $O/stats.log; find $O/stats -name '*kernel_stats.csv' -exec head -20 {} \; ;;
     sync) timeout -k 10 120 tools/micro/sync_latency.bin > $O/sync.log 2>&1 || fail sync $? $O/sync.log; cat $O/sync.log ;;
+    valu) timeout -k 10 200 tools/micro/valu_issue.bin > $O/valu.log 2>&1 || fail valu $? $O/valu.log; cat $O/valu.log ;;
     latst) export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/latst -o run --output-format csv -- python3 tools/lat_seeds.py --workload ${LAT_WL:-m2} --reps 2 base: > $O/latst.log 2>&1 || fail latst $? $O/latst.log; find $O/latst -name '*kernel_stats.csv' -exec head -25 {} \; ;;
   esac
 done
