@@ -111,12 +111,14 @@ template <class T>
 struct PinBuf {
     T* p = nullptr;
     size_t cap = 0;
+    bool coherent = false;      // fine-grained (device writes not cached in its L2s)
     void ensure(size_t n) {
         if (n <= cap) return;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        HIPC(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(T) * n, hipHostMallocDefault));
+        HIPC(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(T) * n,
+                           coherent ? hipHostMallocCoherent : hipHostMallocDefault));
         cap = n;
     }
     ~PinBuf() { if (p) (void)hipHostFree(p); }
@@ -318,6 +320,18 @@ struct Workspace {
     DevBuf<uint32_t> cs_arrive[2];
     hipEvent_t sum_done[2] = {nullptr, nullptr}, sum_k0[2] = {nullptr, nullptr}, sum_k1[2] = {nullptr, nullptr};
     bool spec_pending[2] = {false, false};   // a speculative chunk of this set may still run
+    // score_models' completion flags (ScoreOut::done): the small scorer stores
+    // done_epoch into lo_done[m] after model m's results; the results, list
+    // bits and flags live in coherent pinned memory, so the host waits on the
+    // flags instead of the stream's end-of-kernel signal (~5 us sooner)
+    PinBuf<uint32_t> lo_done;
+    uint32_t done_epoch = 0;
+    Workspace() {
+        lo_sb.hblk.coherent = true;
+        h_lbits.coherent = true;
+        h_mbits.coherent = true;
+        lo_done.coherent = true;
+    }
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
         for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start, vb_flush, sum_done[0],
@@ -337,6 +351,17 @@ namespace {
 // re-summary, 3 collect), chunk number, set | ahead << 1 (issue) or set |
 // locate << 1 (re-summary), slots (issue) or owner + 1 | from_pos << 16.
 thread_local std::vector<uint64_t> t_xlog;
+
+// GCR_LO_TRACE=1 (read at load): host-side timeline of every LO round
+// (lists, fits, launch, wait, pick) printed to stderr per local optimisation
+const bool g_lo_trace = [] {
+    const char* e = getenv("GCR_LO_TRACE");
+    return e && e[0] == '1';
+}();
+thread_local std::vector<std::pair<const char*, Clock::time_point>> t_lot;
+inline void lot(const char* tag) {
+    if (g_lo_trace) t_lot.emplace_back(tag, Clock::now());
+}
 
 // GCR_BACKTRACE=1 (read at load): SIGABRT / SIGSEGV print the native stack
 // to stderr before the default action (diagnostics on the GPU box, which has
@@ -759,6 +784,48 @@ public:
             std::exception_ptr e = err_;
             err_ = nullptr;
             std::rethrow_exception(e);            // the first failure, on the caller
+        }
+    }
+
+    // fn(i) for i in [0, n) started on the workers; the caller goes on (e.g.
+    // launches GPU work) and then calls end(), which helps with what is left
+    // and waits.  false (nothing started) when the pool has no workers or is
+    // busy: the caller then uses parallel_for.  fn must outlive end().
+    bool begin(size_t n, const std::function<void(size_t)>& fn) {
+        if (workers_.empty() || n == 0) return false;
+        // held until end(): a plain try_lock / unlock pair (a shared
+        // std::unique_lock member raced between one caller's unlock and the
+        // next caller's acquire, which then ran two jobs at once)
+        if (!call_mu_.try_lock()) return false;
+        job_ = &fn;
+        n_ = n;
+        next_.store(0, std::memory_order_relaxed);
+        pending_.store(workers_.size(), std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        return true;
+    }
+    void end() {
+        run();
+        const auto t0 = Clock::now();
+        bool told = false;
+        for (unsigned spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin) {
+            if (spin > 4096) std::this_thread::yield();
+            if (!told && (spin & 65535) == 0 && spin && ms_since(t0) > 5000.0) {
+                fprintf(stderr, "gcr: host pool end(): %zu workers pending after 5 s\n",
+                        (size_t)pending_.load(std::memory_order_acquire));
+                told = true;
+            }
+        }
+        job_ = nullptr;
+        call_mu_.unlock();
+        if (err_) {
+            std::exception_ptr e = err_;
+            err_ = nullptr;
+            std::rethrow_exception(e);
         }
     }
 
@@ -2887,8 +2954,30 @@ private:
     // flagged decisions, or one exact.h's bound does not cover, is rescored in
     // the reference's decisions on the host, and its list / MSAC bits marked
     // unusable (sm_lbad_ / sm_mbad_)
+    // Parts (LO trials scored while later trials are still being fitted,
+    // local_optimization): with score_parts_ok(n) a call with launch_only
+    // launches the residuals of models [first, n) and returns; the next call
+    // (same req, first = the models already launched) launches the rest and
+    // the fold of all n, waits and finishes all n.
+    bool score_parts_ok(uint32_t n) const {
+        if constexpr (!kRect) {
+            (void)n;
+            return false;
+        } else {
+            return n <= kSmallScore && n <= kArgModels && small_score_on() && zerocopy_on() && done_wait_on() &&
+                   lo_pipe_on() && score_small_splits(P_->dp, n);
+        }
+    }
+    // GCR_LO_PIPE=1: LO trials scored in two parts while the second half is
+    // fitted -- measured no faster on MI355X (session r5_s13: the first
+    // part's residual launch reaches the GPU only with the second's), so off
+    static bool lo_pipe_on() {
+        const char* e = getenv("GCR_LO_PIPE");                // read per call
+        return e && e[0] == '1';
+    }
     bool score_models(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n /* 2 per model */,
-                      const ListReq* req = nullptr, const Model* decs = nullptr) {
+                      const ListReq* req = nullptr, const Model* decs = nullptr, uint32_t first = 0,
+                      bool launch_only = false) {
         auto& lm = Tr::lomodels(P_->w);
         lm.ensure(n);
         P_->w->lo_sb.ensure(n);
@@ -2898,11 +2987,14 @@ private:
         // small batches: models read from pinned memory and results written
         // into the pinned mirror by the kernels (no copy launches either way)
         const bool zc = small && zerocopy_on();
+        const bool parts = (first > 0 || launch_only) && zc && score_parts_ok(n);
+        if ((first > 0 || launch_only) && !parts)
+            throw std::logic_error("score_models: parts without score_parts_ok");
         const Model* dmodels = lm.p;
         if (zc) {
             auto& hm = Tr::hlomodels(P_->w);
             hm.ensure(kSmallScore);                  // sized once (a pinned reallocation costs milliseconds)
-            std::memcpy(hm.p, models, n * sizeof(Model));
+            std::memcpy(hm.p + first, models + first, (n - first) * sizeof(Model));
             dmodels = dev_view(hm.p);
         } else {
             HIPC(hipMemcpyAsync(lm.p, models, n * sizeof(Model), hipMemcpyHostToDevice, s_));
@@ -2933,14 +3025,46 @@ private:
                     lb.mbits = static_cast<uint64_t*>(dptr);
                 }
             }
-            HIPC(launch_score_small(P_->dp, Tm_, dmodels, nullptr, n,
-                                    zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev(), s_, lists ? &lb : nullptr,
+            ScoreOut so = zc ? P_->w->lo_sb.host_dev() : P_->w->lo_sb.dev();
+            if (parts) {
+                // stage 1: the residuals of models [first, n) (from their
+                // own pinned slots / kernel arguments); stage 2 (the final
+                // call): the fold of all n
+                if (launch_only) {
+                    HIPC(launch_score_small_part(P_->dp, Tm_, dmodels + first, first, n - first, 1, 0, so, s_,
+                                                 lists ? &lb : nullptr, models + first));
+                    return false;
+                }
+                P_->w->lo_done.ensure(kSmallScore);
+                so.done = dev_view(P_->w->lo_done.p);
+                so.epoch = ++P_->w->done_epoch;
+                if (so.epoch == 0) so.epoch = ++P_->w->done_epoch;
+                HIPC(launch_score_small_part(P_->dp, Tm_, dmodels + first, first, n - first, 3, n, so, s_,
+                                             lists ? &lb : nullptr, models + first));
+                wait_done(P_->w->lo_done.p, n, so.epoch);
+                goto scored;
+            }
+            if (zc && done_wait_on()) {
+                P_->w->lo_done.ensure(kSmallScore);             // sized once
+                so.done = dev_view(P_->w->lo_done.p);
+                so.epoch = ++P_->w->done_epoch;
+                if (so.epoch == 0) so.epoch = ++P_->w->done_epoch;     // 0 never marks a model done
+            }
+            lot("setup");
+            HIPC(launch_score_small(P_->dp, Tm_, dmodels, nullptr, n, so, s_, lists ? &lb : nullptr,
                                     kRect ? static_cast<const void*>(models) : nullptr));
+            lot("launched");
+            if (so.done) {
+                wait_done(P_->w->lo_done.p, n, so.epoch);
+                goto scored;
+            }
         } else {
             HIPC(Tr::score(P_, Tm_, lm.p, nullptr, n, identity, P_->w->lo_sb.dev(), s_));
         }
         if (!zc) P_->w->lo_sb.d2h(n, s_);
         HIPC(hipStreamSynchronize(s_));
+    scored:
+        lot("waited");
         st_.launches += 1;
         sm_mbad_.assign(n, 0);
         sm_lbad_.assign(n, 0);
@@ -2963,7 +3087,46 @@ private:
                 if (lists && (P_->w->lo_sb.hlfl.p[i] != 0 || bad)) sm_lbad_[i] = 1;
             }
         }
+        lot("finished");
         return lists;
+    }
+
+    // GCR_DONE_WAIT=0: score_models waits on the stream instead of the
+    // kernels' completion flags (read per call)
+    static bool done_wait_on() {
+        const char* e = getenv("GCR_DONE_WAIT");
+        return !(e && e[0] == '0');
+    }
+    // spin until the small scorer has flagged models 0 .. n-1 with `epoch`;
+    // a stream that drained (or failed) without them is an error
+    void wait_done(const uint32_t* done, uint32_t n, uint32_t epoch) {
+        uint32_t i = 0;
+        const auto t0 = Clock::now();
+        for (uint64_t it = 1;; ++it) {
+            while (i < n && __atomic_load_n(done + i, __ATOMIC_ACQUIRE) == epoch) ++i;
+            if (i == n) break;
+            if ((it & 4095) == 0) {
+                const hipError_t q = hipStreamQuery(s_);
+                if (q == hipSuccess) {              // drained: the flags are visible now, or never come
+                    while (i < n && __atomic_load_n(done + i, __ATOMIC_ACQUIRE) == epoch) ++i;
+                    if (i == n) break;
+                    char msg[160];
+                    snprintf(msg, sizeof(msg),
+                             "small scorer: completion flag %u of %u is %u, expected %u after the stream drained", i, n,
+                             __atomic_load_n(done + i, __ATOMIC_ACQUIRE), epoch);
+                    throw std::runtime_error(msg);
+                }
+                if (q != hipErrorNotReady) HIPC(q);
+                if (ms_since(t0) > 5000.0) {
+                    char msg[160];
+                    snprintf(msg, sizeof(msg), "small scorer: no completion after 5 s (flag %u of %u is %u, expected %u)",
+                             i, n, __atomic_load_n(done + i, __ATOMIC_ACQUIRE), epoch);
+                    throw std::runtime_error(msg);
+                }
+            }
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
     }
 
     // model q's inlier lists from the bits of the last score_models(req) call
@@ -3058,6 +3221,7 @@ private:
     }
 
     // graphCutLocalOptimization (GCRANSAC.h:873-1062)
+    std::vector<uint8_t> drawn_;          // local_optimization: trial q's sample was drawn
     bool local_optimization(Buffer& sfb_buf) {
         const auto t0 = Clock::now();
         HScore max_score = best_;
@@ -3081,8 +3245,10 @@ private:
         // without its own mask launch + synchronisation
         const ListReq lreq{{Tlo_[0], Tlo_[1]}, K_ == 2 ? 0 : 2, lo_reuse_on()};
         bool have_inl = false;
+        if (g_lo_trace) t_lot.clear();
         while (++gc_number_ < 10) {
             bool updated = false;
+            lot("round");
             auto tp = Clock::now();
             if (!have_inl) {
                 if (lo_row_ >= 0 && std::memcmp(&lo_row_model_, &lo_model, sizeof(Model)) == 0 &&
@@ -3095,6 +3261,7 @@ private:
             }
             lo_row_ = -1;
             have_inl = false;
+            lot("lists");
             st_.ms_lo_lists += ms_since(tp);
             tp = Clock::now();
             uint64_t ssz[2] = {0, 0};
@@ -3108,48 +3275,79 @@ private:
             // when every class uses all its inliers each trial refits the same
             // set: one trial decides the round (later ones cannot be strictly better)
             const uint64_t ntrials = all_deterministic ? std::min<uint64_t>(T, 1) : T;
-            // draw the trials' samples in order (a failed draw ends the round,
-            // as in the sequential loop), fit them on the host worker pool,
-            // keep the successful fits in trial order
+            // every trial draws its sample (counter-based: independent of the
+            // others) and fits it on the host worker pool; a failed draw ends
+            // the round at that trial, as in the sequential loop (its fit and
+            // every later trial's are discarded); the successful fits are kept
+            // in trial order
             trial_samples.resize(ntrials);
-            uint64_t ndrawn = 0;
-            for (uint64_t trial = 0; trial < ntrials; ++trial) {
-                bool ok = true;
+            trial_fit.resize(ntrials);
+            trial_ok.assign(ntrials, 0);
+            drawn_.assign(ntrials, 0);
+            auto draw_fit = [&](size_t trial) {
                 auto& smp = trial_samples[trial];
-                for (int c = 0; c < K_ && ok; ++c) {
+                for (int c = 0; c < K_; ++c) {
                     if (ssz[c] < inl[c].size()) {
                         // 7 m points: 49 for the 7-point fundamental matrix
                         uint32_t pos[kMaxLOSample];
                         WordStream ws(prm_.seed, round_id, (uint32_t)trial, kStreamLO, (uint32_t)c);
-                        if (!sample_distinct<kMaxLOSample>(ws, inl[c].size(), (int)ssz[c], pos)) {
-                            ok = false;
-                            break;
-                        }
+                        if (!sample_distinct<kMaxLOSample>(ws, inl[c].size(), (int)ssz[c], pos)) return;
                         smp[c].resize(ssz[c]);
                         for (uint64_t q = 0; q < ssz[c]; ++q) smp[c][q] = inl[c][pos[q]];
                     } else if (m_[c] < inl[c].size()) {
                         smp[c] = inl[c];
                     } else {
-                        ok = false;
+                        return;
                     }
                 }
-                if (!ok) break;
-                ++ndrawn;
+                drawn_[trial] = 1;
+                trial_ok[trial] = Tr::fit(P_, smp.data(), trial_fit[trial], false) ? 1 : 0;
+            };
+            // Pipelined with the GPU (GCR_LO_PIPE=0: off): the first half of
+            // the trials is fitted, its residual launch goes out, and the
+            // second half is fitted while the GPU scores the first; then the
+            // second half's residuals and the fold of all.  Same models in
+            // the same order, so the same scores.
+            uint64_t first_half = 0;                 // trial models already launched
+            const uint64_t half = (ntrials + 1) / 2;
+            const bool pipe = ntrials >= 8 && score_parts_ok((uint32_t)ntrials);
+            uint64_t ndrawn = 0;
+            if (pipe) {
+                host_pool().parallel_for(half, draw_fit);
+                while (ndrawn < half && drawn_[ndrawn]) ++ndrawn;
+                for (uint64_t i = 0; i < ndrawn; ++i)
+                    if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
+                if (ndrawn == half) {                // no failed draw: the second half runs
+                    auto second = [&](size_t k) { draw_fit(half + k); };
+                    const bool async = host_pool().begin(ntrials - half, second);
+                    if (!trial_models.empty()) {
+                        trial_raw.resize(2 * ntrials);
+                        trial_scores.resize(ntrials);
+                        score_models(trial_models.data(), (uint32_t)trial_models.size(), trial_scores.data(),
+                                     trial_raw.data(), &lreq, nullptr, 0, true);
+                        first_half = trial_models.size();
+                    }
+                    if (async) host_pool().end();
+                    else host_pool().parallel_for(ntrials - half, second);
+                    while (ndrawn < ntrials && drawn_[ndrawn]) ++ndrawn;
+                    for (uint64_t i = half; i < ndrawn; ++i)
+                        if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
+                }
+            } else {
+                host_pool().parallel_for(ntrials, draw_fit);
+                while (ndrawn < ntrials && drawn_[ndrawn]) ++ndrawn;
+                for (uint64_t i = 0; i < ndrawn; ++i)
+                    if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
             }
-            trial_fit.resize(ndrawn);
-            trial_ok.assign(ndrawn, 0);
-            host_pool().parallel_for(ndrawn, [&](size_t i) {
-                trial_ok[i] = Tr::fit(P_, trial_samples[i].data(), trial_fit[i], false) ? 1 : 0;
-            });
-            for (uint64_t i = 0; i < ndrawn; ++i)
-                if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
+            lot("fits");
             st_.ms_lo_fit += ms_since(tp);
             tp = Clock::now();
             if (!trial_models.empty()) {
                 trial_scores.resize(trial_models.size());
                 trial_raw.resize(2 * trial_models.size());
                 const bool bits = score_models(trial_models.data(), (uint32_t)trial_models.size(),
-                                               trial_scores.data(), trial_raw.data(), &lreq);
+                                               trial_scores.data(), trial_raw.data(), &lreq, nullptr,
+                                               (uint32_t)first_half);
                 st_.lo_models += trial_models.size();
                 st_.ms_lo_score += ms_since(tp);
                 size_t win = 0;
@@ -3174,7 +3372,19 @@ private:
                     if (lo_lists_from_bits_) list_of((uint32_t)win, lo_msac_lists_, true);
                 }
             }
+            lot("picked");
             if (!updated) break;
+        }
+        if (g_lo_trace && !t_lot.empty()) {
+            std::string line = "gcr LO:";
+            const auto b = t_lot.front().second;
+            for (const auto& e : t_lot) {
+                char buf[64];
+                snprintf(buf, sizeof(buf), " %s %.1f", e.first,
+                         std::chrono::duration<double, std::micro>(e.second - b).count());
+                line += buf;
+            }
+            fprintf(stderr, "%s\n", line.c_str());
         }
         st_.ms_lo += ms_since(t0);
         if (score_less(best_, [&] { return best_model_; }, max_score, [&] { return lo_model; })) {

@@ -79,6 +79,11 @@ struct ScoreOut {
     double* tot;
     uint32_t* fl = nullptr;
     uint32_t* lfl = nullptr;
+    // small scorer, optional: per model, `epoch` stored into done[m] (host
+    // memory, coherent) after model m's results -- the host waits on these
+    // flags instead of the stream's completion signal
+    uint32_t* done = nullptr;
+    uint32_t epoch = 0;
 };
 
 // Draw + validate + solve `nslots` outer-iteration slots [slot0, slot0+nslots).
@@ -305,6 +310,14 @@ constexpr uint32_t kArgModels = 50;
 hipError_t launch_score_small(const DevProblem& p, const double T[2], const void* models, const uint8_t* inc,
                               uint32_t nm, const ScoreOut& out, hipStream_t stream, const ListBits* lists = nullptr,
                               const void* hmodels = nullptr);
+// The split scorer in parts (LO trials scored while the rest are still being
+// fitted): stage 1 = the residual launch of models [mi_base, mi_base + nm)
+// (`models` / `hmodels` point at the part's first model); stage 2 = the fold
+// of models [0, nm_fold).  Only where score_small_splits() holds.
+bool score_small_splits(const DevProblem& p, uint32_t nm_total);
+hipError_t launch_score_small_part(const DevProblem& p, const double T[2], const void* models, uint32_t mi_base,
+                                   uint32_t nm, int stage, uint32_t nm_fold, const ScoreOut& out, hipStream_t stream,
+                                   const ListBits* lists, const void* hmodels);
 
 // Per-feature inlier mask of one model for class `cls`: bit 0 the decision,
 // bit 1 set when the pair's twin r^2 lies in the flag band of T (exact.h:

@@ -1708,6 +1708,15 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
 
 
 // ------------------------------------------------- small-batch scoring ----
+// model mi's results are written: publish done[mi] = epoch to the host
+// (system-scope release first, so the results and the list bits -- coherent
+// host memory -- are visible before the flag)
+__device__ __forceinline__ void signal_done(const ScoreOut& out, uint32_t mi) {
+    if (out.done == nullptr) return;
+    __threadfence_system();
+    __hip_atomic_store(out.done + mi, out.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // LO trials, refits and reconciliations score a handful of models, so the
 // per-workgroup sequential chain of the batch scorers (~90 us at N = 10 000)
 // is the whole cost.  Here every (model, feature) pair is evaluated in
@@ -2419,6 +2428,7 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_chain(DevProblem p, const typ
             out.tot[mi] = tot;
             if (out.fl) out.fl[mi] = fcnt[0];
             if (out.lfl) out.lfl[mi] = fcnt[1];
+            signal_done(out, mi);
         }
     }
 }
@@ -2503,8 +2513,9 @@ template <int KIND>
 __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
                                                         const uint8_t* __restrict__ inc, double T0, double T1,
                                                         uint32_t pad0, uint32_t nchunks, ListBits lb, FlagBand fbm,
-                                                        FlagBand fbl, ArgModels am) {
-    const uint32_t mi = blockIdx.y;
+                                                        FlagBand fbl, ArgModels am, uint32_t mi_base) {
+    const uint32_t ml = blockIdx.y;                           // the model in this launch's part
+    const uint32_t mi = mi_base + ml;                         // ... and in the whole batch
     const uint32_t j = blockIdx.x * (kLrThreads / 64) + (threadIdx.x >> 6);      // chunk
     const int lane = threadIdx.x & 63;
     const bool jin = j < nchunks;                             // the last workgroup's tail
@@ -2518,10 +2529,10 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
     __shared__ ValueConst vc_sh;
     if (threadIdx.x == 0) {
         if constexpr (KIND <= 2) {
-            m_sh = mi < am.n ? am.m[mi] : models[mi];
+            m_sh = ml < am.n ? am.m[ml] : models[ml];
             vc_sh = value_const(m_sh, KIND == 1, KIND == 2);
         } else {
-            m_sh = models[mi];
+            m_sh = models[ml];
         }
     }
     __syncthreads();
@@ -2605,6 +2616,7 @@ __device__ __forceinline__ void lo_fold_model(const DevProblem& p, uint32_t mi, 
         out.tot[mi] = wtt;
         if (out.fl) out.fl[mi] = fsum[0];
         if (out.lfl) out.lfl[mi] = fsum[1];
+        signal_done(out, mi);
     }
 }
 
@@ -4077,11 +4089,14 @@ bool lo_argmodels() {
     return !(e && e[0] == '0');
 }
 
-// GCR_LO_FUSED=0: the split scorer as two launches (k_lo_resid + k_lo_fold)
-// instead of k_lo_split (read per launch)
+// GCR_LO_FUSED=1: the split scorer as ONE launch (k_lo_split) instead of
+// k_lo_resid + k_lo_fold -- measured slower on MI355X (M2 LO trial scoring
+// 0.16 -> 0.23 ms per call, gpurun_out session r5_s6: the fold's 138 KB of
+// LDS makes every residual workgroup a whole-CU 1024-thread workgroup, and
+// each one's arrival needs an L2 writeback), kept as an A/B (read per launch)
 bool lo_fused() {
     const char* e = getenv("GCR_LO_FUSED");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 // k_lo_split's chunks per wave: every workgroup takes a whole CU (the fold's
@@ -4140,7 +4155,7 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
                                    nchunks, cpw, lb, flag_band(T), flag_band(lb.T), am, out);
             } else {
                 hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, mp, inc, T[0], T[1],
-                                   pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am);
+                                   pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am, 0u);
                 hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, p, inc, pad0, nchunks,
                                    out);
             }
@@ -4157,6 +4172,45 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
         case 2: go(std::integral_constant<int, 2>{}); break;
         case 3: go(std::integral_constant<int, 3>{}); break;
         default: go(std::integral_constant<int, 4>{}); break;
+    }
+    return hipGetLastError();
+}
+
+bool score_small_splits(const DevProblem& p, uint32_t nm_total) {
+    const uint32_t ntot = (uint32_t)small_score_pairs(p);
+    return p.solver <= 2 && lo_split() && lo_fold_wide() && !lo_fused() && probe_bits() == 0 && ntot > 0 &&
+           ntot <= 2 * kLoBlock && nm_total <= p.lo.cap_models && p.lo.vals != nullptr && p.lo.meta != nullptr;
+}
+
+hipError_t launch_score_small_part(const DevProblem& p, const double T[2], const void* models, uint32_t mi_base,
+                                   uint32_t nm, int stage, uint32_t nm_fold, const ScoreOut& out, hipStream_t stream,
+                                   const ListBits* lists, const void* hmodels) {
+    if (!score_small_splits(p, std::max(mi_base + nm, nm_fold))) return hipErrorInvalidValue;
+    const ListBits lb = lists ? *lists : ListBits{{0.0, 0.0}, 0, 0.0, nullptr, nullptr};
+    const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
+    const uint32_t nchunks = (uint32_t)small_score_pairs(p) / 64;
+    auto go = [&](auto ktag) {
+        constexpr int KIND = decltype(ktag)::value;
+        using M = typename ModelOf<KIND>::type;
+        if ((stage & 1) && nm > 0) {
+            const dim3 grid((nchunks + kLrThreads / 64 - 1) / (kLrThreads / 64), nm);
+            ArgModels am;
+            am.n = 0;
+            if (hmodels != nullptr && nm <= kArgModels && lo_argmodels()) {
+                std::memcpy(am.m, hmodels, (size_t)nm * sizeof(RectModel));
+                am.n = nm;
+            }
+            hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, static_cast<const M*>(models),
+                               nullptr, T[0], T[1], pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am, mi_base);
+        }
+        if ((stage & 2) && nm_fold > 0)
+            hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm_fold), dim3(kLoThreads), 0, stream, p, nullptr, pad0,
+                               nchunks, out);
+    };
+    switch (p.solver) {
+        case 0: go(std::integral_constant<int, 0>{}); break;
+        case 1: go(std::integral_constant<int, 1>{}); break;
+        default: go(std::integral_constant<int, 2>{}); break;
     }
     return hipGetLastError();
 }

@@ -26,7 +26,13 @@ __global__ void k_spin(long long cycles, volatile unsigned* flag, unsigned epoch
     }
 }
 
-int main() {
+int main(int argc, char** argv) {
+    // argv[1] == "spin": hipSetDeviceFlags(hipDeviceScheduleSpin) before any
+    // other HIP call (HIP's host wait policy); ROC_ACTIVE_WAIT_TIMEOUT in the
+    // environment sets the runtime's active-wait window instead
+    if (argc > 1 && argv[1][0] == 's') CK(hipSetDeviceFlags(hipDeviceScheduleSpin));
+    if (argc > 1 && argv[1][0] == 'y') CK(hipSetDeviceFlags(hipDeviceScheduleYield));
+    if (argc > 1 && argv[1][0] == 'b') CK(hipSetDeviceFlags(hipDeviceScheduleBlockingSync));
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     unsigned* flag = nullptr;

@@ -91,6 +91,7 @@ __device__ __forceinline__ void op1(double& d, float& f, unsigned& u, unsigned l
 constexpr int kMixOps[][2] = {{ADD_F64, 3}, {MUL_F64, 2}, {FMA_F64, 1}, {ADD_U32, 2}, {CNDMASK, 2},
                               {MOV_B32, 1}, {XOR_B32, 1}};
 constexpr int kMixVariant = 99;
+constexpr int kPairBase = 1000;      // OP + kPairBase: OP interleaved with v_add_f64
 
 template <int OP>
 __global__ void k_issue(const double* in, double* out, Stamp* st) {
@@ -113,7 +114,20 @@ __global__ void k_issue(const double* in, double* out, Stamp* st) {
     const unsigned long long c0 = clock64();
 #pragma unroll 1
     for (int it = 0; it < kIters; ++it) {
-        if constexpr (OP == kMixVariant) {
+        if constexpr (OP >= kPairBase) {
+            // OP - kPairBase alternating with v_add_f64 on the other chains:
+            // X(0) A(1) X(2) A(3) .. then A(0) X(1) A(2) X(3) .. (16 X, 16 A)
+#pragma unroll
+            for (int i = 0; i < kChains; i += 2) {
+                op1<OP - kPairBase>(d[i], f[i], u[i], q[i], dc, fc, t, sm);
+                op1<ADD_F64>(d[i + 1], f[i + 1], u[i + 1], q[i + 1], dc, fc, t, sm);
+            }
+#pragma unroll
+            for (int i = 0; i < kChains; i += 2) {
+                op1<ADD_F64>(d[i], f[i], u[i], q[i], dc, fc, t, sm);
+                op1<OP - kPairBase>(d[i + 1], f[i + 1], u[i + 1], q[i + 1], dc, fc, t, sm);
+            }
+        } else if constexpr (OP == kMixVariant) {
             // the mix's instructions in a fixed order, each over all chains
             // (consecutive instructions independent, as in the single-class runs)
 #define GCR_MIX1(O)                                                                    \
@@ -164,11 +178,13 @@ Cost run(const double* in, double* out, Stamp* st, int wps, int ninst, bool prin
     c.mhz = smt / (srt * 10.0) * 1000.0;
     if (print)
         printf("%-20s waves/SIMD %d: %7.3f ns (%6.2f s_memtime cycles) per instruction per SIMD; s_memtime %6.0f MHz\n",
-               OP == kMixVariant ? "MIX" : kName[OP], wps, c.ns, c.cyc, c.mhz);
+               OP == kMixVariant ? "MIX" : (OP >= kPairBase ? "PAIR" : kName[OP % kPairBase]), wps, c.ns, c.cyc,
+               c.mhz);
     return c;
 }
 
-Cost g_cost[NOP_OPS];
+Cost g_cost[NOP_OPS];       // alone, 4 waves per SIMD
+Cost g_marg[NOP_OPS];       // marginal cost inside a stream of v_add_f64 (4 waves per SIMD)
 
 template <int OP>
 void run_all(const double* in, double* out, Stamp* st) {
@@ -176,6 +192,15 @@ void run_all(const double* in, double* out, Stamp* st) {
         const Cost c = run<OP>(in, out, st, wps, 1, true);
         if (wps == 4) g_cost[OP] = c;
     }
+    // marginal: (time of 16 X + 16 v_add_f64) - (time of 16 v_add_f64), per X
+    const Cost p = run<OP + kPairBase>(in, out, st, 4, 2, false);
+    Cost m;
+    m.ns = 2.0 * p.ns - g_cost[ADD_F64].ns;
+    m.cyc = 2.0 * p.cyc - g_cost[ADD_F64].cyc;
+    m.mhz = p.mhz;
+    g_marg[OP] = m;
+    printf("%-20s marginal in a v_add_f64 stream: %7.3f ns (%6.2f s_memtime cycles) per instruction per SIMD\n",
+           kName[OP], m.ns, m.cyc);
     if constexpr (OP + 1 < NOP_OPS) run_all<OP + 1>(in, out, st);
 }
 
@@ -199,8 +224,17 @@ int main() {
         pred_cyc += oc[1] * g_cost[oc[0]].cyc;
     }
     const Cost m = run<kMixVariant>(in, out, st, 4, n, true);
-    printf("MIX model: predicted %.3f ns per mix iteration per SIMD, measured %.3f (residual %+.1f %%); "
+    printf("MIX model (alone costs): predicted %.3f ns per mix iteration per SIMD, measured %.3f (residual %+.1f %%); "
            "s_memtime cycles predicted %.2f measured %.2f\n",
            pred_ns, m.ns * n, 100.0 * (pred_ns - m.ns * n) / (m.ns * n), pred_cyc, m.cyc * n);
+    double mp_ns = 0.0;
+    for (const auto& oc : kMixOps) mp_ns += oc[1] * g_marg[oc[0]].ns;
+    printf("MIX model (marginal costs): predicted %.3f ns per mix iteration per SIMD, measured %.3f (residual %+.1f %%)\n",
+           mp_ns, m.ns * n, 100.0 * (mp_ns - m.ns * n) / (m.ns * n));
+    // machine-readable: per class alone and marginal ns
+    printf("JSON {");
+    for (int i = 0; i < NOP_OPS; ++i)
+        printf("%s\"%s\": [%.4f, %.4f]", i ? ", " : "", kName[i], g_cost[i].ns, g_marg[i].ns);
+    printf(", \"MIX\": [%.4f, %.4f, %.4f]}\n", m.ns * n, pred_ns, mp_ns);
     return 0;
 }
