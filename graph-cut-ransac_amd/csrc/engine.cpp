@@ -263,6 +263,7 @@ struct Workspace {
     DevBuf<double> lo_vals;             // launch_score_small's split scorer (DevProblem::lo)
     DevBuf<uint32_t> lo_meta;
     DevBuf<uint32_t> lo_arrive;         // ... k_lo_split's per-model arrival counters (zeroed once)
+    DevBuf<double> lo_psum;             // ... per chunk inlier value sums (k_lo_approx)
     PinBuf<uint64_t> h_mbits;           // launch_score_small: MSAC inlier ballots (ListBits.mbits)
     PinBuf<uint64_t> h_lbits;           // launch_score_small: LO list bits (ListBits), written by
                                         // the kernel straight into this mapped pinned buffer
@@ -326,11 +327,18 @@ struct Workspace {
     // flags instead of the stream's end-of-kernel signal (~5 us sooner)
     PinBuf<uint32_t> lo_done;
     uint32_t done_epoch = 0;
+    // LO with approximate trial scores: the exact fold of a round's winner
+    // (its results and completion flag), launched behind the round
+    ScoreBufs lo_wb;
+    PinBuf<uint32_t> lo_wdone;
+    uint32_t wdone_epoch = 0;
     Workspace() {
         lo_sb.hblk.coherent = true;
         h_lbits.coherent = true;
         h_mbits.coherent = true;
         lo_done.coherent = true;
+        lo_wb.hblk.coherent = true;
+        lo_wdone.coherent = true;
     }
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
@@ -1211,11 +1219,12 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     if (spairs > 0 && spairs <= kSplitMaxPairs) {
         P->w->lo_vals.ensure(spairs * kSplitModels);
         P->w->lo_meta.ensure(spairs / 64 * kSplitModels);
+        P->w->lo_psum.ensure(spairs / 64 * kSplitModels);
         if (!P->w->lo_arrive.p) {
             P->w->lo_arrive.ensure(kSplitModels);
             HIPC(hipMemsetAsync(P->w->lo_arrive.p, 0, kSplitModels * sizeof(uint32_t), ctx->stream));
         }
-        P->dp.lo = SmallScratch{P->w->lo_vals.p, P->w->lo_meta.p, kSplitModels, P->w->lo_arrive.p};
+        P->dp.lo = SmallScratch{P->w->lo_vals.p, P->w->lo_meta.p, kSplitModels, P->w->lo_arrive.p, P->w->lo_psum.p};
     }
     HIPC(hipMemcpyAsync(P->w->feat.p, hst, total * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     HIPC(hipStreamSynchronize(ctx->stream));
@@ -2418,7 +2427,7 @@ private:
     int lo_row_set_ = 0;
     Model lo_row_model_{};
     bool lo_lists_from_bits_ = false;     // the current LO winner's lists came from its scoring launch
-    std::vector<uint32_t> lo_msac_lists_[2];   // its MSAC lists (ListBits.mbits)
+    std::vector<uint64_t> lo_msac_row_;   // its MSAC list bits (ListBits.mbits row)
 
     bool valid_model(const Model& m) const { return Tr::valid(P_->solver, m); }
 
@@ -3066,6 +3075,15 @@ private:
     scored:
         lot("waited");
         st_.launches += 1;
+        finish_small(models, n, out, raw_n, decs, lists);
+        lot("finished");
+        return lists;
+    }
+
+    // the scores of a small-scorer launch (lo_sb): finished, flagged
+    // decisions and models exact.h does not cover recounted on the host
+    // (sm_mbad_), flagged list decisions marked (sm_lbad_)
+    void finish_small(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n, const Model* decs, bool lists) {
         sm_mbad_.assign(n, 0);
         sm_lbad_.assign(n, 0);
         for (uint32_t i = 0; i < n; ++i) {
@@ -3087,8 +3105,144 @@ private:
                 if (lists && (P_->w->lo_sb.hlfl.p[i] != 0 || bad)) sm_lbad_[i] = 1;
             }
         }
+    }
+
+    // ---- LO trials with approximate scores (GCR_LO_APPROX=0: off) --------
+    // The split scorer's residual launch plus k_lo_approx instead of the
+    // exact fold: exact counts, class sums in a tree order.  A trial
+    // comparison is decided on them when the bound below cannot change it;
+    // a round with one that can is refolded exactly.  The round's winner is
+    // folded exactly behind the round (launch_lo_fold_slots into lo_wb) and
+    // its exact score replaces the approximate one before the next round's
+    // comparisons -- by then the stream has run the fold.
+    // GCR_LO_APPROX: 0 off, 2 every round refolded exactly (tests)
+    static int lo_approx_mode() {
+        const char* e = getenv("GCR_LO_APPROX");             // read per call
+        return !e ? 1 : e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1;
+    }
+    bool approx_ok(uint32_t n) const {
+        if constexpr (!kRect) {
+            (void)n;
+            return false;
+        } else {
+            return n <= kSmallScore && n <= kArgModels && small_score_on() && zerocopy_on() && done_wait_on() &&
+                   lo_approx_mode() != 0 && P_->dp.lo.psum != nullptr && score_small_splits(P_->dp, n);
+        }
+    }
+    // the list bits of a small-scorer launch (ListReq), in the mapped pinned
+    // buffers sized once for the largest launch
+    ListBits list_bits(const ListReq& req) {
+        const size_t pairs = small_score_pairs(P_->dp);
+        ListBits lb{{req.T[0], req.T[1]}, req.rule, prm_.spatial_coherence_weight, nullptr, nullptr};
+        P_->w->h_lbits.ensure(pairs * kSmallScore / 64);
+        lb.bits = dev_view(P_->w->h_lbits.p);
+        if (req.msac) {
+            P_->w->h_mbits.ensure(pairs * kSmallScore / 64);
+            lb.mbits = dev_view(P_->w->h_mbits.p);
+        }
+        return lb;
+    }
+    // a bound on |approximate - exact| of a finished score (value arithmetic):
+    // each class sum within (n + 64) u |v| of the other order's (both within
+    // (n - 1) u sum|a| of the real sum, sum|a| = |real sum| for non-positive
+    // values), the total likewise, and finish()'s rounding on both sides;
+    // doubled
+    double approx_err(const HScore& s, double v0, double v1, double tot) const {
+        constexpr double u = 0x1p-53;
+        const double v[2] = {v0, v1};
+        double e = 0.0, b = std::fabs(tot);
+        double esum = 0.0;
+        for (int c = 0; c < K_; ++c) {
+            const double ec = 2.0 * ((double)s.n[c] + 64.0) * u * std::fabs(v[c]);
+            const double g = 1.0 + 1.0 / Tm_[c];
+            e += ec * g;
+            esum += std::fabs(v[c]);
+            b += (std::fabs(v[c]) + ec) * g + (double)s.n[c];
+        }
+        const double etot = 2.0 * ((double)(s.n[0] + s.n[1]) + 128.0) * u * esum + 2.0 * u * std::fabs(tot);
+        e += etot;
+        b += etot;
+        return 2.0 * (e + 16.0 * u * b) + 0x1p-1000;
+    }
+    // score the trials approximately: out/err (err 0: exact -- a zero score,
+    // or recounted on the host); returns whether list bits came back
+    bool score_models_approx(const Model* models, uint32_t n, HScore* out, double* err, uint32_t* raw_n,
+                             const ListReq& req) {
+        auto& hm = Tr::hlomodels(P_->w);
+        hm.ensure(kSmallScore);
+        std::memcpy(hm.p, models, n * sizeof(Model));
+        P_->w->lo_sb.ensure(n);
+        const bool lists = !(req.rule == 2 && use_graph());
+        const ListBits lb = lists ? list_bits(req) : ListBits{{0.0, 0.0}, 0, 0.0, nullptr, nullptr};
+        ScoreOut so = P_->w->lo_sb.host_dev();
+        P_->w->lo_done.ensure(kSmallScore);
+        so.done = dev_view(P_->w->lo_done.p);
+        so.epoch = ++P_->w->done_epoch;
+        if (so.epoch == 0) so.epoch = ++P_->w->done_epoch;
+        lot("setup");
+        HIPC(launch_score_small_part(P_->dp, Tm_, dev_view(hm.p), 0, n, 1 | 4, n, so, s_, lists ? &lb : nullptr,
+                                     models));
+        lot("launched");
+        wait_done(P_->w->lo_done.p, n, so.epoch);
+        lot("waited");
+        st_.launches += 1;
+        finish_small(models, n, out, raw_n, nullptr, lists);
+        for (uint32_t i = 0; i < n; ++i) {
+            err[i] = 0.0;
+            if (sm_mbad_[i] || out[i].total == 0) continue;        // recounted, or a zero score
+            err[i] = approx_err(out[i], P_->w->lo_sb.hv0.p[i], P_->w->lo_sb.hv1.p[i], P_->w->lo_sb.htot.p[i]);
+        }
         lot("finished");
         return lists;
+    }
+    // the exact scores of the last approximate launch's n models (a round
+    // with an undecided comparison), into out
+    void refold_exact(const Model* models, uint32_t n, HScore* out, uint32_t* raw_n, bool lists) {
+        ScoreOut so = P_->w->lo_sb.host_dev();
+        so.done = dev_view(P_->w->lo_done.p);
+        so.epoch = ++P_->w->done_epoch;
+        if (so.epoch == 0) so.epoch = ++P_->w->done_epoch;
+        HIPC(launch_lo_fold_slots(P_->dp, 0, n, 0, so, s_));
+        wait_done(P_->w->lo_done.p, n, so.epoch);
+        st_.launches += 1;
+        ++st_.lo_refolds;
+        finish_small(models, n, out, raw_n, nullptr, lists);
+    }
+    // the exact fold of model q of the last approximate launch, behind it
+    uint32_t win_epoch_ = 0;
+    void launch_win_fold(uint32_t q) {
+        P_->w->lo_wb.ensure(1);
+        P_->w->lo_wdone.ensure(1);
+        ScoreOut so = P_->w->lo_wb.host_dev();
+        so.done = dev_view(P_->w->lo_wdone.p);
+        so.epoch = ++P_->w->wdone_epoch;
+        if (so.epoch == 0) so.epoch = ++P_->w->wdone_epoch;
+        win_epoch_ = so.epoch;
+        HIPC(launch_lo_fold_slots(P_->dp, q, 1, 0, so, s_));
+    }
+    HScore win_exact() {
+        wait_done(P_->w->lo_wdone.p, 1, win_epoch_);
+        const uint32_t rn[2] = {P_->w->lo_wb.hn0.p[0], P_->w->lo_wb.hn1.p[0]};
+        return finish(rn, P_->w->lo_wb.hv0.p[0], P_->w->lo_wb.hv1.p[0], P_->w->lo_wb.htot.p[0]);
+    }
+    // score_less(a, b) with a, b within ea, eb of their exact scores and ma,
+    // mb their decision models (b: its value model too; a_self: a's as
+    // well): 1 / 0, or -1 when the bounds leave it open
+    int approx_less(const HScore& a, double ea, const Model& ma, bool a_self, const HScore& b, double eb,
+                    const Model& mb) {
+        if (ea == 0.0 && eb == 0.0) return score_less(a, [&] { return ma; }, b, [&] { return mb; }) ? 1 : 0;
+        if (a_self && std::memcmp(&ma, &mb, sizeof(Model)) == 0) {
+            // one model: equal exact scores, a near tie of score_less
+            if (exact_ && sbnd_.finite && dev_of(a) + dev_of(b) > 0.0) ++ec_.near_ties;
+            return 0;
+        }
+        double tol = 0.0;
+        if (exact_ && sbnd_.finite) tol = dev_of(a) + dev_of(b) + 64.0 * 0x1p-53 * (ea + eb);
+        const double m = (tol + ea + eb) * (1.0 + 0x1p-40);
+        const double d = b.sum - a.sum;
+        if (d > m) return 1;
+        if (-d > m) return 0;
+        return -1;
     }
 
     // GCR_DONE_WAIT=0: score_models waits on the stream instead of the
@@ -3143,13 +3297,18 @@ private:
         for (int c = 0; c < 2; ++c) {
             lists[c].clear();
             if (c >= K_) continue;
-            const size_t base = c ? pad0 : 0;
-            for (size_t wi = 0; wi < (N_[c] + 63) / 64; ++wi) {
-                uint64_t b = w[(base >> 6) + wi];
+            const uint64_t* cw = w + ((c ? pad0 : 0) >> 6);
+            const size_t nw = (N_[c] + 63) / 64;
+            size_t n = 0;
+            for (size_t wi = 0; wi < nw; ++wi) n += (size_t)__builtin_popcountll(cw[wi]);
+            lists[c].resize(n);
+            uint32_t* o = lists[c].data();
+            for (size_t wi = 0; wi < nw; ++wi) {
+                uint64_t b = cw[wi];
+                const uint32_t base = (uint32_t)(wi * 64);
                 while (b) {
-                    const int t = __builtin_ctzll(b);
+                    *o++ = base + (uint32_t)__builtin_ctzll(b);
                     b &= b - 1;
-                    lists[c].push_back((uint32_t)(wi * 64 + t));
                 }
             }
         }
@@ -3238,7 +3397,10 @@ private:
         std::vector<char> trial_ok;
         std::vector<Model> trial_models;
         std::vector<HScore> trial_scores;
+        std::vector<double> trial_err;        // approximate scores: their bounds (0: exact)
         std::vector<uint32_t> trial_raw;
+        bool win_pending = false;             // the last winner's exact fold is still to be read
+        bool max_self = false;                // max_score is lo_model's own value score
         const uint64_t T = prm_.max_local_optimization_number;
         // the LO lists (threshold (1.5 thr)^2, labeling rule) of the round's
         // winner come back with the trial scores, so the next round starts
@@ -3343,20 +3505,79 @@ private:
             st_.ms_lo_fit += ms_since(tp);
             tp = Clock::now();
             if (!trial_models.empty()) {
-                trial_scores.resize(trial_models.size());
-                trial_raw.resize(2 * trial_models.size());
-                const bool bits = score_models(trial_models.data(), (uint32_t)trial_models.size(),
-                                               trial_scores.data(), trial_raw.data(), &lreq, nullptr,
-                                               (uint32_t)first_half);
-                st_.lo_models += trial_models.size();
+                const uint32_t nt = (uint32_t)trial_models.size();
+                trial_scores.resize(nt);
+                trial_raw.resize(2 * nt);
+                const bool apx = !pipe && approx_ok(nt);
+                bool bits;
+                if (apx) {
+                    trial_err.resize(nt);
+                    bits = score_models_approx(trial_models.data(), nt, trial_scores.data(), trial_err.data(),
+                                               trial_raw.data(), lreq);
+                } else {
+                    bits = score_models(trial_models.data(), nt, trial_scores.data(), trial_raw.data(), &lreq,
+                                        nullptr, (uint32_t)first_half);
+                }
+                // the previous round's winner: its exact fold ran before this
+                // round's launches on the stream
+                if (win_pending) {
+                    max_score = win_exact();
+                    win_pending = false;
+                }
+                st_.lo_models += nt;
                 st_.ms_lo_score += ms_since(tp);
                 size_t win = 0;
-                for (size_t q = 0; q < trial_models.size(); ++q) {
+                bool decided = false;
+                if (apx) {
+                    // the sequential comparisons on the approximate scores;
+                    // one the bounds leave open: the round folded exactly
+                    const uint64_t nt0 = ec_.near_ties, nf0 = ec_.near_flips;
+                    HScore ms = max_score;
+                    double me = 0.0;
+                    Model mm = lo_model;
+                    bool mself = max_self;
+                    long w = -1;
+                    decided = true;
+                    for (uint32_t q = 0; q < nt; ++q) {
+                        const int d = approx_less(ms, me, mm, mself, trial_scores[q], trial_err[q], trial_models[q]);
+                        if (d < 0) {
+                            decided = false;
+                            break;
+                        }
+                        if (d) {
+                            w = (long)q;
+                            ms = trial_scores[q];
+                            me = trial_err[q];
+                            mm = trial_models[q];
+                            mself = true;
+                        }
+                    }
+                    if (lo_approx_mode() == 2) decided = false;
+                    if (decided && w >= 0) {
+                        updated = true;
+                        win = (size_t)w;
+                        max_score = ms;
+                        max_self = true;
+                        lo_model = mm;
+                        lo_buf = Buffer{true, mm, {trial_raw[2 * win], trial_raw[2 * win + 1]}};
+                        if (me > 0.0) {
+                            launch_win_fold((uint32_t)win);
+                            win_pending = true;
+                        }
+                    }
+                    if (!decided) {
+                        ec_.near_ties = nt0;
+                        ec_.near_flips = nf0;
+                        refold_exact(trial_models.data(), nt, trial_scores.data(), trial_raw.data(), bits);
+                    }
+                }
+                for (size_t q = 0; !decided && q < nt; ++q) {
                     if (score_less(max_score, [&] { return lo_model; }, trial_scores[q],
                                    [&] { return trial_models[q]; })) {
                         updated = true;
                         win = q;
                         max_score = trial_scores[q];
+                        max_self = true;
                         lo_model = trial_models[q];
                         lo_buf = Buffer{true, trial_models[q], {trial_raw[2 * q], trial_raw[2 * q + 1]}};
                     }
@@ -3369,12 +3590,18 @@ private:
                         list_of((uint32_t)win, inl);
                         have_inl = true;
                     }
-                    if (lo_lists_from_bits_) list_of((uint32_t)win, lo_msac_lists_, true);
+                    // the MSAC lists are decoded only if the LO result is adopted
+                    if (lo_lists_from_bits_) {
+                        const size_t rw = small_score_pairs(P_->dp) / 64;
+                        const uint64_t* src = P_->w->h_mbits.p + (size_t)win * rw;
+                        lo_msac_row_.assign(src, src + rw);
+                    }
                 }
             }
             lot("picked");
             if (!updated) break;
         }
+        if (win_pending) max_score = win_exact();
         if (g_lo_trace && !t_lot.empty()) {
             std::string line = "gcr LO:";
             const auto b = t_lot.front().second;
@@ -3392,7 +3619,7 @@ private:
             best_model_ = lo_model;
             best_val_ = lo_model;
             sfb_buf = lo_buf;
-            // lo_msac_lists_ holds lo_model's MSAC lists from its own
+            // lo_msac_row_ holds lo_model's MSAC list bits from its own
             // scoring launch (the round that adopted it; later rounds only
             // score other models)
             lo_cache_.valid = lo_lists_from_bits_;
@@ -3401,8 +3628,7 @@ private:
                 lo_cache_.score = max_score;
                 lo_cache_.raw[0] = lo_buf.n[0];
                 lo_cache_.raw[1] = lo_buf.n[1];
-                lo_cache_.lists[0].swap(lo_msac_lists_[0]);
-                lo_cache_.lists[1].swap(lo_msac_lists_[1]);
+                decode_lists(lo_msac_row_.data(), 0, lo_cache_.lists);
             }
             return true;
         }

@@ -57,6 +57,7 @@ struct SmallScratch {
     uint32_t* meta = nullptr;
     uint32_t cap_models = 0;
     uint32_t* arrive = nullptr;     // per model: k_lo_split's arrival counter (zero between launches)
+    double* psum = nullptr;         // per chunk: its inlier values' sum in any order (k_lo_approx), optional
 };
 
 struct DevProblem {
@@ -313,11 +314,17 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
 // The split scorer in parts (LO trials scored while the rest are still being
 // fitted): stage 1 = the residual launch of models [mi_base, mi_base + nm)
 // (`models` / `hmodels` point at the part's first model); stage 2 = the fold
-// of models [0, nm_fold).  Only where score_small_splits() holds.
+// of models [0, nm_fold); stage 4 (instead of 2, p.lo.psum set) = their
+// approximate scores (k_lo_approx: exact counts and flag counts, class sums
+// in a tree order).  Only where score_small_splits() holds.
 bool score_small_splits(const DevProblem& p, uint32_t nm_total);
 hipError_t launch_score_small_part(const DevProblem& p, const double T[2], const void* models, uint32_t mi_base,
                                    uint32_t nm, int stage, uint32_t nm_fold, const ScoreOut& out, hipStream_t stream,
                                    const ListBits* lists, const void* hmodels);
+// the exact fold (k_lo_fold) of models [src, src + nm) of the last stage-1
+// launch into slots [slot, slot + nm) of `out`
+hipError_t launch_lo_fold_slots(const DevProblem& p, uint32_t src, uint32_t nm, uint32_t slot, const ScoreOut& out,
+                                hipStream_t stream);
 
 // Per-feature inlier mask of one model for class `cls`: bit 0 the decision,
 // bit 1 set when the pair's twin r^2 lies in the flag band of T (exact.h:

@@ -2487,6 +2487,13 @@ __device__ __forceinline__ void lo_resid_chunk(const DevProblem& p, const typena
         nfm = (uint32_t)__builtin_popcountll(__ballot(ev && in_flag_band(r2, fbm.mid[cls], fbm.half[cls])));
         nfl = (uint32_t)__builtin_popcountll(__ballot(ev && lb.bits != nullptr && in_flag_band(r2, fbl.mid[cls], fbl.half[cls])));
     }
+    if (p.lo.psum != nullptr) {
+        // the chunk's inlier values summed in any order (k_lo_approx)
+        double ps = inl ? -r2 : 0.0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) ps += __shfl_xor(ps, d);
+        if (lane == 0) p.lo.psum[wi] = ps;
+    }
     if (lane == 0) {
         if (lb.bits != nullptr) lb.bits[wi] = lbw;
         if (lb.mbits != nullptr) lb.mbits[wi] = w;
@@ -2544,10 +2551,11 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
 // The fold of one model's compacted chunks (k_lo_fold, and the last
 // workgroup of a model in k_lo_split): scan the chunk counts, gather the
 // chunks in feature order into LDS (all of a wave's reads in flight
-// together) and fold them (fold_exact_chains).  1024 threads.
+// together) and fold them (fold_exact_chains).  1024 threads.  Results into
+// slot oi of `out`.
 template <int KIND>
 __device__ __forceinline__ void lo_fold_model(const DevProblem& p, uint32_t mi, uint32_t pad0, uint32_t nchunks,
-                                              const ScoreOut& out) {
+                                              const ScoreOut& out, uint32_t oi) {
     __shared__ double cball[2 * kLoBlock];
     __shared__ uint32_t coff[2 * kLoChunks + 1];
     __shared__ uint32_t wtot[kLoThreads / 64];
@@ -2609,25 +2617,99 @@ __device__ __forceinline__ void lo_fold_model(const DevProblem& p, uint32_t mi, 
         wcc = wtt = r1[0];
     }
     if (t == 0) {
-        out.n0[mi] = cnt0;
-        out.n1[mi] = cntall - cnt0;
-        out.v0[mi] = KIND == 2 ? whold : wcc;
-        out.v1[mi] = KIND == 2 ? wcc : 0.0;
-        out.tot[mi] = wtt;
-        if (out.fl) out.fl[mi] = fsum[0];
-        if (out.lfl) out.lfl[mi] = fsum[1];
+        out.n0[oi] = cnt0;
+        out.n1[oi] = cntall - cnt0;
+        out.v0[oi] = KIND == 2 ? whold : wcc;
+        out.v1[oi] = KIND == 2 ? wcc : 0.0;
+        out.tot[oi] = wtt;
+        if (out.fl) out.fl[oi] = fsum[0];
+        if (out.lfl) out.lfl[oi] = fsum[1];
+        signal_done(out, oi);
+    }
+}
+
+// models [src, src + gridDim.x) into slots [slot, slot + gridDim.x); a dead
+// slot's chunks hold no inliers
+template <int KIND>
+__global__ __launch_bounds__(kLoThreads) void k_lo_fold(DevProblem p, uint32_t pad0, uint32_t nchunks, ScoreOut out,
+                                                       uint32_t src, uint32_t slot) {
+    lo_fold_model<KIND>(p, src + blockIdx.x, pad0, nchunks, out, slot + blockIdx.x);
+}
+
+// The approximate scores of k_lo_resid's models (blockIdx.x) from its chunk
+// partial sums (p.lo.psum): exact counts and flag counts, class sums in a
+// fixed tree order instead of the reference's sequential one.  The host
+// bounds the difference (both orders sum the same non-positive values, so
+// each is within (n - 1) u sum|a| of the real sum) and decides a comparison
+// with them only when the bounds cannot change it; the winner's exact sums
+// follow from k_lo_fold.
+constexpr int kLaThreads = 256;
+template <int KIND>
+__global__ __launch_bounds__(kLaThreads) void k_lo_approx(DevProblem p, uint32_t pad0, uint32_t nchunks, ScoreOut out) {
+    const uint32_t mi = blockIdx.x;
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+    const uint32_t c1 = pad0 / 64u;                           // the first class-1 chunk
+    uint32_t n0 = 0, n1 = 0, fm = 0, fl = 0;
+    double s0 = 0.0, s1 = 0.0;
+    for (uint32_t j = (uint32_t)t; j < nchunks; j += kLaThreads) {
+        const size_t wi = (size_t)mi * nchunks + j;
+        const uint32_t mt = p.lo.meta[wi];
+        const double ps = p.lo.psum[wi];
+        if (j < c1) {
+            n0 += mt & 0xffu;
+            s0 += ps;
+        } else {
+            n1 += mt & 0xffu;
+            s1 += ps;
+        }
+        fm += mt >> 8 & 0xffu;
+        fl += mt >> 16 & 0xffu;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        n0 += (uint32_t)__shfl_xor((int)n0, d);
+        n1 += (uint32_t)__shfl_xor((int)n1, d);
+        fm += (uint32_t)__shfl_xor((int)fm, d);
+        fl += (uint32_t)__shfl_xor((int)fl, d);
+        s0 += __shfl_xor(s0, d);
+        s1 += __shfl_xor(s1, d);
+    }
+    __shared__ uint32_t cn[4][kLaThreads / 64];
+    __shared__ double cs[2][kLaThreads / 64];
+    if (lane == 0) {
+        cn[0][wave] = n0;
+        cn[1][wave] = n1;
+        cn[2][wave] = fm;
+        cn[3][wave] = fl;
+        cs[0][wave] = s0;
+        cs[1][wave] = s1;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t a0 = 0, a1 = 0, af = 0, al = 0;
+        double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+        for (int w = 0; w < kLaThreads / 64; ++w) {
+            a0 += cn[0][w];
+            a1 += cn[1][w];
+            af += cn[2][w];
+            al += cn[3][w];
+            v0 += cs[0][w];
+            v1 += cs[1][w];
+        }
+        out.n0[mi] = a0;
+        out.n1[mi] = a1;
+        out.v0[mi] = v0;
+        out.v1[mi] = KIND == 2 ? v1 : 0.0;
+        out.tot[mi] = KIND == 2 ? v0 + v1 : v0;
+        if (out.fl) out.fl[mi] = af;
+        if (out.lfl) out.lfl[mi] = al;
         signal_done(out, mi);
     }
 }
 
-template <int KIND>
-__global__ __launch_bounds__(kLoThreads) void k_lo_fold(DevProblem p, const uint8_t* __restrict__ inc, uint32_t pad0,
-                                                       uint32_t nchunks, ScoreOut out) {
-    (void)inc;                                               // a dead slot's chunks hold no inliers
-    lo_fold_model<KIND>(p, blockIdx.x, pad0, nchunks, out);
-}
-
-// The split scorer in ONE launch (round 5, the default): 1024-thread
+// The split scorer in ONE launch (GCR_LO_FUSED=1; measured slower than the
+// two launches on MI355X, see launch_score_small): 1024-thread
 // workgroups, blockIdx.y the model, each workgroup evaluating per wave
 // `cpw` chunks of the model (k_lo_resid's work), then counting itself done on
 // the model's arrival counter; the model's last workgroup to arrive folds
@@ -2681,7 +2763,7 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_split(DevProblem p, const typ
     __syncthreads();
     if (!last_sh) return;                                    // workgroup-uniform
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    lo_fold_model<KIND>(p, mi, pad0, nchunks, out);
+    lo_fold_model<KIND>(p, mi, pad0, nchunks, out, mi);
 }
 
 // -------------------------------------------------------------- compact ----
@@ -4147,17 +4229,19 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
                 std::memcpy(am.m, hmodels, (size_t)nm * sizeof(RectModel));
                 am.n = nm;
             }
+            DevProblem q = p;
+            q.lo.psum = nullptr;
             if (lo_fused() && p.lo.arrive != nullptr) {
                 const uint32_t cpw = lo_cpw(nm, nchunks);
                 const uint32_t per = (kLoThreads / 64) * cpw;
                 const dim3 g2((nchunks + per - 1) / per, nm);
-                hipLaunchKernelGGL((k_lo_split<KIND>), g2, dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1], pad0,
+                hipLaunchKernelGGL((k_lo_split<KIND>), g2, dim3(kLoThreads), 0, stream, q, mp, inc, T[0], T[1], pad0,
                                    nchunks, cpw, lb, flag_band(T), flag_band(lb.T), am, out);
             } else {
-                hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, mp, inc, T[0], T[1],
+                hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, q, mp, inc, T[0], T[1],
                                    pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am, 0u);
-                hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, p, inc, pad0, nchunks,
-                                   out);
+                hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, q, pad0, nchunks, out,
+                                   0u, 0u);
             }
         } else if (lo_fold_wide())
             hipLaunchKernelGGL((k_lo_chain<KIND, true>), dim3(nm), dim3(kLoThreads), 0, stream, p, mp, inc, T[0], T[1],
@@ -4189,6 +4273,10 @@ hipError_t launch_score_small_part(const DevProblem& p, const double T[2], const
     const ListBits lb = lists ? *lists : ListBits{{0.0, 0.0}, 0, 0.0, nullptr, nullptr};
     const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
     const uint32_t nchunks = (uint32_t)small_score_pairs(p) / 64;
+    if ((stage & 4) && (stage & 2)) return hipErrorInvalidValue;
+    if ((stage & 4) && p.lo.psum == nullptr) return hipErrorInvalidValue;
+    DevProblem q = p;
+    if (!(stage & 4)) q.lo.psum = nullptr;                   // chunk partial sums only for k_lo_approx
     auto go = [&](auto ktag) {
         constexpr int KIND = decltype(ktag)::value;
         using M = typename ModelOf<KIND>::type;
@@ -4200,17 +4288,36 @@ hipError_t launch_score_small_part(const DevProblem& p, const double T[2], const
                 std::memcpy(am.m, hmodels, (size_t)nm * sizeof(RectModel));
                 am.n = nm;
             }
-            hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, p, static_cast<const M*>(models),
+            hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, q, static_cast<const M*>(models),
                                nullptr, T[0], T[1], pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am, mi_base);
         }
         if ((stage & 2) && nm_fold > 0)
-            hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm_fold), dim3(kLoThreads), 0, stream, p, nullptr, pad0,
-                               nchunks, out);
+            hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm_fold), dim3(kLoThreads), 0, stream, q, pad0, nchunks, out,
+                               0u, 0u);
+        if ((stage & 4) && nm_fold > 0)
+            hipLaunchKernelGGL((k_lo_approx<KIND>), dim3(nm_fold), dim3(kLaThreads), 0, stream, q, pad0, nchunks,
+                               out);
     };
     switch (p.solver) {
         case 0: go(std::integral_constant<int, 0>{}); break;
         case 1: go(std::integral_constant<int, 1>{}); break;
         default: go(std::integral_constant<int, 2>{}); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_lo_fold_slots(const DevProblem& p, uint32_t src, uint32_t nm, uint32_t slot, const ScoreOut& out,
+                                hipStream_t stream) {
+    if (nm == 0) return hipSuccess;
+    if (!score_small_splits(p, src + nm)) return hipErrorInvalidValue;
+    DevProblem q = p;
+    q.lo.psum = nullptr;
+    const uint32_t pad0 = (p.cls[0].n + 63u) & ~63u;
+    const uint32_t nchunks = (uint32_t)small_score_pairs(p) / 64;
+    switch (p.solver) {
+        case 0: hipLaunchKernelGGL((k_lo_fold<0>), dim3(nm), dim3(kLoThreads), 0, stream, q, pad0, nchunks, out, src, slot); break;
+        case 1: hipLaunchKernelGGL((k_lo_fold<1>), dim3(nm), dim3(kLoThreads), 0, stream, q, pad0, nchunks, out, src, slot); break;
+        default: hipLaunchKernelGGL((k_lo_fold<2>), dim3(nm), dim3(kLoThreads), 0, stream, q, pad0, nchunks, out, src, slot); break;
     }
     return hipGetLastError();
 }

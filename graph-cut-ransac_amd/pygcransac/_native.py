@@ -74,6 +74,7 @@ class Stats(C.Structure):
         ("ms_exact", C.c_double),
         ("near_ties", C.c_uint64),
         ("near_tie_flips", C.c_uint64),
+        ("lo_refolds", C.c_uint64),
     ]
 
     def as_dict(self):

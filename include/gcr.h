@@ -118,6 +118,9 @@ typedef struct gcr_stats {
      * than their proven bounds are compared by their glibc scores */
     uint64_t near_ties;           /* comparisons decided in glibc                   */
     uint64_t near_tie_flips;      /* ... whose outcome differs from the values'     */
+    /* LO trials are compared on approximate scores within a proven bound of
+     * the exact ones; a round the bound leaves open is folded exactly */
+    uint64_t lo_refolds;          /* LO rounds folded exactly for a comparison      */
 } gcr_stats;
 
 /* ---- context ---------------------------------------------------------- */

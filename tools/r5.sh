@@ -6,6 +6,7 @@
 #   bench  python bench.py (BENCH_ARGS)
 #   benchf bench.py --workload f
 #   stats  rocprofv3 --kernel-trace --stats of bench.py (BENCH_ARGS) into $O/stats
+#   trace  tools/lo_trace.py host timeline of the LO rounds
 #   latst  rocprofv3 --kernel-trace --stats of the latency leg only
 # Every GPU step has its own time limit; any failure ends the session.
 set -u
@@ -23,6 +24,7 @@ for s in $STEPS; do
     stats) (cd /tmp && true); export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python3 bench.py --cpu-seconds 0 ${BENCH_ARGS:-} > $O/stats.log 2>&1 || fail stats $? $O/stats.log; find $O/stats -name '*kernel_stats.csv' -exec head -20 {} \; ;;
     sync) timeout -k 10 120 tools/micro/sync_latency.bin > $O/sync.log 2>&1 || fail sync $? $O/sync.log; cat $O/sync.log ;;
     valu) timeout -k 10 200 tools/micro/valu_issue.bin > $O/valu.log 2>&1 || fail valu $? $O/valu.log; cat $O/valu.log ;;
+    trace) GCR_LO_TRACE=1 timeout -k 10 200 python -u tools/lo_trace.py ${LAT_WL:-m2} 2> $O/trace.txt > $O/trace.log || fail trace $? $O/trace.log; python3 tools/lo_trace.py --parse $O/trace.txt ;;
     latst) export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/latst -o run --output-format csv -- python3 tools/lat_seeds.py --workload ${LAT_WL:-m2} --reps 2 base: > $O/latst.log 2>&1 || fail latst $? $O/latst.log; find $O/latst -name '*kernel_stats.csv' -exec head -25 {} \; ;;
   esac
 done
