@@ -290,8 +290,11 @@ struct Workspace {
     DevBuf<QRFState> rf_qrf;            // GPU refit: fused-pass QR driver state
     PinBuf<double> rf_hpart;
     PinBuf<double> rf_htop;             // GPU refit: async upload ring
-    DevBuf<DD> rf_gram;                 // GPU refit (Gram path): per-tile double-double sums
-    PinBuf<DD> rf_hgram;                //   and their pinned host image
+    DevBuf<DD> rf_gram;                 // GPU refit (Gram path): per-tile double-double sums,
+    DevBuf<double> rf_lines;            //   the orientation inliers' lines,
+    PinBuf<DD> rf_hgout;                //   the Gram matrix (coherent pinned memory)
+    PinBuf<uint32_t> rf_gdone;          //   and its completion flag
+    uint32_t gdone_epoch = 0;
     // the next chunk of slots, generated and scored on the side stream while
     // the host replays the current one (RunnerT prefetch); swapped in whole
     DevBuf<uint8_t> pf_inc;
@@ -339,6 +342,8 @@ struct Workspace {
         lo_done.coherent = true;
         lo_wb.hblk.coherent = true;
         lo_wdone.coherent = true;
+        rf_hgout.coherent = true;
+        rf_gdone.coherent = true;
     }
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
@@ -366,9 +371,45 @@ const bool g_lo_trace = [] {
     const char* e = getenv("GCR_LO_TRACE");
     return e && e[0] == '1';
 }();
-thread_local std::vector<std::pair<const char*, Clock::time_point>> t_lot;
+thread_local std::vector<std::pair<const char*, Clock::time_point>> t_lot, t_run;
 inline void lot(const char* tag) {
     if (g_lo_trace) t_lot.emplace_back(tag, Clock::now());
+}
+// ... and of the whole run (main loop, LO, final refit): "gcr RUN:"
+inline void rlot(const char* tag) {
+    if (g_lo_trace) t_run.emplace_back(tag, Clock::now());
+}
+void lot_print(const char* label, std::vector<std::pair<const char*, Clock::time_point>>& v) {
+    if (!g_lo_trace || v.empty()) return;
+    std::string line = label;
+    const auto b = v.front().second;
+    for (const auto& e : v) {
+        char buf[64];
+        snprintf(buf, sizeof(buf), " %s %.1f", e.first, std::chrono::duration<double, std::micro>(e.second - b).count());
+        line += buf;
+    }
+    fprintf(stderr, "%s\n", line.c_str());
+    v.clear();
+}
+
+// spin until a kernel has stored `epoch` into the coherent host flag; a
+// stream that drained (or failed) without it is an error, as is 5 s without it
+void wait_flag(const uint32_t* flag, uint32_t epoch, hipStream_t s, const char* what) {
+    const auto t0 = Clock::now();
+    for (uint64_t it = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != epoch; ++it) {
+        if ((it & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == epoch) break;
+                throw std::runtime_error(std::string(what) + ": completion flag missing after the stream drained");
+            }
+            if (q != hipErrorNotReady) HIPC(q);
+            if (std::chrono::duration<double>(Clock::now() - t0).count() > 5.0)
+                throw std::runtime_error(std::string(what) + ": no completion after 5 s");
+        }
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
 }
 
 // GCR_BACKTRACE=1 (read at load): SIGABRT / SIGSEGV print the native stack
@@ -709,8 +750,9 @@ struct GpuSiftSolver final : SiftSystemSolver {
         HIPC(hipStreamSynchronize(s));          // the pinned ring must outlive its uploads
     }
     // the double-double Gram matrix of the same rows (gram.h): one kernel
-    // builds every row once and reduces it in its tile, the tiles come back
-    // through pinned memory and are added here in order
+    // builds every row once and reduces it in its tile, a second combines
+    // the tiles into the matrix, written into coherent pinned memory with a
+    // completion flag the host waits on
     bool gram(const std::vector<uint32_t>& si, const std::vector<uint32_t>& oi, size_t rows, DD g[kGramN]) override {
         hipStream_t s = P->ctx->stream;
         const size_t ns = si.size(), no = oi.size();
@@ -720,17 +762,26 @@ struct GpuSiftSolver final : SiftSystemSolver {
         P->w->rf_idx.ensure(all_s + all_o);
         P->w->rf_hidx.ensure(all_s + all_o);
         P->w->rf_gram.ensure(tiles_max * kGramN);
-        P->w->rf_hgram.ensure(tiles_max * kGramN);
+        P->w->rf_hgout.ensure(kGramN);
+        P->w->rf_gdone.ensure(1);
+        GramFinal fin;
+        fin.out = dev_view(P->w->rf_hgout.p);
+        fin.done = dev_view(P->w->rf_gdone.p);
+        fin.epoch = ++P->w->gdone_epoch;
+        if (fin.epoch == 0) fin.epoch = ++P->w->gdone_epoch;
+        P->w->rf_lines.ensure(3 * all_o);
+        rlot("g_setup");
+        // the index lists through pinned memory, read in place by the prep kernel
         std::memcpy(P->w->rf_hidx.p, si.data(), ns * sizeof(uint32_t));
         std::memcpy(P->w->rf_hidx.p + ns, oi.data(), no * sizeof(uint32_t));
-        HIPC(hipMemcpyAsync(P->w->rf_idx.p, P->w->rf_hidx.p, (ns + no) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-        HIPC(launch_sift_gram(P->dp.cls[0], P->dp.cls[1], P->w->rf_idx.p, (uint32_t)ns, P->w->rf_idx.p + ns,
-                              (uint32_t)no, rows, P->w->rf_gram.p, s));
-        HIPC(hipMemcpyAsync(P->w->rf_hgram.p, P->w->rf_gram.p, tiles * kGramN * sizeof(DD), hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
-        for (int k = 0; k < kGramN; ++k) g[k] = DD{0.0, 0.0};
-        for (size_t t = 0; t < tiles; ++t)
-            for (int k = 0; k < kGramN; ++k) g[k] = dd_add(g[k], P->w->rf_hgram.p[t * kGramN + k]);
+        rlot("g_h2d");
+        HIPC(launch_sift_gram(P->dp.cls[0], P->dp.cls[1], dev_view(P->w->rf_hidx.p), (uint32_t)ns, (uint32_t)no, rows,
+                              P->w->rf_idx.p, P->w->rf_lines.p, P->w->rf_gram.p, fin, s));
+        rlot("g_launch");
+        wait_flag(P->w->rf_gdone.p, fin.epoch, s, "gram refit");
+        rlot("g_synced");
+        for (int k = 0; k < kGramN; ++k) g[k] = P->w->rf_hgout.p[k];
+        (void)tiles;
         return true;
     }
     void for_ranges(size_t n, const std::function<void(size_t, size_t)>& fn) override;
@@ -2142,11 +2193,14 @@ public:
     // Full GCRANSAC::run; fills outputs, returns total inlier count.
     int run(uint8_t* mask0, uint8_t* mask1, double* H, gcr_rect_model* model_out) {
         const auto t_all = Clock::now();
+        if (g_lo_trace) t_run.clear();
+        rlot("start");
         await_spec(P_->w);                // either replay path reuses set 0 / 1's buffers
         if (comm_ && !summary_replay_on())
             throw std::runtime_error("GCR_REPLAY=slots exchanges per-hypothesis records: use the callback exchange");
         if (summary_replay_on()) replay_summaries();
         else replay_slots();
+        rlot("loop");
 
         int total = 0;
         Model out_model = Tr::def();
@@ -2158,10 +2212,12 @@ public:
             if (do_lo_ && lo_number_ == 0) {
                 ++lo_number_;
                 local_optimization(bufs_[off_]);
+                rlot("lo");
             }
             const auto t_ref = Clock::now();
             resolve(bufs_[0]);            // the reference's counts and models in both buffers
             resolve(bufs_[1]);
+            rlot("resolved");
             bool diff = false;
             for (int c = 0; c < K_; ++c) if (bufs_[off_].n[c] != best_.n[c]) diff = true;
             if (diff) off_ = 1 - off_;
@@ -2207,15 +2263,19 @@ public:
             }
             // iteratedLeastSquaresFitting never succeeds (GCRANSAC.h:1092-1098):
             // one non-minimal fit on the buffer's inliers, kept if strictly better.
+            rlot("rescored");
             if (!have_lists) inlier_lists(bufs_[off_].model, Tm_, 0, lists);
+            rlot("lists");
             Model refit;
             const auto t_fit = Clock::now();
             const bool fitted = Tr::fit(P_, lists, refit, true);
             st_.ms_refit_fit = ms_since(t_fit);
+            rlot("fit");
             if (fitted) {
                 HScore s;
                 uint32_t rn[2];
                 const bool rl = score_models(&refit, 1, &s, rn, &msac) && !sm_lbad_[0];
+                rlot("refit_scored");
                 const int idx = 1 - off_;
                 bufs_[idx] = Buffer{true, refit, {rn[0], rn[1]}};
                 if (score_less(best_, [&] { return best_model_; }, s, [&] { return refit; })) {
@@ -2232,8 +2292,11 @@ public:
             out_model = best_model_;
             st_.score = best_.sum;
             st_.ms_refit = ms_since(t_ref);
+            rlot("masks");
         }
         drain_prefetch();                 // the side stream idle before the workspace is reused
+        rlot("end");
+        lot_print("gcr RUN:", t_run);
         Tr::output(out_model, H, model_out);
         st_.iteration_number = it_;
         st_.local_optimization_number = lo_number_;
@@ -3602,17 +3665,7 @@ private:
             if (!updated) break;
         }
         if (win_pending) max_score = win_exact();
-        if (g_lo_trace && !t_lot.empty()) {
-            std::string line = "gcr LO:";
-            const auto b = t_lot.front().second;
-            for (const auto& e : t_lot) {
-                char buf[64];
-                snprintf(buf, sizeof(buf), " %s %.1f", e.first,
-                         std::chrono::duration<double, std::micro>(e.second - b).count());
-                line += buf;
-            }
-            fprintf(stderr, "%s\n", line.c_str());
-        }
+        lot_print("gcr LO:", t_lot);
         st_.ms_lo += ms_since(t0);
         if (score_less(best_, [&] { return best_model_; }, max_score, [&] { return lo_model; })) {
             best_ = max_score;

@@ -23,7 +23,10 @@
 // then pair rows i < j in lexicographic order) in tiles of kGramTile rows;
 // inside a tile, lane l (0..255) accumulates rows tile*kGramTile + l + 256 u
 // (u increasing); the 256 lane sums are combined by the halving tree
-// x[l] += x[l + h], h = 128 .. 1; the tile sums are added in tile order.
+// x[l] += x[l + h], h = 128 .. 1.  The tile sums: lane l (0..63) adds tiles
+// l, l + 64, l + 128, ... in order to +0, then the halving tree h = 32 .. 1
+// (one parallel combination on the device instead of a sequential chain of
+// every tile).
 #pragma once
 
 #include "gcr_hd.h"
@@ -121,6 +124,33 @@ GCR_HD void pair_of(uint64_t p, uint64_t n, uint64_t& i, uint64_t& j) {
     while ((uint64_t)ii + 2 < n && ((uint64_t)ii + 1) * (2 * n - (uint64_t)ii - 2) / 2 <= p) ++ii;
     i = (uint64_t)ii;
     j = p - i * (2 * n - i - 1) / 2 + i + 1;
+}
+
+// the halving tree over kGramLanes lane sums (lane[l * kGramN + k]) into
+// lane 0
+GCR_HD void gram_lane_tree(DD* lane) {
+    for (int h = kGramLanes / 2; h >= 1; h >>= 1)
+        for (int l = 0; l < h; ++l)
+            for (int k = 0; k < kGramN; ++k)
+                lane[(size_t)l * kGramN + k] = dd_add(lane[(size_t)l * kGramN + k], lane[(size_t)(l + h) * kGramN + k]);
+}
+
+// the tile sums (tiles[t * kGramN + k], nt tiles) into the matrix g, in the
+// order above (host restatement of k_sift_gram's last workgroup)
+constexpr int kGramTileLanes = 64;      // lanes of the tile-sum combination
+inline void gram_combine_tiles(const DD* tiles, size_t nt, DD g[kGramN]) {
+    DD lane[kGramTileLanes * kGramN];
+    for (int l = 0; l < kGramTileLanes; ++l) {
+        DD* a = lane + (size_t)l * kGramN;
+        for (int k = 0; k < kGramN; ++k) a[k] = DD{0.0, 0.0};
+        for (size_t t = (size_t)l; t < nt; t += kGramTileLanes)
+            for (int k = 0; k < kGramN; ++k) a[k] = dd_add(a[k], tiles[t * kGramN + k]);
+    }
+    for (int h = kGramTileLanes / 2; h >= 1; h >>= 1)
+        for (int l = 0; l < h; ++l)
+            for (int k = 0; k < kGramN; ++k)
+                lane[(size_t)l * kGramN + k] = dd_add(lane[(size_t)l * kGramN + k], lane[(size_t)(l + h) * kGramN + k]);
+    for (int k = 0; k < kGramN; ++k) g[k] = lane[k];
 }
 
 // index of (a, b), a <= b, in the product order

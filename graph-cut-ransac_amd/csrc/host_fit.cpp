@@ -198,8 +198,7 @@ bool gram_refit_on() {
 void gram_sift_host(const HostClass& sc, const HostClass& oc, const std::vector<uint32_t>& si,
                     const std::vector<uint32_t>& oi, size_t rows, DD g[kGramN]) {
     const size_t ns = si.size(), no = oi.size();
-    for (int k = 0; k < kGramN; ++k) g[k] = DD{0.0, 0.0};
-    std::vector<DD> lane((size_t)kGramLanes * kGramN);
+    std::vector<DD> lane((size_t)kGramLanes * kGramN), tiles;
     for (size_t base = 0; base < rows; base += kGramTile) {
         for (auto& v : lane) v = DD{0.0, 0.0};
         for (int l = 0; l < kGramLanes; ++l) {
@@ -224,12 +223,10 @@ void gram_sift_host(const HostClass& sc, const HostClass& oc, const std::vector<
                 gram_add_row(acc, row);
             }
         }
-        for (int h = kGramLanes / 2; h >= 1; h >>= 1)
-            for (int l = 0; l < h; ++l)
-                for (int k = 0; k < kGramN; ++k)
-                    lane[(size_t)l * kGramN + k] = dd_add(lane[(size_t)l * kGramN + k], lane[(size_t)(l + h) * kGramN + k]);
-        for (int k = 0; k < kGramN; ++k) g[k] = dd_add(g[k], lane[k]);
+        gram_lane_tree(lane.data());
+        tiles.insert(tiles.end(), lane.begin(), lane.begin() + kGramN);
     }
+    gram_combine_tiles(tiles.data(), tiles.size() / kGramN, g);
 }
 
 void gram_solve3(const DD g[kGramN], size_t rows, double x[3]) {

@@ -129,10 +129,20 @@ hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32
                             const uint32_t* oi, uint32_t no, size_t rows, double* A0, double* A1, double* A2,
                             double* b, hipStream_t stream);
 // The hybrid system's double-double Gram matrix in gram.h's order: tile t's
-// kGramN entries at tiles[t * kGramN ..] (ceil(rows / kGramTile) tiles); the
-// caller adds the tiles in order.
-hipError_t launch_sift_gram(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns, const uint32_t* oi,
-                            uint32_t no, size_t rows, DD* tiles, hipStream_t stream);
+// kGramN entries at tiles[t * kGramN ..] (ceil(rows / kGramTile) tiles), and
+// with fin.out set the matrix itself -- the tiles combined in gram.h's order
+// by a second one-workgroup launch -- at fin.out[0 .. kGramN), then fin.epoch
+// stored into fin.done (optional; coherent host memory for the host to wait on).
+struct GramFinal {
+    DD* out = nullptr;
+    uint32_t* done = nullptr;
+    uint32_t epoch = 0;
+};
+// hidx: the index lists (si[ns] then oi[no]) in pinned host memory, mapped;
+// idx (ns + no) and lines (3 no) device scratch.
+hipError_t launch_sift_gram(const DevClass& sc, const DevClass& oc, const uint32_t* hidx, uint32_t ns, uint32_t no,
+                            size_t rows, uint32_t* idx, double* lines, DD* tiles, const GramFinal& fin,
+                            hipStream_t stream);
 // Block partials of sum_{i in [lo, hi)} a[i] * c[i] for the aligned blocks of
 // kSumBlock (qr3.h) rows that intersect [lo, hi), each summed in row order;
 // partials[0 .. nblocks) in block order.  Returns the block count via nblocks.

@@ -2926,37 +2926,131 @@ __device__ __forceinline__ void sift_row_at(const DevClass& sc, const DevClass& 
     sift_pair_row(oc.x[a], oc.y[a], oc.c0[a], oc.c1[a], oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], out);
 }
 
-// The hybrid system's double-double Gram matrix (gram.h): one workgroup per
-// tile of kGramTile rows, lane l accumulating rows tile + l + 256 u; each
-// lane's pair index advances by 256 pairs per step (a carry into the next
-// first index when it runs past the end of a row), so the pair decode runs
-// once per lane; the first index's feature stays in registers.  The 256 lane
-// sums are combined by gram.h's halving tree in LDS.
+// The hybrid system's double-double Gram matrix (gram.h): k_gram_prep copies
+// the index lists in and computes every orientation inlier's line once;
+// k_sift_gram, one workgroup per tile of kGramTile rows, lane l accumulating
+// rows tile + l + 256 u.  Rows go in batches of kGramBatch per lane: the
+// batch's (i, j) first (each lane's pair index advances by 256 pairs per row,
+// a carry into the next first index when it runs past the end of a row),
+// then every line load of the batch, then the arithmetic -- one round trip
+// per batch instead of two dependent ones per row (measured: the kernel was
+// memory-latency bound, 55 % of its wave cycles waiting).  The 256 lane sums are
+// combined by gram.h's halving tree in LDS into the tile's sums
+// (k_gram_final combines the tiles: a last-arrival combination inside this
+// kernel needs an agent-scope release per workgroup -- an L2 writeback on
+// gfx950 -- and measured ~40 us slower).
 constexpr int kGramBlock = kGramLanes;
-__global__ __launch_bounds__(kGramBlock) void k_sift_gram(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
-                                                          uint32_t ns, const uint32_t* __restrict__ oi, uint32_t no,
-                                                          uint64_t rows, DD* __restrict__ tiles) {
+constexpr int kGramPer = (int)(kGramTile / kGramLanes);
+
+// a double-double shuffled down by h lanes (wave-wide)
+__device__ __forceinline__ DD dd_shfl_down(DD x, int h) { return DD{__shfl_down(x.hi, h), __shfl_down(x.lo, h)}; }
+
+// gram.h's halving tree x[l] += x[l + h], h = 128 .. 1, over the 256 lane
+// sums red[k][0 .. 256) of every product k, the work spread over the four
+// waves: levels 128 and 64 as (product, lane) items over all threads, then
+// wave w takes products w, w + 4, ... through levels 32 .. 1 with shuffles
+// (the same additions in the same order); product k's sum to out[k]
+__device__ __forceinline__ void gram_tree_out(DD (*red)[kGramBlock], int t, DD* __restrict__ out) {
+    static_assert(kGramBlock == 256, "gram tree");
+    for (int i = t; i < kGramN * 128; i += kGramBlock) {
+        const int k = i >> 7, l = i & 127;
+        red[k][l] = dd_add(red[k][l], red[k][l + 128]);
+    }
+    __syncthreads();
+    for (int i = t; i < kGramN * 64; i += kGramBlock) {
+        const int k = i >> 6, l = i & 63;
+        red[k][l] = dd_add(red[k][l], red[k][l + 64]);
+    }
+    __syncthreads();
+    const int wave = t >> 6, lane = t & 63;
+    for (int k = wave; k < kGramN; k += kGramBlock / 64) {
+        DD x = red[k][lane];
+#pragma unroll
+        for (int h = 32; h >= 1; h >>= 1) x = dd_add(x, dd_shfl_down(x, h));
+        if (lane == 0) out[k] = x;
+    }
+}
+
+// the tile sums combined in gram.h's order (one workgroup, after
+// k_sift_gram on the stream): wave k takes product k, lane l adds tiles
+// l, l + 64, ... in order (their loads in flight eight at a time), then the
+// halving tree with shuffles; the matrix to fin.out, then fin.epoch to fin.done
+constexpr int kGramFinalLanes = 64;
+__global__ __launch_bounds__(64 * kGramN) void k_gram_final(const DD* __restrict__ tiles, uint32_t ntiles, GramFinal fin) {
+    const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    DD acc{0.0, 0.0};
+#pragma unroll 1
+    for (uint32_t t0 = (uint32_t)lane; t0 < ntiles; t0 += 8 * kGramFinalLanes) {
+        DD v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t t = t0 + (uint32_t)q * kGramFinalLanes;
+            v[q] = t < ntiles ? tiles[(size_t)t * kGramN + k] : DD{0.0, 0.0};
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (t0 + (uint32_t)q * kGramFinalLanes < ntiles) acc = dd_add(acc, v[q]);
+    }
+#pragma unroll
+    for (int h = 32; h >= 1; h >>= 1) acc = dd_add(acc, dd_shfl_down(acc, h));
+    if (lane == 0) fin.out[k] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0 && fin.done != nullptr) {
+        __threadfence_system();
+        __hip_atomic_store(fin.done, fin.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// the index lists from pinned host memory (hidx: si then oi) into idx, and
+// the line (line_from) of every orientation inlier, SoA, into lines[3][no]
+__global__ __launch_bounds__(kGramBlock) void k_gram_prep(DevClass oc, const uint32_t* __restrict__ hidx, uint32_t ns,
+                                                          uint32_t no, uint32_t* __restrict__ idx,
+                                                          double* __restrict__ lines) {
+    const uint32_t t = blockIdx.x * kGramBlock + threadIdx.x;
+    if (t >= ns + no) return;
+    const uint32_t v = hidx[t];
+    idx[t] = v;
+    if (t < ns) return;
+    double l[3];
+    line_from(oc.x[v], oc.y[v], oc.c0[v], oc.c1[v], l);
+    const uint32_t i = t - ns;
+    lines[i] = l[0];
+    lines[no + i] = l[1];
+    lines[2 * (size_t)no + i] = l[2];
+}
+
+template <int kGramBatch>
+__global__ __launch_bounds__(kGramBlock) void k_sift_gram(DevClass sc, const uint32_t* __restrict__ si, uint32_t ns,
+                                                          const double* __restrict__ lines, uint32_t no, uint64_t rows,
+                                                          DD* __restrict__ tiles) {
+    static_assert(kGramPer % kGramBatch == 0, "gram batches");
     __shared__ DD red[kGramN][kGramBlock];
     const int l = threadIdx.x;
     const uint64_t base = (uint64_t)blockIdx.x * kGramTile;
+    const double* L0 = lines;
+    const double* L1 = lines + no;
+    const double* L2 = lines + 2 * (size_t)no;
     DD acc[kGramN];
 #pragma unroll
     for (int k = 0; k < kGramN; ++k) acc[k] = DD{0.0, 0.0};
     bool have = false;
-    uint64_t pi = 0, pj = 0, ci = ~0ull;
-    double xi = 0.0, yi = 0.0, cosi = 0.0, sini = 0.0;
-    for (uint32_t u = 0; u < (uint32_t)(kGramTile / kGramLanes); ++u) {
-        const uint64_t r = base + (uint64_t)l + (uint64_t)kGramLanes * u;
-        if (r >= rows) break;
-        double row[4];
-        if (r < ns) {
-            const uint32_t j = si[r];
-            const double w = 1.0;
-            row[0] = w * sc.x[j];
-            row[1] = w * sc.y[j];
-            row[2] = w * sc.c0[j];
-            row[3] = w;
-        } else {
+    uint64_t pi = 0, pj = 0;
+    for (int g = 0; g < kGramPer; g += kGramBatch) {
+        if (base + (uint64_t)l + (uint64_t)kGramLanes * (uint64_t)g >= rows) break;
+        // 1) the batch's rows: a scale row's feature index, a pair row's (i, j)
+        uint32_t ja[kGramBatch], jb[kGramBatch];
+        int kind[kGramBatch];                                 // 0 none, 1 scale row, 2 pair row
+#pragma unroll
+        for (int b = 0; b < kGramBatch; ++b) {
+            const uint64_t r = base + (uint64_t)l + (uint64_t)kGramLanes * (uint64_t)(g + b);
+            kind[b] = 0;
+            ja[b] = jb[b] = 0;
+            if (r >= rows) continue;
+            if (r < ns) {
+                kind[b] = 1;
+                ja[b] = (uint32_t)r;
+                continue;
+            }
             if (!have) {
                 pair_of(r - ns, no, pi, pj);
                 have = true;
@@ -2967,39 +3061,62 @@ __global__ __launch_bounds__(kGramBlock) void k_sift_gram(DevClass sc, DevClass 
                     ++pi;
                 }
             }
-            if (pi != ci) {
-                const uint32_t a = oi[pi];
-                xi = oc.x[a];
-                yi = oc.y[a];
-                cosi = oc.c0[a];
-                sini = oc.c1[a];
-                ci = pi;
-            }
-            const uint32_t c = oi[pj];
-            sift_pair_row(xi, yi, cosi, sini, oc.x[c], oc.y[c], oc.c0[c], oc.c1[c], row);
-            // row[2] == 0: the same sums as gram_add_row while the row and
-            // the four accumulators its zeros would touch are finite (an
-            // infinite accumulator plus a zero double-double is NaN)
-            if (__builtin_isfinite(row[0]) && __builtin_isfinite(row[1]) && __builtin_isfinite(row[3]) &&
-                __builtin_isfinite(acc[2].hi) && __builtin_isfinite(acc[5].hi) && __builtin_isfinite(acc[7].hi) &&
-                __builtin_isfinite(acc[8].hi)) {
-                gram_add_pair_row(acc, row);
-                continue;
+            kind[b] = 2;
+            ja[b] = (uint32_t)pi;
+            jb[b] = (uint32_t)pj;
+        }
+        // 2) every load of the batch (one round trip; a scale row's feature
+        //    index is a second)
+        double fa[kGramBatch][3], fb[kGramBatch][3];
+#pragma unroll
+        for (int b = 0; b < kGramBatch; ++b) {
+            if (kind[b] == 1) {
+                const uint32_t j = si[ja[b]];
+                fa[b][0] = sc.x[j];
+                fa[b][1] = sc.y[j];
+                fa[b][2] = sc.c0[j];
+                fb[b][0] = fb[b][1] = fb[b][2] = 0.0;
+            } else if (kind[b] == 2) {
+                fa[b][0] = L0[ja[b]];
+                fa[b][1] = L1[ja[b]];
+                fa[b][2] = L2[ja[b]];
+                fb[b][0] = L0[jb[b]];
+                fb[b][1] = L1[jb[b]];
+                fb[b][2] = L2[jb[b]];
+            } else {
+                fa[b][0] = fa[b][1] = fa[b][2] = fb[b][0] = fb[b][1] = fb[b][2] = 0.0;
             }
         }
-        gram_add_row(acc, row);
+        // 3) the rows, in order
+#pragma unroll
+        for (int b = 0; b < kGramBatch; ++b) {
+            if (kind[b] == 0) continue;
+            double row[4];
+            if (kind[b] == 1) {
+                const double w = 1.0;
+                row[0] = w * fa[b][0];
+                row[1] = w * fa[b][1];
+                row[2] = w * fa[b][2];
+                row[3] = w;
+            } else {
+                sift_pair_row_lines(fa[b], fb[b], row);
+                // row[2] == 0: the same sums as gram_add_row while the row and
+                // the four accumulators its zeros would touch are finite (an
+                // infinite accumulator plus a zero double-double is NaN)
+                if (__builtin_isfinite(row[0]) && __builtin_isfinite(row[1]) && __builtin_isfinite(row[3]) &&
+                    __builtin_isfinite(acc[2].hi) && __builtin_isfinite(acc[5].hi) && __builtin_isfinite(acc[7].hi) &&
+                    __builtin_isfinite(acc[8].hi)) {
+                    gram_add_pair_row(acc, row);
+                    continue;
+                }
+            }
+            gram_add_row(acc, row);
+        }
     }
 #pragma unroll
     for (int k = 0; k < kGramN; ++k) red[k][l] = acc[k];
     __syncthreads();
-    for (int h = kGramBlock / 2; h >= 1; h >>= 1) {
-        if (l < h) {
-#pragma unroll
-            for (int k = 0; k < kGramN; ++k) red[k][l] = dd_add(red[k][l], red[k][l + h]);
-        }
-        __syncthreads();
-    }
-    if (l < kGramN) tiles[(size_t)blockIdx.x * kGramN + l] = red[l][0];
+    gram_tree_out(red, l, tiles + (size_t)blockIdx.x * kGramN);
 }
 
 __global__ __launch_bounds__(kRowBlock) void k_sift_rows(DevClass sc, DevClass oc, const uint32_t* __restrict__ si,
@@ -3962,11 +4079,24 @@ hipError_t launch_sift_rows(const DevClass& sc, const DevClass& oc, const uint32
     return hipGetLastError();
 }
 
-hipError_t launch_sift_gram(const DevClass& sc, const DevClass& oc, const uint32_t* si, uint32_t ns, const uint32_t* oi,
-                            uint32_t no, size_t rows, DD* tiles, hipStream_t stream) {
+hipError_t launch_sift_gram(const DevClass& sc, const DevClass& oc, const uint32_t* hidx, uint32_t ns, uint32_t no,
+                            size_t rows, uint32_t* idx, double* lines, DD* tiles, const GramFinal& fin,
+                            hipStream_t stream) {
     if (rows == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sift_gram, dim3((unsigned)((rows + kGramTile - 1) / kGramTile)), dim3(kGramBlock), 0, stream,
-                       sc, oc, si, ns, oi, no, (uint64_t)rows, tiles);
+    if (ns + no > 0)
+        hipLaunchKernelGGL(k_gram_prep, dim3((ns + no + kGramBlock - 1) / kGramBlock), dim3(kGramBlock), 0, stream, oc,
+                           hidx, ns, no, idx, lines);
+    const dim3 grid((unsigned)((rows + kGramTile - 1) / kGramTile));
+    const char* e = getenv("GCR_GRAM_BATCH");                 // read per call (measurements)
+    const int batch = e ? atoi(e) : 1;
+    if (batch == 1)
+        hipLaunchKernelGGL(k_sift_gram<1>, grid, dim3(kGramBlock), 0, stream, sc, idx, ns, lines, no, (uint64_t)rows, tiles);
+    else if (batch == 2)
+        hipLaunchKernelGGL(k_sift_gram<2>, grid, dim3(kGramBlock), 0, stream, sc, idx, ns, lines, no, (uint64_t)rows, tiles);
+    else
+        hipLaunchKernelGGL(k_sift_gram<4>, grid, dim3(kGramBlock), 0, stream, sc, idx, ns, lines, no, (uint64_t)rows, tiles);
+    if (fin.out != nullptr)
+        hipLaunchKernelGGL(k_gram_final, dim3(1), dim3(64 * kGramN), 0, stream, tiles, grid.x, fin);
     return hipGetLastError();
 }
 

@@ -332,11 +332,9 @@ GCR_HD void cross3(const double a[3], const double b[3], double o[3]) {
 // (setOrientationConstraint, two_sift.hpp:238-258): vp = l_i x l_j scaled by
 // 1 / max|vp| when that exceeds 1 (cwiseAbs().maxCoeff(), left fold), weight
 // w_i * w_j = 1 on the Python path; row (w vp0, w vp1, 0 | w vp2).
-GCR_HD void sift_pair_row(double xi, double yi, double ci, double si, double xj, double yj, double cj, double sj,
-                          double row[4]) {
-    double l1[3], l2[3], vp[3];
-    line_from(xi, yi, ci, si, l1);
-    line_from(xj, yj, cj, sj, l2);
+// ... from the two lines (line_from of features i and j)
+GCR_HD void sift_pair_row_lines(const double l1[3], const double l2[3], double row[4]) {
+    double vp[3];
     cross3(l1, l2, vp);
     const double a0 = __builtin_fabs(vp[0]), a1 = __builtin_fabs(vp[1]), a2 = __builtin_fabs(vp[2]);
     double mx = (a0 < a1) ? a1 : a0;
@@ -348,6 +346,13 @@ GCR_HD void sift_pair_row(double xi, double yi, double ci, double si, double xj,
     row[1] = w * vp[1];
     row[2] = 0.0;
     row[3] = w * vp[2];
+}
+GCR_HD void sift_pair_row(double xi, double yi, double ci, double si, double xj, double yj, double cj, double sj,
+                          double row[4]) {
+    double l1[3], l2[3];
+    line_from(xi, yi, ci, si, l1);
+    line_from(xj, yj, cj, sj, l2);
+    sift_pair_row_lines(l1, l2, row);
 }
 
 // ------------------------------------------------------- minimal solvers ---

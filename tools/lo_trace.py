@@ -10,16 +10,19 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if len(sys.argv) > 2 and sys.argv[1] == "--parse":
-    deltas = {}
-    for ln in open(sys.argv[2]):
-        if not ln.startswith("gcr LO:"):
-            continue
-        toks = ln.split()[2:]
-        ev = [(toks[i], float(toks[i + 1])) for i in range(0, len(toks), 2)]
-        for (a, ta), (b, tb) in zip(ev, ev[1:]):
-            deltas.setdefault(f"{a}->{b}", []).append(tb - ta)
-    for k, v in sorted(deltas.items(), key=lambda kv: -statistics.median(kv[1])):
-        print(f"{k:24s} n={len(v):4d} median {statistics.median(v):7.1f} us  mean {statistics.mean(v):7.1f}")
+    for label in ("LO:", "RUN:"):
+        deltas = {}
+        for ln in open(sys.argv[2]):
+            if not ln.startswith("gcr " + label):
+                continue
+            toks = ln.split()[2:]
+            ev = [(toks[i], float(toks[i + 1])) for i in range(0, len(toks), 2)]
+            for (a, ta), (b, tb) in zip(ev, ev[1:]):
+                deltas.setdefault(f"{a}->{b}", []).append(tb - ta)
+        if deltas:
+            print(label)
+        for k, v in sorted(deltas.items(), key=lambda kv: -statistics.median(kv[1])):
+            print(f"  {k:24s} n={len(v):4d} median {statistics.median(v):7.1f} us  mean {statistics.mean(v):7.1f}")
     sys.exit(0)
 sys.path[:0] = [REPO, os.path.join(REPO, "graph-cut-ransac_amd"), os.path.join(REPO, "tools")]
 import bench  # noqa: E402

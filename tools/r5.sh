@@ -6,7 +6,9 @@
 #   bench  python bench.py (BENCH_ARGS)
 #   benchf bench.py --workload f
 #   stats  rocprofv3 --kernel-trace --stats of bench.py (BENCH_ARGS) into $O/stats
-#   trace  tools/lo_trace.py host timeline of the LO rounds
+#   trace  tools/lo_trace.py host timeline of the LO rounds (per TRACE_ENVS entry)
+#   ktrace rocprofv3 kernel trace of the latency leg, one call's dispatch timeline
+#   pmclat rocprofv3 --pmc passes (PMC_FILE lines) over the latency leg, kernels matching PMC_MATCH
 #   latst  rocprofv3 --kernel-trace --stats of the latency leg only
 # Every GPU step has its own time limit; any failure ends the session.
 set -u
@@ -24,7 +26,9 @@ for s in $STEPS; do
     stats) (cd /tmp && true); export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv -- python3 bench.py --cpu-seconds 0 ${BENCH_ARGS:-} > $O/stats.log 2>&1 || fail stats $? $O/stats.log; find $O/stats -name '*kernel_stats.csv' -exec head -20 {} \; ;;
     sync) timeout -k 10 120 tools/micro/sync_latency.bin > $O/sync.log 2>&1 || fail sync $? $O/sync.log; cat $O/sync.log ;;
     valu) timeout -k 10 200 tools/micro/valu_issue.bin > $O/valu.log 2>&1 || fail valu $? $O/valu.log; cat $O/valu.log ;;
-    trace) GCR_LO_TRACE=1 timeout -k 10 200 python -u tools/lo_trace.py ${LAT_WL:-m2} 2> $O/trace.txt > $O/trace.log || fail trace $? $O/trace.log; python3 tools/lo_trace.py --parse $O/trace.txt ;;
+    trace) for te in ${TRACE_ENVS:-X=0}; do echo "-- $te"; env $te GCR_LO_TRACE=1 timeout -k 10 200 python -u tools/lo_trace.py ${LAT_WL:-m2} 2> $O/trace_$te.txt > $O/trace.log || fail trace $? $O/trace.log; python3 tools/lo_trace.py --parse $O/trace_$te.txt; done ;;
+    ktrace) export TMPDIR=/tmp; for te in ${KTRACE_ENVS:-X=0}; do echo "-- $te"; export $te; timeout -k 10 300 rocprofv3 --kernel-trace -d $O/ktrace_$te -o run --output-format csv -- python3 tools/lat_seeds.py --workload ${LAT_WL:-m2} --reps 1 base: > $O/ktrace.log 2>&1 || fail ktrace $? $O/ktrace.log; python3 tools/trace_gaps.py $(find $O/ktrace_$te -name '*kernel_trace.csv' | head -1) --summary; done ;;
+    pmclat) export TMPDIR=/tmp; i=0; while IFS= read -r ctrs; do [ -z "$ctrs" ] && continue; i=$((i+1)); echo "-- pass$i: $ctrs"; timeout -s KILL 90 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d $O/pmclat$i -o run -- python3 tools/lat_seeds.py --workload ${LAT_WL:-m2} --reps 1 base: > $O/pmclat$i.log 2>&1 || fail pmclat $? $O/pmclat$i.log; python3 tools/pmc_kernel.py $(find $O/pmclat$i -name '*counter_collection.csv' | head -1) --match "${PMC_MATCH:-.}"; done < ${PMC_FILE:-tools/pmc_lat.txt} ;;
     latst) export TMPDIR=/tmp; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/latst -o run --output-format csv -- python3 tools/lat_seeds.py --workload ${LAT_WL:-m2} --reps 2 base: > $O/latst.log 2>&1 || fail latst $? $O/latst.log; find $O/latst -name '*kernel_stats.csv' -exec head -25 {} \; ;;
   esac
 done
