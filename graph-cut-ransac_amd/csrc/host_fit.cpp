@@ -112,6 +112,27 @@ bool normalize_ok(int K, const HostClass* cls, const std::vector<uint32_t>* idx)
     size_t tot = 0;
     for (int c = 0; c < K; ++c) tot += idx[c].size();
     if (tot < 1) return false;
+    // Shortcut (same answer): the mean distance to ANY centre is at least
+    // diameter / (2 n), and the computed mean is within (3 n u) of the real
+    // one, so two points more than 4 n 1e-9 apart in x or y make it > 1e-9.
+    // The first point against the next few settles every ordinary call; NaN
+    // and degenerate sets take the full computation below.
+    {
+        const double thr = 4.0 * (double)tot * 1e-9;
+        const HostClass* c0 = nullptr;
+        uint32_t j0 = 0;
+        int seen = 0;
+        for (int c = 0; c < K && seen < 64; ++c)
+            for (uint32_t j : idx[c]) {
+                if (++seen > 64) break;
+                if (!c0) {
+                    c0 = &cls[c];
+                    j0 = j;
+                    continue;
+                }
+                if (std::fabs(cls[c].x[j] - c0->x[j0]) > thr || std::fabs(cls[c].y[j] - c0->y[j0]) > thr) return true;
+            }
+    }
     double x0 = 0.0, y0 = 0.0;
     for (int c = 0; c < K; ++c)
         for (uint32_t j : idx[c]) { x0 += cls[c].x[j]; y0 += cls[c].y[j]; }
