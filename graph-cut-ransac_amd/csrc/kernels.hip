@@ -2456,7 +2456,7 @@ struct ArgModels {
 // the value formula, the MSAC ballot and the chunk's inlier values compacted
 // to its start in p.lo.vals, its counts in p.lo.meta, the list / MSAC
 // ballots into ListBits (k_lo_resid, k_lo_split)
-template <int KIND>
+template <int KIND, bool kWT = false>
 __device__ __forceinline__ void lo_resid_chunk(const DevProblem& p, const typename ModelOf<KIND>::type& m,
                                                const ValueConst& vc, const uint8_t* __restrict__ inc, uint32_t mi,
                                                uint32_t j, int lane, double T0, double T1, uint32_t pad0,
@@ -2492,12 +2492,17 @@ __device__ __forceinline__ void lo_resid_chunk(const DevProblem& p, const typena
         double ps = inl ? -r2 : 0.0;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) ps += __shfl_xor(ps, d);
-        if (lane == 0) p.lo.psum[wi] = ps;
+        if (lane == 0) {
+            if constexpr (kWT) __hip_atomic_store(p.lo.psum + wi, ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else p.lo.psum[wi] = ps;
+        }
     }
     if (lane == 0) {
         if (lb.bits != nullptr) lb.bits[wi] = lbw;
         if (lb.mbits != nullptr) lb.mbits[wi] = w;
-        p.lo.meta[wi] = (uint32_t)__builtin_popcountll(w) | nfm << 8 | nfl << 16;
+        const uint32_t mt = (uint32_t)__builtin_popcountll(w) | nfm << 8 | nfl << 16;
+        if constexpr (kWT) __hip_atomic_store(p.lo.meta + wi, mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else p.lo.meta[wi] = mt;
     }
 }
 
@@ -2517,10 +2522,19 @@ __device__ __forceinline__ void lo_pair_features(const DevProblem& p, uint32_t j
 }
 
 template <int KIND>
+__device__ __forceinline__ void lo_approx_reduce(const DevProblem& p, uint32_t mi, uint32_t pad0, uint32_t nchunks,
+                                                 const ScoreOut& out, bool wt);
+// kFuse (approximate LO scoring in one launch): each chunk's psum and meta
+// are stored write-through (sc1) and drained, the workgroup counts itself in
+// on the model's arrival counter, and the model's last workgroup reduces
+// them with sc1 loads (lo_approx_reduce) -- k_lo_approx's work, without the
+// second launch and without a release fence (MI355X guide, inter-workgroup
+// hand-off by write-through stores)
+template <int KIND, bool kFuse = false>
 __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
                                                         const uint8_t* __restrict__ inc, double T0, double T1,
                                                         uint32_t pad0, uint32_t nchunks, ListBits lb, FlagBand fbm,
-                                                        FlagBand fbl, ArgModels am, uint32_t mi_base) {
+                                                        FlagBand fbl, ArgModels am, uint32_t mi_base, ScoreOut aout) {
     const uint32_t ml = blockIdx.y;                           // the model in this launch's part
     const uint32_t mi = mi_base + ml;                         // ... and in the whole batch
     const uint32_t j = blockIdx.x * (kLrThreads / 64) + (threadIdx.x >> 6);      // chunk
@@ -2543,9 +2557,29 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
         }
     }
     __syncthreads();
-    if (!jin) return;                                        // wave-uniform, after the barrier
-    lo_resid_chunk<KIND>(p, m_sh, vc_sh, inc, mi, j, lane, T0, T1, pad0, nchunks, lb, fbm, fbl, x, y, f2, f3, cls,
-                         fi);
+    if constexpr (!kFuse) {
+        if (!jin) return;                                    // wave-uniform, after the barrier
+        lo_resid_chunk<KIND>(p, m_sh, vc_sh, inc, mi, j, lane, T0, T1, pad0, nchunks, lb, fbm, fbl, x, y, f2, f3, cls,
+                             fi);
+    } else {
+        __shared__ uint32_t last_sh;
+        if (jin)
+            lo_resid_chunk<KIND, true>(p, m_sh, vc_sh, inc, mi, j, lane, T0, T1, pad0, nchunks, lb, fbm, fbl, x, y, f2,
+                                       f3, cls, fi);
+        // every storing wave drains its write-through stores, then one
+        // arrival per workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t prev = __hip_atomic_fetch_add(p.lo.arrive + mi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_sh = prev + 1u == gridDim.x ? 1u : 0u;
+            if (last_sh) __hip_atomic_store(p.lo.arrive + mi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!last_sh) return;                                // workgroup-uniform
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the arrival
+        lo_approx_reduce<KIND>(p, mi, pad0, nchunks, aout, true);
+    }
 }
 
 // The fold of one model's compacted chunks (k_lo_fold, and the last
@@ -2644,17 +2678,22 @@ __global__ __launch_bounds__(kLoThreads) void k_lo_fold(DevProblem p, uint32_t p
 // with them only when the bounds cannot change it; the winner's exact sums
 // follow from k_lo_fold.
 constexpr int kLaThreads = 256;
+static_assert(kLaThreads == kLrThreads, "k_lo_resid<kFuse> reduces in its own workgroup");
+// the reduction of model mi's chunks (wt: loads write-through, sc1, for
+// chunks stored write-through by other workgroups of the same launch)
 template <int KIND>
-__global__ __launch_bounds__(kLaThreads) void k_lo_approx(DevProblem p, uint32_t pad0, uint32_t nchunks, ScoreOut out) {
-    const uint32_t mi = blockIdx.x;
+__device__ __forceinline__ void lo_approx_reduce(const DevProblem& p, uint32_t mi, uint32_t pad0, uint32_t nchunks,
+                                                 const ScoreOut& out, bool wt) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
     const uint32_t c1 = pad0 / 64u;                           // the first class-1 chunk
     uint32_t n0 = 0, n1 = 0, fm = 0, fl = 0;
     double s0 = 0.0, s1 = 0.0;
     for (uint32_t j = (uint32_t)t; j < nchunks; j += kLaThreads) {
         const size_t wi = (size_t)mi * nchunks + j;
-        const uint32_t mt = p.lo.meta[wi];
-        const double ps = p.lo.psum[wi];
+        const uint32_t mt = wt ? __hip_atomic_load(p.lo.meta + wi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : p.lo.meta[wi];
+        const double ps = wt ? __hip_atomic_load(p.lo.psum + wi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : p.lo.psum[wi];
         if (j < c1) {
             n0 += mt & 0xffu;
             s0 += ps;
@@ -2706,6 +2745,10 @@ __global__ __launch_bounds__(kLaThreads) void k_lo_approx(DevProblem p, uint32_t
         if (out.lfl) out.lfl[mi] = al;
         signal_done(out, mi);
     }
+}
+template <int KIND>
+__global__ __launch_bounds__(kLaThreads) void k_lo_approx(DevProblem p, uint32_t pad0, uint32_t nchunks, ScoreOut out) {
+    lo_approx_reduce<KIND>(p, blockIdx.x, pad0, nchunks, out, false);
 }
 
 // The split scorer in ONE launch (GCR_LO_FUSED=1; measured slower than the
@@ -4310,6 +4353,15 @@ bool lo_fused() {
     const char* e = getenv("GCR_LO_FUSED");
     return e && e[0] == '1';
 }
+// GCR_LO_APPROX_FUSE=1: the approximate LO scores by k_lo_resid's last
+// workgroups instead of a second launch (k_lo_approx) -- measured slower on
+// MI355X (session r5_s24: the fused residual launch 30 us against 12 + 5;
+// every wave drains its list-bit stores to host memory before its arrival),
+// so off (read per call)
+bool lo_approx_fuse() {
+    const char* e = getenv("GCR_LO_APPROX_FUSE");
+    return e && e[0] == '1';
+}
 
 // k_lo_split's chunks per wave: every workgroup takes a whole CU (the fold's
 // LDS), so the launch is sized to about one workgroup per CU -- the fewest
@@ -4369,7 +4421,7 @@ hipError_t launch_score_small(const DevProblem& p, const double T[2], const void
                                    nchunks, cpw, lb, flag_band(T), flag_band(lb.T), am, out);
             } else {
                 hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, q, mp, inc, T[0], T[1],
-                                   pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am, 0u);
+                                   pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am, 0u, out);
                 hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm), dim3(kLoThreads), 0, stream, q, pad0, nchunks, out,
                                    0u, 0u);
             }
@@ -4418,8 +4470,18 @@ hipError_t launch_score_small_part(const DevProblem& p, const double T[2], const
                 std::memcpy(am.m, hmodels, (size_t)nm * sizeof(RectModel));
                 am.n = nm;
             }
-            hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, q, static_cast<const M*>(models),
-                               nullptr, T[0], T[1], pad0, nchunks, lb, flag_band(T), flag_band(lb.T), am, mi_base);
+            // stage 4 with the whole batch in this launch: the approximate
+            // scores by its last workgroups (GCR_LO_APPROX_FUSE=0: k_lo_approx)
+            if ((stage & 4) && mi_base == 0 && nm == nm_fold && p.lo.arrive != nullptr && lo_approx_fuse()) {
+                hipLaunchKernelGGL((k_lo_resid<KIND, true>), grid, dim3(kLrThreads), 0, stream, q,
+                                   static_cast<const M*>(models), nullptr, T[0], T[1], pad0, nchunks, lb, flag_band(T),
+                                   flag_band(lb.T), am, mi_base, out);
+                stage &= ~4;
+            } else {
+                hipLaunchKernelGGL((k_lo_resid<KIND>), grid, dim3(kLrThreads), 0, stream, q,
+                                   static_cast<const M*>(models), nullptr, T[0], T[1], pad0, nchunks, lb, flag_band(T),
+                                   flag_band(lb.T), am, mi_base, out);
+            }
         }
         if ((stage & 2) && nm_fold > 0)
             hipLaunchKernelGGL((k_lo_fold<KIND>), dim3(nm_fold), dim3(kLoThreads), 0, stream, q, pad0, nchunks, out,

@@ -35,15 +35,19 @@ def _m1(seed, n):
 def test_approx_modes_agree(monkeypatch, kind, seed, n):
     run = _m2 if kind == "m2" else _m1
     res = {}
-    for mode in ("0", "1", "2"):
-        monkeypatch.setenv("GCR_LO_APPROX", mode)
+    for mode in ("0", "1", "2", "1u"):
+        monkeypatch.setenv("GCR_LO_APPROX", mode[0])
+        # "1u": the approximate scores by k_lo_resid's last workgroups
+        # (GCR_LO_APPROX_FUSE=1) instead of k_lo_approx's own launch
+        monkeypatch.setenv("GCR_LO_APPROX_FUSE", "1" if mode == "1u" else "0")
         res[mode] = run(seed, n)
     monkeypatch.delenv("GCR_LO_APPROX")
+    monkeypatch.delenv("GCR_LO_APPROX_FUSE")
     base = res["0"]
     st0 = base[-1]
     assert st0["lo_refolds"] == 0
     assert st0["local_optimization_number"] > 0
-    for mode in ("1", "2"):
+    for mode in ("1", "2", "1u"):
         r = res[mode]
         for a, b in zip(base[:-2], r[:-2]):
             assert np.array_equal(np.asarray(a), np.asarray(b)), mode
@@ -53,6 +57,7 @@ def test_approx_modes_agree(monkeypatch, kind, seed, n):
     # (almost) none open in mode 1
     assert res["2"][-1]["lo_refolds"] >= st0["local_optimization_number"]
     assert res["1"][-1]["lo_refolds"] <= 1
+    assert res["1u"][-1]["lo_refolds"] == res["1"][-1]["lo_refolds"]
 
 
 def test_approx_matches_oracle():
