@@ -48,38 +48,130 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X vector fp64 spec
 N_SIMD = 256 * 4               # CUs x SIMDs
 CLOCK_GHZ = 2.4                # MI355X peak engine clock (spec)
-# VALU issue ceiling: one wave64 VALU instruction per SIMD every 4 cycles (16
-# lanes per cycle; full-rate fp64 on CDNA4), in G wave-instructions/s
-VALU_ISSUE_PEAK = N_SIMD * CLOCK_GHZ / 4.0
-# Issue cycles per wave64 VALU instruction on one SIMD (SQ_INSTS_VALU_* class)
-# at the scorers' occupancy (4 waves per SIMD; one wave alone issues every
-# ~6.4 cycles, the guide's constants table quotes 4 for f32), measured by tools/micro/valu_issue.hip on
-# MI355X (profiles/r4_valu_issue.log: 16 independent chains per wave, per-SIMD
-# cycles at 4 waves): f64 add / mul / fma 3.03, v_rcp_f64 / v_sqrt_f64 10.5,
-# f32 add 2.02, f32 fma / pk_fma 2.97-3.03, f32 transcendentals 5.48, u32 add
-# 2.13, cvt_f64_i32 3.20.  MUL_F32 is taken as ADD_F32 and INT64 (64-bit
-# shifts / adds) as the f64 ALU rate (not measured); the other VALU
-# instructions (moves, compares, selects, bit ops) at the 32-bit rate.
-VALU_CLASS_COST = {
-    "SQ_INSTS_VALU_ADD_F32": 2.02, "SQ_INSTS_VALU_MUL_F32": 2.02, "SQ_INSTS_VALU_FMA_F32": 2.97,
-    "SQ_INSTS_VALU_TRANS_F32": 5.48,
-    "SQ_INSTS_VALU_ADD_F64": 3.03, "SQ_INSTS_VALU_MUL_F64": 3.03, "SQ_INSTS_VALU_FMA_F64": 3.03,
-    "SQ_INSTS_VALU_TRANS_F64": 10.53,
-    "SQ_INSTS_VALU_INT32": 2.13, "SQ_INSTS_VALU_INT64": 3.03, "SQ_INSTS_VALU_CVT": 3.20,
+# VALU issue costs, NANOSECONDS per wave64 instruction per SIMD, measured by
+# tools/micro/valu_issue.hip on MI355X (profiles/r5_valu_issue.log): 16
+# independent chains per wave, 4 waves per SIMD, each SIMD's cost = the span
+# of its own waves (first start to last end, s_memrealtime, SIMDs told apart
+# by HW_ID / XCC_ID) over the instructions they issued.  Round 4's per-wave
+# figure (3.03 "cycles" for f64) assumed the 4 waves of a SIMD overlap for
+# their whole run; their spans show they do not (4.4 s_memtime cycles per f64
+# instruction at the measured ~2.3 GHz, against the spec's 4).  Priced without
+# any clock assumption.  Classes = the SQ_INSTS_VALU_* counters; MUL_F32 is
+# taken as ADD_F32.
+VALU_CLASS_NS = {
+    "SQ_INSTS_VALU_ADD_F32": 1.193, "SQ_INSTS_VALU_MUL_F32": 1.193, "SQ_INSTS_VALU_FMA_F32": 1.738,
+    "SQ_INSTS_VALU_TRANS_F32": 3.470,
+    "SQ_INSTS_VALU_ADD_F64": 1.885, "SQ_INSTS_VALU_MUL_F64": 1.916, "SQ_INSTS_VALU_FMA_F64": 1.967,
+    "SQ_INSTS_VALU_TRANS_F64": 6.813,
+    "SQ_INSTS_VALU_INT32": 1.199, "SQ_INSTS_VALU_INT64": 1.987, "SQ_INSTS_VALU_CVT": 1.860,
 }
-VALU_OTHER_COST = 2.13
+# the "other" bucket, per opcode (same micro-benchmark); v_cndmask_b32 at its
+# SGPR-mask form (the VCC form's 8.0 ns alone is a back-to-back VCC-read
+# penalty: 2.0 ns inside an instruction stream); the compare and readlane
+# loops also issue the consumers of their SGPR results (two v_xor_b32 per
+# compare, one v_add_u32 per readlane: tools/isa_loops.py on the micro's
+# code), which are taken off (compare 4.897 / 6.017 - 2 x 1.208, readlane
+# 3.803 - 1.199); unlisted 32-bit ops at the v_xor_b32 cost, unlisted 64-bit
+# ops at the v_max_f64 cost
+VALU_OP_NS = {
+    "v_mov_b32": 1.039, "v_mov_b64": 1.834, "v_cndmask_b32": 1.931, "v_xor_b32": 1.208,
+    "v_writelane_b32": 1.848, "v_readlane_b32": 2.604, "v_readfirstlane_b32": 2.604,
+    "v_mbcnt_lo_u32_b32": 1.841, "v_mbcnt_hi_u32_b32": 1.841, "v_max_f64": 1.878, "v_min_f64": 1.878,
+    "v_ldexp_f64": 1.955, "v_fract_f64": 1.929, "v_div_scale_f64": 1.860, "v_div_fmas_f64": 1.826,
+    "v_div_fixup_f64": 1.839, "v_cmp_int": 2.481, "v_cmp_f64": 3.601,
+}
+# the model checked on a known mix (the micro-benchmark's MIX kernel: 3 f64
+# add, 2 mul, 1 fma, 2 u32 add, 2 cndmask, 1 mov, 1 xor per iteration):
+# predicted 20.155 ns against 19.241 measured per iteration per SIMD
+VALU_MODEL_CHECK = {"mix_predicted_ns": 20.155, "mix_measured_ns": 19.241, "residual": 20.155 / 19.241 - 1.0,
+                    "source": "profiles/r5_valu_issue.log (tools/micro/valu_issue.hip)"}
 
 
-def weighted_issue_cycles(pmc):
-    """Issue cycles of one launch's VALU instructions on their SIMDs, summed
-    over the SIMDs: per-class counts x VALU_CLASS_COST (the rest at
-    VALU_OTHER_COST); None unless every class counter was collected."""
-    if not pmc or not pmc.get("SQ_INSTS_VALU") or any(k not in pmc for k in VALU_CLASS_COST):
+def op_ns(op):
+    """issue cost of one other-bucket VALU opcode (llvm-objdump mnemonic)"""
+    o = op.split("_e32")[0].split("_e64")[0].split("_sdwa")[0].split("_dpp")[0]
+    if o.startswith(("v_cmp", "v_cmpx")):
+        return VALU_OP_NS["v_cmp_f64"] if "f64" in o else VALU_OP_NS["v_cmp_int"]
+    if o in VALU_OP_NS:
+        return VALU_OP_NS[o]
+    return VALU_OP_NS["v_max_f64"] if "f64" in o or "b64" in o or "64" in o else VALU_OP_NS["v_xor_b32"]
+
+
+def other_split(pmc, mix):
+    """The other bucket's executed opcode counts: each region's execution count
+    of profiles/valu_mix.json (tools/valu_mix.py: loops of the kernel's code,
+    their static per-class counts and other-opcode histograms) fitted by
+    non-negative least squares to the PMC per-class counts and total, then the
+    regions' other histograms weighted by them.  Returns (counts, fit residual)
+    or None."""
+    try:
+        import numpy as np
+        from scipy.optimize import nnls
+    except ImportError:
         return None
-    classed = sum(pmc[k] for k in VALU_CLASS_COST)
+    classes = [k.replace("SQ_INSTS_VALU_", "") for k in VALU_CLASS_NS]
+    groups = {}
+    for g in mix["regions"]:                      # identical regions (unrolled copies) fit as one
+        key = json.dumps([g["classes"], g["other"]], sort_keys=True)
+        groups.setdefault(key, g)
+    regs = list(groups.values())
+    rows = [[g["classes"].get(c, 0) for g in regs] for c in classes] + [[g["valu"] for g in regs]]
+    rhs = [pmc.get("SQ_INSTS_VALU_" + c, 0.0) for c in classes] + [pmc["SQ_INSTS_VALU"]]
+    A, b = np.array(rows, float), np.array(rhs, float)
+    sc = 1.0 / np.maximum(b, 1e3)
+    w, _ = nnls(A * sc[:, None], b * sc)
+    pred = A @ w
+    counts = {}
+    for g, wi in zip(regs, w):
+        for op, n in g["other"].items():
+            counts[op] = counts.get(op, 0.0) + n * wi
+    other_pmc = pmc["SQ_INSTS_VALU"] - sum(pmc.get(k, 0.0) for k in VALU_CLASS_NS)
+    fit = {"max_class_rel_err": float(max(abs(p - q) / max(q, 1.0) for p, q in zip(pred[:-1], b[:-1])
+                                          if q > 0.001 * b[-1])),
+           "other_fit": float(sum(counts.values())), "other_pmc": float(other_pmc), "regions": len(regs)}
+    return counts, fit
+
+
+def valu_issue_ns(pmc, mix=None):
+    """SIMD-nanoseconds of issue of one launch's VALU instructions, summed over
+    the SIMDs: per-class counts x VALU_CLASS_NS, the other bucket split by
+    opcode (other_split) and priced per opcode (op_ns) -- or, without a
+    matching valu_mix entry, at the v_xor_b32 cost.  None unless every class
+    counter was collected."""
+    if not pmc or not pmc.get("SQ_INSTS_VALU") or any(k not in pmc for k in VALU_CLASS_NS):
+        return None
+    classed = sum(pmc[k] for k in VALU_CLASS_NS)
     other = max(0.0, pmc["SQ_INSTS_VALU"] - classed)
-    cycles = sum(pmc[k] * c for k, c in VALU_CLASS_COST.items()) + other * VALU_OTHER_COST
-    return cycles, {k.replace("SQ_INSTS_VALU_", ""): pmc[k] for k in VALU_CLASS_COST}, other
+    ns = sum(pmc[k] * c for k, c in VALU_CLASS_NS.items())
+    split = other_split(pmc, mix) if mix else None
+    info = {"per_class_insts": {k.replace("SQ_INSTS_VALU_", ""): pmc[k] for k in VALU_CLASS_NS},
+            "other_insts": other}
+    if split:
+        counts, fit = split
+        tot = sum(counts.values()) or 1.0
+        # the fitted mix's average cost, applied to the measured other count
+        avg = sum(n * op_ns(op) for op, n in counts.items()) / tot
+        ns += other * avg
+        top = sorted(counts.items(), key=lambda kv: -kv[1])[:12]
+        info.update({"other_avg_ns": avg, "other_split_fit": fit,
+                     "other_top_share": {op: n / tot for op, n in top}})
+    else:
+        ns += other * VALU_OP_NS["v_xor_b32"]
+        info["other_avg_ns"] = VALU_OP_NS["v_xor_b32"]
+    return ns, info
+
+
+def valu_mix_entry(kernel, build_id):
+    """profiles/valu_mix.json's entry for `kernel` of this kernel build, or None"""
+    path = os.path.join(REPO, "profiles", "valu_mix.json")
+    try:
+        with open(path) as f:
+            ent = json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
+    if ent is None or ent.get("kernel_build_id") != build_id:
+        return None
+    return ent
 
 
 def score_kernel_name(kind, slots):
@@ -487,27 +579,25 @@ def main():
                      "source": "profiles/pmc_traffic.json (rocprofv3 --pmc, separate passes)"})
 
     # VALU issue bound of the dominant kernel: the committed PMC pass's VALU
-    # instruction count over what the 1024 SIMDs can issue (one wave64 fp64
-    # instruction per 4 cycles) during the live average launch
+    # instructions priced per class (and the other bucket per opcode) in
+    # measured ns of one SIMD's issue, over what the 1024 SIMDs offer during
+    # the live average launch
     valu_issue = None
+    issue = None
     if pmc and pmc.get("SQ_INSTS_VALU") and avg_kernel_s > 0:
-        floor4_s = pmc["SQ_INSTS_VALU"] * 4.0 / (N_SIMD * CLOCK_GHZ * 1e9)
-        valu_issue = {"insts_per_launch": pmc["SQ_INSTS_VALU"], "clock_ghz": CLOCK_GHZ,
-                      # every instruction at 4 cycles (round 3's figure)
-                      "uniform4_floor_ms": floor4_s * 1e3, "frac_uniform4": floor4_s / avg_kernel_s,
+        valu_issue = {"insts_per_launch": pmc["SQ_INSTS_VALU"],
                       "wait_frac": (pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
                                     if pmc.get("SQ_WAVE_CYCLES") and pmc.get("SQ_WAIT_ANY") else None),
                       "rocprof_avg_ms": pmc.get("rocprof_avg_ms"),
                       "source": f"profiles/pmc_traffic.json ({pmc.get('source')}, kernel build {build_id})"}
-        w = weighted_issue_cycles(pmc)
-        if w is not None:
-            cycles, per_class, other = w
-            floor_s = cycles / (N_SIMD * CLOCK_GHZ * 1e9)
-            valu_issue.update({"per_class_insts": per_class, "other_insts": other,
-                               "class_cost_cycles": {k.replace("SQ_INSTS_VALU_", ""): c
-                                                     for k, c in VALU_CLASS_COST.items()},
-                               "other_cost_cycles": VALU_OTHER_COST,
-                               "weighted_floor_ms": floor_s * 1e3, "frac": floor_s / avg_kernel_s})
+        issue = valu_issue_ns(pmc, valu_mix_entry(kernel_name, build_id))
+        if issue is not None:
+            ns, info = issue
+            floor_s = ns * 1e-9 / N_SIMD
+            valu_issue.update(info)
+            valu_issue.update({"class_cost_ns": {k.replace("SQ_INSTS_VALU_", ""): c for k, c in VALU_CLASS_NS.items()},
+                               "op_cost_ns": VALU_OP_NS, "model_check": VALU_MODEL_CHECK,
+                               "issue_floor_ms": floor_s * 1e3, "frac": floor_s / avg_kernel_s})
 
     # wall time to 0.99 confidence: full estimator call (incl. upload, LO, refit)
     latency = None
@@ -583,11 +673,11 @@ def main():
                 # dominant kernel is fp64 VALU issue, not HBM
                 # null when no PMC pass of this kernel build exists
                 "bound": "valu" if valu_issue and "frac" in valu_issue else None,
-                # issue cycles (per-class weighted) / s, against 1024 SIMDs x 2.4 GHz
-                "achieved": (weighted_issue_cycles(pmc)[0] / avg_kernel_s / 1e9
-                             if valu_issue and "frac" in valu_issue else None),
-                "peak": N_SIMD * CLOCK_GHZ,
-                "unit": "G VALU issue cycles/s",
+                # SIMDs kept busy issuing VALU (priced instructions, ns of issue
+                # per second of the launch), against the 1024 SIMDs
+                "achieved": (issue[0] * 1e-9 / avg_kernel_s if valu_issue and "frac" in valu_issue else None),
+                "peak": N_SIMD,
+                "unit": "SIMDs busy issuing VALU (measured per-instruction issue costs)",
                 "frac": valu_issue.get("frac") if valu_issue else None,
                 "traffic": traffic_per_launch(pmc),
                 "valu_issue": valu_issue,
@@ -614,11 +704,12 @@ def main():
                 },
                 "note": ("achieved/frac: the dominant kernel's VALU instructions per class "
                          "(SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_{F32,F64}, INT32, INT64, CVT; rocprofv3 --pmc passes of "
-                         "this same kernel build, profiles/pmc_traffic.json) x their issue cycles on one SIMD "
-                         "(valu_issue.class_cost_cycles: the guide's constants table and "
-                         "tools/micro/valu_issue.hip) / its live average duration, against 1024 SIMDs x 2.4 GHz "
-                         "of issue cycles; valu_issue.frac_uniform4 prices every instruction at 4 cycles (round "
-                         "3). null when no PMC pass exists for this kernel build; the rest of the time is latency "
+                         "this same kernel build, profiles/pmc_traffic.json) and the rest split by opcode "
+                         "(profiles/valu_mix.json: the kernel's loops, their execution counts fitted to the class "
+                         "counters) x their measured issue ns per SIMD (valu_issue.class_cost_ns / op_cost_ns, "
+                         "tools/micro/valu_issue.hip per-SIMD spans; model checked on a known mix: "
+                         "valu_issue.model_check) / the live average launch = SIMDs busy issuing, against 1024. "
+                         "null when no PMC pass exists for this kernel build; the rest of the time is latency "
                          "(valu_issue.wait_frac)"),
             },
             "valu": valu,

@@ -37,6 +37,8 @@ const char* kName[] = {"v_add_f64", "v_fma_f64", "v_mul_f64", "v_rcp_f64", "v_sq
 
 struct Stamp {
     unsigned long long mt, rt;      // s_memtime, s_memrealtime deltas of the timed loop
+    unsigned long long r0, r1;      // s_memrealtime at the loop's start and end (absolute)
+    unsigned hwid, xcc;             // HW_ID (simd / cu / sh / se) and XCC_ID of the wave
 };
 
 template <int OP>
@@ -143,16 +145,22 @@ __global__ void k_issue(const double* in, double* out, Stamp* st) {
     }
     const unsigned long long c1 = clock64();
     const unsigned long long r1 = wall_clock64();
+    unsigned hwid, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     double s = 0.0;
     for (int i = 0; i < kChains; ++i) s += d[i] + (double)f[i] + (double)u[i] + (double)q[i];
     out[blockIdx.x * blockDim.x + t] = s;
-    if ((t & 63) == 0) st[blockIdx.x * (blockDim.x / 64) + t / 64] = Stamp{c1 - c0, r1 - r0};
+    if ((t & 63) == 0) st[blockIdx.x * (blockDim.x / 64) + t / 64] = Stamp{c1 - c0, r1 - r0, r0, r1, hwid, xcc};
 }
 
 struct Cost {
     double ns;          // per instruction per SIMD (realtime)
     double cyc;         // per instruction per SIMD (s_memtime)
     double mhz;         // s_memtime rate
+    double ns_span;     // per instruction per SIMD from each SIMD's own span (HW_ID): the waves that
+                        // ran on it, first start to last end, over the instructions they issued
+    int simds, max_wps; // SIMDs seen, the most waves any one of them ran
 };
 
 template <int OP>
@@ -176,10 +184,39 @@ Cost run(const double* in, double* out, Stamp* st, int wps, int ninst, bool prin
     c.cyc = smt / insts / wps;
     c.ns = srt * 10.0 / insts / wps;            // 100 MHz ticks -> ns
     c.mhz = smt / (srt * 10.0) * 1000.0;
+    // per SIMD (xcc, se, sh, cu, simd): its waves' span and instruction count
+    struct S { unsigned long long lo, hi; int n; };
+    static S sim[1 << 15];
+    static unsigned keys[4096];
+    int nk = 0;
+    for (int i = 0; i < nw; ++i) {
+        const unsigned hw = h[i].hwid;
+        const unsigned key = ((h[i].xcc & 15u) << 11) | (((hw >> 13) & 7u) << 8) | (((hw >> 12) & 1u) << 7) |
+                             (((hw >> 8) & 15u) << 3) | ((hw >> 4) & 3u);
+        if (sim[key].n == 0) {
+            keys[nk++] = key;
+            sim[key] = S{h[i].r0, h[i].r1, 0};
+        }
+        sim[key].lo = h[i].r0 < sim[key].lo ? h[i].r0 : sim[key].lo;
+        sim[key].hi = h[i].r1 > sim[key].hi ? h[i].r1 : sim[key].hi;
+        ++sim[key].n;
+    }
+    double acc = 0.0;
+    int mx = 0;
+    for (int k = 0; k < nk; ++k) {
+        const S& e = sim[keys[k]];
+        acc += (double)(e.hi - e.lo) * 10.0 / (insts * e.n);
+        mx = e.n > mx ? e.n : mx;
+        sim[keys[k]] = S{0, 0, 0};
+    }
+    c.ns_span = acc / nk;
+    c.simds = nk;
+    c.max_wps = mx;
     if (print)
-        printf("%-20s waves/SIMD %d: %7.3f ns (%6.2f s_memtime cycles) per instruction per SIMD; s_memtime %6.0f MHz\n",
+        printf("%-20s waves/SIMD %d: %7.3f ns (%6.2f s_memtime cycles) per instruction per SIMD; s_memtime %6.0f MHz; "
+               "per-SIMD span %7.3f ns (%d SIMDs, at most %d waves on one)\n",
                OP == kMixVariant ? "MIX" : (OP >= kPairBase ? "PAIR" : kName[OP % kPairBase]), wps, c.ns, c.cyc,
-               c.mhz);
+               c.mhz, c.ns_span, c.simds, c.max_wps);
     return c;
 }
 
@@ -194,13 +231,15 @@ void run_all(const double* in, double* out, Stamp* st) {
     }
     // marginal: (time of 16 X + 16 v_add_f64) - (time of 16 v_add_f64), per X
     const Cost p = run<OP + kPairBase>(in, out, st, 4, 2, false);
-    Cost m;
+    Cost m{};
+    m.ns_span = 2.0 * p.ns_span - g_cost[ADD_F64].ns_span;
     m.ns = 2.0 * p.ns - g_cost[ADD_F64].ns;
     m.cyc = 2.0 * p.cyc - g_cost[ADD_F64].cyc;
     m.mhz = p.mhz;
     g_marg[OP] = m;
-    printf("%-20s marginal in a v_add_f64 stream: %7.3f ns (%6.2f s_memtime cycles) per instruction per SIMD\n",
-           kName[OP], m.ns, m.cyc);
+    printf("%-20s marginal in a v_add_f64 stream: %7.3f ns (%6.2f s_memtime cycles) per instruction per SIMD; "
+           "per-SIMD span %7.3f ns\n",
+           kName[OP], m.ns, m.cyc, m.ns_span);
     if constexpr (OP + 1 < NOP_OPS) run_all<OP + 1>(in, out, st);
 }
 
@@ -231,10 +270,21 @@ int main() {
     for (const auto& oc : kMixOps) mp_ns += oc[1] * g_marg[oc[0]].ns;
     printf("MIX model (marginal costs): predicted %.3f ns per mix iteration per SIMD, measured %.3f (residual %+.1f %%)\n",
            mp_ns, m.ns * n, 100.0 * (mp_ns - m.ns * n) / (m.ns * n));
-    // machine-readable: per class alone and marginal ns
+    double ps_ns = 0.0, pm_ns = 0.0;
+    for (const auto& oc : kMixOps) {
+        ps_ns += oc[1] * g_cost[oc[0]].ns_span;
+        pm_ns += oc[1] * g_marg[oc[0]].ns_span;
+    }
+    printf("MIX model (per-SIMD spans): alone %.3f, marginal %.3f ns predicted, measured %.3f (residuals %+.1f %%, "
+           "%+.1f %%)\n",
+           ps_ns, pm_ns, m.ns_span * n, 100.0 * (ps_ns - m.ns_span * n) / (m.ns_span * n),
+           100.0 * (pm_ns - m.ns_span * n) / (m.ns_span * n));
+    // machine-readable: per class [alone, marginal] ns per instruction per
+    // SIMD from the per-SIMD spans, and the mix [measured, alone model,
+    // marginal model]; the clock the s_memtime counter ran at
     printf("JSON {");
     for (int i = 0; i < NOP_OPS; ++i)
-        printf("%s\"%s\": [%.4f, %.4f]", i ? ", " : "", kName[i], g_cost[i].ns, g_marg[i].ns);
-    printf(", \"MIX\": [%.4f, %.4f, %.4f]}\n", m.ns * n, pred_ns, mp_ns);
+        printf("%s\"%s\": [%.4f, %.4f]", i ? ", " : "", kName[i], g_cost[i].ns_span, g_marg[i].ns_span);
+    printf(", \"MIX\": [%.4f, %.4f, %.4f], \"s_memtime_mhz\": %.0f}\n", m.ns_span * n, ps_ns, pm_ns, m.mhz);
     return 0;
 }
