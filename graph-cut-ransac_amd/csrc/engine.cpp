@@ -392,6 +392,14 @@ void lot_print(const char* label, std::vector<std::pair<const char*, Clock::time
     v.clear();
 }
 
+// one step of a host spin-wait on a completion flag: a pause, or -- while
+// several gcr_solve_batch threads share the cores -- a yield, so a waiting
+// thread hands its core to another problem's host work
+inline void spin_pause() {
+    if (g_solving.load(std::memory_order_relaxed) > 1) std::this_thread::yield();
+    else __builtin_ia32_pause();
+}
+
 // spin until a kernel has stored `epoch` into the coherent host flag; a
 // stream that drained (or failed) without it is an error, as is 5 s without it
 void wait_flag(const uint32_t* flag, uint32_t epoch, hipStream_t s, const char* what) {
@@ -407,7 +415,7 @@ void wait_flag(const uint32_t* flag, uint32_t epoch, hipStream_t s, const char* 
             if (std::chrono::duration<double>(Clock::now() - t0).count() > 5.0)
                 throw std::runtime_error(std::string(what) + ": no completion after 5 s");
         }
-        __builtin_ia32_pause();
+        spin_pause();
     }
     std::atomic_thread_fence(std::memory_order_acquire);
 }
@@ -3341,7 +3349,7 @@ private:
                     throw std::runtime_error(msg);
                 }
             }
-            __builtin_ia32_pause();
+            spin_pause();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
     }
