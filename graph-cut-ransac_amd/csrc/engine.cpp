@@ -3471,6 +3471,7 @@ private:
         std::vector<double> trial_err;        // approximate scores: their bounds (0: exact)
         std::vector<uint32_t> trial_raw;
         bool win_pending = false;             // the last winner's exact fold is still to be read
+        long fold_due = -1;                   // ... and to be launched (its model index)
         bool max_self = false;                // max_score is lo_model's own value score
         const uint64_t T = prm_.max_local_optimization_number;
         // the LO lists (threshold (1.5 thr)^2, labeling rule) of the round's
@@ -3545,6 +3546,10 @@ private:
             const uint64_t half = (ntrials + 1) / 2;
             const bool pipe = ntrials >= 8 && score_parts_ok((uint32_t)ntrials);
             uint64_t ndrawn = 0;
+            if (pipe && fold_due >= 0) {
+                launch_win_fold((uint32_t)fold_due);
+                fold_due = -1;
+            }
             if (pipe) {
                 host_pool().parallel_for(half, draw_fit);
                 while (ndrawn < half && drawn_[ndrawn]) ++ndrawn;
@@ -3566,6 +3571,18 @@ private:
                     for (uint64_t i = half; i < ndrawn; ++i)
                         if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
                 }
+            } else if (fold_due >= 0) {
+                // the last round's winner's exact fold goes out from the pool
+                // as its first item, beside the fits (before this round's
+                // launches on the stream: they follow the parallel_for)
+                host_pool().parallel_for(ntrials + 1, [&](size_t i) {
+                    if (i == 0) launch_win_fold((uint32_t)fold_due);
+                    else draw_fit(i - 1);
+                });
+                fold_due = -1;
+                while (ndrawn < ntrials && drawn_[ndrawn]) ++ndrawn;
+                for (uint64_t i = 0; i < ndrawn; ++i)
+                    if (trial_ok[i]) trial_models.push_back(trial_fit[i]);
             } else {
                 host_pool().parallel_for(ntrials, draw_fit);
                 while (ndrawn < ntrials && drawn_[ndrawn]) ++ndrawn;
@@ -3632,7 +3649,7 @@ private:
                         lo_model = mm;
                         lo_buf = Buffer{true, mm, {trial_raw[2 * win], trial_raw[2 * win + 1]}};
                         if (me > 0.0) {
-                            launch_win_fold((uint32_t)win);
+                            fold_due = (long)win;        // launched beside the next round's fits
                             win_pending = true;
                         }
                     }
@@ -3672,6 +3689,7 @@ private:
             lot("picked");
             if (!updated) break;
         }
+        if (fold_due >= 0) launch_win_fold((uint32_t)fold_due);
         if (win_pending) max_score = win_exact();
         lot_print("gcr LO:", t_lot);
         st_.ms_lo += ms_since(t0);
