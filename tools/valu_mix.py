@@ -34,9 +34,9 @@ def pmc_class(op):
     if re.match(r"v_mul_f64$", o): return "MUL_F64"
     if re.match(r"v_(fma|fmac)_f64$", o): return "FMA_F64"
     if re.match(r"v_(rcp|rsq|sqrt)_f64$", o): return "TRANS_F64"
-    if re.match(r"v_(add|sub|subrev)_f32$", o): return "ADD_F32"
-    if re.match(r"v_mul_f32$", o): return "MUL_F32"
-    if re.match(r"v_(fma|fmac|mac|mad|pk_fma|pk_mul|pk_add)_f32$", o): return "FMA_F32"
+    if re.match(r"v_(add|sub|subrev|pk_add)_f32$", o): return "ADD_F32"
+    if re.match(r"v_(mul|pk_mul)_f32$", o): return "MUL_F32"
+    if re.match(r"v_(fma|fmac|mac|mad|pk_fma)_f32$", o): return "FMA_F32"
     if re.match(r"v_(exp|log|rcp|rsq|sqrt|sin|cos)_f32$", o): return "TRANS_F32"
     if re.match(r"v_cvt_", o): return "CVT"
     if re.match(r"v_(lshl_add|lshlrev|lshrrev|ashrrev|add|sub|mad)_u64|v_mad_u64_u32|v_mad_i64_i32|v_lshl_add_u64", o):
