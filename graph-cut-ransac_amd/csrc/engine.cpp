@@ -243,6 +243,8 @@ struct BufferT {             // one of temp_inner_inliers[2]
 struct Workspace {
     DevBuf<double> feat;                // feature SoA (make_problem)
     PinBuf<double> feat_stage;          // its pinned host image (one upload)
+    hipEvent_t feat_ev = nullptr;       // ... recorded after the upload
+    bool feat_ev_pending = false;
     DevBuf<uint8_t> inc;
     DevBuf<RectModel> models;
     PinBuf<uint8_t> h_inc;
@@ -348,7 +350,7 @@ struct Workspace {
     ~Workspace() {
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
         for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start, vb_flush, sum_done[0],
-                             sum_done[1], sum_k0[0], sum_k0[1], sum_k1[0], sum_k1[1]})
+                             sum_done[1], sum_k0[0], sum_k0[1], sum_k1[0], sum_k1[1], feat_ev})
             if (e) (void)hipEventDestroy(e);
     }
 };
@@ -1155,51 +1157,121 @@ size_t gpu_refit_rows() {
 //                as ONE glibc sincos(theta): the reference is built with GCC,
 //                which fuses those adjacent cos/sin calls into sincos, and
 //                sincos differs from separate sin/cos in ~0.1% of arguments.
-void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1, size_t n1, HostClass* hc) {
-    if (solver == 3 || solver == 4) {        // correspondences (x1, y1, x2, y2)
-        HostClass& h = hc[0];
-        h.n = n0;
-        h.x.resize(n0); h.y.resize(n0); h.a.resize(n0); h.c0.resize(n0); h.c1.assign(n0, 0.0);
-        for (size_t i = 0; i < n0; ++i) {
-            h.x[i] = f0[4 * i];
-            h.y[i] = f0[4 * i + 1];
-            h.a[i] = f0[4 * i + 2];
-            h.c0[i] = f0[4 * i + 3];
-        }
-        hc[1] = HostClass{};
-        return;
-    }
+// One parallel pass over the features (host pool, element-wise, so the split
+// changes no value): the host SoA columns and constants, the pinned staging
+// image of the device SoA (class c's five columns of np[c] doubles each, at
+// off[c]), each column's largest finite |value| (amax: +inf if a NaN or an
+// infinity occurs) and the scale-range flag of exact.h (scales_in_range).
+struct FillOut {
+    double amax[2][4];
+    bool scales_ok;
+};
+FillOut fill_host_classes(int solver, const double* f0, size_t n0, const double* f1, size_t n1, HostClass* hc,
+                          double* hst, const size_t np[2], const size_t off[2]) {
+    const bool corr = solver == 3 || solver == 4;
     const int K = solver == 2 ? 2 : 1;
     const double kScalePower = (solver == 1) ? (-1.0 / 3.0) : (1.0 / 3.0);
     const double* src[2] = {f0, f1};
     const size_t ns[2] = {n0, K == 2 ? n1 : 0};
-    for (int c = 0; c < K; ++c) {
+    FillOut res{};
+    res.scales_ok = true;
+    struct Part {
+        int c;
+        size_t lo, hi;
+        double mx[4];
+        bool bad[4];
+        bool range;
+    };
+    // both classes' parts in ONE pool job (16 per large class)
+    Part pr[32];
+    int np_ = 0;
+    double* d[2][5];
+    for (int c = 0; c < 2; ++c) {
         HostClass& h = hc[c];
         const size_t n = ns[c];
+        if (c >= K) {
+            h = HostClass{};
+            continue;
+        }
         h.n = n;
         h.x.resize(n); h.y.resize(n); h.a.resize(n); h.c0.resize(n); h.c1.resize(n);
-        auto fill = [&](size_t lo, size_t hi) {
-            for (size_t i = lo; i < hi; ++i) {
-                h.x[i] = src[c][3 * i];
-                h.y[i] = src[c][3 * i + 1];
-                h.a[i] = src[c][3 * i + 2];
-                if (c == 0) {
-                    h.c0[i] = std::pow(h.a[i], kScalePower);
-                    h.c1[i] = 0.0;
-                } else {
-                    double sn, cs;
-                    ::sincos(h.a[i], &sn, &cs);
-                    h.c0[i] = cs;
-                    h.c1[i] = sn;
-                }
-            }
-        };
-        // the glibc pow / sincos of a large class on the host pool (element-
-        // wise, so the split does not change any value)
+        for (int q = 0; q < 5; ++q) d[c][q] = hst + off[c] + (size_t)q * np[c];
         const size_t parts = n >= 4096 ? 16 : 1;
         const size_t step = (n + parts - 1) / parts;
-        host_pool().parallel_for(parts, [&](size_t p) { fill(std::min(n, p * step), std::min(n, (p + 1) * step)); });
+        for (size_t p = 0; p < parts; ++p)
+            pr[np_++] = Part{c, std::min(n, p * step), std::min(n, (p + 1) * step), {}, {}, true};
     }
+    auto fill = [&](size_t pi) {
+        Part& o = pr[pi];
+        const int c = o.c;
+        HostClass& h = hc[c];
+        double* const* dd = d[c];
+        for (int q = 0; q < 4; ++q) {
+            o.mx[q] = 0.0;
+            o.bad[q] = false;
+        }
+        o.range = true;
+        for (size_t i = o.lo; i < o.hi; ++i) {
+            double v[5];
+            if (corr) {
+                v[0] = src[0][4 * i];
+                v[1] = src[0][4 * i + 1];
+                v[2] = src[0][4 * i + 2];
+                v[3] = src[0][4 * i + 3];
+                v[4] = 0.0;
+            } else {
+                v[0] = src[c][3 * i];
+                v[1] = src[c][3 * i + 1];
+                v[2] = src[c][3 * i + 2];
+                if (c == 0) {
+                    v[3] = std::pow(v[2], kScalePower);
+                    v[4] = 0.0;
+                    const double sc = v[2];
+                    if (sc > 0.0 && sc < HUGE_VAL && !(sc >= 0x1p-200 && sc <= 0x1p200)) o.range = false;
+                } else {
+                    double sn, cs;
+                    ::sincos(v[2], &sn, &cs);
+                    v[3] = cs;
+                    v[4] = sn;
+                }
+            }
+            h.x[i] = v[0]; h.y[i] = v[1]; h.a[i] = v[2]; h.c0[i] = v[3]; h.c1[i] = v[4];
+            for (int q = 0; q < 5; ++q) dd[q][i] = v[q];
+            for (int q = 0; q < 4; ++q) {
+                const double a = std::fabs(v[q]);
+                if (!(a < HUGE_VAL)) o.bad[q] = true;
+                else if (a > o.mx[q]) o.mx[q] = a;
+            }
+        }
+    };
+    host_pool().parallel_for((size_t)np_, fill);
+    for (int c = 0; c < 2; ++c) {
+        for (int q = 0; q < 4; ++q) {
+            double mx = 0.0;
+            bool bad = false;
+            for (int p = 0; p < np_; ++p)
+                if (pr[p].c == c) {
+                    bad = bad || pr[p].bad[q];
+                    mx = std::max(mx, pr[p].mx[q]);
+                }
+            res.amax[c][q] = c < K ? (bad ? HUGE_VAL : mx) : 0.0;
+        }
+        if (c >= K) continue;
+        if (c == 0 && solver <= 2)
+            for (int p = 0; p < np_; ++p) res.scales_ok = res.scales_ok && (pr[p].c != 0 || pr[p].range);
+        for (int q = 0; q < 5; ++q)
+            for (size_t i = ns[c]; i < np[c]; ++i) d[c][q][i] = 0.0;      // pads
+    }
+    return res;
+}
+
+// the host classes alone (debug and host-only entry points)
+void fill_host_classes(int solver, const double* f0, size_t n0, const double* f1, size_t n1, HostClass* hc) {
+    const size_t n1k = solver == 2 ? n1 : 0;
+    const size_t np[2] = {(n0 + 1) & ~size_t(1), (n1k + 1) & ~size_t(1)};
+    const size_t off[2] = {0, 5 * np[0]};
+    std::vector<double> stage(5 * (np[0] + np[1]));
+    (void)fill_host_classes(solver, f0, n0, f1, n1, hc, stage.data(), np, off);
 }
 
 int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const double* f1, size_t n1,
@@ -1218,8 +1290,8 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     P->solver = solver;
     P->K = K;
     const size_t ns[2] = {n0, K == 2 ? n1 : 0};
-    fill_host_classes(solver, f0, n0, f1, n1, P->hc);
-    if (solver <= 2) P->scales_ok = scales_in_range(P->hc[0].a.data(), P->hc[0].n);
+    std::vector<std::pair<const char*, Clock::time_point>> st;      // GCR_LO_TRACE: "gcr SETUP:"
+    if (g_lo_trace) st.emplace_back("start", Clock::now());
     // SoA, every array padded to an even length (zeros) so that 16-byte
     // LDS-DMA strips (k_score_split staging) are aligned and in bounds
     const size_t np[2] = {(ns[0] + 1) & ~size_t(1), (ns[1] + 1) & ~size_t(1)};
@@ -1243,34 +1315,25 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
     // the whole SoA image (pads zeroed) is staged in pinned memory and goes
     // up in ONE copy (ten pageable copies cost ~150 us of a one-shot call)
     P->w->feat_stage.ensure(total);
+    // the staging image of this workspace's previous upload must have been read
+    if (P->w->feat_ev_pending) {
+        HIPC(hipEventSynchronize(P->w->feat_ev));
+        P->w->feat_ev_pending = false;
+    }
+    if (g_lo_trace) st.emplace_back("ws", Clock::now());
     double* hst = P->w->feat_stage.p;
-    size_t off = 0;
+    const size_t off[2] = {0, 5 * np[0]};
+    const FillOut fo = fill_host_classes(solver, f0, n0, f1, n1, P->hc, hst, np, off);
+    if (solver <= 2) P->scales_ok = fo.scales_ok;
+    if (g_lo_trace) st.emplace_back("fill", Clock::now());
     P->dp.solver = solver;
     for (int c = 0; c < 2; ++c) {
         DevClass& d = P->dp.cls[c];
         d.n = (uint32_t)ns[c];
-        {
-            const std::vector<double>* ax[4] = {&P->hc[c].x, &P->hc[c].y, &P->hc[c].a, &P->hc[c].c0};
-            for (int q = 0; q < 4; ++q) {
-                double mx = 0.0;
-                bool bad = false;                       // a NaN or infinity anywhere
-                for (size_t i = 0; i < ns[c] && i < ax[q]->size(); ++i) {
-                    const double v = std::fabs((*ax[q])[i]);
-                    if (!(v < HUGE_VAL)) bad = true;
-                    else if (v > mx) mx = v;
-                }
-                d.amax[q] = bad ? HUGE_VAL : mx;
-            }
-        }
+        for (int q = 0; q < 4; ++q) d.amax[q] = fo.amax[c][q];
         if (ns[c] == 0) { d.x = d.y = d.a = d.c0 = d.c1 = nullptr; continue; }
-        const std::vector<double>* arrs[5] = {&P->hc[c].x, &P->hc[c].y, &P->hc[c].a, &P->hc[c].c0, &P->hc[c].c1};
         const double** dst[5] = {&d.x, &d.y, &d.a, &d.c0, &d.c1};
-        for (int q = 0; q < 5; ++q) {
-            std::memcpy(hst + off, arrs[q]->data(), ns[c] * sizeof(double));
-            for (size_t i = ns[c]; i < np[c]; ++i) hst[off + i] = 0.0;
-            *dst[q] = P->w->feat.p + off;
-            off += np[c];
-        }
+        for (int q = 0; q < 5; ++q) *dst[q] = P->w->feat.p + off[c] + (size_t)q * np[c];
     }
     // the split small-batch scorer's scratch (launch_score_small)
     P->dp.lo = SmallScratch{};
@@ -1285,8 +1348,19 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
         }
         P->dp.lo = SmallScratch{P->w->lo_vals.p, P->w->lo_meta.p, kSplitModels, P->w->lo_arrive.p, P->w->lo_psum.p};
     }
+    if (g_lo_trace) st.emplace_back("staged", Clock::now());
+    // the upload stays asynchronous: the problem's kernels follow it on the
+    // stream, and the side stream (speculative chunks, generation) waits on
+    // its event; the next problem on this workspace waits before restaging
     HIPC(hipMemcpyAsync(P->w->feat.p, hst, total * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-    HIPC(hipStreamSynchronize(ctx->stream));
+    if (!P->w->feat_ev) HIPC(hipEventCreateWithFlags(&P->w->feat_ev, hipEventDisableTiming));
+    HIPC(hipEventRecord(P->w->feat_ev, ctx->stream));
+    HIPC(hipStreamWaitEvent(ctx->side, P->w->feat_ev, 0));
+    P->w->feat_ev_pending = true;
+    if (g_lo_trace) {
+        st.emplace_back("queued", Clock::now());
+        lot_print("gcr SETUP:", st);
+    }
     *out = P.release();
     return GCR_OK;
 }

@@ -7,6 +7,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <memory>
+#include <type_traits>
 #include <vector>
 
 #include "fund.h"
@@ -20,8 +22,30 @@ namespace gcr {
 // constants (same values the GPU holds):
 //   scale class:       c0 = pow(s, kScalePower)      (glibc, +1/3 or -1/3)
 //   orientation class: c0 = cos(theta), c1 = sin(theta)
+// std::vector storage that default-initialises (no zero fill on resize): the
+// feature columns are filled in parallel right after sizing
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+using HVec = std::vector<double, DefaultInitAlloc<double>>;
+
 struct HostClass {
-    std::vector<double> x, y, a, c0, c1;
+    HVec x, y, a, c0, c1;
     size_t n = 0;
 };
 

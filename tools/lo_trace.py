@@ -10,7 +10,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if len(sys.argv) > 2 and sys.argv[1] == "--parse":
-    for label in ("LO:", "RUN:"):
+    for label in ("LO:", "RUN:", "SETUP:"):
         deltas = {}
         for ln in open(sys.argv[2]):
             if not ln.startswith("gcr " + label):
