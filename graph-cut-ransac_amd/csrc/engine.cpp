@@ -348,6 +348,8 @@ struct Workspace {
         rf_gdone.coherent = true;
     }
     ~Workspace() {
+        // the pinned staging image may still be read by the problem upload
+        if (feat_ev_pending && feat_ev) (void)hipEventSynchronize(feat_ev);
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
         for (hipEvent_t e : {vb_gen[0], vb_gen[1], vb_done[0], vb_done[1], vb_start, vb_flush, sum_done[0],
                              sum_done[1], sum_k0[0], sum_k0[1], sum_k1[0], sum_k1[1], feat_ev})

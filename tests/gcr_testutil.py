@@ -110,9 +110,13 @@ class CorrProblem:
                                          C.byref(h)))
         self.h = h.value
 
-    def __del__(self):
+    def close(self):
         if self.h:
             N.lib.gcr_problem_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
     def generate(self, seed, slot0, n):
         """homography: inc (n,), models (n, 9); fundamental: (n, 3), (n, 3, 9)"""
