@@ -4126,6 +4126,29 @@ int gcr_solve_batch(int device, gcr_batch_item* items, size_t n, int concurrency
                 release();
                 return rc;
             }
+    // Problems are handed out longest first (an estimate of each call's
+    // wall time: features x a per-estimator rate, from the configs[4] bench's
+    // per-kind phase sums), so the batch does not end on one long problem
+    // started last while the other threads idle.  Every problem is solved
+    // on its own, so the order does not change any result.
+    // GCR_BATCH_ORDER=index: index order (A/B).
+    std::vector<size_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = i;
+    const char* eo = getenv("GCR_BATCH_ORDER");
+    if (!(eo && std::strcmp(eo, "index") == 0)) {
+        auto est = [&](size_t i) {
+            const gcr_batch_item& it = items[i];
+            // ms per 1000 features (configs[4] mix, 8 threads per GPU)
+            const double rate = it.solver == GCR_SOLVER_FUNDAMENTAL7 ? 0.68
+                                : it.solver == GCR_SOLVER_HOMOGRAPHY4 ? 0.37
+                                : it.solver == GCR_SOLVER_SIFT22      ? 0.29
+                                                                      : 0.20;
+            return 0.25 + rate * 1e-3 * (double)(it.n0 + (it.f1 ? it.n1 : 0));
+        };
+        std::vector<double> cost(n);
+        for (size_t i = 0; i < n; ++i) cost[i] = est(i);
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return cost[a] > cost[b]; });
+    }
     std::atomic<size_t> next{0};
     std::atomic<int> first_err{GCR_OK};
     std::mutex err_mu;
@@ -4135,8 +4158,8 @@ int gcr_solve_batch(int device, gcr_batch_item* items, size_t n, int concurrency
         struct Leave {
             ~Leave() { g_solving.fetch_sub(1, std::memory_order_relaxed); }
         } leave;
-        for (size_t i; (i = next.fetch_add(1)) < n;) {
-            gcr_batch_item& it = items[i];
+        for (size_t k; (k = next.fetch_add(1)) < n;) {
+            gcr_batch_item& it = items[order[k]];
             it.result = run_oneshot(ctx, it.solver, it.f0, it.n0, it.f1, it.n1, &it.params, it.mask0_out,
                                     it.mask1_out, it.H_out, &it.model_out, &it.stats_out);
             if (it.result < 0) {

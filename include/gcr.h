@@ -178,9 +178,11 @@ typedef struct gcr_batch_item {
     int result;                  /* inlier count (0: no model) or error code        */
 } gcr_batch_item;
 /* Solve n independent problems on one device.  `concurrency` host threads,
- * each with its own context (HIP stream + workspace), take problems in index
- * order from a shared counter, so one problem's host phases (replay, LO fits,
- * refit control) overlap another's kernels.  Results are per item; returns
+ * each with its own context (HIP stream + workspace), take problems from a
+ * shared counter, longest first (estimated from the solver and the feature
+ * count), so one problem's host phases (replay, LO fits, refit control)
+ * overlap another's kernels and the batch does not end on a long problem
+ * started last.  Results are per item; returns
  * GCR_OK, or the first error code (message in gcr_last_error()). */
 int gcr_solve_batch(int device, gcr_batch_item* items, size_t n, int concurrency);
 
