@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <numeric>
 #include <vector>
 
@@ -500,6 +501,7 @@ private:
 struct CellScratch {
     MaxFlow g;
     std::vector<int32_t> local;
+    std::vector<double> tr;                  // graphcut_clique's terminal capacities
 };
 
 // A two-point cell in closed form: the same unary / pairwise arithmetic as
@@ -594,9 +596,93 @@ inline void graphcut_cell_bk(const double* q, const double* r2, double sqt, doub
     for (uint32_t a = 0; a < k; ++a) seg[nodes[a]] = g.is_sink((int32_t)a) ? 1 : 0;
 }
 
+// A cell in which at most one node can push flow, decided without running
+// BK.  The terms are those graphcut_cell_bk builds (add_term1 per node, then
+// add_term2 for every pair a < b in cell order).  With 0 < lambda < inf and
+// q in [0, 1], A_ab = (0.5 (q_a + q_b)) lambda <= lambda, so every pair
+// takes add_term2's last branch: node a's terminal capacity tr_a is its unary
+// term minus A_ab for every later b, in order (add_tweights' two cases round
+// alike: 0 - fl(A - t) == fl(t - A)), and the arcs are a -> b with
+// fl(lambda - A_ab), b -> a with lambda.
+// - No tr positive and none zero: BK never augments; every node is in the
+//   sink tree from the start.
+// - Exactly one tr_v > 0, every other tr < 0, and tr_v below every -tr_j and
+//   every arc capacity out of v: BK's first active node is v (which meets a
+//   sink node j) or a sink node j (which meets v), so the first augmentation
+//   is s -> v -> j -> t and carries exactly tr_v.  That leaves tr_v == 0
+//   (x - x), tr_j < 0 and the arc v -> j with capacity > 0 (a difference of
+//   unequal floats is never zero), so no source node remains and v rejoins
+//   the sink tree over a residual arc (the node that met it is processed
+//   again; or, when v itself was processed, the next active sink node).
+// Either way every node is SINK.  Anything else (a NaN, a zero, more
+// sources, an arc or sink capacity at or below tr_v) returns false and BK
+// decides.  With the default lambda (0.975) nearly every cell qualifies: an
+// outlier's unary term (1 - lambda) is outweighed by its first pairwise term,
+// so only a cell's last node can be a source.  tests/cpp/gc_clique.cpp
+// checks it against graphcut_cell_bk.
+inline bool graphcut_clique(const double* q, const double* r2, double sqt, double lambda, const uint32_t* nodes,
+                            uint32_t k, CellScratch& cs, uint8_t* seg) {
+    if (!(lambda > 0.0) || !(lambda <= 1.7976931348623157e308)) return false;
+    const double oml = 1.0 - lambda;
+    if (cs.tr.size() < k) cs.tr.resize(k);
+    double* tr = cs.tr.data();
+    for (uint32_t a = 0; a < k; ++a) {
+        const uint32_t i = nodes[a];
+        const double energy = 1.0 - q[i];
+        if (!(q[i] >= 0.0 && q[i] <= 1.0)) return false;
+        // add_term1 on a fresh node: tr = 0 - ck or cs - 0
+        tr[a] = (r2[i] <= sqt) ? 0.0 - oml * energy : oml * (1.0 - energy) - 0.0;
+    }
+    for (uint32_t a = 0; a + 1 < k; ++a) {
+        const double qa = q[nodes[a]];
+        double t = tr[a];
+        for (uint32_t b = a + 1; b < k; ++b) {
+            const double e00 = 0.5 * (qa + q[nodes[b]]);
+            const double A = e00 * lambda;
+            t = t - A;
+        }
+        tr[a] = t;
+    }
+    uint32_t npos = 0, v = 0;
+    for (uint32_t a = 0; a < k; ++a) {
+        if (!(tr[a] < 0.0)) {
+            if (!(tr[a] > 0.0)) return false;               // zero or NaN
+            ++npos;
+            v = a;
+        }
+    }
+    if (npos > 1) return false;
+    if (npos == 1) {
+        const double f = tr[v];
+        if (!(f < lambda)) return false;                     // arcs v -> j, j < v
+        const double qv = q[nodes[v]];
+        for (uint32_t j = 0; j < k; ++j) {
+            if (j == v) continue;
+            if (!(f < -tr[j])) return false;
+            if (j > v) {
+                const double e00 = 0.5 * (qv + q[nodes[j]]);
+                const double A = e00 * lambda;
+                if (!(f < lambda - A)) return false;         // arc v -> j
+            }
+        }
+    }
+    for (uint32_t a = 0; a < k; ++a) seg[nodes[a]] = 1;
+    return true;
+}
+
+// GCR_GC_CLIQUE=0 (read once): every cell of three or more points through BK
+inline bool gc_clique_on() {
+    static const bool on = [] {
+        const char* e = getenv("GCR_GC_CLIQUE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 inline void graphcut_cell(const double* q, const double* r2, double sqt, double lambda, const uint32_t* nodes,
                           uint32_t k, CellScratch& cs, uint8_t* seg) {
     if (k == 2 && graphcut_pair(q, r2, sqt, lambda, nodes, seg)) return;
+    if (k > 2 && gc_clique_on() && graphcut_clique(q, r2, sqt, lambda, nodes, k, cs, seg)) return;
     graphcut_cell_bk(q, r2, sqt, lambda, nodes, k, cs, seg);
 }
 

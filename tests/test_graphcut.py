@@ -286,6 +286,24 @@ def test_two_point_cells_closed_form_equals_bk(tmp_path):
     assert "mismatches 0" in out.stdout
 
 
+def test_clique_cells_closed_form_equal_bk(tmp_path):
+    # graphcut.h graphcut_clique (cells of >= 3 points with at most one source
+    # node: nearly every cell at the default lambda) decides BK's labeling
+    # without running it; checked against graphcut_cell_bk on 2 M random
+    # cells of 3 .. 40 points with deliberate ties (residuals at the truncated
+    # threshold, zero and equal residuals, NaN, lambda tiny / huge / 1)
+    import os
+    import subprocess
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe = str(tmp_path / "gc_clique")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                           os.path.join(here, "cpp", "gc_clique.cpp"), "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "mismatches 0" in out.stdout
+
+
 def test_scheduled_labeling_equals_serial(tmp_path):
     # the engine's path: gc_schedule's cost-balanced jobs (largest cells
     # first, q written per cell) in schedule order, reversed, shuffled and on
