@@ -2726,7 +2726,7 @@ private:
     // neighbourhood graph (homography / fundamental matrix with a grid and
     // lambda > 0): the grid's edges are built once per run, on first use
     NeighbourEdges edges_;
-    std::vector<double> gc_q_;
+    std::vector<uint8_t> gc_cseg_;
     std::vector<uint8_t> gc_seg_;
     int graph_state_ = -1;        // -1 unknown, 0 no pairwise terms, 1 edges_ built
     bool use_graph() {
@@ -3484,18 +3484,20 @@ private:
             }
             HIPC(hipStreamSynchronize(s_));
             st_.launches += 1;
+            lot("gc_resid");
             lists[1].clear();
             // the cells are independent components: cut them on the host
             // pool, in the cost-balanced jobs of gc_schedule
-            gc_q_.resize(n);
+            gc_cseg_.resize(edges_.nodes.size());
             gc_seg_.resize(n);
-            graphcut_labeling_jobs(P_->w->h_r2.p, T[0], prm_.spatial_coherence_weight, edges_, gc_q_.data(),
+            graphcut_labeling_jobs(P_->w->h_r2.p, T[0], prm_.spatial_coherence_weight, edges_, gc_cseg_.data(),
                                    gc_seg_.data(), [](size_t njobs, const auto& fn) {
                                        host_pool().parallel_for(njobs, [&](size_t j) {
                                            thread_local CellScratch cs;
                                            fn(j, cs);
                                        });
                                    });
+            lot("gc_cut");
             lists[0].resize(n);
             uint32_t* lp = lists[0].data();
             size_t m = 0;

@@ -45,13 +45,17 @@ struct NeighbourEdges {
     std::vector<uint32_t> off, nodes;
     // points outside every multi-point cell (the terminal test), ascending
     std::vector<uint32_t> singles;
+    // per point: its position in nodes, or kNoPos for a single
+    static constexpr uint32_t kNoPos = 0xffffffffu;
+    std::vector<uint32_t> pos_of;
     // the labeling's work units for a pool (gc_schedule): job j covers
-    // cells order[jobs[j].b .. jobs[j].e) (kind 0) or singles[b .. e) (kind 1)
+    // cells order[jobs[j].b .. jobs[j].e); range r the points
+    // [ranges[r].b, ranges[r].e) of the assembly pass
     struct Job {
         uint32_t kind, b, e;
     };
     std::vector<uint32_t> order;
-    std::vector<Job> jobs;
+    std::vector<Job> jobs, ranges;
     size_t cells() const { return off.empty() ? 0 : off.size() - 1; }
 };
 
@@ -109,8 +113,11 @@ inline void grid_edges(const double* const* coords, int dims, size_t n, const do
     out.singles.clear();
     for (size_t i = 0; i < n; ++i)
         if (!in_cell[i]) out.singles.push_back((uint32_t)i);
+    out.pos_of.assign(n, NeighbourEdges::kNoPos);
+    for (size_t q = 0; q < out.nodes.size(); ++q) out.pos_of[out.nodes[q]] = (uint32_t)q;
     out.order.clear();
     out.jobs.clear();
+    out.ranges.clear();
     if (!with_edges) return;
     // labeling()'s order: for every point i in row order, every later point
     // of its cell, ascending
@@ -131,17 +138,19 @@ inline void grid_edges(const double* const* coords, int dims, size_t n, const do
 
 // The labeling's work units for `parts` workers drawing jobs in order (the
 // host pool hands them out dynamically): a cell costs ~ 8 + k^2 (BK on a
-// k-clique; measured 27 us at k = 61, ~0.15 us at k = 3), a single point ~1/4.
-// Cells costing more than a job's share (total / 4 parts) get a job each,
-// largest first; the remaining cells and then the single points are packed
-// in index order into jobs of about that share.  Any order gives the same
-// labeling: every cell is cut on its own (graphcut_labeling below).
+// k-clique; measured 27 us at k = 61, ~0.15 us at k = 3).  Cells costing
+// more than a job's share (total / 4 parts) get a job each, largest first;
+// the remaining cells are packed in index order into jobs of about that
+// share.  Any order gives the same labeling: every cell is cut on its own
+// (graphcut_labeling below).  The assembly pass takes 2 parts contiguous
+// point ranges (multiples of 64 points).
 inline void gc_schedule(NeighbourEdges& g, size_t parts) {
     g.order.clear();
     g.jobs.clear();
+    g.ranges.clear();
     const size_t nc = g.cells();
     auto cost = [&](size_t c) { const double k = g.off[c + 1] - g.off[c]; return 8.0 + k * k; };
-    double total = 0.25 * (double)g.singles.size();
+    double total = 0.0;
     for (size_t c = 0; c < nc; ++c) total += cost(c);
     const double share = total / (double)(4 * std::max<size_t>(parts, 1)) + 1.0;
     std::vector<uint32_t> big, rest;
@@ -163,9 +172,9 @@ inline void gc_schedule(NeighbourEdges& g, size_t parts) {
         }
     }
     if (b < g.order.size()) g.jobs.push_back({0u, b, (uint32_t)g.order.size()});
-    const size_t per = std::max<size_t>(256, (size_t)(4.0 * share));
-    for (size_t i = 0; i < g.singles.size(); i += per)
-        g.jobs.push_back({1u, (uint32_t)i, (uint32_t)std::min(g.singles.size(), i + per)});
+    const size_t n = g.pos_of.size();
+    const size_t per = std::max<size_t>(1024, ((n + 2 * parts - 1) / std::max<size_t>(2 * parts, 1) + 63) & ~(size_t)63);
+    for (size_t i = 0; i < n; i += per) g.ranges.push_back({1u, (uint32_t)i, (uint32_t)std::min(n, i + per)});
 }
 
 // Boykov-Kolmogorov max-flow, Graph<double,double,double> semantics.
@@ -502,6 +511,8 @@ struct CellScratch {
     MaxFlow g;
     std::vector<int32_t> local;
     std::vector<double> tr;                  // graphcut_clique's terminal capacities
+    std::vector<double> lq, lr;              // graphcut_labeling_jobs: the cell's q and r2
+    std::vector<uint32_t> ln;                //   and its nodes renumbered 0 .. k-1
 };
 
 // A two-point cell in closed form: the same unary / pairwise arithmetic as
@@ -624,23 +635,51 @@ inline bool graphcut_clique(const double* q, const double* r2, double sqt, doubl
                             uint32_t k, CellScratch& cs, uint8_t* seg) {
     if (!(lambda > 0.0) || !(lambda <= 1.7976931348623157e308)) return false;
     const double oml = 1.0 - lambda;
-    if (cs.tr.size() < k) cs.tr.resize(k);
+    if (cs.tr.size() < 2 * (size_t)k + 4) cs.tr.resize(2 * (size_t)k + 4);
     double* tr = cs.tr.data();
+    double* ql = tr + k + 4;                                 // the cell's q, contiguous
     for (uint32_t a = 0; a < k; ++a) {
         const uint32_t i = nodes[a];
-        const double energy = 1.0 - q[i];
-        if (!(q[i] >= 0.0 && q[i] <= 1.0)) return false;
+        const double qi = q[i];
+        if (!(qi >= 0.0 && qi <= 1.0)) return false;
+        ql[a] = qi;
+        const double energy = 1.0 - qi;
         // add_term1 on a fresh node: tr = 0 - ck or cs - 0
         tr[a] = (r2[i] <= sqt) ? 0.0 - oml * energy : oml * (1.0 - energy) - 0.0;
     }
-    for (uint32_t a = 0; a + 1 < k; ++a) {
-        const double qa = q[nodes[a]];
-        double t = tr[a];
-        for (uint32_t b = a + 1; b < k; ++b) {
-            const double e00 = 0.5 * (qa + q[nodes[b]]);
-            const double A = e00 * lambda;
-            t = t - A;
+    // each row's subtractions in order (b ascending); four rows side by side
+    // so that their dependent chains overlap
+    auto A = [&](double qa, double qb) {
+        const double e00 = 0.5 * (qa + qb);
+        return e00 * lambda;
+    };
+    // (lane-wise vector arithmetic: every lane rounds as the scalar code)
+    typedef double v4 __attribute__((vector_size(32)));
+    uint32_t a = 0;
+    for (; a + 4 < k; a += 4) {
+        const double q0 = ql[a], q1 = ql[a + 1], q2 = ql[a + 2];
+        double t0 = tr[a], t1 = tr[a + 1], t2 = tr[a + 2];
+        t0 = t0 - A(q0, q1);
+        t0 = t0 - A(q0, q2);
+        t1 = t1 - A(q1, q2);
+        t0 = t0 - A(q0, ql[a + 3]);
+        t1 = t1 - A(q1, ql[a + 3]);
+        t2 = t2 - A(q2, ql[a + 3]);
+        const v4 q4 = {q0, q1, q2, ql[a + 3]};
+        v4 t4 = {t0, t1, t2, tr[a + 3]};
+        for (uint32_t b = a + 4; b < k; ++b) {
+            const v4 e00 = 0.5 * (q4 + ql[b]);
+            t4 = t4 - e00 * lambda;
         }
+        tr[a] = t4[0];
+        tr[a + 1] = t4[1];
+        tr[a + 2] = t4[2];
+        tr[a + 3] = t4[3];
+    }
+    for (; a + 1 < k; ++a) {
+        const double qa = ql[a];
+        double t = tr[a];
+        for (uint32_t b = a + 1; b < k; ++b) t = t - A(qa, ql[b]);
         tr[a] = t;
     }
     uint32_t npos = 0, v = 0;
@@ -655,15 +694,11 @@ inline bool graphcut_clique(const double* q, const double* r2, double sqt, doubl
     if (npos == 1) {
         const double f = tr[v];
         if (!(f < lambda)) return false;                     // arcs v -> j, j < v
-        const double qv = q[nodes[v]];
+        const double qv = ql[v];
         for (uint32_t j = 0; j < k; ++j) {
             if (j == v) continue;
             if (!(f < -tr[j])) return false;
-            if (j > v) {
-                const double e00 = 0.5 * (qv + q[nodes[j]]);
-                const double A = e00 * lambda;
-                if (!(f < lambda - A)) return false;         // arc v -> j
-            }
+            if (j > v && !(f < lambda - A(qv, ql[j]))) return false;   // arc v -> j
         }
     }
     for (uint32_t a = 0; a < k; ++a) seg[nodes[a]] = 1;
@@ -701,30 +736,44 @@ inline uint8_t gc_terminal(double r2, double q, double sqt, double oml) {
     return tr < 0 ? 1 : 0;
 }
 
-// One labeling over the schedule of gc_schedule (every cell and single point
-// in exactly one job; a cell job writes q and seg of its own nodes only, so
-// the jobs run concurrently): for_jobs(njobs, fn) calls fn(j, scratch) for
-// every job.  q and seg are sized by the caller (n).
+// One labeling over the schedule of gc_schedule, in two passes of
+// concurrent jobs (for_jobs(njobs, fn) calls fn(j, scratch) for every job
+// and returns when all are done).  Cell jobs cut each cell on local copies
+// of its q and r2 (nodes renumbered 0 .. k-1, the cell order kept) and
+// write its labels to cseg[off[c] .. off[c+1]) -- contiguous per cell, so
+// concurrent jobs do not share cache lines the way writes to the cells'
+// scattered points would.  Range jobs then assemble seg over contiguous point
+// ranges: a cell point's label from cseg, a single point's terminal test.
+// cseg holds nodes.size() bytes, seg n.
 template <class ForJobs>
-inline void graphcut_labeling_jobs(const double* r2, double sqt, double lambda, const NeighbourEdges& g, double* q,
-                                   uint8_t* seg, ForJobs&& for_jobs) {
+inline void graphcut_labeling_jobs(const double* r2, double sqt, double lambda, const NeighbourEdges& g,
+                                   uint8_t* cseg, uint8_t* seg, ForJobs&& for_jobs) {
     const double oml = 1.0 - lambda;
     for_jobs(g.jobs.size(), [&](size_t j, CellScratch& cs) {
         const NeighbourEdges::Job jb = g.jobs[j];
-        if (jb.kind == 1) {
-            for (uint32_t t = jb.b; t < jb.e; ++t) {
-                const uint32_t i = g.singles[t];
-                q[i] = gc_q(r2[i], sqt);
-                seg[i] = gc_terminal(r2[i], q[i], sqt, oml);
-            }
-            return;
-        }
         for (uint32_t t = jb.b; t < jb.e; ++t) {
             const uint32_t c = g.order[t];
             const uint32_t* nodes = g.nodes.data() + g.off[c];
             const uint32_t k = g.off[c + 1] - g.off[c];
-            for (uint32_t a = 0; a < k; ++a) q[nodes[a]] = gc_q(r2[nodes[a]], sqt);
-            graphcut_cell(q, r2, sqt, lambda, nodes, k, cs, seg);
+            if (cs.lq.size() < k) {
+                cs.lq.resize(k);
+                cs.lr.resize(k);
+                cs.ln.resize(k);
+            }
+            for (uint32_t a = 0; a < k; ++a) {
+                const double v = r2[nodes[a]];
+                cs.lr[a] = v;
+                cs.lq[a] = gc_q(v, sqt);
+                cs.ln[a] = a;
+            }
+            graphcut_cell(cs.lq.data(), cs.lr.data(), sqt, lambda, cs.ln.data(), k, cs, cseg + g.off[c]);
+        }
+    });
+    for_jobs(g.ranges.size(), [&](size_t j, CellScratch&) {
+        const NeighbourEdges::Job jb = g.ranges[j];
+        for (uint32_t i = jb.b; i < jb.e; ++i) {
+            const uint32_t p = g.pos_of[i];
+            seg[i] = p != NeighbourEdges::kNoPos ? cseg[p] : gc_terminal(r2[i], gc_q(r2[i], sqt), sqt, oml);
         }
     });
 }

@@ -1,5 +1,6 @@
 // The engine's labeling path (graphcut.h gc_schedule + graphcut_labeling_jobs:
-// cost-balanced jobs, q written per cell, jobs in any order or concurrently)
+// cost-balanced cell jobs writing cell-ordered labels, then the assembly
+// ranges; jobs in any order or concurrently)
 // against the serial driver (terminal test for every point, then every cell
 // in key order), on random 4-D grids with clustered points (cells of 2 to
 // ~100 points), ties at the truncated threshold, and several pool sizes; jobs
@@ -46,7 +47,7 @@ int main() {
         for (size_t parts : {1, 3, 8, 16, 64}) {
             gcr::gc_schedule(e, parts);
             for (int order = 0; order < 4; ++order) {
-                std::vector<double> q2(n, -1.0);
+                std::vector<uint8_t> cseg(e.nodes.size() + 1, 9);
                 std::vector<uint8_t> seg(n, 9);
                 auto for_jobs = [&](size_t nj, const auto& fn) {
                     std::vector<size_t> ord(nj);
@@ -67,7 +68,7 @@ int main() {
                         });
                     for (auto& t : th) t.join();
                 };
-                gcr::graphcut_labeling_jobs(r2.data(), sqt, lam, e, q2.data(), seg.data(), for_jobs);
+                gcr::graphcut_labeling_jobs(r2.data(), sqt, lam, e, cseg.data(), seg.data(), for_jobs);
                 ++runs;
                 if (std::memcmp(seg.data(), ref.data(), n) != 0) {
                     if (++bad <= 5) std::printf("mismatch it %d parts %zu order %d\n", it, parts, order);

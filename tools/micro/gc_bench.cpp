@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
                 kmax, ns, us);
 
     // the jobs on T spinning threads
-    std::vector<double> q2(n);
+    std::vector<uint8_t> q2(e.nodes.size() + 1);
     std::vector<uint8_t> seg2(n);
     std::atomic<size_t> next{0}, done{0};
     std::atomic<int> gen{0};
