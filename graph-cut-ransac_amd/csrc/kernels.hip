@@ -4678,9 +4678,16 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
     ga.hmap = hmap;
     ga.hcount = hcount;
     ga.probe = probe_bits();
+    // the feature-major scorer also for launches of >= 16384 hypotheses (the
+    // replay's large chunks), instead of k_score_split<KIND, 64, 120>;
+    // GCR_GEO_FM_LARGE=0 (read per launch) restores the split scorer there
+    const char* el = getenv("GCR_GEO_FM_LARGE");
+    const bool fm_large = !(el && el[0] == '0');
+    const int sh = split_h(nh);
+    const bool fm = use_fm() && (sh == 16 || (sh == 64 && fm_large));
     if (compact) {
         if (hmap == nullptr || hcount == nullptr) return hipErrorInvalidValue;
-        if (split_h(nh) == 16 && use_fm()) {
+        if (fm && sh == 16) {
             ga.scan = true;                     // the feature-major scorer compacts in its prologue
         } else {
             const hipError_t e = launch_compact(inc, nh, const_cast<uint32_t*>(hmap), const_cast<uint32_t*>(hcount),
@@ -4700,7 +4707,7 @@ hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* model
         else if (h == 16) go(ktag, std::integral_constant<int, 16>{}, std::integral_constant<int, 420>{});
         else go(ktag, std::integral_constant<int, 4>{}, std::integral_constant<int, 960>{});
     };
-    if (split_h(nh) == 16 && use_fm()) {
+    if (fm) {
         // the feature-major scorer with the division-free band prefilter:
         // h_band (transfer error) or f_band (Sampson distance)
         constexpr size_t dyn = fm_dyn_lds_bytes<16, false>();
