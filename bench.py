@@ -220,10 +220,13 @@ def pmc_entry(kernel, slots, build_id=None):
 
 # The fundamental matrix yields 1-3 models per 7-point sample (≈1.07 live per
 # slot at the F config), and the batch scorer runs one workgroup of 16 live
-# hypotheses per CU: 4096 slots give ≈4380 live models, 274 workgroups on 256
-# CUs, so the launch takes two waves of workgroups (182 us) for 7 % more work.
-# 3712 slots keep the live count (≈3970, +3 sigma 4040) within one wave.
-F_SLOTS = 3712
+# hypotheses per CU.  Rounds 2-4 used 3712 slots (≈3970 live models, one wave
+# of workgroups).  Since round 5 the large correspondence launches use the
+# same feature-major scorer (k_compact first), and the generator -- latency-
+# bound at ~1 wave per SIMD -- hides more of its latency in bigger launches:
+# 3712 / 7424 / 11136 / 14848 / 22272 / 29696 slots -> 3.21 / 3.65 / 3.94 /
+# 4.25 / 4.25 / 4.22 x 10^7 hypotheses/s (two-stream pipeline, one box).
+F_SLOTS = 14848
 # full estimator calls timed for the 0.99-confidence wall time (seeds 100..);
 # the number of graph-cut rounds, hence the time, varies with the seed
 # (1.3-3.1 ms for M2), so the median is taken over 11 calls
@@ -252,7 +255,7 @@ def parse(argv=None):
                     help="batch workload: spatial_coherence_weight of the H / F problems (default: the entry "
                          "points' 0.975, graph-cut LO with pairwise terms; 0 isolates the graph-cut share)")
     ap.add_argument("--slots", type=int, default=None,
-                    help="outer-iteration slots per launch (default 4096; f: 3712, see F_SLOTS)")
+                    help="outer-iteration slots per launch (default 4096; f: 14848, see F_SLOTS)")
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak",
                     help="weak: one problem per rank (default); strong: one problem, every chunk of slots "
                          "sharded over the ranks (budget = steps x slots, default 65536 slots per step)")

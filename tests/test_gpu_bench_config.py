@@ -6,8 +6,8 @@ fused generate + score + per-workgroup-best kernel k_score_fm<K, 16, true>
 plus k_select_wg, consecutive launches chained (each launch's look-ahead wave
 generates the next batch's slots, which NB >= 2 exercises); at 16384 slots k_score_split<K, 64, 120, true>; the
 homography generates in k_generate<3, 16> and scores in k_score_fm<3, 16,
-false>; the fundamental matrix at 3712 slots (bench F_SLOTS) in
-k_generate_f + k_compact + k_score_fm<4, 16, false> (f_band prefilter,
+false>; the fundamental matrix at 14848 slots (bench F_SLOTS; 3712 before
+round 5) in k_generate_fw + k_compact + k_score_fm<4, 16, false> (f_band prefilter,
 compaction map).  Correspondence batches run as a two-stream pipeline (batch
 b + 1 generated on the side stream while batch b is scored, alternating
 buffer sets), which the NB consecutive batches exercise.  Each batch's
@@ -123,7 +123,8 @@ def _f_oracle_slot(args):
     return inc, [O.f_score(corr, m, thr) for m in ms]
 
 
-@pytest.mark.parametrize("solver,nslots", [(N.SOLVER_HOMOGRAPHY4, 4096), (N.SOLVER_FUNDAMENTAL7, 3712)])
+@pytest.mark.parametrize("solver,nslots", [(N.SOLVER_HOMOGRAPHY4, 4096), (N.SOLVER_FUNDAMENTAL7, 3712),
+                                           (N.SOLVER_FUNDAMENTAL7, 14848)])
 def test_correspondence_verify_matches_oracle_replay_at_bench_config(solver, nslots):
     if solver == N.SOLVER_HOMOGRAPHY4:
         corr, _, _, thr = S.problem_h(5000, 0.5, seed=SEED)
@@ -221,7 +222,7 @@ def test_deferred_selection_equals_per_batch(kind, nslots, nb, monkeypatch):
 
 
 @pytest.mark.parametrize("solver,nslots,nb", [(N.SOLVER_HOMOGRAPHY4, 4096, 70), (N.SOLVER_FUNDAMENTAL7, 3712, 30),
-                                              (N.SOLVER_HOMOGRAPHY4, 2048, 3)])
+                                              (N.SOLVER_FUNDAMENTAL7, 14848, 9), (N.SOLVER_HOMOGRAPHY4, 2048, 3)])
 def test_correspondence_deferred_selection_equals_per_batch(solver, nslots, nb, monkeypatch):
     # the pipelined correspondence verify_batches scores batch b into ring set
     # b % R (R = 64 at 4096 homography slots, 23 at 3712 fundamental-matrix
