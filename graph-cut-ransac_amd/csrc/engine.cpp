@@ -1546,10 +1546,27 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
         }
         return VBufs{inc.p, mod.p, per(P) > 1 ? map.p : nullptr, per(P) > 1 ? cnt.p : nullptr, sb.dev()};
     }
+    // Multi-model slots (F) are scored compacted.  launch_score_geo compacts
+    // in the feature-major scorer's prologue when it runs at H = 16
+    // (split_h) and otherwise with k_compact on the scoring stream; in that
+    // case verify_gen compacts instead, behind the generator on its own
+    // stream, so that the pipeline's scoring stream goes straight to the
+    // scorer (the ~24 us k_compact of a 14848-slot batch overlaps the
+    // previous batch's scoring).  GCR_GEN_COMPACT=0 (read per call): the
+    // scoring launch compacts.
+    static bool gen_compacts(uint32_t nh) {
+        const char* e = getenv("GCR_GEN_COMPACT");
+        if (e && e[0] == '0') return false;
+        const char* sc = getenv("GCR_SCORER");
+        return !(split_h(nh) == 16 && !(sc && sc[0] == 's'));
+    }
     static hipError_t verify_gen(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, const VBufs& b,
                                  hipStream_t s) {
-        // multi-model slots are compacted by the scoring launch (verify_score)
-        return launch_generate_geo(P->dp, seed, s0, n, b.inc, b.models, s);
+        hipError_t e = launch_generate_geo(P->dp, seed, s0, n, b.inc, b.models, s);
+        const uint32_t nh = n * (uint32_t)per(P);
+        if (e == hipSuccess && b.hmap != nullptr && gen_compacts(nh))
+            e = launch_compact(b.inc, nh, b.hmap, b.hcount, s);
+        return e;
     }
     // rec == nullptr: score only (the ring's deferred selection reduces it)
     static hipError_t verify_score(gcr_problem* P, const double Tm[2], uint64_t s0, uint32_t n, const uint32_t m[2],
@@ -1557,7 +1574,7 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
         const uint32_t nh = n * (uint32_t)per(P);
         if (e0) (void)hipEventRecord(e0, s);
         hipError_t e = launch_score_geo(P->dp, Tm[0], b.models, b.inc, nh, b.sb, s, b.hmap, b.hcount,
-                                        b.hmap != nullptr);
+                                        b.hmap != nullptr && !gen_compacts(nh));
         if (e != hipSuccess) return e;
         if (e1) (void)hipEventRecord(e1, s);
         if (rec == nullptr) return hipSuccess;
