@@ -186,8 +186,12 @@ def score_kernel_name(kind, slots):
     # and score unfused
     fused = "false" if kind >= 3 else "true"
     # H = 16 launches use the feature-major scorer unless GCR_SCORER=split
-    # (kernels.hip use_fm)
-    if h == 16 and not os.environ.get("GCR_SCORER", "").startswith("s"):
+    # (kernels.hip use_fm); so do correspondence launches of >= 16384
+    # hypotheses unless GCR_GEO_FM_LARGE=0 (kernels.hip launch_score_geo)
+    fm = not os.environ.get("GCR_SCORER", "").startswith("s")
+    if h == 16 and fm:
+        return f"k_score_fm<{kind}, 16, {fused}>"
+    if h == 64 and kind >= 3 and fm and os.environ.get("GCR_GEO_FM_LARGE", "1") != "0":
         return f"k_score_fm<{kind}, 16, {fused}>"
     return f"k_score_split<{kind}, {h}, {dict([(64, 120), (16, 420), (4, 960)])[h]}, {fused}>"
 
