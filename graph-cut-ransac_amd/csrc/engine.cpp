@@ -55,6 +55,7 @@
 #include "philox.h"
 #include "qr3.h"
 #include "graphcut.h"
+#include "host_pool.h"
 
 using namespace gcr;
 
@@ -805,170 +806,14 @@ struct GpuSiftSolver final : SiftSystemSolver {
 // min(16, hardware threads) -- one GPU's CPU share on an MI355X node; the
 // 50 LO fits of a graph-cut round take 42 us on 16 threads, 70 on 8.
 
-class HostPool {
-public:
-    explicit HostPool(unsigned n) {
-        for (unsigned t = 1; t < n; ++t) workers_.emplace_back([this] { loop(); });
-    }
-    size_t threads() const { return workers_.size() + 1; }
-    ~HostPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-            gen_.fetch_add(1, std::memory_order_release);
-        }
-        cv_.notify_all();
-        for (auto& w : workers_) w.join();
-    }
-    // fn(i) for i in [0, n); the calling thread works too
-    void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
-        if (n == 0) return;
-        if (workers_.empty() || n == 1) {
-            for (size_t i = 0; i < n; ++i) fn(i);
-            return;
-        }
-        // one job at a time; a caller that finds the pool busy (concurrent
-        // problems on other host threads) runs its job itself instead of
-        // queueing behind the other job
-        std::unique_lock<std::mutex> call(call_mu_, std::try_to_lock);
-        if (!call.owns_lock()) {
-            for (size_t i = 0; i < n; ++i) fn(i);
-            return;
-        }
-        job_ = &fn;
-        n_ = n;
-        next_.store(0, std::memory_order_relaxed);
-        pending_.store(workers_.size(), std::memory_order_relaxed);
-        {
-            // publish under the lock so a worker about to block cannot miss it
-            std::lock_guard<std::mutex> lk(mu_);
-            gen_.fetch_add(1, std::memory_order_release);
-        }
-        cv_.notify_all();
-        run();
-        // the workers are awake (spinning or just woken) and the jobs are
-        // short: wait for the stragglers by polling
-        for (unsigned spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin)
-            if (spin > 4096) std::this_thread::yield();
-        job_ = nullptr;
-        if (err_) {
-            std::exception_ptr e = err_;
-            err_ = nullptr;
-            std::rethrow_exception(e);            // the first failure, on the caller
-        }
-    }
-
-    // fn(i) for i in [0, n) started on the workers; the caller goes on (e.g.
-    // launches GPU work) and then calls end(), which helps with what is left
-    // and waits.  false (nothing started) when the pool has no workers or is
-    // busy: the caller then uses parallel_for.  fn must outlive end().
-    bool begin(size_t n, const std::function<void(size_t)>& fn) {
-        if (workers_.empty() || n == 0) return false;
-        // held until end(): a plain try_lock / unlock pair (a shared
-        // std::unique_lock member raced between one caller's unlock and the
-        // next caller's acquire, which then ran two jobs at once)
-        if (!call_mu_.try_lock()) return false;
-        job_ = &fn;
-        n_ = n;
-        next_.store(0, std::memory_order_relaxed);
-        pending_.store(workers_.size(), std::memory_order_relaxed);
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            gen_.fetch_add(1, std::memory_order_release);
-        }
-        cv_.notify_all();
-        return true;
-    }
-    void end() {
-        run();
-        const auto t0 = Clock::now();
-        bool told = false;
-        for (unsigned spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin) {
-            if (spin > 4096) std::this_thread::yield();
-            if (!told && (spin & 65535) == 0 && spin && ms_since(t0) > 5000.0) {
-                fprintf(stderr, "gcr: host pool end(): %zu workers pending after 5 s\n",
-                        (size_t)pending_.load(std::memory_order_acquire));
-                told = true;
-            }
-        }
-        job_ = nullptr;
-        call_mu_.unlock();
-        if (err_) {
-            std::exception_ptr e = err_;
-            err_ = nullptr;
-            std::rethrow_exception(e);
-        }
-    }
-
-private:
-    void run() {
-        try {
-            for (size_t i; (i = next_.fetch_add(1)) < n_;) (*job_)(i);
-        } catch (...) {
-            std::lock_guard<std::mutex> lk(err_mu_);
-            if (!err_) err_ = std::current_exception();
-            next_.store(n_);                      // stop handing out work
-        }
-    }
-    // A worker polls for the next job for ~spin_us() after finishing one (the
-    // LO rounds call the pool every ~100 us: a condition-variable wake-up of
-    // 15 threads costs tens of us per call), then blocks.  GCR_POOL_SPIN_US
-    // sets the window (default 300, 0 = always block); while more than one
-    // thread of gcr_solve_batch is solving, workers block at once (their
-    // spinning would take cores from those threads).
-    static int64_t spin_us() {
-        static const int64_t us = [] {
-            const char* e = getenv("GCR_POOL_SPIN_US");
-            return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)300;
-        }();
-        return g_solving.load(std::memory_order_relaxed) > 1 ? 0 : us;
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            uint64_t g = gen_.load(std::memory_order_acquire);
-            if (g == seen) {
-                const auto t0 = Clock::now();
-                const int64_t window = spin_us();
-                unsigned k = 0;
-                while (window > 0 && (g = gen_.load(std::memory_order_acquire)) == seen) {
-                    if ((++k & 255) == 0 &&
-                        std::chrono::duration_cast<std::chrono::microseconds>(Clock::now() - t0).count() > window)
-                        break;
-#if defined(__x86_64__)
-                    __builtin_ia32_pause();
-#endif
-                }
-                if (g == seen) {
-                    std::unique_lock<std::mutex> lk(mu_);
-                    cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
-                    g = gen_.load(std::memory_order_acquire);
-                }
-            }
-            if (stop_) return;
-            seen = g;
-            run();
-            pending_.fetch_sub(1, std::memory_order_acq_rel);
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex mu_, call_mu_, err_mu_;
-    std::exception_ptr err_;
-    std::condition_variable cv_;
-    const std::function<void(size_t)>* job_ = nullptr;
-    size_t n_ = 0;
-    std::atomic<size_t> next_{0};
-    std::atomic<size_t> pending_{0};
-    std::atomic<uint64_t> gen_{0};
-    bool stop_ = false;
-};
-
 HostPool& host_pool() {
-    static HostPool pool([] {
-        const char* e = getenv("GCR_HOST_THREADS");
-        long n = e ? atol(e) : (long)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-        return (unsigned)std::max(1L, std::min(64L, n));
-    }());
+    static HostPool pool(
+        [] {
+            const char* e = getenv("GCR_HOST_THREADS");
+            long n = e ? atol(e) : (long)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+            return (unsigned)std::max(1L, std::min(64L, n));
+        }(),
+        &g_solving);
     return pool;
 }
 

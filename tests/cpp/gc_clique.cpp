@@ -7,16 +7,20 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <random>
 #include <vector>
 
-int main() {
+// optional argument: the number of random cells (default 2 M; the
+// sanitizer builds in tests/test_sanitizers.py run fewer)
+int main(int argc, char** argv) {
+    const long cells = argc > 1 ? atol(argv[1]) : 2000000;
     std::mt19937_64 rng(20261018);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     const double lams[] = {0.5, 0.975, 1.0, 1e-300, 1e300, 0.0, -1.0};
     gcr::CellScratch cs;
     long checked = 0, bad = 0, skipped = 0, one_source = 0;
-    for (long it = 0; it < 2000000; ++it) {
+    for (long it = 0; it < cells; ++it) {
         const uint32_t k = 3 + (uint32_t)(rng() % (it & 1 ? 6 : 38));
         const double sqt = (it & 7) == 0 ? 1.0 : 0.1 + 4.0 * U(rng);
         std::vector<double> r2(k), q(k);

@@ -11,14 +11,18 @@
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <random>
 #include <thread>
 
-int main() {
+// optional argument: the number of random grids (default 60; the sanitizer
+// builds in tests/test_sanitizers.py run fewer)
+int main(int argc, char** argv) {
+    const int grids = argc > 1 ? atoi(argv[1]) : 60;
     std::mt19937_64 rng(777);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     long bad = 0, runs = 0;
-    for (int it = 0; it < 60; ++it) {
+    for (int it = 0; it < grids; ++it) {
         const size_t n = 200 + rng() % 6000;
         const int clusters = 1 + (int)(rng() % 40);
         std::vector<double> cols[4];
