@@ -111,13 +111,13 @@ constexpr double kLn2LoT = cf(0x3d2ef35793c76730ull);
 
 // table log of a normal, finite, positive x, x = 2^k z, z in [OFF, 2 OFF),
 // OFF = 0x1.5fp-1 (1.0 in the middle of subinterval 80)
-GCR_HD double log_tab_core(uint64_t ix, int32_t kadj) {
+GCR_HD double log_tab_core(uint64_t ix, int32_t kadj, const double* __restrict__ tab = kLogTab) {
     constexpr uint64_t kOff = 0x3fe5f00000000000ull;
     const uint64_t tmp = ix - kOff;
     const uint32_t i = (uint32_t)(tmp >> 45) & 127u;
     const int32_t k = ((int32_t)(uint32_t)(tmp >> 32) >> 20) + kadj;   // the exponent of x / OFF (32-bit ops)
     const double z = as_f64(ix - (tmp & 0xfff0000000000000ull));
-    const double invc = kLogTab[2 * i], logc = kLogTab[2 * i + 1];
+    const double invc = tab[2 * i], logc = tab[2 * i + 1];
     const double r = fma_rn(z, invc, -1.0);                 // z / c - 1, one rounding
     const double kd = (double)k;
     const double w = fma_rn(kd, kLn2HiT, logc);              // k ln2hi exact
@@ -146,6 +146,14 @@ GCR_HD double dm_log(double x) {
     if (!(x >= 0x1p-1022 && x < HUGE_VAL)) return log_tab_special(x);
     return log_tab_core(as_u64(x), 0);
 }
+// the same log reading the table from a copy (k_score_fm keeps one in LDS:
+// a dependent lookup in L2 sat on the exact pass's critical path)
+GCR_HD double dm_log(double x, const double* __restrict__ tab) {
+    if (!(x >= 0x1p-1022 && x < HUGE_VAL)) return log_tab_special(x);
+    return log_tab_core(as_u64(x), 0, tab);
+}
+// the table's size in doubles (for such copies)
+constexpr int kLogTabSize = 256;
 
 // --------------------------------------------------------------- t^-3 -----
 // t^-3 = 1 / ((t*t)*t): two roundings in the cube and one in the IEEE

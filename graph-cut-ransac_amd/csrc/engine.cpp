@@ -407,8 +407,30 @@ inline void spin_pause() {
 
 // spin until a kernel has stored `epoch` into the coherent host flag; a
 // stream that drained (or failed) without it is an error, as is 5 s without it
+// A slow completion is not an error (a co-tenant process, or gcr_solve_batch's
+// threads sharing the hardware queues, can delay a valid kernel): the wait
+// goes on for as long as the stream runs -- as the hipStreamSynchronize it
+// replaces did -- and says so once on stderr after GCR_WAIT_WARN_MS (default
+// 5000; 0: never).  Errors come from hipStreamQuery.
+double wait_warn_ms() {
+    static const double v = [] {
+        const char* e = getenv("GCR_WAIT_WARN_MS");
+        return e ? atof(e) : 5000.0;
+    }();
+    return v;
+}
+void slow_wait_note(const char* what, Clock::time_point t0, bool& told) {
+    if (told) return;
+    const double lim = wait_warn_ms();
+    if (lim > 0.0 && ms_since(t0) > lim) {
+        fprintf(stderr, "gcr: %s still running after %.0f ms (waiting on)\n", what, lim);
+        told = true;
+    }
+}
+
 void wait_flag(const uint32_t* flag, uint32_t epoch, hipStream_t s, const char* what) {
     const auto t0 = Clock::now();
+    bool told = false;
     for (uint64_t it = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != epoch; ++it) {
         if ((it & 4095) == 0) {
             const hipError_t q = hipStreamQuery(s);
@@ -417,8 +439,7 @@ void wait_flag(const uint32_t* flag, uint32_t epoch, hipStream_t s, const char* 
                 throw std::runtime_error(std::string(what) + ": completion flag missing after the stream drained");
             }
             if (q != hipErrorNotReady) HIPC(q);
-            if (std::chrono::duration<double>(Clock::now() - t0).count() > 5.0)
-                throw std::runtime_error(std::string(what) + ": no completion after 5 s");
+            slow_wait_note(what, t0, told);
         }
         spin_pause();
     }
@@ -487,7 +508,42 @@ struct gcr_comm {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
     gcr_ctx* ctx = nullptr;
+    bool aborted = false;               // ncclCommAbort'ed after an error: every later run fails
 };
+
+namespace {
+// GCR_COMM_TIMEOUT_MS (read per wait): a collective's completion not seen
+// within this many ms is an error (0 / unset: no limit, the RCCL default)
+double comm_timeout_ms() {
+    const char* e = getenv("GCR_COMM_TIMEOUT_MS");
+    return e ? atof(e) : 0.0;
+}
+
+// Wait for an event behind a collective of `comm`, polling the
+// communicator's asynchronous error state (a peer that failed or left makes
+// RCCL report ncclRemoteError / ncclSystemError here instead of leaving the
+// kernel spinning).  Throws on an error or past the time limit; the caller's
+// error path then aborts the communicator (gcr_problem_run_comm).
+void comm_sync(hipEvent_t ev, ncclComm_t comm, const char* what) {
+    const auto t0 = Clock::now();
+    const double limit = comm_timeout_ms();
+    for (uint64_t it = 1;; ++it) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) hip_check(q, what);
+        if ((it & 255) == 0) {
+            ncclResult_t ae = ncclSuccess;
+            const ncclResult_t r = ncclCommGetAsyncError(comm, &ae);
+            if (r != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress))
+                throw std::runtime_error(std::string(what) + ": RCCL asynchronous error: " +
+                                         ncclGetErrorString(r != ncclSuccess ? r : ae));
+            if (limit > 0.0 && ms_since(t0) > limit)
+                throw std::runtime_error(std::string(what) + ": no completion within GCR_COMM_TIMEOUT_MS");
+            std::this_thread::yield();
+        }
+    }
+}
+}  // namespace
 
 struct gcr_problem {
     gcr_ctx* ctx = nullptr;
@@ -1158,15 +1214,18 @@ int make_problem(gcr_ctx* ctx, int solver, const double* f0, size_t n0, const do
         P->w = P->own.get();
     }
     await_spec(P->w);                   // a recycled workspace: its last speculative chunk reads feat
-    P->w->feat.ensure(total);
-    // the whole SoA image (pads zeroed) is staged in pinned memory and goes
-    // up in ONE copy (ten pageable copies cost ~150 us of a one-shot call)
-    P->w->feat_stage.ensure(total);
-    // the staging image of this workspace's previous upload must have been read
+    // this workspace's previous upload (queued, possibly never waited for:
+    // a problem created and destroyed without running) reads the staging
+    // image and writes the device SoA: it must be done before either buffer
+    // is reallocated below
     if (P->w->feat_ev_pending) {
         HIPC(hipEventSynchronize(P->w->feat_ev));
         P->w->feat_ev_pending = false;
     }
+    P->w->feat.ensure(total);
+    // the whole SoA image (pads zeroed) is staged in pinned memory and goes
+    // up in ONE copy (ten pageable copies cost ~150 us of a one-shot call)
+    P->w->feat_stage.ensure(total);
     if (g_lo_trace) st.emplace_back("ws", Clock::now());
     double* hst = P->w->feat_stage.p;
     const size_t off[2] = {0, 5 * np[0]};
@@ -1411,8 +1470,7 @@ struct GeoTraits {                 // homography (3) and fundamental matrix (4)
     static bool gen_compacts(uint32_t nh) {
         const char* e = getenv("GCR_GEN_COMPACT");
         if (e && e[0] == '0') return false;
-        const char* sc = getenv("GCR_SCORER");
-        return !(split_h(nh) == 16 && !(sc && sc[0] == 's'));
+        return !geo_scorer_scans(nh);
     }
     static hipError_t verify_gen(gcr_problem* P, uint64_t seed, uint64_t s0, uint32_t n, const VBufs& b,
                                  hipStream_t s) {
@@ -1863,7 +1921,8 @@ public:
         Workspace* w = P_->w;
         xlog(3, c.no, (uint64_t)c.set, 0);
         const auto t0 = Clock::now();
-        HIPC(hipEventSynchronize(w->sum_done[c.set]));
+        if (comm_) comm_sync(w->sum_done[c.set], comm_->comm, "chunk all-gather");
+        else HIPC(hipEventSynchronize(w->sum_done[c.set]));
         st_.ms_score += ms_since(t0);
         BlockSummary mine = empty_summary();
         if (rank_nslots(c, rank_) > 0) {
@@ -1903,7 +1962,7 @@ public:
             const auto t0 = Clock::now();
             exchange(c.set, side);
             HIPC(hipEventRecord(P_->ctx->ev1, side));
-            HIPC(hipEventSynchronize(P_->ctx->ev1));
+            comm_sync(P_->ctx->ev1, comm_->comm, "re-summary all-gather");
             st_.ms_score += ms_since(t0);
             for (int r = 0; r < world_; ++r) all[r] = w->hsum[c.set].p[1 + r];
             return;
@@ -3280,6 +3339,7 @@ private:
     void wait_done(const uint32_t* done, uint32_t n, uint32_t epoch) {
         uint32_t i = 0;
         const auto t0 = Clock::now();
+        bool told = false;
         for (uint64_t it = 1;; ++it) {
             while (i < n && __atomic_load_n(done + i, __ATOMIC_ACQUIRE) == epoch) ++i;
             if (i == n) break;
@@ -3295,12 +3355,7 @@ private:
                     throw std::runtime_error(msg);
                 }
                 if (q != hipErrorNotReady) HIPC(q);
-                if (ms_since(t0) > 5000.0) {
-                    char msg[160];
-                    snprintf(msg, sizeof(msg), "small scorer: no completion after 5 s (flag %u of %u is %u, expected %u)",
-                             i, n, __atomic_load_n(done + i, __ATOMIC_ACQUIRE), epoch);
-                    throw std::runtime_error(msg);
-                }
+                slow_wait_note("small scorer", t0, told);
             }
             spin_pause();
         }
@@ -3891,6 +3946,18 @@ int gcr_comm_create(gcr_ctx* ctx, int rank, int world, const uint8_t id[GCR_COMM
     });
 }
 
+namespace {
+void abort_comm(gcr_comm* comm, Workspace* w) {
+    if (comm->comm) (void)ncclCommAbort(comm->comm);
+    comm->comm = nullptr;
+    comm->aborted = true;
+    (void)hipStreamSynchronize(comm->ctx->side);
+    (void)hipStreamSynchronize(comm->ctx->stream);
+    (void)hipGetLastError();
+    for (int k = 0; k < 2; ++k) w->spec_pending[k] = false;
+}
+}  // namespace
+
 void gcr_comm_destroy(gcr_comm* comm) {
     if (!comm) return;
     (void)hipSetDevice(comm->ctx->device);
@@ -3898,7 +3965,7 @@ void gcr_comm_destroy(gcr_comm* comm) {
     // on the side stream (gcr_problem_run_comm also drains it; this covers a
     // caller that destroys the communicator first)
     (void)hipStreamSynchronize(comm->ctx->side);
-    if (comm->comm) (void)ncclCommDestroy(comm->comm);
+    if (comm->comm) (void)ncclCommDestroy(comm->comm);   // an aborted one is already gone
     delete comm;
 }
 
@@ -3908,6 +3975,7 @@ int gcr_problem_run_comm(gcr_problem* prob, const gcr_params* params, gcr_comm* 
     if (comm->ctx != prob->ctx) return set_err(GCR_EINVAL, "communicator and problem on different contexts");
     if (int e = check_params(params, prob->solver)) return e;
     if (!mask0_out || !H_out || (prob->K == 2 && !mask1_out)) return set_err(GCR_EINVAL, "null output buffer");
+    if (comm->aborted) return set_err(GCR_EINVAL, "communicator was aborted after an earlier error");
     return guard([&]() -> int {
         HIPC(hipSetDevice(prob->ctx->device));
         auto go = [&](auto&& r) {
@@ -3920,9 +3988,23 @@ int gcr_problem_run_comm(gcr_problem* prob, const gcr_params* params, gcr_comm* 
             fill_stats(stats_out, r.stats());
             return total;
         };
-        if (prob->solver == GCR_SOLVER_FUNDAMENTAL7) return go(FundRunner(prob, *params));
-        if (prob->solver == GCR_SOLVER_HOMOGRAPHY4) return go(GeoRunner(prob, *params));
-        return go(Runner(prob, *params));
+        try {
+            if (prob->solver == GCR_SOLVER_FUNDAMENTAL7) return go(FundRunner(prob, *params));
+            if (prob->solver == GCR_SOLVER_HOMOGRAPHY4) return go(GeoRunner(prob, *params));
+            return go(Runner(prob, *params));
+        } catch (...) {
+            // An error on this rank (a HIP or RCCL failure, a peer's failure
+            // seen by comm_sync, bad input found mid-run): the other ranks
+            // may be inside -- or about to issue -- the same collective, so
+            // the communicator is aborted rather than left half-used.  That
+            // ends this rank's queued collectives and tears down its
+            // connections, which the peers' RCCL proxies report as an
+            // asynchronous error to their own comm_sync waits, which then
+            // abort their communicators in turn.  The problem's chunk sets
+            // are drained and may be reused by a later single-rank run.
+            abort_comm(comm, prob->w);
+            throw;
+        }
     });
 }
 

@@ -264,6 +264,8 @@ hipError_t launch_generate_geo(const DevProblem& p, uint64_t seed, uint64_t slot
 // Hypotheses per workgroup of the batch scorers at a launch of nh (64, 16 or
 // 4; GCR_SPLIT_H pins one for sweeps).
 int split_h(uint32_t nh);
+// launch_score_geo(compact = true) compacts in the scorer's prologue at nh
+bool geo_scorer_scans(uint32_t nh);
 // compact: inc covers all nh hypotheses and the launch compacts them itself
 // (hmap / hcount written: in the scorer's prologue, or by k_compact first)
 hipError_t launch_score_geo(const DevProblem& p, double T, const GeoModel* models, const uint8_t* inc, uint32_t nh,

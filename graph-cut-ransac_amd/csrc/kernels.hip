@@ -488,6 +488,9 @@ struct GenArgs {
     // timing probes only (GCR_PROBE, results invalid when set): bit 0 skips
     // the chain fold, bit 1 the exact pass, bit 2 the band test, bit 3 the
     // prologue's attempts (every slot takes attempt 0's default model)
+    // k_score_fm: bit 8 no wait for the chain before the exact pass, bit 9
+    // no inlier-count atomics; valid A/B: bit 10 the rectification fp64
+    // bands instead of the packed fp32 pre-band
     uint32_t probe;
     GenChain chain;                     // k_score_fm<.., true>: batch chaining
     // k_score_fm, KIND >= 3: compact in the prologue instead of k_compact --
@@ -1123,6 +1126,121 @@ __device__ __forceinline__ void pb_test(const HPairBand& b, float x1, float y1, 
     hpb_test(b, x1, y1, x2, y2, r0, r1);
 }
 
+// Rectification (KIND <= 2): a conservative packed-fp32 pre-band in front of
+// the exact pass, two hypotheses per instruction, in place of the fp64 bands
+// scale_band / orient_band.  It rejects a pair only when the fp64 band
+// would reject it -- with every fp32 rounding bounded -- so the survivors
+// are a superset of the fp64 band's, and the exact pass decides them as
+// before (results unchanged; GCR_PROBE bit 10 runs the fp64 bands instead).
+// u = 2^-24 below; X, Y (and G = X + Y) are the class's largest |x|, |y|
+// (DevClass::amax, +inf when any coordinate is not finite: then nothing is
+// rejected).
+//
+// Scale: t = 1 - h7 x - h8 y in fp32 (two fma) is within 4u S of the real t
+// (S = |h7| X + |h8| Y + 1, input roundings included); tl = t - B, th = t + B
+// with B >= 6u S bracket the fp64 band's t strictly (its own error is
+// 3 2^-53 S).  A pair is rejected iff tl > 0 and s < lo'' tl^3 or
+// s > hi'' th^3, where lo'' = lo (1 - 2^-19) and hi'' = hi (1 + 2^-19)
+// (fp32 products: 4 roundings of s and of the cube, < 2^-20 in all) -- then
+// the fp64 band's t > 0, s > 0 and s < lo t^3 (or s > hi t^3) hold too.
+// Only scales in [2^-100, 2^100] are tested (others are NaN here: never
+// rejected), and only bands with lo, hi in [2^-20, 2^20] (else lo'' = 0,
+// hi'' = inf): an overflowing cube then means lo t^3 > 2^107 > s, an
+// underflowing one hi t^3 < 2^-105 < s.
+//
+// Orientation: with g = x st - y ct, numer = st - g h7, denom = ct + g h8,
+// U = denom cf + numer sf, V = numer cf - denom sf (the fp64 band's u, v
+// before |.|), every fp32 value is within E = 32u (G max(|h7|, |h8|) + 1)
+// (+ G 2^-140 for subnormal h, + 2^-90) of the real one.  A pair is rejected
+// iff |U| - T |V| > E' and |V| - T |U| > E' with T = tan_tau (1 + 2^-18)
+// rounded up and E' = E (1 + T) 1.01: then min(|u|, |v|) > tan_tau max and
+// max > 2^-900 hold in fp64 as well (its errors are ~2^-50 (G H + 1)).
+struct RPairBand {                 // hypotheses 2 j (.x) and 2 j + 1 (.y)
+    fpb_f2 nh7, nh8, tb, lo, hi;   // scale: -h7, -h8, B, lo'', hi''
+    fpb_f2 h7, h8, cf, sf, tq, eq; // orientation: h7, h8, cos / sin of phi (twin), T, E'
+    fpb_f2 pad[5];
+};
+static_assert(sizeof(RPairBand) == 16 * 8, "RPairBand layout: 16 float pairs");
+
+__device__ __forceinline__ void rpb_setup(RPairBand* rp, int t, const HypConst& q, const DevClass& c0,
+                                          const DevClass& c1, double tan_tau1, bool orient, bool valid) {
+    constexpr double u = 0x1p-24;
+    float* b = reinterpret_cast<float*>(&rp[t >> 1]);
+    const int hf = t & 1;                    // this thread's 4-byte half of each pair
+    if (!valid) {
+        // an invalid hypothesis (no model, or past the launch's count):
+        // t = 1, lo'' = inf rejects every scale in range; T = 0, E' = -1
+        // every finite direction (its results are discarded anyway; a NaN /
+        // out-of-range feature survives and only costs an exact evaluation)
+        const float c[11] = {0.0f, 0.0f, 0.0f, __builtin_inff(), __builtin_inff(), 0.0f, 0.0f, 1.0f, 0.0f, 0.0f,
+                             -1.0f};
+        for (int k = 0; k < 11; ++k) b[2 * k + hf] = c[k];
+        return;
+    }
+    const double a7 = __builtin_fabs(q.h7), a8 = __builtin_fabs(q.h8);
+    {
+        const double X = c0.amax[0], Y = c0.amax[1];
+        const double tb = 6.0 * u * ((a7 * X + a8 * Y) + 1.0) + (X + Y) * 0x1p-140;
+        b[2 * 0 + hf] = (float)(-q.h7);
+        b[2 * 1 + hf] = (float)(-q.h8);
+        b[2 * 2 + hf] = fpb_up(tb);          // +inf when not finite or huge: nothing rejected
+        const bool lo_ok = q.lo >= 0x1p-20 && q.lo <= 0x1p20;
+        const bool hi_ok = q.hi >= 0x1p-20 && q.hi <= 0x1p20;
+        b[2 * 3 + hf] = lo_ok ? (float)(q.lo * (1.0 - 0x1p-19)) : 0.0f;
+        b[2 * 4 + hf] = hi_ok ? (float)(q.hi * (1.0 + 0x1p-19)) : __builtin_inff();
+    }
+    if (orient) {
+        const double G = c1.amax[0] + c1.amax[1];
+        const double e = 32.0 * u * (G * __builtin_fmax(a7, a8) + 1.0) + G * 0x1p-140 + 0x1p-90;
+        const double tq = tan_tau1 * (1.0 + 0x1p-18);
+        b[2 * 5 + hf] = (float)q.h7;
+        b[2 * 6 + hf] = (float)q.h8;
+        b[2 * 7 + hf] = (float)q.cf;
+        b[2 * 8 + hf] = (float)q.sf;
+        b[2 * 9 + hf] = fpb_up(tq);
+        b[2 * 10 + hf] = fpb_up(e * (1.0 + tq) * 1.01);
+    }
+}
+
+// the fields of one class's test, read from LDS one pair ahead (the queue
+// writes in between are LDS stores the compiler cannot move reads across)
+struct RScaleC {
+    fpb_f2 nh7, nh8, tb, lo, hi;
+};
+struct ROrientC {
+    fpb_f2 h7, h8, cf, sf, tq, eq;
+};
+__device__ __forceinline__ RScaleC rpb_scale_c(const RPairBand& b) { return RScaleC{b.nh7, b.nh8, b.tb, b.lo, b.hi}; }
+__device__ __forceinline__ ROrientC rpb_orient_c(const RPairBand& b) {
+    return ROrientC{b.h7, b.h8, b.cf, b.sf, b.tq, b.eq};
+}
+
+// reject masks (ballots) of the pair's two hypotheses; sf: the scale in fp32,
+// NaN when outside [2^-100, 2^100]
+__device__ __forceinline__ void rpb_scale(const RScaleC& b, float x, float y, float sf, uint64_t& r0,
+                                          uint64_t& r1) {
+    const fpb_f2 X = {x, x}, Y = {y, y}, one = {1.0f, 1.0f};
+    const fpb_f2 t = fpb_fma(b.nh7, X, fpb_fma(b.nh8, Y, one));
+    const fpb_f2 tl = t - b.tb, th = t + b.tb;
+    const fpb_f2 a = ((tl * tl) * tl) * b.lo;
+    const fpb_f2 c = ((th * th) * th) * b.hi;
+    r0 = __builtin_amdgcn_ballot_w64(tl.x > 0.0f) &
+         (__builtin_amdgcn_ballot_w64(sf < a.x) | __builtin_amdgcn_ballot_w64(sf > c.x));
+    r1 = __builtin_amdgcn_ballot_w64(tl.y > 0.0f) &
+         (__builtin_amdgcn_ballot_w64(sf < a.y) | __builtin_amdgcn_ballot_w64(sf > c.y));
+}
+
+__device__ __forceinline__ void rpb_orient(const ROrientC& b, float g, float ct, float st, uint64_t& r0,
+                                           uint64_t& r1) {
+    const fpb_f2 G = {g, g}, ST = {st, st}, CT = {ct, ct};
+    const fpb_f2 N = fpb_fma(-G, b.h7, ST), D = fpb_fma(G, b.h8, CT);
+    const fpb_f2 U = __builtin_elementwise_abs(fpb_fma(D, b.cf, N * b.sf));
+    const fpb_f2 V = __builtin_elementwise_abs(fpb_fma(N, b.cf, -(D * b.sf)));
+    const fpb_f2 P1 = fpb_fma(-b.tq, V, U), P2 = fpb_fma(-b.tq, U, V);
+    r0 = __builtin_amdgcn_ballot_w64(P1.x > b.eq.x) & __builtin_amdgcn_ballot_w64(P2.x > b.eq.x);
+    r1 = __builtin_amdgcn_ballot_w64(P1.y > b.eq.y) & __builtin_amdgcn_ballot_w64(P2.y > b.eq.y);
+}
+
 template <int KIND, int H, bool kGen>
 __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(KIND >= 3 ? 8 : 1))) void k_score_fm(DevProblem p, double T0, double T1, double band0,
                                                             double tan_tau1, FlagBand fband,
@@ -1144,12 +1262,16 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     static_assert(!kDyn || fm_dyn_lds_bytes<H, kGen>() == (size_t)kW * H * kReg * 8 + (size_t)kW * kCap * 2,
                   "dynamic LDS layout");
     __shared__ double2 outv_st[kDyn ? 1 : kW][H][kReg / 2];
-    __shared__ uint16_t queue_st[kDyn ? 1 : kW][kCap];  // survivors: q | lane << 4 | k << 10
+    // survivors: q | lane << 4 | k << 10; the rectification pre-band's
+    // branch-free writes put non-survivors in 32 spare entries per wave
+    // (lanes l and l + 32 share one: either value may land, neither is read)
+    constexpr int kQStride = kDyn ? kCap : kCap + 32;
+    __shared__ uint16_t queue_st[kDyn ? 1 : kW][kQStride];
     extern __shared__ double2 fm_dyn_lds[];
     double2 (*const outv)[H][kReg / 2] =
         kDyn ? reinterpret_cast<double2 (*)[H][kReg / 2]>(fm_dyn_lds) : outv_st;
-    uint16_t (*const queue)[kCap] =
-        kDyn ? reinterpret_cast<uint16_t (*)[kCap]>(fm_dyn_lds + (size_t)kW * H * (kReg / 2)) : queue_st;
+    uint16_t (*const queue)[kQStride] =
+        kDyn ? reinterpret_cast<uint16_t (*)[kQStride]>(fm_dyn_lds + (size_t)kW * H * (kReg / 2)) : queue_st;
     __shared__ uint32_t wcnt[2][kW][H];                 // survivors of (wave, q) in the round
     __shared__ uint32_t ready[kW], done[kW];
     __shared__ HypConst hyp[H];
@@ -1157,7 +1279,15 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     __shared__ uint32_t cnt_sh[2][H];
     __shared__ uint32_t fl_sh[H];                       // flagged pairs (exact.h), rectification solvers
     using PairBand = std::conditional_t<KIND == 3, HPairBand, FPairBand>;
-    __shared__ PairBand fpb[KIND >= 3 ? (H + 1) / 2 : 1];
+    static_assert(KIND >= 3 || (H & 1) == 0, "rectification pre-band: hypotheses in pairs");
+    static_assert(sizeof(PairBand) == sizeof(RPairBand), "pair-band records share one LDS array");
+    // the correspondence pre-band records or the rectification ones
+    __shared__ RPairBand pb_st[(H + 1) / 2];
+    PairBand* const fpb = reinterpret_cast<PairBand*>(pb_st);
+    RPairBand* const rpb = pb_st;
+    // the value log's table (detmath.h) in LDS: the fused variant has the
+    // room (the others read it from L2)
+    __shared__ double logtab_sh[kGen ? dm::kLogTabSize : 1];
     __shared__ int gen_a[kGen ? H : 1];
     __shared__ RectModel gen_m[kGen ? H : 1];
     __shared__ double fin_sh[kGen ? H : 1];
@@ -1275,6 +1405,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             else m = models[mi];
         }
         hyp[t] = make_hyp<KIND>(m, band0);
+        if constexpr (KIND <= 2) rpb_setup(rpb, t, hyp[t], p.cls[0], p.cls[1], tan_tau1, KIND == 2, v);
         if constexpr (KIND == 4) fpb_setup(fpb, t, m.h, v, T0, p.cls[0]);
         if constexpr (KIND == 3) hpb_setup(fpb, t, m.h, v, band0, p.cls[0]);
         hval[t] = v ? 1u : 0u;
@@ -1289,6 +1420,10 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
         if ((H & 1) && t == H) hpb_setup(fpb, t, hyp[0].g, false, band0, p.cls[0]);
     }
     GCR_STAMP(6, 15u);
+    if constexpr (kGen) {
+        for (int i = t; i < dm::kLogTabSize; i += kSplitThreads) logtab_sh[i] = dm::kLogTab[i];
+    }
+    const double* const logtab = kGen ? logtab_sh : dm::kLogTab;
     if (t < kW) { ready[t] = 0; done[t] = 0; }
     __syncthreads();
     GCR_STAMP(7, 15u);
@@ -1474,6 +1609,64 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                         qn += c;
                     }
                 }
+                } else if (!(gen.probe & 1024u)) {
+                    // rectification: the packed fp32 pre-band (above), two
+                    // hypotheses per pass; every mask a direct compare ballot
+                    const uint64_t okm = (gen.probe & 4u) ? 0ull : __builtin_amdgcn_ballot_w64(ok);
+                    float pa = 0.0f, pb = 0.0f, pc = 0.0f;
+                    if (cls == 0) {
+                        pa = (float)f0;
+                        pb = (float)f1;
+                        pc = (f2 >= 0x1p-100 && f2 <= 0x1p100) ? (float)f2 : __builtin_nanf("");
+                    } else {
+                        const float xf = (float)f0, yf = (float)f1;
+                        pb = (float)f2;                     // cos theta
+                        pc = (float)f3;                     // sin theta
+                        pa = __builtin_fmaf(xf, pc, -(yf * pb));   // g = x st - y ct
+                    }
+                    // one survivor record per hypothesis, branch-free (one
+                    // basic block per class for all H, so the scheduler
+                    // overlaps the pairs): a non-survivor lane writes its
+                    // entry to a spare slot; invalid hypotheses reject every
+                    // feature by their constants (rpb_setup)
+                    auto emit = [&](auto qc, uint64_t rej) {
+                        constexpr int q = decltype(qc)::value;
+                        const uint64_t m = okm & ~rej;
+                        const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        const bool cand = __builtin_amdgcn_inverse_ballot_w64(m);
+                        qw[cand ? qn + k : (uint32_t)(kCap + (lane & 31))] = (uint16_t)(q | (lane << 4) | (k << 10));
+                        const uint32_t c = (uint32_t)__builtin_popcountll(m);
+                        my_n = write_lane<q>(my_n, c);
+                        qn += c;
+                    };
+                    // the next pair's constants are read before this pair's
+                    // queue writes (the reads cannot be moved across them)
+                    if (cls == 0) {
+                        RScaleC cur = rpb_scale_c(rpb[0]);
+                        static_for<0, H / 2>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            RScaleC nxt = cur;
+                            if constexpr (j + 1 < H / 2) nxt = rpb_scale_c(rpb[j + 1]);
+                            uint64_t r0, r1;
+                            rpb_scale(cur, pa, pb, pc, r0, r1);
+                            emit(std::integral_constant<int, 2 * j>{}, r0);
+                            emit(std::integral_constant<int, 2 * j + 1>{}, r1);
+                            cur = nxt;
+                        });
+                    } else {
+                        ROrientC cur = rpb_orient_c(rpb[0]);
+                        static_for<0, H / 2>([&](auto jc) {
+                            constexpr int j = decltype(jc)::value;
+                            ROrientC nxt = cur;
+                            if constexpr (j + 1 < H / 2) nxt = rpb_orient_c(rpb[j + 1]);
+                            uint64_t r0, r1;
+                            rpb_orient(cur, pa, pb, pc, r0, r1);
+                            emit(std::integral_constant<int, 2 * j>{}, r0);
+                            emit(std::integral_constant<int, 2 * j + 1>{}, r1);
+                            cur = nxt;
+                        });
+                    }
                 } else if (cls == 0) {
                     run_band([&](int q) { return C4{hyp[q].h7, hyp[q].h8, hyp[q].lo, hyp[q].hi}; },
                              [&](const C4& c) {
@@ -1503,6 +1696,13 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                 double x, y, a2, a3;
                 uint32_t e;
             };
+            // the round's class columns, selected once (uniform pointers:
+            // no per-batch address arithmetic on a class index)
+            const double* const fx = cls == 0 ? p.cls[0].x : p.cls[1].x;
+            const double* const fy = cls == 0 ? p.cls[0].y : p.cls[1].y;
+            const double* const fa2 = cls == 0 ? p.cls[0].a : p.cls[1].c0;
+            const double* const fa3 = KIND >= 3 ? p.cls[0].c0 : p.cls[1].c1;
+            const uint32_t fbase = (cls == 0 ? r : r - r0) * kRound + wave * 64;
             auto fetch = [&](uint32_t j0) {
                 Surv sv;
                 const uint32_t j = j0 + lane;
@@ -1517,13 +1717,11 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                     if (KIND >= 3 || cls == 1) sv.a3 = __shfl(f3, src);
                 } else {
                     // ... or re-read from L2 (keeps the LDS pipe to the chain)
-                    const DevClass& c = p.cls[cls];
-                    const uint32_t fi = (cls == 0 ? r : r - r0) * kRound + wave * 64 + src;
-                    sv.x = c.x[fi];
-                    sv.y = c.y[fi];
-                    sv.a2 = cls == 0 ? c.a[fi] : c.c0[fi];
-                    if (KIND >= 3) sv.a3 = c.c0[fi];
-                    else if (cls == 1) sv.a3 = c.c1[fi];
+                    const uint32_t fi = fbase + (uint32_t)src;
+                    sv.x = fx[fi];
+                    sv.y = fy[fi];
+                    sv.a2 = fa2[fi];
+                    if (KIND >= 3 || cls == 1) sv.a3 = fa3[fi];
                 }
                 return sv;
             };
@@ -1532,7 +1730,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             Surv cur{0.0, 0.0, 0.0, 0.0, 0u};
             if (ahead && qn > 0) cur = fetch(0);
             // the chain has folded this wave's previous runs (outv reuse)
-            if (r > 0) fm_wait_ge(&done[wave], r);
+            if (r > 0 && !(gen.probe & 256u)) fm_wait_ge(&done[wave], r);
             GCR_STAMP(2, r);
             double* ow = reinterpret_cast<double*>(&outv[wave][0][0]);
             for (uint32_t j0 = 0; j0 < qn; j0 += 64) {
@@ -1554,7 +1752,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                         m.h7 = hq.h7;
                         m.h8 = hq.h8;
                         if (cls == 0) {
-                            r2 = scale_sq_value<KIND == 1, true>(cur.x, cur.y, cur.a2, m, hq.ac, hq.cut);
+                            r2 = scale_sq_value<KIND == 1, true>(cur.x, cur.y, cur.a2, m, hq.ac, hq.cut, logtab);
                             inl = r2 <= T0;
                         } else {
                             r2 = orient_sq_value<true>(cur.x, cur.y, cur.a2, cur.a3, m, hq.cf, hq.sf, hq.cphi, hq.cphi2);
@@ -1562,7 +1760,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                         }
                     }
                     ow[q * kReg + k] = inl ? -r2 : 0.0;
-                    if (inl) atomicAdd(&cnt_sh[cls][q], 1u);
+                    if (inl && !(gen.probe & 512u)) atomicAdd(&cnt_sh[cls][q], 1u);
                     // a decision the host rechecks with glibc (exact.h); rare
                     if (KIND <= 2 && in_flag_band(r2, fband.mid[cls], fband.half[cls])) atomicAdd(&fl_sh[q], 1u);
                 }
@@ -2528,8 +2726,8 @@ __device__ __forceinline__ void lo_approx_reduce(const DevProblem& p, uint32_t m
 // are stored write-through (sc1) and drained, the workgroup counts itself in
 // on the model's arrival counter, and the model's last workgroup reduces
 // them with sc1 loads (lo_approx_reduce) -- k_lo_approx's work, without the
-// second launch and without a release fence (MI355X guide, inter-workgroup
-// hand-off by write-through stores)
+// second launch; the arrival is an agent-scope release / acquire pair, as in
+// k_lo_split (opt-in, GCR_LO_APPROX_FUSE=1: measured slower than two launches)
 template <int KIND, bool kFuse = false>
 __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typename ModelOf<KIND>::type* __restrict__ models,
                                                         const uint8_t* __restrict__ inc, double T0, double T1,
@@ -2571,13 +2769,18 @@ __global__ __launch_bounds__(kLrThreads) void k_lo_resid(DevProblem p, const typ
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            const uint32_t prev = __hip_atomic_fetch_add(p.lo.arrive + mi, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // release at agent scope: this workgroup's chunk results before
+            // its arrival (the write-through stores alone are not ordered by
+            // the memory model)
+            const uint32_t prev = __hip_atomic_fetch_add(p.lo.arrive + mi, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
             last_sh = prev + 1u == gridDim.x ? 1u : 0u;
             if (last_sh) __hip_atomic_store(p.lo.arrive + mi, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         if (!last_sh) return;                                // workgroup-uniform
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the loads below the arrival
+        // acquire at agent scope: every other workgroup's released results
+        // are visible to the reduction's loads (k_lo_split's pattern)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         lo_approx_reduce<KIND>(p, mi, pad0, nchunks, aout, true);
     }
 }
@@ -4046,6 +4249,12 @@ bool use_fm() {
     }();
     return fm;
 }
+
+// the correspondence scorer compacts a launch of nh hypotheses itself, in
+// the feature-major scorer's prologue (launch_score_geo with compact = true
+// at H = 16); the engine's verify pipeline compacts behind the generator
+// otherwise.  One cached source (use_fm) for both sides.
+bool geo_scorer_scans(uint32_t nh) { return use_fm() && split_h(nh) == 16; }
 
 template <int H, bool kGen>
 void launch_fm_t(const DevProblem& p, const double T[2], uint32_t nh, const ScoreOut& out, const GenArgs& g,

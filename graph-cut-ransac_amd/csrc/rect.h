@@ -185,7 +185,8 @@ GCR_HD ValueConst value_const(const RectModel& m, bool original, bool orient) {
 }
 
 template <bool kOriginal, bool kIdentity>
-GCR_HD double scale_sq_value(double x, double y, double sc, const RectModel& m, double ac, double cut) {
+GCR_HD double scale_sq_value(double x, double y, double sc, const RectModel& m, double ac, double cut,
+                             const double* __restrict__ logtab = dm::kLogTab) {
     double px = x, py = y, ps = sc;
     if (!kIdentity) {
         px = m.s * (x - m.x0 * 1.0);
@@ -196,7 +197,7 @@ GCR_HD double scale_sq_value(double x, double y, double sc, const RectModel& m, 
     const double u = (t * t) * t;
     const double arg = kOriginal ? ps / (ac * u) : (ac * ps) / u;
     if (!(arg >= cut)) return DBL_MAX * DBL_MAX;          // the cut, negative, NaN: outlier
-    const double r = __builtin_fabs(dm::dm_log(arg));
+    const double r = __builtin_fabs(dm::dm_log(arg, logtab));
     return r * r;
 }
 

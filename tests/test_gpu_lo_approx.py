@@ -60,12 +60,56 @@ def test_approx_modes_agree(monkeypatch, kind, seed, n):
     assert res["1u"][-1]["lo_refolds"] == res["1"][-1]["lo_refolds"]
 
 
+_STATS = ("iteration_number", "local_optimization_number", "graph_cut_number", "slots", "hypotheses")
+
+
+def _model7(m):
+    return np.array([m.x0, m.y0, m.s, m.h7, m.h8, m.alpha, m.phi])
+
+
+def _assert_glibc(out, g):
+    H, ms, mo, model, st = out
+    assert np.array_equal(ms, g["scale_mask"]) and np.array_equal(mo, g["orientation_mask"])
+    assert np.array_equal(_model7(model), O.model7(g["model"]))
+    assert np.array_equal(H, g["H"])
+    assert [st[k] for k in _STATS] == [g["stats"][k] for k in _STATS]
+
+
 def test_approx_matches_oracle():
     fs, fo, ts, to, t0, t1 = S.problem_m2(3000, 3000, seed=17)
-    H, ms, mo, model, st = pygcransac.findRectifyingHomographySIFT(fs, fo, t0, t1, 0.0, 1000, 1000, 50, seed=17,
-                                                                   device=0, return_stats=True)
+    out = pygcransac.findRectifyingHomographySIFT(fs, fo, t0, t1, 0.0, 1000, 1000, 50, seed=17, device=0,
+                                                  return_stats=True)
+    H, ms, mo, model, st = out
+    # the reference's arithmetic: masks, model and homography bits, statistics
+    g = O.rect_sift(fs, fo, t0, t1, min_it=1000, max_it=1000, lo=50, seed=17, math_mode=O.MATH_GLIBC)
+    _assert_glibc(out, g)
+    # TWIN mode: the same decisions with the product's value score, bit for bit
     tw = O.rect_sift(fs, fo, t0, t1, min_it=1000, max_it=1000, lo=50, seed=17, math_mode=O.MATH_TWIN)
     assert st["score"] == tw["stats"]["score"]
     assert st["local_optimization_number"] == tw["stats"]["local_optimization_number"]
     assert st["graph_cut_number"] == tw["stats"]["graph_cut_number"]
     assert st["near_ties"] == tw["stats"]["near_ties"]
+
+
+def test_approx_at_boundary_thresholds(monkeypatch):
+    """Thresholds between the glibc and twin r^2 of pairs near the threshold
+    under the first chain member of the run (gcr_testutil.first_member_model:
+    a decision every run with this seed takes): the approximate LO
+    comparisons still give GLIBC mode's run, with some decision taken in
+    glibc on the host (test_gpu_glibc.py shows such cases change the result
+    when the twins decide, GCR_EXACT=0)."""
+    from gcr_testutil import boundary_thresholds, first_member_model
+    from pygcransac import _native as N
+
+    fs, fo, ts, to, t0, t1 = S.problem_m2(3000, 3000, seed=17)
+    m = first_member_model(O, N.SOLVER_SIFT22, fs, fo, t0, t1, 17)
+    cases = boundary_thresholds(O, N.SOLVER_SIFT22, fs, fo, t0, t1, m, per_class=2, window=1.0)
+    assert cases
+    pairs = 0
+    for cls, i, a, b in cases:
+        g = O.rect_sift(fs, fo, a, b, min_it=1000, max_it=1000, lo=50, seed=17, math_mode=O.MATH_GLIBC)
+        out = pygcransac.findRectifyingHomographySIFT(fs, fo, a, b, 0.0, 1000, 1000, 50, seed=17, device=0,
+                                                      return_stats=True)
+        _assert_glibc(out, g)
+        pairs += out[-1]["exact_pairs"]
+    assert pairs > 0

@@ -128,3 +128,91 @@ def test_engine_comm_world1_equals_single_rank(kind, budget, monkeypatch):
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
     _sharded_vs_single(kind, budget, monkeypatch, {})
     _sharded_vs_single(kind, budget, monkeypatch, {"GCR_SUMMARY_CAP": "1"})
+
+
+# -------------------------------------------- engine communicator, world 2 ----
+# Two ranks on two GPUs: fresh processes, each
+# binding its own GPU before any HIP call, exchange over gcr_comm (RCCL inside
+# libgcr) and over the gloo callback; both ranks must return the single-rank
+# run bit for bit and log the same exchange sequence.  Runs only where two or
+# more GPUs are visible (the driver's multi-GPU node); the one-GPU box skips.
+CHILD2 = textwrap.dedent("""
+    import json, os, sys
+    import numpy as np
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    os.environ["GCR_EXCHANGE_LOG"] = "1"
+    sys.path.insert(0, os.environ["GCR_PKG"])
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + os.environ["GCR_PORT"], rank=rank,
+                            world_size=world)
+    from pygcransac import _native as N
+    from pygcransac import distributed as D
+    from pygcransac import synthetic as S
+    fs, fo, _, _, t0, t1 = S.problem_m2(1500, 1300, seed=61)
+    params = dict(scale_residual_thresh=t0, orientation_residual_thresh=t1, seed=11,
+                  min_iteration_number=0, max_iteration_number=10**7, confidence=0.99)
+    out = {}
+    comm = D.Comm(dist, rank, world, device=rank)
+    try:
+        H, masks, st, rec = D.run_problem_sharded(N.SOLVER_SIFT22, fs, fo, params, rank, world, device=rank,
+                                                  comm=comm)
+        out["comm_log"] = [list(map(int, x)) for x in N.exchange_log()]
+    finally:
+        comm.close()
+    H2, masks2, st2, rec2 = D.run_problem_sharded(N.SOLVER_SIFT22, fs, fo, params, rank, world, dist=dist,
+                                                  device=rank)
+    out["cb_log"] = [list(map(int, x)) for x in N.exchange_log()]
+    out["H"] = np.asarray(H).view(np.uint64).tolist()
+    out["H2"] = np.asarray(H2).view(np.uint64).tolist()
+    out["masks"] = [np.asarray(m).tolist() for m in masks]
+    out["masks2"] = [np.asarray(m).tolist() for m in masks2]
+    out["stats"] = {k: st[k] for k in ("iteration_number", "hypotheses", "slots", "local_optimization_number",
+                                        "graph_cut_number")}
+    out["score"] = float(st["score"]).hex()
+    dist.barrier()
+    dist.destroy_process_group()
+    print("RESULT " + json.dumps(out))
+""")
+
+
+def _gpu_count_without_hip():
+    # torch.cuda.device_count() does not initialise HIP on this image, so the
+    # children below start on an untouched runtime either way
+    import torch
+
+    return torch.cuda.device_count()
+
+
+@pytest.mark.timeout(600)
+def test_engine_comm_world2_equals_single_rank():
+    if _gpu_count_without_hip() < 2:
+        pytest.skip("two GPUs needed for a world-2 RCCL run (this box has one)")
+    import json
+
+    import numpy as np
+
+    port = str(_free_port())
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, GCR_PKG=PKG, GCR_PORT=port, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1")
+        procs.append(subprocess.Popen([sys.executable, "-c", CHILD2], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    res = []
+    for p in procs:
+        o, e = p.communicate(timeout=540)
+        assert p.returncode == 0, o[-2000:] + e[-3000:]
+        res.append(json.loads(o.split("RESULT ", 1)[1]))
+    # the single-rank run in this process
+    from pygcransac import distributed as D
+    from pygcransac import synthetic as S
+
+    fs, fo, _, _, t0, t1 = S.problem_m2(1500, 1300, seed=61)
+    params = dict(scale_residual_thresh=t0, orientation_residual_thresh=t1, seed=11,
+                  min_iteration_number=0, max_iteration_number=10**7, confidence=0.99)
+    H, masks, st, _ = D.run_problem_sharded(N.SOLVER_SIFT22, fs, fo, params, 0, 1, device=0)
+    for r in res:
+        assert r["comm_log"] and r["comm_log"] == r["cb_log"] == res[0]["comm_log"]
+        assert r["H"] == r["H2"] == np.asarray(H).view(np.uint64).tolist()
+        assert r["masks"] == r["masks2"] == [np.asarray(m).tolist() for m in masks]
+        assert r["stats"] == {k: st[k] for k in r["stats"]}
+        assert r["score"] == float(st["score"]).hex()

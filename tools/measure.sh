@@ -1,11 +1,13 @@
 #!/bin/bash
-# round-5 measurement session: GPU suite, smoke, driver-shaped bench line (M2
-# with the latency leg and the CPU baseline), F line, rocprofv3 kernel stats
-# of both, PMC passes of both (tools/pmc_sets_r4.txt, one rocprofv3 run per
-# counter set).  Every GPU step has its own time limit; any failure ends it.
+# Measurement session (any round): GPU suite, smoke, the driver-shaped bench
+# line (M2 with the latency leg and the CPU baseline), the F line, rocprofv3
+# kernel stats of both, and the PMC passes of both (tools/pmc_sets_r4.txt, one
+# rocprofv3 run per counter set).  Every GPU step has its own time limit; any
+# failure ends the session.
+#   OUT=gpurun_out/<dir> PART=run|prof|all tools/measure.sh
 # PART=run: suite, smoke, bench lines; PART=prof: kernel stats and PMC passes.
 set -u
-O=${OUT:-gpurun_out/r5_final}; mkdir -p $O
+O=${OUT:-gpurun_out/measure}; mkdir -p $O
 step() { echo "== $1"; }
 PART=${PART:-all}
 if [ "$PART" != "prof" ]; then
