@@ -1703,6 +1703,8 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             const double* const fa2 = cls == 0 ? p.cls[0].a : p.cls[1].c0;
             const double* const fa3 = KIND >= 3 ? p.cls[0].c0 : p.cls[1].c1;
             const uint32_t fbase = (cls == 0 ? r : r - r0) * kRound + wave * 64;
+            const double fl_mid = cls == 0 ? fband.mid[0] : fband.mid[1];
+            const double fl_half = cls == 0 ? fband.half[0] : fband.half[1];
             auto fetch = [&](uint32_t j0) {
                 Surv sv;
                 const uint32_t j = j0 + lane;
@@ -1762,7 +1764,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                     ow[q * kReg + k] = inl ? -r2 : 0.0;
                     if (inl && !(gen.probe & 512u)) atomicAdd(&cnt_sh[cls][q], 1u);
                     // a decision the host rechecks with glibc (exact.h); rare
-                    if (KIND <= 2 && in_flag_band(r2, fband.mid[cls], fband.half[cls])) atomicAdd(&fl_sh[q], 1u);
+                    if (KIND <= 2 && in_flag_band(r2, fl_mid, fl_half)) atomicAdd(&fl_sh[q], 1u);
                 }
                 cur = nxt_s;
             }
