@@ -406,7 +406,7 @@ inline void spin_pause() {
 }
 
 // spin until a kernel has stored `epoch` into the coherent host flag; a
-// stream that drained (or failed) without it is an error, as is 5 s without it
+// stream that drained (or failed) without it is an error.
 // A slow completion is not an error (a co-tenant process, or gcr_solve_batch's
 // threads sharing the hardware queues, can delay a valid kernel): the wait
 // goes on for as long as the stream runs -- as the hipStreamSynchronize it

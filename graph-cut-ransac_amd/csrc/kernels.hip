@@ -921,7 +921,22 @@ __device__ __forceinline__ uint64_t stamp_now() {
         if (blockIdx.x < kStWG && (rr) < (uint32_t)kStRounds && lane == 0)                    \
             g_stamps[blockIdx.x][wave][rr][slot] = (v);                                       \
     } while (0)
+// every workgroup's start and end on the global 100 MHz clock (s_memrealtime),
+// last launch only (tools/wg_spans.py: the spread behind a launch's tail)
+constexpr int kSpanWG = 4096;
+__device__ uint64_t g_wgspan[kSpanWG][2];
+__device__ __forceinline__ uint64_t realtime_now() {
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define GCR_WGSPAN(i)                                                                         \
+    do {                                                                                      \
+        const uint64_t _t = realtime_now();                                                   \
+        if (blockIdx.x < (uint32_t)kSpanWG && (threadIdx.x & 63) == 0) g_wgspan[blockIdx.x][i] = _t; \
+    } while (0)
 #else
+#define GCR_WGSPAN(i) do {} while (0)
 #define GCR_STAMP(slot, rr) do {} while (0)
 #define GCR_STAMP_VAL(slot, rr, v) do {} while (0)
 #endif
@@ -1352,6 +1367,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
         }
     }
     GCR_STAMP(5, 15u);
+    if (threadIdx.x == 0) GCR_WGSPAN(0);
     // ---- prologue: this workgroup's H slots (kGen), k_generate's rule, or
     // (chained batches) the previous launch's look-ahead wave's results
     if constexpr (kGen) {
@@ -1695,6 +1711,9 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             struct Surv {
                 double x, y, a2, a3;
                 uint32_t e;
+#ifdef GCR_FM_HQ_AHEAD
+                double h7, h8, c0, c1, c2, c3;    // the entry's hypothesis constants, read with it
+#endif
             };
             // the round's class columns, selected once (uniform pointers:
             // no per-batch address arithmetic on a class index)
@@ -1725,11 +1744,28 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                     sv.a2 = fa2[fi];
                     if (KIND >= 3 || cls == 1) sv.a3 = fa3[fi];
                 }
+#ifdef GCR_FM_HQ_AHEAD
+                if constexpr (KIND <= 2) {
+                    const HypConst& hq = hyp[sv.e & 15u];
+                    sv.h7 = hq.h7;
+                    sv.h8 = hq.h8;
+                    if (cls == 0) {
+                        sv.c0 = hq.ac;
+                        sv.c1 = hq.cut;
+                        sv.c2 = sv.c3 = 0.0;
+                    } else {
+                        sv.c0 = hq.cf;
+                        sv.c1 = hq.sf;
+                        sv.c2 = hq.cphi;
+                        sv.c3 = hq.cphi2;
+                    }
+                }
+#endif
                 return sv;
             };
             // GCR_PROBE bit 6: no look-ahead (each batch fetched when used)
             const bool ahead = KIND < 3 && !(gen.probe & 64u);     // (registers, see above)
-            Surv cur{0.0, 0.0, 0.0, 0.0, 0u};
+            Surv cur{};
             if (ahead && qn > 0) cur = fetch(0);
             // the chain has folded this wave's previous runs (outv reuse)
             if (r > 0 && !(gen.probe & 256u)) fm_wait_ge(&done[wave], r);
@@ -1751,6 +1787,17 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                         inl = r2 <= T0;
                     } else {
                         RectModel m = default_model();
+#ifdef GCR_FM_HQ_AHEAD
+                        m.h7 = cur.h7;
+                        m.h8 = cur.h8;
+                        if (cls == 0) {
+                            r2 = scale_sq_value<KIND == 1, true>(cur.x, cur.y, cur.a2, m, cur.c0, cur.c1, logtab);
+                            inl = r2 <= T0;
+                        } else {
+                            r2 = orient_sq_value<true>(cur.x, cur.y, cur.a2, cur.a3, m, cur.c0, cur.c1, cur.c2, cur.c3);
+                            inl = r2 <= T1;
+                        }
+#else
                         m.h7 = hq.h7;
                         m.h8 = hq.h8;
                         if (cls == 0) {
@@ -1760,6 +1807,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                             r2 = orient_sq_value<true>(cur.x, cur.y, cur.a2, cur.a3, m, hq.cf, hq.sf, hq.cphi, hq.cphi2);
                             inl = r2 <= T1;
                         }
+#endif
                     }
                     ow[q * kReg + k] = inl ? -r2 : 0.0;
                     if (inl && !(gen.probe & 512u)) atomicAdd(&cnt_sh[cls][q], 1u);
@@ -1822,11 +1870,12 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                 const bool nhave = w + 1 < kW && ((rmask >> (w + 1)) & 1ull);
                 const uint32_t nn = nhave ? wcnt[r & 1][w + 1][h] : 0u;
                 if (fold_on) {
-                    // whole batches of kFmCB 16-byte reads (zero-padded runs),
-                    // all in flight before their adds (a software-pipelined
-                    // variant, the next batch in flight during the adds,
-                    // measured slower: 175 vs 128 us)
+                    // whole batches of kFmCB 16-byte reads (zero-padded runs)
                     const double2* reg = outv[w][h];
+                    // all of a batch's reads in flight before its adds, one
+                    // batch at a time (a ping-pong variant with the next
+                    // batch's reads in flight during the adds measured
+                    // slower in rounds 1 and 6: MEASUREMENTS.md §2)
                     for (uint32_t j = 0; j < n; j += 2 * kFmCB) {
                         double2 v[kFmCB];
 #pragma unroll
@@ -1903,6 +1952,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                 gen.wg[blockIdx.x] = b;
             }
         }
+        GCR_WGSPAN(1);
     }
 }
 
@@ -5031,6 +5081,10 @@ hipError_t launch_compact(const uint8_t* inc, uint32_t n, uint32_t* map, uint32_
 extern "C" int gcr_debug_stamps(uint64_t* host, size_t bytes) {
     const size_t n = bytes < sizeof(gcr::g_stamps) ? bytes : sizeof(gcr::g_stamps);
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(gcr::g_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
+}
+extern "C" int gcr_debug_wgspans(uint64_t* host, size_t bytes) {
+    const size_t n = bytes < sizeof(gcr::g_wgspan) ? bytes : sizeof(gcr::g_wgspan);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gcr::g_wgspan), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? (int)n : -1;
 }
 #endif
 
