@@ -924,7 +924,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
 // every workgroup's start and end on the global 100 MHz clock (s_memrealtime),
 // last launch only (tools/wg_spans.py: the spread behind a launch's tail)
 constexpr int kSpanWG = 4096;
-__device__ uint64_t g_wgspan[kSpanWG][2];
+__device__ uint64_t g_wgspan[kSpanWG][3];    // start, end, exact-pass survivors
 __device__ __forceinline__ uint64_t realtime_now() {
     uint64_t t;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1368,6 +1368,10 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     }
     GCR_STAMP(5, 15u);
     if (threadIdx.x == 0) GCR_WGSPAN(0);
+#ifdef GCR_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < (uint32_t)kSpanWG) g_wgspan[blockIdx.x][2] = 0;
+    __syncthreads();
+#endif
     // ---- prologue: this workgroup's H slots (kGen), k_generate's rule, or
     // (chained batches) the previous launch's look-ahead wave's results
     if constexpr (kGen) {
@@ -1818,6 +1822,9 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             }
             GCR_STAMP(3, r);
             GCR_STAMP_VAL(6, r, (uint64_t)qn);
+#ifdef GCR_STAMPS
+            if (lane == 0 && blockIdx.x < (uint32_t)kSpanWG) atomicAdd((unsigned long long*)&g_wgspan[blockIdx.x][2], (unsigned long long)qn);
+#endif
             // 4) zero-pad each run to a whole chain batch
             {
                 const int q = lane % H, part = lane / H;

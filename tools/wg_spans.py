@@ -49,7 +49,7 @@ def main():
     N.check(N.lib.gcr_problem_verify_batches(ph.value, C.byref(p), 0, a.slots, a.steps, res, C.byref(st)))
     N.check(N.lib.gcr_synchronize(ctx))
     nwg = a.slots // 16
-    buf = np.zeros((4096, 2), dtype=np.uint64)
+    buf = np.zeros((4096, 3), dtype=np.uint64)
     fn = N.lib.gcr_debug_wgspans
     fn.argtypes = [C.c_void_p, C.c_size_t]
     n = fn(buf.ctypes.data, buf.nbytes)
@@ -62,6 +62,14 @@ def main():
     print(f"workgroups {nwg}: start spread {start.max():.2f} us; duration mean {dur.mean():.2f} "
           f"p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} max {dur.max():.2f} us; "
           f"launch span {end.max():.2f} us; mean/span {dur.mean() / end.max():.3f}")
+    surv = s[:, 2].astype(np.float64)
+    if surv.std() > 0:
+        print(f"  exact-pass survivors per workgroup: mean {surv.mean():.0f} min {surv.min():.0f} max {surv.max():.0f};"
+              f" correlation with duration {np.corrcoef(surv, dur)[0, 1]:.3f}")
+        order = np.argsort(surv)
+        q = len(order) // 4
+        print(f"  duration by survivor quartile: " + ", ".join(
+            f"{dur[order[k * q:(k + 1) * q]].mean():.1f}" for k in range(4)) + " us")
     hist, edges = np.histogram(dur, bins=10)
     for h, e0, e1 in zip(hist, edges[:-1], edges[1:]):
         print(f"  {e0:7.2f}-{e1:7.2f} us {h:4d} " + "#" * int(h // 2))
