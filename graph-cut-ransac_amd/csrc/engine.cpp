@@ -273,8 +273,8 @@ struct Workspace {
     PinBuf<uint8_t> h_mask_all;
     DevBuf<BatchRecord> recs;           // verify_batches: one record per batch
     PinBuf<BatchRecord> h_recs;         // ... and their pinned host image
-    DevBuf<uint8_t> pg_inc[2];          // verify_batches: slots generated one launch ahead
-    DevBuf<RectModel> pg_models[2];
+    DevBuf<uint8_t> pg_inc[4];          // verify_batches: slots generated one (two, overlapped) launches ahead
+    DevBuf<RectModel> pg_models[4];
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<WgBest> vb_wg;               // verify_batches: a ring of batches' workgroup bests and
     DevBuf<RectModel> vb_models;        // models, reduced by one deferred selection launch
@@ -1333,43 +1333,60 @@ struct RectTraits {
     // batch b of nb: chained launches (the previous launch generated this
     // batch's slots, this one generates the next batch's) when the kernel
     // at this batch size supports it (verify_chains)
+    // ahead = 2 (verify_batches' two-stream overlap): batches alternate
+    // between two streams, batch b chains to b + 2 (same stream) and uses
+    // buffer set b & 1 for its per-slot outputs; its ring selection is left
+    // to the caller (select_flush), which orders it after both streams
     static hipError_t verify(gcr_problem* P, const double Tm[2], uint64_t seed, uint64_t s0, uint32_t n,
                              const uint32_t m[2], size_t wg_cap, BatchRecord* rec, hipEvent_t e0, hipEvent_t e1,
-                             hipStream_t s, uint32_t b = 0, uint32_t nb = 1) {
+                             hipStream_t s, uint32_t b = 0, uint32_t nb = 1, uint32_t ahead = 1) {
         GenChain ch;
-        if (nb > 1 && verify_chains(n) && chain_on()) {
-            Workspace* w = P->w;
-            for (int k = 0; k < 2; ++k) {
+        Workspace* w = P->w;
+        if (nb > ahead && verify_chains(n) && chain_on()) {
+            const uint32_t nbuf = 2 * ahead;
+            for (uint32_t k = 0; k < nbuf; ++k) {
                 w->pg_inc[k].ensure(n);
                 w->pg_models[k].ensure(n);
             }
-            if (b > 0) {
-                ch.pre_inc = w->pg_inc[b & 1].p;
-                ch.pre_models = w->pg_models[b & 1].p;
+            if (b >= ahead) {
+                ch.pre_inc = w->pg_inc[b % nbuf].p;
+                ch.pre_models = w->pg_models[b % nbuf].p;
             }
-            if (b + 1 < nb) {
-                ch.next_inc = w->pg_inc[(b + 1) & 1].p;
-                ch.next_models = w->pg_models[(b + 1) & 1].p;
+            if (b + ahead < nb) {
+                ch.next_inc = w->pg_inc[(b + ahead) % nbuf].p;
+                ch.next_models = w->pg_models[(b + ahead) % nbuf].p;
             }
+            ch.ahead = ahead;
         }
+        const bool set1 = ahead == 2 && (b & 1);
+        if (set1) {
+            w->pf_inc.ensure(n);
+            w->pf_sb.ensure(n);
+        }
+        uint8_t* const inc = set1 ? w->pf_inc.p : w->inc.p;
+        const ScoreOut sb = set1 ? w->pf_sb.dev() : w->sb.dev();
         if (!defer_on()) {
-            return launch_verify_fused(P->dp, Tm, seed, s0, n, m, P->w->inc.p, P->w->models.p, P->w->sb.dev(),
-                                       P->w->wg.p, wg_cap, rec, e0, e1, s, ch);
+            return launch_verify_fused(P->dp, Tm, seed, s0, n, m, inc, P->w->models.p, sb, P->w->wg.p, wg_cap, rec,
+                                       e0, e1, s, ch);
         }
         // deferred selection: batch b leaves its workgroup bests and models in
         // ring slot b % R; one launch reduces a whole ring (one workgroup per
         // batch) after its last batch, so the per-batch reduction kernel and
         // its launch leave the chain of scoring launches
         const uint32_t R = select_ring(n);
-        Workspace* w = P->w;
         w->vb_wg.ensure((size_t)R * wg_cap);
         w->vb_models.ensure((size_t)R * n);
         const uint32_t k = b % R;
-        hipError_t e = launch_verify_fused(P->dp, Tm, seed, s0, n, m, w->inc.p, w->vb_models.p + (size_t)k * n,
-                                           w->sb.dev(), w->vb_wg.p + (size_t)k * wg_cap, wg_cap, nullptr, e0, e1, s,
-                                           ch);
-        if (e != hipSuccess || !(k == R - 1 || b + 1 == nb)) return e;
-        return launch_select_batches(w->vb_wg.p, wg_cap, w->vb_models.p, s0 - (uint64_t)k * n, n, k + 1, rec - k, s);
+        hipError_t e = launch_verify_fused(P->dp, Tm, seed, s0, n, m, inc, w->vb_models.p + (size_t)k * n, sb,
+                                           w->vb_wg.p + (size_t)k * wg_cap, wg_cap, nullptr, e0, e1, s, ch);
+        if (e != hipSuccess || ahead != 1 || !(k == R - 1 || b + 1 == nb)) return e;
+        return select_flush(P, s0 - (uint64_t)k * n, n, k + 1, wg_cap, rec - k, s);
+    }
+    // the deferred selection of ring batches 0 .. count - 1 (slots from s0):
+    // their records to rec[0 .. count)
+    static hipError_t select_flush(gcr_problem* P, uint64_t s0, uint32_t n, uint32_t count, size_t wg_cap,
+                                   BatchRecord* rec, hipStream_t s) {
+        return launch_select_batches(P->w->vb_wg.p, wg_cap, P->w->vb_models.p, s0, n, count, rec, s);
     }
     // true when batch b's launch directly follows a deferred selection launch
     // (verify_batches does not time those batches: their start event measured
@@ -1381,6 +1398,11 @@ struct RectTraits {
     // GCR_VERIFY_DEFER=0: every fused launch reduces its own batch (A/B)
     static bool defer_on() {
         const char* e = getenv("GCR_VERIFY_DEFER");
+        return !(e && e[0] == '0');
+    }
+    // GCR_VERIFY_OVERLAP=0: chained fused batches on one stream (A/B)
+    static bool overlap_on() {
+        const char* e = getenv("GCR_VERIFY_OVERLAP");
         return !(e && e[0] == '0');
     }
     // GCR_VERIFY_CHAIN=0: every launch generates its own slots (A/B)
@@ -2341,6 +2363,14 @@ public:
         return (d ? 1 : 0) | (ec_.near_ties > nt0 ? 2 : 0) | (sc[0].sum < sc[1].sum ? 4 : 0);
     }
 
+    // verify_batches' two-stream overlap of the fused launches (see there):
+    // chained H = 16 launches with deferred selection, at least 4 batches
+    bool overlap_batches(uint32_t nslots, uint32_t nb) const {
+        if constexpr (Tr::kFusedVerify)
+            return nb >= 4 && Tr::overlap_on() && Tr::defer_on() && Tr::chain_on() && verify_chains(nslots);
+        return false;
+    }
+
     // One hot-path batch (bench): generate + score + first strict maximum.
     // `nb` back-to-back batches of `nslots` slots starting at slot0, each
     // generated, scored and reduced to its first strict best on the device by
@@ -2421,6 +2451,50 @@ public:
                     HIPC(hipEventRecord(w->vb_flush, s_));
                 }
                 timed += t;
+            }
+        } else if (overlap_batches(nslots, nb)) {
+            if constexpr (Tr::kFusedVerify) {
+                // two-stream overlap of the fused launches: batch b on s_ (b
+                // even) or the side stream (b odd), chained to b + 2 on the
+                // same stream.  One launch's workgroups finish unevenly (one
+                // per CU, ~0.76 of the launch busy on average, MEASUREMENTS
+                // round 6) and the other stream's next launch takes the CUs
+                // they free.  A ring's selection runs on s_ after both
+                // streams' batches of the ring, and the side stream's first
+                // batch after it waits for it (ring slots are reused).  One
+                // event pair brackets the whole call: the per-launch time is
+                // the span over the launches.
+                Workspace* w = P_->w;
+                hipStream_t side = P_->ctx->side;
+                for (hipEvent_t* e : {&w->vb_gen[0], &w->vb_gen[1], &w->vb_start, &w->vb_flush})
+                    if (*e == nullptr) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+                const uint32_t R = Tr::select_ring(nslots);
+                HIPC(hipEventRecord(P_->w->evs[0], s_));
+                HIPC(hipEventRecord(w->vb_start, s_));
+                HIPC(hipStreamWaitEvent(side, w->vb_start, 0));
+                bool side_wait = false;             // the side stream must wait for the last selection
+                for (uint32_t b = 0; b < nb; ++b) {
+                    const uint32_t k = b % R;
+                    const uint64_t s0 = slot0 + (uint64_t)b * nslots;
+                    hipStream_t st = (b & 1) ? side : s_;
+                    if ((b & 1) && side_wait) {
+                        HIPC(hipStreamWaitEvent(side, w->vb_flush, 0));
+                        side_wait = false;
+                    }
+                    HIPC(Tr::verify(P_, Tm_, prm_.seed, s0, nslots, m32, wg_cap, drecs + b, nullptr, nullptr, st, b,
+                                    nb, 2));
+                    if (k == R - 1 || b + 1 == nb) {
+                        HIPC(hipEventRecord(w->vb_gen[1], side));
+                        HIPC(hipStreamWaitEvent(s_, w->vb_gen[1], 0));
+                        HIPC(Tr::select_flush(P_, s0 - (uint64_t)k * nslots, nslots, k + 1, wg_cap, drecs + (b - k),
+                                              s_));
+                        HIPC(hipEventRecord(w->vb_flush, s_));
+                        side_wait = true;
+                    }
+                }
+                HIPC(hipEventRecord(P_->w->evs[1], s_));
+                span_launches = nb;
+                timed = 1;
             }
         } else {
             // one event pair around launches 1 .. nb-2 only where each verify

@@ -232,11 +232,15 @@ struct WgBest {
 // the launch's prologue generates them), `next` receives the next batch's
 // (slots slot0 + nslots ...), generated by a dedicated wave while this batch
 // is scored (null: none).  Same models and attempt counts as the prologue.
+// `ahead`: the batch `next` belongs to, counted from this one (2 when
+// consecutive batches alternate between two streams: batch b generates batch
+// b + 2's slots, which the same stream scores next).
 struct GenChain {
     const uint8_t* pre_inc = nullptr;
     const RectModel* pre_models = nullptr;
     uint8_t* next_inc = nullptr;
     RectModel* next_models = nullptr;
+    uint32_t ahead = 1;
 };
 // rec == nullptr: the launch leaves its workgroup records in `wg` (and its
 // models in `models`) for a later launch_select_batches instead of reducing

@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
         if (wave == kW) {
             // ------------------------------------------ look-ahead generator
             // the next batch's slots of this workgroup (blockIdx.x * H + sl,
-            // slot index slot0 + nh + ...), k_generate_fw's widening lane
+            // slot index slot0 + ahead nh + ...), k_generate_fw's widening lane
             // groups: the H slots start with 64 / H lanes each, and after
             // every round the unfinished ones share the whole wave (64 /
             // pow2ceil(k) lanes for k left) from one wave-uniform lowest
@@ -1489,7 +1489,7 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                 bool ok = false;
                 if (si >= 0 && a < 101)
                     ok = (gen.probe & 8u) ? a == 0
-                                          : attempt<KIND>(p, gen.seed, gen.slot0 + nh + hs0 + (uint32_t)si, a, m);
+                                          : attempt<KIND>(p, gen.seed, gen.slot0 + (uint64_t)gen.chain.ahead * nh + hs0 + (uint32_t)si, a, m);
                 const uint64_t mask = __ballot(ok);
                 nx += 1u << lw;
                 const bool out_of_attempts = nx >= 101;

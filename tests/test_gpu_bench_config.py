@@ -184,26 +184,33 @@ def test_chained_batches_equal_unchained(kind, monkeypatch):
     prob = Problem(kind, f0, f1)
     p = N.default_params()
     p.scale_residual_thresh, p.orientation_residual_thresh, p.seed = thr0, thr1, SEED
+    # GCR_VERIFY_OVERLAP=0 keeps chained launches on one stream (the
+    # default alternates two streams, each launch chained to the one two
+    # batches ahead)
     outs = []
-    for chain in ("1", "0"):
+    for chain, overlap in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("GCR_VERIFY_CHAIN", chain)
+        monkeypatch.setenv("GCR_VERIFY_OVERLAP", overlap)
         res = (N.BatchResult * 6)()
         N.check(N.lib.gcr_problem_verify_batches(prob.h, C.byref(p), SLOT0, 4096, 6, res, None))
         outs.append([(r.models, r.iterations, r.best_slot, bits(r.best_score).item(), r.best_inliers[0],
                       r.best_inliers[1], bits([r.best_model.h7, r.best_model.h8, r.best_model.alpha,
                                                r.best_model.phi]).tolist()) for r in res])
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]
     assert all(o[2] >= 0 for o in outs[0])
 
 
 @pytest.mark.parametrize("kind,nslots,nb", [(N.SOLVER_SIFT22, 4096, 70), (N.SOLVER_SCALE3, 4096, 3),
-                                            (N.SOLVER_SIFT22, 16384, 18), (N.SOLVER_SIFT22, 1500, 5)])
+                                            (N.SOLVER_SIFT22, 16384, 18), (N.SOLVER_SIFT22, 1500, 5),
+                                            (N.SOLVER_SCALE3, 3000, 67)])
 def test_deferred_selection_equals_per_batch(kind, nslots, nb, monkeypatch):
     # verify_batches leaves each fused launch's workgroup bests and models in
     # a ring and reduces a whole ring in one launch (64 batches at 4096 slots,
     # 16 at 16384: 70 and 18 batches cross a ring boundary and end on a partial
-    # ring).  GCR_VERIFY_DEFER=0 reduces every batch right after its launch;
-    # the records must be identical batch for batch
+    # ring).  GCR_VERIFY_DEFER=0 reduces every batch right after its launch
+    # (on one stream); with the ring, chained H = 16 batches alternate two
+    # streams (3000 slots: partial workgroups, an odd batch count crossing a
+    # ring boundary); the records must be identical batch for batch
     f0, f1, thr0, thr1 = _rect_problem(kind)
     prob = Problem(kind, f0, f1)
     p = N.default_params()
