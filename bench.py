@@ -14,8 +14,11 @@ selected -- all on the device: one fused kernel (k_score_fm<..., true>:
 in-kernel generation, exact MSAC sums, per-workgroup best) plus k_select_wg.
 The correspondence workloads (h, f) generate in their own kernel and are
 pipelined over two streams (batch b + 1 generated while batch b is scored).
-The K timed steps are queued back to back on one HIP stream (gcr_problem_verify_batches)
-and bracketed by device synchronisation.  Features are uploaded once before
+The K timed steps are queued back to back (gcr_problem_verify_batches; for the
+rectification workloads consecutive fused launches alternate between two HIP
+streams, so one launch's workgroups take the CUs the other's early finishers
+free -- GCR_VERIFY_OVERLAP=0 keeps them on one stream) and bracketed by device
+synchronisation.  Features are uploaded once before
 timing (HBM-resident).  `value` is the whole-job hypotheses/s; the end-to-end
 latency of a full estimator call at confidence 0.99 (including LO and the
 final refit) is reported beside it.
@@ -691,12 +694,18 @@ def main():
                 "kernel": kernel_name,
                 "kernel_build_id": build_id,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
-                "avg_kernel_ms_note": ("HIP events on the engine's stream: when no deferred selection falls "
-                                       "inside a call's launches 1..K-2 (K <= 64), one event pair brackets those "
-                                       "back-to-back launches and their mean is taken (GCR_TIMING_SPAN); "
-                                       "otherwise pairs around every 4th launch (GCR_TIMING_STRIDE), never the "
-                                       "launch right after a deferred-selection flush. The mean is extrapolated "
-                                       "to all launches. The whole queue, selections included, is ms_per_step"),
+                "avg_kernel_ms_note": ("HIP events on the engine's stream. Overlapped launches (rectification, "
+                                       "two streams, GCR_VERIFY_OVERLAP): one event pair brackets the whole call "
+                                       "and the per-launch time is that span over the launches -- the throughput "
+                                       "time of one launch; a rocprofv3 dispatch lasts longer, since its "
+                                       "workgroups also wait for CUs the other stream's launch holds "
+                                       "(profiles/*_span.txt: first start to last end over the dispatches). "
+                                       "One stream: when no deferred selection falls inside a call's launches "
+                                       "1..K-2 (K <= 64), one event pair brackets those back-to-back launches "
+                                       "and their mean is taken (GCR_TIMING_SPAN); otherwise pairs around every "
+                                       "4th launch (GCR_TIMING_STRIDE), never the launch right after a "
+                                       "deferred-selection flush. The mean is extrapolated to all launches. The "
+                                       "whole queue, selections included, is ms_per_step"),
                 "hypotheses_per_launch": models_per_launch,
                 "algorithmic_hbm": {
                     "achieved_gbs": achieved,

@@ -28,6 +28,10 @@ fi
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 step stats_m2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_m2 -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 --no-latency > $O/stats_m2.log 2>&1 || { tail -20 $O/stats_m2.log; exit 1; }
+python3 tools/dispatch_span.py $(find $O/stats_m2 -name "*kernel_trace.csv" | head -1) > $O/stats_m2_span.txt && cat $O/stats_m2_span.txt
+step stats_m2_one_stream
+GCR_VERIFY_OVERLAP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_m2_1s -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-seconds 0 --no-latency > $O/stats_m2_1s.log 2>&1 || { tail -20 $O/stats_m2_1s.log; exit 1; }
+python3 tools/dispatch_span.py $(find $O/stats_m2_1s -name "*kernel_trace.csv" | head -1) > $O/stats_m2_1s_span.txt && cat $O/stats_m2_1s_span.txt
 step stats_f
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats_f -o run --output-format csv -- python3 bench.py --workload f --steps 200 --warmup 20 --cpu-seconds 0 --no-latency > $O/stats_f.log 2>&1 || { tail -20 $O/stats_f.log; exit 1; }
 step pmc_m2
