@@ -320,6 +320,7 @@ struct Workspace {
     PinBuf<BlockSummary> hsum[2];       // [0] this rank's, then the all-gathered ones
     DevBuf<BlockSummary> dall[2];       // gcr_comm: the all-gathered summaries on the device
     PinBuf<uint64_t> h_cbits[2];        // small-scored chunks: every slot's LO list bits (ListBits)
+    PinBuf<uint64_t> h_cmbits[2];       // ... and its MSAC ballots (ListBits::mbits)
     // small-scored chunks: the split scorer's scratch of each chunk set.  Such
     // a chunk may run on the side stream while the replay stream scores LO
     // trials / the refit through DevProblem::lo, so they never share one.
@@ -1679,6 +1680,12 @@ public:
         const char* e = getenv("GCR_CHUNK_LISTS");         // read per run
         return !(e && e[0] == '0');
     }
+    // GCR_CHUNK_MSAC=0: small-scored chunks mirror no MSAC ballots (the final
+    // refit's lists of a chunk-found best come from mask launches)
+    static bool chunk_msac_on() {
+        const char* e = getenv("GCR_CHUNK_MSAC");          // read per run
+        return !(e && e[0] == '0');
+    }
 
     // GCR_LO_REUSE=0: the final refit always rescores the buffer model
     static bool lo_reuse_on() {
@@ -1853,6 +1860,7 @@ public:
         }
         const int set = c.set;
         if (lo_row_ >= 0 && lo_row_set_ == set) lo_row_ = -1;   // its list bits are about to be rewritten
+        if (msac_row_ >= 0 && msac_row_set_ == set) msac_row_ = -1;
         w->hsum[set].ensure((size_t)world_ + 1);
         w->dsum[set].ensure(1);
         const uint32_t n = rank_nslots(c, rank_);
@@ -1891,8 +1899,17 @@ public:
                     void* dptr = nullptr;
                     HIPC(hipHostGetDevicePointer(&dptr, w->h_cbits[set].p, 0));
                     lb.bits = static_cast<uint64_t*>(dptr);
+                    // the MSAC ballots as well: a run whose best stays a
+                    // hypothesis of this chunk takes its final-refit lists
+                    // from them (no mask launches and synchronisation)
+                    if (chunk_msac_on()) {
+                        w->h_cmbits[set].ensure(pairs * kSmallScore / 64);
+                        HIPC(hipHostGetDevicePointer(&dptr, w->h_cmbits[set].p, 0));
+                        lb.mbits = static_cast<uint64_t*>(dptr);
+                    }
                 }
                 chunk_lists_[set] = cl;
+                chunk_msac_[set] = cl && lb.mbits != nullptr;
                 DevProblem dpc = P_->dp;                  // this set's own split-scorer scratch
                 if (dpc.lo.vals) {
                     w->cs_vals[set].ensure(pairs * kSplitModels);
@@ -1907,6 +1924,7 @@ public:
                                         set_sb(set).dev(), s, cl ? &lb : nullptr));
             } else {
                 chunk_lists_[set] = false;
+                chunk_msac_[set] = false;
                 HIPC(Tr::score(P_, Tm_, set_models(set).p, set_inc(set).p, (uint32_t)np, true, set_sb(set).dev(),
                                s));
             }
@@ -2182,6 +2200,11 @@ public:
                         lo_row_set_ = c.set;
                         lo_row_model_ = best_model_;
                         lo_row_lfl_ = h.lfl;
+                        // ... and its MSAC lists, for the final refit
+                        msac_row_ = (kP == 1 && chunk_msac_[c.set]) ? (int64_t)h.pos : -1;
+                        msac_row_set_ = c.set;
+                        msac_row_model_ = best_model_;
+                        msac_row_fl_ = h.fl;
                         bool nonmin = false;
                         for (int cc = 0; cc < K_; ++cc) if (best_.n[cc] > m_[cc]) { nonmin = true; break; }
                         slot_lo = (it_ > 20) && nonmin;
@@ -2319,6 +2342,16 @@ public:
             // iteratedLeastSquaresFitting never succeeds (GCRANSAC.h:1092-1098):
             // one non-minimal fit on the buffer's inliers, kept if strictly better.
             rlot("rescored");
+            // a best that is still the chunk hypothesis it was found as: its
+            // MSAC lists from that chunk's ballots, when none of its decisions
+            // was flagged (the same rule as its raw counts, gen_buf)
+            if (!have_lists && msac_row_ >= 0 &&
+                std::memcmp(&msac_row_model_, &bufs_[off_].model, sizeof(Model)) == 0 &&
+                (msac_row_fl_ == 0 || !exact_) && !unsafe(bufs_[off_].model)) {
+                decode_lists(P_->w->h_cmbits[msac_row_set_].p, (uint32_t)msac_row_, lists);
+                have_lists = true;
+                ++st_.chunk_msac_lists;
+            }
             if (!have_lists) inlier_lists(bufs_[off_].model, Tm_, 0, lists);
             rlot("lists");
             Model refit;
@@ -2621,6 +2654,11 @@ private:
     } lo_cache_;
     bool chunk_lists_[2] = {false, false};    // the set's chunk was small-scored with LO list bits
     int64_t lo_row_ = -1;                       // the last new best's row in those bits (-1: none)
+    bool chunk_msac_[2] = {false, false};       // ... and also mirrored its MSAC ballots (h_cmbits)
+    int64_t msac_row_ = -1;                     // the last new best's row in the MSAC bits (-1: none)
+    int msac_row_set_ = 0;
+    Model msac_row_model_{};
+    uint32_t msac_row_fl_ = 0;                  // its flagged MSAC decisions in that launch
     int lo_row_set_ = 0;
     Model lo_row_model_{};
     bool lo_lists_from_bits_ = false;     // the current LO winner's lists came from its scoring launch

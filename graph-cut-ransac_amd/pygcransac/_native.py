@@ -75,6 +75,7 @@ class Stats(C.Structure):
         ("near_ties", C.c_uint64),
         ("near_tie_flips", C.c_uint64),
         ("lo_refolds", C.c_uint64),
+        ("chunk_msac_lists", C.c_uint64),
     ]
 
     def as_dict(self):

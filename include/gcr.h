@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GCR_ABI_VERSION 4
+#define GCR_ABI_VERSION 5
 
 /* error codes */
 #define GCR_OK 0
@@ -121,6 +121,9 @@ typedef struct gcr_stats {
     /* LO trials are compared on approximate scores within a proven bound of
      * the exact ones; a round the bound leaves open is folded exactly */
     uint64_t lo_refolds;          /* LO rounds folded exactly for a comparison      */
+    /* the final refit's inlier lists decoded from the MSAC ballots of the
+     * chunk launch that found the best (1) instead of mask launches (0) */
+    uint64_t chunk_msac_lists;
 } gcr_stats;
 
 /* ---- context ---------------------------------------------------------- */

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version_and_defaults():
-    assert N.lib.gcr_abi_version() == 4          # 4: gcr_stats counts the glibc near-tie comparisons
+    assert N.lib.gcr_abi_version() == 5          # 5: gcr_stats.chunk_msac_lists
     p = N.default_params()
     assert (p.min_iteration_number, p.max_iteration_number, p.max_local_optimization_number) == (10000, 10000, 50)
     assert p.spatial_coherence_weight == 0.0 and p.confidence == 0.95

@@ -65,3 +65,31 @@ def test_chunk_list_bits_equal_mask_launches(budget, monkeypatch):
         a = run_problem(kind, budget, monkeypatch, {})
         b = run_problem(kind, budget, monkeypatch, {"GCR_CHUNK_LISTS": "0"})
         assert a == b, kind
+
+
+@pytest.mark.parametrize("budget", ["fixed", "adaptive", "tiny", "floor"])
+def test_chunk_msac_bits_equal_mask_launches(budget, monkeypatch):
+    # small-scored chunks also mirror every slot's MSAC ballots, and the final
+    # refit of a run whose best is still the chunk hypothesis it was found as
+    # takes its inlier lists from them (GCR_CHUNK_MSAC=0: mask launches):
+    # identical runs for every estimator and budget
+    from test_gpu_summary import SOLVERS, _run as run_problem
+
+    for kind in SOLVERS:
+        a = run_problem(kind, budget, monkeypatch, {})
+        b = run_problem(kind, budget, monkeypatch, {"GCR_CHUNK_MSAC": "0"})
+        assert a == b, kind
+
+
+def test_chunk_msac_lists_used_at_the_bench_call():
+    # bench.py's latency call (M2 5000 + 5000, seeds 100..110): over the
+    # eleven seeds some runs end on a chunk-found best whose refit lists come
+    # from the chunk's MSAC ballots (test_gpu_glibc.py checks those calls
+    # against the oracle's GLIBC mode)
+    fs, fo, _, _, ts, to = S.problem_m2(5000, 5000, seed=20251121)
+    used = 0
+    for seed in range(100, 111):
+        out = pygcransac.findRectifyingHomographySIFT(fs, fo, ts, to, 0.0, 0, 10**7, 50, seed=seed,
+                                                      confidence=0.99, return_stats=True)
+        used += out[-1]["chunk_msac_lists"]
+    assert used > 0
