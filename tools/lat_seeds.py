@@ -57,3 +57,6 @@ for seed in range(100, 111):
         row.append(f"{name}: {statistics.median(x[0] for x in r):6.3f} ms it {r[0][1]:5d} slots {r[0][2]:6d} "
                    f"lo {r[0][3]} gc {r[0][4]} pf {r[0][5]} {ph}")
     print("  |  ".join(row))
+for name, _ in sets:
+    per = [statistics.median(x[0] for x in res[(name, seed)]) for seed in range(100, 111)]
+    print(f"{name}: median over seeds {statistics.median(per):.3f} ms, worst {max(per):.3f} ms")
