@@ -492,6 +492,10 @@ def main():
     p.orientation_residual_thresh = thr1
     p.seed = seed
 
+    rec_dt = np.dtype([("models", "<u8"), ("iterations", "<u8"), ("best_slot", "<i8"), ("best_score", "<f8"),
+                       ("best_inliers", "<u8", 2), ("best_model", "<f8", 7)])
+    assert rec_dt.itemsize == C.sizeof(N.BatchResult)
+
     def steps(k0, n, st_acc):
         res = (N.BatchResult * n)()
         st = N.Stats()
@@ -500,12 +504,18 @@ def main():
         if st_acc is not None:
             st_acc["kernel_ms"] += st.ms_score_kernel
             st_acc["launches"] += n
-            for r in res:           # first strict best over the batches, in slot order
-                st_acc["models"] += r.models
-                if r.best_slot >= 0 and r.best_score > st_acc["best_score"]:
-                    st_acc["best_score"] = r.best_score
-                    st_acc["best_model"] = (r.best_model.h7, r.best_model.h8, r.best_model.alpha,
-                                            r.best_model.phi)
+            # the batch records read as one array (per-record ctypes access
+            # cost ~2 us a record inside the timed region)
+            rec = np.frombuffer(res, dtype=rec_dt, count=n)
+            st_acc["models"] += int(rec["models"].sum())
+            # first strict best over the batches, in slot order
+            ok = (rec["best_slot"] >= 0) & (rec["best_score"] > st_acc["best_score"])
+            if ok.any():
+                sc = np.where(ok, rec["best_score"], -np.inf)
+                i = int(np.argmax(sc))              # the first index of the maximum
+                st_acc["best_score"] = float(rec["best_score"][i])
+                bm = rec["best_model"][i]           # x0, y0, s, h7, h8, alpha, phi
+                st_acc["best_model"] = (float(bm[3]), float(bm[4]), float(bm[5]), float(bm[6]))
 
     def barrier():
         N.check(N.lib.gcr_synchronize(ctx))
