@@ -275,6 +275,7 @@ struct Workspace {
     PinBuf<BatchRecord> h_recs;         // ... and their pinned host image
     DevBuf<uint8_t> pg_inc[4];          // verify_batches: slots generated one (two, overlapped) launches ahead
     DevBuf<RectModel> pg_models[4];
+    DevBuf<uint8_t> pg_hyp[4], pg_pair[4];   // their band / value constants (GenChain::next_hyp)
     DevBuf<WgBest> wg;                  // verify_batches: per-workgroup bests
     DevBuf<WgBest> vb_wg;               // verify_batches: a ring of batches' workgroup bests and
     DevBuf<RectModel> vb_models;        // models, reduced by one deferred selection launch
@@ -1370,13 +1371,27 @@ struct RectTraits {
                 w->pg_inc[k].ensure(n);
                 w->pg_models[k].ensure(n);
             }
+            const bool pc = preconst_on();
+            if (pc)
+                for (uint32_t k = 0; k < nbuf; ++k) {
+                    w->pg_hyp[k].ensure((size_t)n * kFmHypBytes);
+                    w->pg_pair[k].ensure((size_t)(n + 1) / 2 * kFmPairBytes);
+                }
             if (b >= ahead) {
                 ch.pre_inc = w->pg_inc[b % nbuf].p;
                 ch.pre_models = w->pg_models[b % nbuf].p;
+                if (pc) {
+                    ch.pre_hyp = w->pg_hyp[b % nbuf].p;
+                    ch.pre_pair = w->pg_pair[b % nbuf].p;
+                }
             }
             if (b + ahead < nb) {
                 ch.next_inc = w->pg_inc[(b + ahead) % nbuf].p;
                 ch.next_models = w->pg_models[(b + ahead) % nbuf].p;
+                if (pc) {
+                    ch.next_hyp = w->pg_hyp[(b + ahead) % nbuf].p;
+                    ch.next_pair = w->pg_pair[(b + ahead) % nbuf].p;
+                }
             }
             ch.ahead = ahead;
         }
@@ -1423,6 +1438,13 @@ struct RectTraits {
         return !(e && e[0] == '0');
     }
     static bool overlap_on() { return verify_overlap_on(); }
+    // GCR_FM_PRECONST=0 (read per call): chained launches compute their
+    // slots' constants in the prologue instead of copying the look-ahead
+    // wave's (A/B)
+    static bool preconst_on() {
+        const char* e = getenv("GCR_FM_PRECONST");
+        return !(e && e[0] == '0');
+    }
     // GCR_VERIFY_CHAIN=0: every launch generates its own slots (A/B)
     static bool chain_on() {
         const char* e = getenv("GCR_VERIFY_CHAIN");

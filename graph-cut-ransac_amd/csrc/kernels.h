@@ -235,12 +235,22 @@ struct WgBest {
 // `ahead`: the batch `next` belongs to, counted from this one (2 when
 // consecutive batches alternate between two streams: batch b generates batch
 // b + 2's slots, which the same stream scores next).
+// `const` (optional, both or neither): the look-ahead wave also writes each
+// generated slot's band and value constants (HypConst, kFmHypBytes per slot)
+// and its half of the packed-fp32 pre-band record (RPairBand, kFmPairBytes
+// per two slots), which the next launch's prologue copies instead of
+// computing them.
+constexpr size_t kFmHypBytes = 80, kFmPairBytes = 128;
 struct GenChain {
     const uint8_t* pre_inc = nullptr;
     const RectModel* pre_models = nullptr;
     uint8_t* next_inc = nullptr;
     RectModel* next_models = nullptr;
     uint32_t ahead = 1;
+    const void* pre_hyp = nullptr;
+    const void* pre_pair = nullptr;
+    void* next_hyp = nullptr;
+    void* next_pair = nullptr;
 };
 // rec == nullptr: the launch leaves its workgroup records in `wg` (and its
 // models in `models`) for a later launch_select_batches instead of reducing

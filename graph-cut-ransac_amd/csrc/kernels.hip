@@ -1177,6 +1177,7 @@ struct RPairBand {                 // hypotheses 2 j (.x) and 2 j + 1 (.y)
 };
 static_assert(sizeof(RPairBand) == 16 * 8, "RPairBand layout: 16 float pairs");
 
+static_assert(sizeof(HypConst) == kFmHypBytes && sizeof(RPairBand) == kFmPairBytes, "GenChain constant records");
 __device__ __forceinline__ void rpb_setup(RPairBand* rp, int t, const HypConst& q, const DevClass& c0,
                                           const DevClass& c1, double tan_tau1, bool orient, bool valid) {
     constexpr double u = 0x1p-24;
@@ -1306,11 +1307,39 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     __shared__ int gen_a[kGen ? H : 1];
     __shared__ RectModel gen_m[kGen ? H : 1];
     __shared__ double fin_sh[kGen ? H : 1];
+    // the look-ahead wave's generated slots (models, attempts)
+    __shared__ RectModel nx_m[kGen ? H : 1];
+    __shared__ int nx_a[kGen ? H : 1];
 
     const int t = threadIdx.x;
     const int wave = t >> 6;
     const int lane = t & 63;
     const bool chain_wave = wave == kFmWaves;
+
+    const uint32_t n0 = p.cls[0].n;
+    const uint32_t n1 = (KIND == 2) ? p.cls[1].n : 0;
+    const uint32_t r0 = (n0 + kRound - 1) / kRound;
+    const uint32_t rounds = r0 + (n1 + kRound - 1) / kRound;
+    // a compute lane's feature of round rr (x, y, s | x2 | cos, - | y2 | sin)
+    // (round 0's requested before the prologue instead of after it: 51.6
+    // vs 52.6 x 10^7 hyp/s, the register it holds across the prologue
+    // costs the main loop more than the overlap saves)
+    auto load = [&](uint32_t rr, double* f, bool& ok) {
+        const int cls = rr < r0 ? 0 : 1;
+        const DevClass& c = p.cls[cls];
+        const uint32_t i = (cls == 0 ? rr : rr - r0) * kRound + wave * 64 + lane;
+        ok = i < c.n;
+        const uint32_t ic = ok ? i : 0u;
+        f[0] = c.x[ic];
+        f[1] = c.y[ic];
+        if (cls == 0) {
+            f[2] = c.a[ic];
+            f[3] = (KIND >= 3) ? c.c0[ic] : 0.0;
+        } else {
+            f[2] = c.c0[ic];
+            f[3] = c.c1[ic];
+        }
+    };
 
     __shared__ uint32_t smap[KIND >= 3 ? H : 1];
     if constexpr (KIND >= 3) {
@@ -1376,16 +1405,18 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     // (chained batches) the previous launch's look-ahead wave's results
     if constexpr (kGen) {
       if (gen.chain.pre_inc != nullptr) {
+        // the previous launch's look-ahead results (each thread t < H its
+        // own slot: no barrier before the slot's outputs)
         if (t < H) {
             const uint32_t hs = blockIdx.x * H + t;
             const uint8_t iv = hs < nh ? gen.chain.pre_inc[hs] : (uint8_t)102;
+            const RectModel m = iv > 101 ? default_model() : gen.chain.pre_models[hs];
             gen_a[t] = iv > 101 ? 127 : (int)iv - 1;
-            gen_m[t] = iv > 101 ? default_model() : gen.chain.pre_models[hs];
-        }
-        __syncthreads();
-        if (t < H && blockIdx.x * H + t < nh) {
-            gen.inc[blockIdx.x * H + t] = gen.chain.pre_inc[blockIdx.x * H + t];
-            gen.models[blockIdx.x * H + t] = gen_m[t];
+            gen_m[t] = m;
+            if (hs < nh) {
+                gen.inc[hs] = iv;
+                gen.models[hs] = m;
+            }
         }
       } else {
         const int G = gen.glanes ? (int)gen.glanes : kSplitThreads / H;
@@ -1424,8 +1455,24 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
             if constexpr (kGen && KIND < 3) m = gen_m[t];
             else m = models[mi];
         }
-        hyp[t] = make_hyp<KIND>(m, band0);
-        if constexpr (KIND <= 2) rpb_setup(rpb, t, hyp[t], p.cls[0], p.cls[1], tan_tau1, KIND == 2, v);
+        bool copied = false;
+        if constexpr (kGen && KIND <= 2) {
+            // constants the previous launch's look-ahead wave computed for
+            // this slot (the same make_hyp / rpb_setup of the same model)
+            if (gen.chain.pre_inc != nullptr && gen.chain.pre_hyp != nullptr && hg < nh) {
+                hyp[t] = static_cast<const HypConst*>(gen.chain.pre_hyp)[hg];
+                const float* src = reinterpret_cast<const float*>(static_cast<const RPairBand*>(gen.chain.pre_pair) +
+                                                                  (hg >> 1));
+                float* dst = reinterpret_cast<float*>(&rpb[t >> 1]);
+#pragma unroll
+                for (int k = 0; k < 11; ++k) dst[2 * k + (t & 1)] = src[2 * k + (hg & 1)];
+                copied = true;
+            }
+        }
+        if (!copied) {
+            hyp[t] = make_hyp<KIND>(m, band0);
+            if constexpr (KIND <= 2) rpb_setup(rpb, t, hyp[t], p.cls[0], p.cls[1], tan_tau1, KIND == 2, v);
+        }
         if constexpr (KIND == 4) fpb_setup(fpb, t, m.h, v, T0, p.cls[0]);
         if constexpr (KIND == 3) hpb_setup(fpb, t, m.h, v, band0, p.cls[0]);
         hval[t] = v ? 1u : 0u;
@@ -1447,11 +1494,6 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
     if (t < kW) { ready[t] = 0; done[t] = 0; }
     __syncthreads();
     GCR_STAMP(7, 15u);
-
-    const uint32_t n0 = p.cls[0].n;
-    const uint32_t n1 = (KIND == 2) ? p.cls[1].n : 0;
-    const uint32_t r0 = (n0 + kRound - 1) / kRound;
-    const uint32_t rounds = r0 + (n1 + kRound - 1) / kRound;
 
     if constexpr (kGen) {
         if (wave == kW) {
@@ -1515,10 +1557,25 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
                 if (win) {
                     gen.chain.next_inc[hs] = (uint8_t)(a + 1);
                     gen.chain.next_models[hs] = m;
+                    nx_m[si] = m;
+                    nx_a[si] = (int)a;
                 } else if (fail) {              // every attempt failed (inc 102, no model)
                     gen.chain.next_inc[hs] = 102;
                     gen.chain.next_models[hs] = default_model();
+                    nx_a[si] = 127;
                 }
+            }
+            if (gen.chain.next_hyp == nullptr) return;
+            // the slots' constants for the next launch's prologue (make_hyp
+            // and rpb_setup as the prologue would run them), one lane a slot
+            __builtin_amdgcn_wave_barrier();
+            if (lane < (int)live) {
+                const bool v = nx_a[lane] != 127;
+                const RectModel m = v ? nx_m[lane] : default_model();
+                const HypConst q = make_hyp<KIND>(m, band0);
+                static_cast<HypConst*>(gen.chain.next_hyp)[hs0 + (uint32_t)lane] = q;
+                rpb_setup(static_cast<RPairBand*>(gen.chain.next_pair) + (hs0 >> 1), lane, q, p.cls[0], p.cls[1],
+                          tan_tau1, KIND == 2, v);
             }
             return;
         }
@@ -1529,23 +1586,6 @@ __global__ __launch_bounds__(kSplitThreads) __attribute__((amdgpu_waves_per_eu(K
         uint64_t vmask = __ballot(lane < H && hval[lane < H ? lane : 0] != 0);
         if (gen.probe & 4u) vmask = 0;
         uint16_t* qw = queue[wave];
-        // this lane's feature of round rr (x, y, s | x2 | cos, - | y2 | sin)
-        auto load = [&](uint32_t rr, double* f, bool& ok) {
-            const int cls = rr < r0 ? 0 : 1;
-            const DevClass& c = p.cls[cls];
-            const uint32_t i = (cls == 0 ? rr : rr - r0) * kRound + wave * 64 + lane;
-            ok = i < c.n;
-            const uint32_t ic = ok ? i : 0u;
-            f[0] = c.x[ic];
-            f[1] = c.y[ic];
-            if (cls == 0) {
-                f[2] = c.a[ic];
-                f[3] = (KIND >= 3) ? c.c0[ic] : 0.0;
-            } else {
-                f[2] = c.c0[ic];
-                f[3] = c.c1[ic];
-            }
-        };
         double nxt[4];
         bool nok = false;
         if (rounds > 0) load(0, nxt, nok);

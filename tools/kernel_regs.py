@@ -8,7 +8,7 @@ import sys
 import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-OBJ = os.path.join(os.path.dirname(__file__), "..", "graph-cut-ransac_amd", "csrc", "_build", "kernels.o")
+OBJ = os.path.join(os.path.dirname(__file__), "..", "graph-cut-ransac_amd", "csrc", "_build", os.environ.get("KOBJ", "kernels.o"))
 
 
 def main():
