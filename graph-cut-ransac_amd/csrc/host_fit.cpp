@@ -527,21 +527,62 @@ bool fit_f8_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, Geo
     }) * inv_n;
     if (!(d1 > 1e-12) || !(d2 > 1e-12)) return false;
     const double s1 = std::sqrt(2.0) / d1, s2 = std::sqrt(2.0) / d2;
-    // A^T A, upper triangle, accumulated in blocked order (all entries in one pass)
+    // A^T A, upper triangle, accumulated in blocked order.  Each block's rows
+    // r = (u2 u1, u2 v1, u2, v2 u1, v2 v1, v2, u1, v1, 1) go to a scratch
+    // block first; two passes over it then add r[p] * r[0..7] four entries
+    // per instruction (rows 0..3 of the triangle, then rows 4..7; column 8 is
+    // r[p] * 1 = r[p], entry (8, 8) the row count).  Every entry is still its
+    // own row-ordered sum of r[p] * r[q] (the lower 4 x 4 halves computed on
+    // the way are dropped), so the result is the scalar loop's bit for bit,
+    // 1.5x faster with the box's compiler (MEASUREMENTS.md).
+    typedef double v4d __attribute__((vector_size(32)));
+    alignas(64) static thread_local double rows[kSumBlock][8];
+    auto ld4 = [](const double* p) {
+        v4d v;
+        __builtin_memcpy(&v, p, sizeof v);
+        return v;
+    };
     double ata[9][9] = {};
     size_t i = 0;
     while (i < n) {
-        const size_t end = std::min(n, (i / kSumBlock + 1) * kSumBlock);
-        double part[9][9] = {};
-        for (; i < end; ++i) {
+        const size_t m = std::min(n, (i / kSumBlock + 1) * kSumBlock) - i;
+        for (size_t t = 0; t < m; ++t, ++i) {
             const double u1 = (c.x[idx[i]] - mx1) * s1, v1 = (c.y[idx[i]] - my1) * s1;
             const double u2 = (c.a[idx[i]] - mx2) * s2, v2 = (c.c0[idx[i]] - my2) * s2;
-            const double r[9] = {u2 * u1, u2 * v1, u2, v2 * u1, v2 * v1, v2, u1, v1, 1.0};
-            for (int p = 0; p < 9; ++p)
-                for (int q = p; q < 9; ++q) part[p][q] += r[p] * r[q];
+            double* r = rows[t];
+            r[0] = u2 * u1; r[1] = u2 * v1; r[2] = u2; r[3] = v2 * u1;
+            r[4] = v2 * v1; r[5] = v2; r[6] = u1; r[7] = v1;
         }
-        for (int p = 0; p < 9; ++p)
-            for (int q = p; q < 9; ++q) ata[p][q] += part[p][q];
+        v4d lo[8] = {}, c8lo = {};
+        for (size_t t = 0; t < m; ++t) {
+            const v4d R0 = ld4(rows[t]), R1 = ld4(rows[t] + 4);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const v4d b = {rows[t][p], rows[t][p], rows[t][p], rows[t][p]};
+                lo[2 * p] += b * R0;
+                lo[2 * p + 1] += b * R1;
+            }
+            c8lo += R0;
+        }
+        v4d hi[4] = {}, c8hi = {};
+        double c88 = 0.0;
+        for (size_t t = 0; t < m; ++t) {
+            const v4d R1 = ld4(rows[t] + 4);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const v4d b = {rows[t][4 + p], rows[t][4 + p], rows[t][4 + p], rows[t][4 + p]};
+                hi[p] += b * R1;
+            }
+            c8hi += R1;
+            c88 += 1.0;
+        }
+        for (int p = 0; p < 4; ++p) {
+            for (int q = p; q < 8; ++q) ata[p][q] += q < 4 ? lo[2 * p][q] : lo[2 * p + 1][q - 4];
+            for (int q = 4 + p; q < 8; ++q) ata[4 + p][q] += hi[p][q - 4];
+            ata[p][8] += c8lo[p];
+            ata[4 + p][8] += c8hi[p];
+        }
+        ata[8][8] += c88;
     }
     for (int p = 0; p < 9; ++p)
         for (int q = 0; q < p; ++q) ata[p][q] = ata[q][p];
