@@ -446,43 +446,72 @@ bool fit_h4_nonminimal(const HostClass& c, const std::vector<uint32_t>& idx, Geo
     return true;
 }
 
+// Cyclic Jacobi, rotations in (p, q) row order until the off-diagonal sum
+// is exactly zero.  Stored as padded rows so that the two rotated rows are
+// updated four entries per instruction: for k outside {p, q} the row update
+// cs * a[p][k] - sn * a[q][k] is bit for bit the column update of a[k][p]
+// (the matrix stays exactly symmetric), so the columns are mirrored from the
+// rows, and the 2 x 2 block is computed in the column-then-row order of the
+// plain loop.  The eigenvectors are kept transposed (rows contiguous).
+// Identical to the scalar loop bit for bit (the oracle's), 1.36x faster
+// (MEASUREMENTS.md).
 template <int N>
 void jacobi_eigen(double (&a)[N][N], double (&v)[N][N], double (&d)[N]) {
+    constexpr int L = (N + 3) & ~3;
+    typedef double v4d __attribute__((vector_size(32)));
+    alignas(32) double A[N][L] = {}, VT[N][L] = {};
     for (int i = 0; i < N; ++i)
-        for (int j = 0; j < N; ++j) v[i][j] = i == j ? 1.0 : 0.0;
+        for (int j = 0; j < N; ++j) {
+            A[i][j] = a[i][j];
+            VT[i][j] = i == j ? 1.0 : 0.0;
+        }
+    auto rotate = [](double* rp, double* rq, double cs, double sn) {
+        const v4d cv = {cs, cs, cs, cs}, sv = {sn, sn, sn, sn};
+        for (int k = 0; k < L; k += 4) {
+            v4d x, y;
+            __builtin_memcpy(&x, rp + k, sizeof x);
+            __builtin_memcpy(&y, rq + k, sizeof y);
+            const v4d nx = cv * x - sv * y, ny = sv * x + cv * y;
+            __builtin_memcpy(rp + k, &nx, sizeof nx);
+            __builtin_memcpy(rq + k, &ny, sizeof ny);
+        }
+    };
     for (int sweep = 0; sweep < 64; ++sweep) {
         double off = 0.0;
         for (int p = 0; p < N; ++p)
-            for (int q = p + 1; q < N; ++q) off += a[p][q] * a[p][q];
+            for (int q = p + 1; q < N; ++q) off += A[p][q] * A[p][q];
         if (!(off > 0.0)) break;
         for (int p = 0; p < N; ++p)
             for (int q = p + 1; q < N; ++q) {
-                const double apq = a[p][q];
+                const double apq = A[p][q];
                 if (apq == 0.0) continue;
-                const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+                const double app = A[p][p], aqq = A[q][q], aqp = A[q][p];
+                const double theta = (aqq - app) / (2.0 * apq);
                 double t = 1.0 / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
                 if (theta < 0.0) t = -t;
                 const double cs = 1.0 / std::sqrt(t * t + 1.0), sn = t * cs;
-                for (int k = 0; k < N; ++k) {           // columns p, q
-                    const double akp = a[k][p], akq = a[k][q];
-                    a[k][p] = cs * akp - sn * akq;
-                    a[k][q] = sn * akp + cs * akq;
-                }
-                for (int k = 0; k < N; ++k) {           // rows p, q
-                    const double apk = a[p][k], aqk = a[q][k];
-                    a[p][k] = cs * apk - sn * aqk;
-                    a[q][k] = sn * apk + cs * aqk;
-                }
-                a[p][q] = 0.0;
-                a[q][p] = 0.0;
+                // the block: columns p, q first (k = p, q), then rows p, q
+                const double cpp = cs * app - sn * apq, cpq = sn * app + cs * apq;
+                const double cqp = cs * aqp - sn * aqq, cqq = sn * aqp + cs * aqq;
+                const double npp = cs * cpp - sn * cqp, nqq = sn * cpq + cs * cqq;
+                rotate(A[p], A[q], cs, sn);
                 for (int k = 0; k < N; ++k) {
-                    const double vkp = v[k][p], vkq = v[k][q];
-                    v[k][p] = cs * vkp - sn * vkq;
-                    v[k][q] = sn * vkp + cs * vkq;
+                    A[k][p] = A[p][k];
+                    A[k][q] = A[q][k];
                 }
+                A[p][p] = npp;
+                A[q][q] = nqq;
+                A[p][q] = 0.0;
+                A[q][p] = 0.0;
+                rotate(VT[p], VT[q], cs, sn);
             }
     }
-    for (int k = 0; k < N; ++k) d[k] = a[k][k];
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) {
+            a[i][j] = A[i][j];
+            v[i][j] = VT[j][i];
+        }
+    for (int k = 0; k < N; ++k) d[k] = A[k][k];
 }
 
 template void jacobi_eigen<3>(double (&)[3][3], double (&)[3][3], double (&)[3]);
