@@ -2839,7 +2839,25 @@ private:
             if (P_->solver >= 3 && prm_.cell_number > 0 && prm_.spatial_coherence_weight > 0) {
                 const HostClass& c = P_->hc[0];
                 const double* cols[4] = {c.x.data(), c.y.data(), c.a.data(), c.c0.data()};
-                grid_edges(cols, 4, c.n, prm_.cell_size, prm_.cell_number, edges_, false);
+                // a cell size of 0 (image size unknown to the caller): the
+                // column's extent (largest finite coordinate + 1, at least 1)
+                // over the cells, as pygcransac.grid_cell_sizes computes it
+                double cs[4];
+                for (int d = 0; d < 4; ++d) {
+                    cs[d] = prm_.cell_size[d];
+                    if (cs[d] != 0.0) continue;
+                    double top = 0.0;
+                    bool any = false;
+                    for (size_t i = 0; i < c.n; ++i) {
+                        const double v = cols[d][i];
+                        if (std::isfinite(v) && (!any || v > top)) {
+                            top = v;
+                            any = true;
+                        }
+                    }
+                    cs[d] = (any ? std::max(1.0, top + 1.0) : 1.0) / static_cast<double>(prm_.cell_number);
+                }
+                grid_edges(cols, 4, c.n, cs, prm_.cell_number, edges_, false);
                 gc_schedule(edges_, host_pool().threads());
                 graph_state_ = edges_.cells() > 0 ? 1 : 0;
             }
@@ -3930,8 +3948,8 @@ int check_params(const gcr_params* p, int solver) {
             return set_err(GCR_EINVAL, "a neighbourhood grid is only supported for the homography and fundamental "
                                        "matrix estimators (the rectification entry points use an empty grid)");
         for (int d = 0; d < 4; ++d)
-            if (!(p->cell_size[d] > 0.0) || !std::isfinite(p->cell_size[d]))
-                return set_err(GCR_EINVAL, "neighbourhood cell sizes must be positive and finite");
+            if (!(p->cell_size[d] >= 0.0) || !std::isfinite(p->cell_size[d]))
+                return set_err(GCR_EINVAL, "neighbourhood cell sizes must be positive and finite (or 0: from the data)");
     }
     return GCR_OK;
 }

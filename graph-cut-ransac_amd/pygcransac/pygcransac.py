@@ -393,13 +393,26 @@ def grid_cell_sizes(correspondences, h1, w1, h2, w2, neighborhood_size):
     return [v / k for v in sizes]
 
 
-def _set_grid(p, correspondences, h1, w1, h2, w2, neighborhood_size):
+def grid_params(correspondences, h1, w1, h2, w2, neighborhood_size, from_data=True):
+    """(cell_number, cell sizes or None) of gcr_params' neighbourhood grid.
+    from_data=False leaves an unknown image size's cells at 0 for the engine
+    to take from the data (the same values, computed natively)."""
     cells = _as_size_t(neighborhood_size, "neighborhood_size")
     if cells > 0xFFFFFFFF:
         raise ValueError("neighborhood_size does not fit 32 bits")
+    if not cells:
+        return cells, None
+    if from_data:
+        return cells, grid_cell_sizes(correspondences, h1, w1, h2, w2, cells)
+    k = float(cells)
+    return cells, [float(v) / k if float(v) > 0.0 and math.isfinite(float(v)) else 0.0 for v in (w1, h1, w2, h2)]
+
+
+def _set_grid(p, correspondences, h1, w1, h2, w2, neighborhood_size):
+    cells, sizes = grid_params(correspondences, h1, w1, h2, w2, neighborhood_size)
     p.cell_number = cells
     if cells:
-        p.cell_size[:] = grid_cell_sizes(correspondences, h1, w1, h2, w2, cells)
+        p.cell_size[:] = sizes
 
 
 def _correspondence_call(entry, correspondences, h1, w1, h2, w2, probabilities, threshold, conf,

@@ -72,7 +72,10 @@ typedef struct gcr_params {
      * over (x1, y1, x2, y2) whose cells give labeling()'s pairwise terms
      * (GridNeighborhoodGraph<4>, grid_neighborhood_graph.h:229-301); cell
      * sizes in pixels, cell_number cells along every axis; 0 = the empty grid
-     * of the reference's entry points (no pairwise terms) */
+     * of the reference's entry points (no pairwise terms).  A cell size of
+     * exactly 0 (ABI 5) is taken from the data: the column's largest finite
+     * coordinate + 1 (at least 1) over cell_number, as
+     * pygcransac.grid_cell_sizes computes it for an unknown image size */
     double cell_size[4];
     uint32_t cell_number;
     uint32_t reserved;
