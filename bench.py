@@ -881,8 +881,15 @@ def bench_batch(args, rank, world, dist, device, coll_dev):
     problems = batch_problems(args.problems, lam=args.batch_lambda)
     solve_many = D.batch_solver(device, args.concurrency)
     shares = D.assign_lpt([D.problem_cost(p) for p in problems], world)
-    warm = [problems[i] for i in shares[rank][:max(1, args.warmup // 50)]]
-    solve_many(warm)                                   # untimed warm-up
+    # untimed warm-up: the share's 2 x concurrency costliest problems, so that
+    # every solving thread's context exists and its workspace has grown to
+    # the largest problem before the timed job (a single warm-up problem
+    # left 7 of 8 contexts and their device allocations to the timed region:
+    # 290 vs 210 ms per 1024 problems, tools/batch_split.py)
+    costs = [D.problem_cost(problems[i]) for i in shares[rank]]
+    top = sorted(range(len(costs)), key=lambda j: -costs[j])[:max(2 * args.concurrency, args.warmup // 50)]
+    warm = [problems[shares[rank][j]] for j in sorted(top)]
+    solve_many(warm)
 
     def barrier():
         N.check(N.lib.gcr_synchronize(N.context(device)))
