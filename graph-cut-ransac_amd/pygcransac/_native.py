@@ -10,6 +10,8 @@ import ctypes as C
 import os
 import threading
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # GCR_LIB selects an alternative in-tree build of the same engine (the
 # diagnostic libgcr_stamps.so of tools/stamp_probe.py)
@@ -79,7 +81,13 @@ class Stats(C.Structure):
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        # one read of the whole struct through a numpy record (ints and floats
+        # as getattr would give them), not 30-odd ctypes attribute reads
+        return dict(zip(_STATS_NAMES, np.frombuffer(self, dtype=_STATS_DT)[0].tolist()))
+
+
+_STATS_DT = np.dtype(Stats)
+_STATS_NAMES = _STATS_DT.names
 
 
 class BatchResult(C.Structure):
@@ -132,9 +140,12 @@ def _load():
     L.gcr_destroy.restype = None
     L.gcr_default_params.argtypes = [C.POINTER(Params)]
     L.gcr_default_params.restype = None
-    L.gcr_rect_scale_only.argtypes = [vp, dp, C.c_size_t, C.POINTER(Params), C.c_int, u8p, dp,
+    # the public entry points take their arrays as plain addresses (c_void_p
+    # also accepts typed pointers): the wrappers pass ndarray.ctypes.data,
+    # a third of their per-call Python cost otherwise
+    L.gcr_rect_scale_only.argtypes = [vp, vp, C.c_size_t, C.POINTER(Params), C.c_int, vp, vp,
                                       C.POINTER(RectModel), C.POINTER(Stats)]
-    L.gcr_rect_sift.argtypes = [vp, dp, C.c_size_t, dp, C.c_size_t, C.POINTER(Params), u8p, u8p, dp,
+    L.gcr_rect_sift.argtypes = [vp, vp, C.c_size_t, vp, C.c_size_t, C.POINTER(Params), vp, vp, vp,
                                 C.POINTER(RectModel), C.POINTER(Stats)]
     L.gcr_problem_create.argtypes = [vp, C.c_int, dp, C.c_size_t, dp, C.c_size_t, C.POINTER(vp)]
     L.gcr_problem_destroy.argtypes = [vp]
@@ -176,7 +187,7 @@ def _load():
     L.gcr_host_fit_nonminimal.argtypes = [C.c_int, dp, C.c_size_t, dp, C.c_size_t, u32p, C.c_size_t, u32p,
                                           C.c_size_t, C.POINTER(RectModel)]
     L.gcr_debug_fit_nonminimal.argtypes = [vp, u32p, C.c_size_t, u32p, C.c_size_t, C.c_int, C.POINTER(RectModel)]
-    L.gcr_find_homography.argtypes = [vp, dp, C.c_size_t, C.POINTER(Params), u8p, dp, C.POINTER(Stats)]
+    L.gcr_find_homography.argtypes = [vp, vp, C.c_size_t, C.POINTER(Params), vp, vp, C.POINTER(Stats)]
     L.gcr_debug_generate_h.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, u8p, dp]
     L.gcr_debug_score_h.argtypes = [vp, C.POINTER(Params), dp, C.c_uint32, u32p, dp, dp]
     L.gcr_debug_mask_h.argtypes = [vp, C.POINTER(Params), dp, C.c_int, u8p]

@@ -48,6 +48,9 @@ class _F64:
         return obj.__dict__[self.name]
 
     def __set__(self, obj, value):
+        if type(value) is float:                     # the common case, no ABC checks
+            obj.__dict__[self.name] = value
+            return
         if isinstance(value, (str, bytes)) or not isinstance(value, (numbers.Real, np.floating, np.integer)):
             raise TypeError(f"incompatible type for double attribute: {type(value).__name__}")
         obj.__dict__[self.name] = float(value)
@@ -220,6 +223,8 @@ def _as_features(arr):
 
 
 def _as_size_t(v, name):
+    if type(v) is int and 0 <= v <= 0xFFFFFFFFFFFFFFFF:
+        return v
     if isinstance(v, (bool, np.bool_)):
         v = int(v)
     if not isinstance(v, (numbers.Integral, np.integer)) or v < 0:
@@ -230,6 +235,8 @@ def _as_size_t(v, name):
 
 
 def _as_double(v, name):
+    if type(v) is float:
+        return v
     if isinstance(v, (str, bytes)) or not isinstance(v, (numbers.Real, np.floating, np.integer)):
         raise TypeError(f"incompatible function arguments: {name} must be a float")
     return float(v)
@@ -249,19 +256,25 @@ def _params(thr0, thr1, lam, min_it, max_it, lo, seed, confidence, batch_slots):
     return p
 
 
+_DP, _U8P = C.POINTER(C.c_double), C.POINTER(C.c_uint8)
+
+
 def _dp(a):
-    return a.ctypes.data_as(C.POINTER(C.c_double))
+    return C.cast(a.ctypes.data, _DP)
 
 
 def _u8(a):
-    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+    return C.cast(a.ctypes.data, _U8P)
 
 
 def _fill(model, m: N.RectModel, sift: bool):
-    model.x0, model.y0, model.s = m.x0, m.y0, m.s
-    model.h7, model.h8, model.alpha = m.h7, m.h8, m.alpha
+    # the engine's doubles straight into the model's slots (_F64 stores
+    # Python floats under "_" + name; ctypes double fields read as floats)
+    d = model.__dict__
+    d["_x0"], d["_y0"], d["_s"] = m.x0, m.y0, m.s
+    d["_h7"], d["_h8"], d["_alpha"] = m.h7, m.h8, m.alpha
     if sift:
-        model.phi = m.phi
+        d["_phi"] = m.phi
     return model
 
 
@@ -288,10 +301,10 @@ def _scale_only(original, features, scale_residual_thresh, spatial_coherence_wei
     m = N.RectModel()
     st = N.Stats()
     ctx = N.context(device)
-    rc = N.lib.gcr_rect_scale_only(ctx, _dp(f), n, C.byref(p), 1 if original else 0, _u8(mask), _dp(H),
-                                   C.byref(m), C.byref(st))
+    rc = N.lib.gcr_rect_scale_only(ctx, f.ctypes.data, n, C.byref(p), 1 if original else 0, mask.ctypes.data,
+                                   H.ctypes.data, C.byref(m), C.byref(st))
     num_inliers = N.check(rc)
-    inliers = mask.astype(bool)
+    inliers = mask.view(bool)
     extra = (st.as_dict(),) if return_stats else ()
     if num_inliers == 0:
         return (None, inliers) + extra
@@ -356,10 +369,10 @@ def findRectifyingHomographySIFT(scale_features, orientation_features, scale_res
     m = N.RectModel()
     st = N.Stats()
     ctx = N.context(device)
-    rc = N.lib.gcr_rect_sift(ctx, _dp(fs), ns, _dp(fo), no, C.byref(p), _u8(ms), _u8(mo), _dp(H), C.byref(m),
-                             C.byref(st))
+    rc = N.lib.gcr_rect_sift(ctx, fs.ctypes.data, ns, fo.ctypes.data, no, C.byref(p), ms.ctypes.data,
+                             mo.ctypes.data, H.ctypes.data, C.byref(m), C.byref(st))
     num_inliers = N.check(rc)
-    s_in, o_in = ms.astype(bool), mo.astype(bool)
+    s_in, o_in = ms.view(bool), mo.view(bool)
     extra = (st.as_dict(),) if return_stats else ()
     if num_inliers == 0:
         return (None, s_in, o_in, None) + extra
@@ -438,9 +451,9 @@ def _correspondence_call(entry, correspondences, h1, w1, h2, w2, probabilities, 
     M = np.zeros(9, dtype=np.float64)
     st = N.Stats()
     ctx = N.context(device)
-    rc = entry(ctx, _dp(f), n, C.byref(p), _u8(mask), _dp(M), C.byref(st))
+    rc = entry(ctx, f.ctypes.data, n, C.byref(p), mask.ctypes.data, M.ctypes.data, C.byref(st))
     num_inliers = N.check(rc)
-    inliers = mask.astype(bool)
+    inliers = mask.view(bool)
     extra = (st.as_dict(),) if return_stats else ()
     if num_inliers == 0:
         return (None, inliers) + extra
