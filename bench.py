@@ -257,7 +257,7 @@ def parse(argv=None):
                          "f: configs[3] 7-pt fundamental matrix, N=10000, 80%% outliers; "
                          "batch: configs[4] mixed H / F / rectification problems, full estimator calls")
     ap.add_argument("--problems", type=int, default=1024, help="batch workload: problems in the whole job")
-    ap.add_argument("--concurrency", type=int, default=8, help="batch workload: host threads per GPU")
+    ap.add_argument("--concurrency", type=int, default=12, help="batch workload: host threads per GPU")
     ap.add_argument("--batch-lambda", type=float, default=None,
                     help="batch workload: spatial_coherence_weight of the H / F problems (default: the entry "
                          "points' 0.975, graph-cut LO with pairwise terms; 0 isolates the graph-cut share)")
