@@ -86,3 +86,46 @@ def test_rectification_rejects_a_grid():
                                    300, C.byref(p), 0, m.ctypes.data_as(C.POINTER(C.c_uint8)),
                                    H.ctypes.data_as(C.POINTER(C.c_double)), None, None)
     assert rc == N.GCR_EINVAL
+
+
+def _direct_h(corr, thr, cell_size, cells=8, seed=2):
+    """gcr_find_homography with explicit gcr_params grid fields."""
+    import ctypes as C
+
+    c = np.ascontiguousarray(corr, dtype=np.float64)
+    p = N.default_params()
+    p.scale_residual_thresh = thr
+    p.spatial_coherence_weight = 0.975
+    p.min_iteration_number, p.max_iteration_number = 50, 2000
+    p.confidence, p.seed = 0.99, seed
+    p.cell_number = cells
+    p.cell_size[:] = list(cell_size)
+    mask = np.zeros(c.shape[0], np.uint8)
+    M = np.zeros(9)
+    rc = N.lib.gcr_find_homography(N.context(0), c.ctypes.data, c.shape[0], C.byref(p), mask.ctypes.data,
+                                   M.ctypes.data, None)
+    return rc, mask.view(bool), M.reshape(3, 3)
+
+
+def test_zero_cell_sizes_are_taken_from_the_data():
+    # ABI 5: cell_size[d] == 0 -> the column's largest finite coordinate + 1
+    # over the cells, computed by the engine; equal to the Python sizing
+    # (grid_cell_sizes) the direct entry point applies, so the run is the
+    # oracle's with those sizes bit for bit.  One known axis mixed in.
+    corr, _, _, thr = S.problem_h(1800, 0.5, seed=91)
+    sizes = P.grid_cell_sizes(corr, 0, W1, 0, 0, 8)
+    rc, mask, M = _direct_h(corr, thr, [W1 / 8.0, 0.0, 0.0, 0.0])
+    # grid_cell_sizes' argument order is (h1, w1, h2, w2); its sizes (w1, h1, w2, h2)
+    assert rc > 0 and sizes[0] == W1 / 8.0
+    ref = O.find_homography(corr, thr, lam=0.975, min_it=50, max_it=2000, confidence=0.99, seed=2,
+                            cell_size=sizes, cell_number=8)
+    assert np.array_equal(mask, ref["mask"]) and np.array_equal(bits(M), bits(ref["H"]))
+    rc2, mask2, M2 = _direct_h(corr, thr, sizes)
+    assert rc2 == rc and np.array_equal(mask2, mask) and np.array_equal(bits(M2), bits(M))
+
+
+def test_negative_or_nonfinite_cell_sizes_are_rejected():
+    corr, _, _, thr = S.problem_h(300, 0.5, seed=92)
+    for bad in ([-1.0, 10.0, 10.0, 10.0], [10.0, float("inf"), 10.0, 10.0], [10.0, 10.0, float("nan"), 10.0]):
+        rc, _, _ = _direct_h(corr, thr, bad)
+        assert rc == N.GCR_EINVAL, bad
